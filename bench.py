@@ -1,0 +1,170 @@
+"""Benchmark: PhysicsNet training steps/s on MI355X (BASELINE.json metric
+"video-seqs/sec (train step) spring_color B=100").
+
+One step = forward (encoder U-Net, localiser, velocity MLP, 46-step physics
+rollout, STN decoder over all frames), fused loss, backward, gradient
+all-reduce (N>1, RCCL), RMSprop — the reference's train loop body
+(nn/network/base.py:139-152) in fresh-loss mode, through the drop-in
+PhysicsNet API.  Inputs are synthetic spring_color videos rendered on the host
+once and kept resident in HBM (data="synthetic").
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Weak scaling: B sequences per rank.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 (vector == f32 MFMA), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=100, help="sequences per rank")
+    ap.add_argument("--task", default="spring_color")
+    ap.add_argument("--seq_len", type=int, default=50, help="4 in / 6 pred / 40 extrap")
+    ap.add_argument("--ae", type=float, default=3.0)
+    ap.add_argument("--lr", type=float, default=6e-4)
+    ap.add_argument("--nbatches", type=int, default=4, help="distinct resident batches cycled through")
+    ap.add_argument("--probe", default="auto", help="kernel tag timed with HIP events for the roofline")
+    ap.add_argument("--cpu_baseline", type=int, default=1)
+    ap.add_argument("--cpu_seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(task, seq_len, ae, budget_s):
+    """The oracle (torch CPU restatement of the reference, pinned to the
+    reference's golden vectors) timed on a bounded sample of the same
+    workload: fresh-mode train steps of B_s sequences at the same seq_len."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    from oracle import physics_oracle as O
+    from paig_reproduction_amd.nn.datasets.synth import render_sequences, as_model_input
+    from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cell, _, _, ins, pred, size, _ = O.TASKS[task]
+    cfg = O.Cfg(task, cell, seq_len, ins, pred, size, ae)
+    torch.manual_seed(0)
+    m = PhysicsNet(task, 100, 1, cell, seq_len, ins, pred, ae, False, True, size * size, "", "conv_st_decoder")
+    state = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    Bs = 10
+    x = torch.from_numpy(as_model_input(render_sequences(task, Bs, seq_len, seed=7)))
+    O.train_step(state, cfg, x)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.train_step(state, cfg, x)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 50:
+            break
+    return {"value": round(n * Bs / el, 3), "unit": "video-seqs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} fresh-mode train steps x {Bs} seqs ({task}, seq_len {seq_len}), oracle/physics_oracle.py "
+                      f"on torch CPU, {threads} threads, {el:.1f}s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+
+    from paig_reproduction_amd.nn.datasets.synth import render_sequences, as_model_input
+    from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
+    from paig_reproduction_amd import engine as E
+
+    cells = {"spring_color": "spring_ode_cell", "bouncing_balls": "bouncing_ode_cell", "3bp_color": "gravity_ode_cell",
+             "spring_color_half": "spring_ode_cell"}
+    ins, pred, size = {"3bp_color": (4, 12, 36)}.get(a.task, (4, 6, 32))
+    torch.manual_seed(0)
+    m = PhysicsNet(a.task, 100, 1, cells[a.task], a.seq_len, ins, pred, a.ae, False, True, size * size,
+                   "conv_encoder", "conv_st_decoder", device=dev).to(dev)
+    m.build_optimizer(a.lr, "rmsprop", True)
+    if world > 1:
+        for t in m.state_dict().values():
+            dist.broadcast(t, 0)
+
+    data = [torch.from_numpy(as_model_input(render_sequences(a.task, a.batch, a.seq_len, seed=1000 * rank + i)))
+            .to(dev) for i in range(a.nbatches)]
+
+    probe = E.KernelProbe(a.probe if a.probe != "auto" else "conv_wgrad:c10")
+    m._native().probe = None
+
+    def step(i, timed):
+        x = data[i % len(data)]
+        m._native().probe = probe if timed else None
+        m.output = m(x)
+        loss, _ = m.compute_loss()
+        m.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        m.optimizer.step()
+        return loss
+
+    for i in range(a.warmup):
+        step(i, False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(i, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    lossv = float(loss.item())
+
+    seqs = world * a.batch * a.steps
+    value = seqs / el
+    kd = probe.summary()
+    roof = None
+    if kd is not None:
+        achieved = kd["flops"] / (kd["avg_ms"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": kd["tag"], "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                "avg_us": round(kd["avg_ms"] * 1e3, 2), "launches": kd["n"], "algorithmic_flops": kd["flops"]}
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_baseline:
+        cpu = cpu_baseline(a.task, a.seq_len, a.ae, a.cpu_seconds)
+    if rank == 0:
+        line = {
+            "metric": "video-seqs/sec (train step) spring_color B=100",
+            "value": round(value, 2), "unit": "video-seqs/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"{a.task} PhysicsNet train step (fwd+loss+bwd+allreduce+RMSprop), "
+                                   f"B={a.batch}/rank, 32x32x3, seq_len {a.seq_len} "
+                                   f"({ins} in / {pred} pred / {a.seq_len - ins - pred} extrap)",
+                       "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "final_loss": round(lossv, 4),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+/*
+ * paig_hip.h — C ABI of libpaig_hip.so, the MI355X (gfx950) kernels of the
+ * PhysicsNet training step (Luka140/paig_reproduction).
+ *
+ * The reference has no FFI of its own: every FLOP of its hot path is an aten
+ * op called from Python.  Each entry point below replaces a group of those
+ * calls (cited per function); the Python binding (paig_reproduction_amd/_lib.py,
+ * ctypes) is what the reference-side PhysicsNet/BaseNetTorch surface calls.
+ *
+ * Conventions
+ *   - return 0 on success, else PAIG_E_SHAPE (1001), PAIG_E_UNSUPPORTED (1002)
+ *     or a hipError_t; never throws/aborts.  paig_last_error() explains.
+ *   - all pointers are device pointers (fp32 unless the name says f64/double);
+ *     `stream` is a hipStream_t; every call is asynchronous on it and is
+ *     graph-capturable (no allocation, no host synchronisation).
+ *   - frame views: frame f of an activation [.., C, H, W] starts at
+ *       p + (grp > 0 ? (f / grp) * fs + (f % grp) * gs : f * fs)
+ *     so the first Te frames of each sequence of a [B, T, C, H, W] input are
+ *     addressed in place (grp = Te, fs = T*C*H*W, gs = C*H*W).
+ *   - the library never allocates: workspaces/slabs are caller-provided,
+ *     sized with the *_workspace / *_blocks / *_len queries.
+ */
+#ifndef PAIG_HIP_H
+#define PAIG_HIP_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* paig_last_error(void);
+int paig_abi_version(void);
+
+/* ---- U-Net convolutions -------------------------------------------------
+ * replaces aten conv2d / convolution_backward for ShallowUNet and UNet
+ * (nn/network/blocks.py:246-276 and :113-170, forward :278-308, :172-237).
+ * flags: 1 ReLU, 2 multiply by (aux > 0) [ReLU' of the layer input],
+ *        4 accumulate into out, 8 dgrad (in = dY, weight read transposed and
+ *        flipped, Cin/Cout are the DGRAD kernel's in/out channel counts).  */
+int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                    const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin, int Cout,
+                    int H, int W, int ks, int flags, void* stream);
+/* per-block partial [Cout*Cin*ks*ks | Cout] weight+bias grads into slab rows */
+int paig_conv2d_wgrad(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
+                      float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
+                      void* stream);
+
+/* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
+int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,
+                      void* stream);
+/* dx = (dx + scatter_argmax(dy)) * (x > 0) */
+int paig_maxpool2_bwd_relu(const float* x, long long x_fs, const float* dy, long long dy_fs, float* dx, long long dx_fs,
+                           int F, int C, int H, int W, void* stream);
+int paig_upsample2_fwd(const float* s, long long s_fs, float* u, long long u_fs, int F, int C, int Hs, int Ws, int Ho,
+                       int Wo, void* stream);
+int paig_upsample2_bwd(const float* du, long long du_fs, const float* s, long long s_fs, float* ds, long long ds_fs,
+                       int F, int C, int Hs, int Ws, int Ho, int Wo, int relu_mask, void* stream);
+
+/* ---- encoder head: cat(ones)+softmax+mask*image (blocks.py:84-93),
+ *      tanh position head (blocks.py:101-102) */
+int paig_mask_softmax_fwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs, float* masks,
+                          float* objs, int F, int K, int C, int HW, void* stream);
+int paig_mask_softmax_bwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs,
+                          const float* masks, const float* dobjs, float* dlogits, int F, int K, int C, int HW,
+                          void* stream);
+int paig_pos_head_fwd(const float* h3, float* pos, int N, int K, float half, void* stream);
+int paig_pos_head_bwd(const float* h3, const float* dpos, float* dh3, int N, int K, float half, void* stream);
+
+/* ---- dense layers on MFMA (l1/l2/l3 blocks.py:71-75,98-100; velocity MLP
+ *      blocks.py:23-29,43-48; VariableFromNetwork blocks.py:311-322)
+ * C = alpha op(A) op(B) (+beta C) (+bias[n]) -> act (0 none,1 relu,2 tanh,3 sigmoid)
+ *     -> * aux' (auxm 0 none, 1 relu'(aux), 2 tanh'(aux)=1-aux^2)          */
+size_t paig_gemm_workspace(int M, int N, int K);
+int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
+              long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
+              const float* aux, long long ldaux, float* ws, size_t ws_floats, void* stream);
+size_t paig_colsum_workspace(int M, int N);
+int paig_colsum(const float* X, int M, int N, long long ld, float* out, int accumulate, float* ws, void* stream);
+int paig_slab_reduce(const float* slab, int nblk, long long ld, int len, float* out, int accumulate, void* stream);
+int paig_axpby(const float* x, float* y, long long n, float a, float b, void* stream);
+
+/* VariableFromNetwork: y = W2 tanh(W1 ones + b1) + b2 (ypost = sigmoid(y) if given) */
+int paig_vfn_fwd(const float* W1, const float* b1, const float* W2, const float* b2, float* hout, float* y,
+                 float* ypost, int P, void* stream);
+int paig_vfn_bwd_blocks(int P);
+int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,
+                 float* dW2, float* db2, float* part, int P, void* stream);
+
+/* ---- velocity encoder input packing (blocks.py:33-45) */
+int paig_vel_pack(const float* pos, float* X, int B, int Te, int K, int S, int alt, void* stream);
+int paig_vel_unpack_add(const float* dX, const float* dpos0, float* dpos, int B, int Te, int K, int S, int alt,
+                        void* stream);
+
+/* ---- physics rollout: all R steps x 5 substeps (cells.py:31-51, 60-83,
+ *      96-106; loop physics_models.py:231-239).  cell 0 spring, 1 bouncing,
+ *      2 gravity.  dt/p0/p1 are device 0-dim params (p0,p1 = k,equil | g,m). */
+int paig_rollout_fwd(int cell, const float* pos0, long long pos0_ld, const float* vel0, const float* dt,
+                     const double* p0, const double* p1, float* pvs, int B, int D, int R, void* stream);
+int paig_rollout_bwd_blocks(int B);
+int paig_rollout_bwd(int cell, const float* pvs, const float* dpos_roll, const float* dpvs, const float* dt,
+                     const double* p0, const double* p1, float* dpos0, float* dvel0, double* part, double* gparam0,
+                     double* gparam1, int accumulate, int B, int D, int R, void* stream);
+
+/* ---- spatial-transformer decoder + compositing + per-frame SSE
+ *      (conv_st_decoder physics_models.py:151-199, stn stn.py:5-16,
+ *       compute_loss physics_models.py:119-135), all frames in one launch */
+int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                     const float* cont, const float* bg, float* out, long long out_fs, const float* tgt,
+                     long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F, int K, int h, int H,
+                     void* stream);
+int paig_decoder_bwd_blocks(int F);
+size_t paig_decoder_slab_len(int K, int h, int H);
+size_t paig_decoder_bwd_scratch(int F, int K, int h, int H);
+int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                     const float* cont, const float* bg, const float* tgt, long long tgt_fs, int tgt_grp,
+                     long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
+                     float* slab, float* scratch, int F, int K, int h, int H, void* stream);
+
+/* ---- losses (physics_models.py:119-142): means of the per-frame SSE;
+ *      extrap is NaN when there are no extrapolation steps (mean of empty) */
+int paig_loss_reduce(const float* sse_rec, const float* sse_roll, int B, int Te, int R, int pred, float* pred_out,
+                     float* extrap_out, float* recons_out, void* stream);
+int paig_loss_bwd(const float* dpred, const float* dext, const float* drec, float* wrec, float* wroll, int B, int Te,
+                  int R, int pred, void* stream);
+int paig_frame_sse(const float* a, long long a_fs, int a_grp, long long a_gs, const float* b, long long b_fs, int b_grp,
+                   long long b_gs, float* sse, int F, int n, void* stream);
+int paig_frame_sse_bwd(const float* a, long long a_fs, int a_grp, long long a_gs, const float* b, long long b_fs,
+                       int b_grp, long long b_gs, const float* w, float* da, int F, int n, void* stream);
+
+/* ---- optimizers over the flat parameter buffer (base.py:12-17, torch defaults) */
+int paig_rmsprop_f32(float* p, const float* g, float* sa, long long n, float lr, float alpha, float eps, void* stream);
+int paig_rmsprop_f64(double* p, const double* g, double* sa, long long n, double lr, double alpha, double eps,
+                     void* stream);
+int paig_adam_f32(float* p, const float* g, float* m, float* v, long long n, float lr, float b1, float b2, float eps,
+                  float bc1, float bc2sqrt, void* stream);
+int paig_adam_f64(double* p, const double* g, double* m, double* v, long long n, double lr, double b1, double b2,
+                  double eps, double bc1, double bc2sqrt, void* stream);
+int paig_sgd_f32(float* p, const float* g, float* buf, long long n, float lr, float mom, int first, void* stream);
+int paig_sgd_f64(double* p, const double* g, double* buf, long long n, double lr, double mom, int first, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PAIG_HIP_H */

@@ -1,0 +1,131 @@
+"""ctypes binding of libpaig_hip.so (the C ABI declared in include/paig_hip.h).
+
+The library is built in-tree (``make -C paig_reproduction_amd/csrc`` or
+``__graft_entry__.build()``).  There is deliberately no fallback: if the
+library cannot be loaded, every product call raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads torch's HIP runtime first; the .so binds to it)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpaig_hip.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+F32 = ctypes.c_float
+F64 = ctypes.c_double
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); must mirror include/paig_hip.h exactly
+SIGNATURES = {
+    "paig_last_error": (ctypes.c_char_p, []),
+    "paig_abi_version": (I, []),
+    "paig_conv2d_fwd": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P]),
+    "paig_conv2d_wgrad": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, P]),
+    "paig_maxpool2_fwd": (I, [P, LL, P, LL, I, I, I, I, P]),
+    "paig_maxpool2_bwd_relu": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
+    "paig_upsample2_fwd": (I, [P, LL, P, LL, I, I, I, I, I, I, P]),
+    "paig_upsample2_bwd": (I, [P, LL, P, LL, P, LL, I, I, I, I, I, I, I, P]),
+    "paig_mask_softmax_fwd": (I, [P, P, LL, I, LL, P, P, I, I, I, I, P]),
+    "paig_mask_softmax_bwd": (I, [P, P, LL, I, LL, P, P, P, I, I, I, I, P]),
+    "paig_pos_head_fwd": (I, [P, P, I, I, F32, P]),
+    "paig_pos_head_bwd": (I, [P, P, P, I, I, F32, P]),
+    "paig_gemm_workspace": (SZ, [I, I, I]),
+    "paig_gemm": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, SZ, P]),
+    "paig_colsum_workspace": (SZ, [I, I]),
+    "paig_colsum": (I, [P, I, I, LL, P, I, P, P]),
+    "paig_slab_reduce": (I, [P, I, LL, I, P, I, P]),
+    "paig_axpby": (I, [P, P, LL, F32, F32, P]),
+    "paig_vfn_fwd": (I, [P, P, P, P, P, P, P, I, P]),
+    "paig_vfn_bwd_blocks": (I, [I]),
+    "paig_vfn_bwd": (I, [P, P, I, P, P, P, P, P, P, P, I, P]),
+    "paig_vel_pack": (I, [P, P, I, I, I, I, I, P]),
+    "paig_vel_unpack_add": (I, [P, P, P, I, I, I, I, I, P]),
+    "paig_rollout_fwd": (I, [I, P, LL, P, P, P, P, P, I, I, I, P]),
+    "paig_rollout_bwd_blocks": (I, [I]),
+    "paig_rollout_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P]),
+    "paig_decoder_fwd": (I, [P, LL, LL, I, P, P, P, P, LL, P, LL, I, LL, P, I, I, I, I, P]),
+    "paig_decoder_bwd_blocks": (I, [I]),
+    "paig_decoder_slab_len": (SZ, [I, I, I]),
+    "paig_decoder_bwd_scratch": (SZ, [I, I, I, I]),
+    "paig_decoder_bwd": (I, [P, LL, LL, I, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, P]),
+    "paig_loss_reduce": (I, [P, P, I, I, I, I, P, P, P, P]),
+    "paig_loss_bwd": (I, [P, P, P, P, P, I, I, I, I, P]),
+    "paig_frame_sse": (I, [P, LL, I, LL, P, LL, I, LL, P, I, I, P]),
+    "paig_frame_sse_bwd": (I, [P, LL, I, LL, P, LL, I, LL, P, P, I, I, P]),
+    "paig_rmsprop_f32": (I, [P, P, P, LL, F32, F32, F32, P]),
+    "paig_rmsprop_f64": (I, [P, P, P, LL, F64, F64, F64, P]),
+    "paig_adam_f32": (I, [P, P, P, P, LL, F32, F32, F32, F32, F32, F32, P]),
+    "paig_adam_f64": (I, [P, P, P, P, LL, F64, F64, F64, F64, F64, F64, P]),
+    "paig_sgd_f32": (I, [P, P, P, LL, F32, F32, I, P]),
+    "paig_sgd_f64": (I, [P, P, P, LL, F64, F64, I, P]),
+}
+
+_QUERY = {"paig_last_error", "paig_abi_version", "paig_gemm_workspace", "paig_colsum_workspace",
+          "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
+          "paig_decoder_bwd_scratch"}
+
+
+class PaigError(RuntimeError):
+    pass
+
+
+class _Lib:
+    def __init__(self, path=LIB_PATH):
+        if not os.path.exists(path):
+            raise PaigError(f"libpaig_hip.so not built at {path}: run `make -C paig_reproduction_amd/csrc` "
+                            "(or __graft_entry__.build()); there is no CPU fallback")
+        self.path = path
+        self.dll = ctypes.CDLL(path)
+        self.fns = {}
+        for name, (rt, args) in SIGNATURES.items():
+            f = getattr(self.dll, name)
+            f.restype = rt
+            f.argtypes = args
+            self.fns[name] = f
+
+    def __getattr__(self, name):
+        fns = self.__dict__.get("fns")
+        if fns is None or name not in fns:
+            raise AttributeError(name)
+        f = fns[name]
+        if name in _QUERY:
+            return f
+
+        def call(*a):
+            rc = f(*a)
+            if rc != 0:
+                msg = self.fns["paig_last_error"]().decode(errors="replace")
+                raise PaigError(f"{name} failed (rc={rc}): {msg}")
+            return rc
+
+        call.__name__ = name
+        return call
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _Lib()
+    return _lib
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(t):
+    if not (torch.is_tensor(t) and t.is_cuda):
+        raise PaigError("paig_reproduction_amd runs only on a HIP device (MI355X); got a "
+                        f"{'CPU' if torch.is_tensor(t) else type(t).__name__} tensor. There is no CPU fallback.")

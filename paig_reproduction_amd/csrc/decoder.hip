@@ -1,0 +1,408 @@
+// Spatial-transformer decoder + compositing + per-frame SSE, forward and
+// backward, batched over every decoded frame of a step in one launch.
+//
+// Reference: PhysicsNet.conv_st_decoder, nn/network/physics_models.py:151-199
+// and stn(), nn/network/stn.py:5-16 (aten affine_grid + grid_sample, bilinear,
+// zeros padding, align_corners=False), compositing softmax :192-198, loss
+// :119-135.  The reference calls the decoder once per rollout step and
+// rebuilds every warp grid; here one launch covers all B*T frames.
+//
+// Per object k the warp is a pure translation: theta = [[1,0,t2],[0,1,t5]],
+// t2 = (H/2 - x_k)/h (fp32, as the reference), the grid is formed in fp64 as
+// affine_grid does (Q9) and cast to fp32 before grid_sample's unnormalize.
+// Sources (template+5, sigmoid(content): [K][.][h][h]) are staged in LDS once
+// per block; the background (already sigmoid'ed) is read from global.
+//
+// Backward recomputes the forward per pixel, forms dL/dout = 2*dsse[f]*(out -
+// target) (+ an optional dense dL/dout), and produces
+//   * dpos[f][2k+{0,1}] = -(sum_p dix_p * h/2) / h   (grid_sample grid-grad
+//     -> affine_grid -> theta -> loc chain), reduced in fp64 per frame;
+//   * per-block partial source gradients (template, content, background),
+//     gathered (not scattered) from a per-frame pixel-gradient image, so the
+//     sum is deterministic; paig_slab_reduce finishes it.
+#include "common.h"
+
+namespace {
+
+struct Src {
+  const float* tmpl;  // [K][h*h] raw template logits (VariableFromNetwork)
+  const float* cont;  // [K][3][h*h] raw content logits
+  const float* bg;    // [3][H*W] background, already sigmoid'ed
+};
+
+struct PosView {
+  const float* p;
+  long long outer, inner;
+  int grp;
+  __device__ __forceinline__ const float* at(int f) const {
+    return grp > 0 ? p + (long long)(f / grp) * outer + (long long)(f % grp) * inner : p + (long long)f * inner;
+  }
+};
+
+// affine_grid base coordinate: linspace(-1, 1, n)[j] * (n - 1) / n  in fp64
+__device__ __forceinline__ double base_coord(int j, int n) {
+  const double step = 2.0 / (double)(n - 1);
+  const double v = (j < n / 2) ? -1.0 + step * (double)j : 1.0 - step * (double)(n - 1 - j);
+  return v * (double)(n - 1) / (double)n;
+}
+
+// grid_sample unnormalized source coordinate for output index j
+__device__ __forceinline__ float src_coord(int j, int n, double t, int h) {
+  const float g = (float)(base_coord(j, n) + t);
+  return ((g + 1.f) * (float)h - 1.f) / 2.f;
+}
+
+struct Bil {
+  int x0, y0;
+  float fx, fy;  // ix - x0, iy - y0
+};
+
+__device__ __forceinline__ Bil bil(float ix, float iy) {
+  Bil b;
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  b.x0 = (int)fx0;
+  b.y0 = (int)fy0;
+  b.fx = ix - fx0;
+  b.fy = iy - fy0;
+  return b;
+}
+
+__device__ __forceinline__ float tap(const float* s, int h, int y, int x) {
+  return (x >= 0 && x < h && y >= 0 && y < h) ? s[y * h + x] : 0.f;
+}
+
+// value and d/dix, d/diy of the bilinear sample of source s (h x h, zero padded)
+__device__ __forceinline__ void sample(const float* s, int h, const Bil& b, float& v, float& dx, float& dy) {
+  const float nw = tap(s, h, b.y0, b.x0), ne = tap(s, h, b.y0, b.x0 + 1);
+  const float sw = tap(s, h, b.y0 + 1, b.x0), se = tap(s, h, b.y0 + 1, b.x0 + 1);
+  const float ex = 1.f - b.fx, ey = 1.f - b.fy;
+  v = nw * ex * ey + ne * b.fx * ey + sw * ex * b.fy + se * b.fx * b.fy;
+  dx = (ne - nw) * ey + (se - sw) * b.fy;
+  dy = (sw - nw) * ex + (se - ne) * b.fx;
+}
+
+template <int K>
+__device__ __forceinline__ void stage_sources(const Src& S, int h, float* T, float* Cn) {
+  const int hh = h * h;
+  for (int i = threadIdx.x; i < K * hh; i += blockDim.x) T[i] = S.tmpl[i] + 5.f;
+  for (int i = threadIdx.x; i < K * 3 * hh; i += blockDim.x) Cn[i] = 1.f / (1.f + expf(-S.cont[i]));
+}
+
+// forward composite of one pixel; returns out[3], masks m[K+1], samples
+template <int K>
+__device__ __forceinline__ void composite(const float* T, const float* Cn, const float* bg, int HW, int p, int h,
+                                          const Bil* bl, float* out, float* m, float (*cs)[3]) {
+  const int hh = h * h;
+  float lg[K + 1];
+  float mx = 1.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float v, dx, dy;
+    sample(T + k * hh, h, bl[k], v, dx, dy);
+    lg[k] = v - 5.f;
+    mx = fmaxf(mx, lg[k]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      sample(Cn + (k * 3 + c) * hh, h, bl[k], v, dx, dy);
+      cs[k][c] = v;
+    }
+  }
+  lg[K] = 1.f;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k <= K; ++k) {
+    m[k] = expf(lg[k] - mx);
+    s += m[k];
+  }
+#pragma unroll
+  for (int k = 0; k <= K; ++k) m[k] = m[k] / s;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float o = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) o += m[k] * cs[k][c];
+    out[c] = o + m[K] * bg[c * HW + p];
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(256)
+dec_fwd_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse, int F, int h, int H) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int hh = h * h, HW = H * H;
+  float* T = lds;
+  float* Cn = T + K * hh;
+  __shared__ float red[4];
+  stage_sources<K>(S, h, T, Cn);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int f = blockIdx.x; f < F; f += gridDim.x) {
+    const float* pf = pos.at(f);
+    double tx[K], ty[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      tx[k] = (double)(((float)H / 2.f - pf[2 * k]) / (float)h);
+      ty[k] = (double)(((float)H / 2.f - pf[2 * k + 1]) / (float)h);
+    }
+    float* of = out.frame(f);
+    const float* tf = sse ? tgt.frame(f) : nullptr;
+    float acc = 0.f;
+    for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+      const int i = p / H, j = p % H;
+      Bil bl[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) bl[k] = bil(src_coord(j, H, tx[k], h), src_coord(i, H, ty[k], h));
+      float o[3], m[K + 1], cs[K][3];
+      composite<K>(T, Cn, S.bg, HW, p, h, bl, o, m, cs);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        of[c * HW + p] = o[c];
+        if (tf) {
+          const float d = tf[c * HW + p] - o[c];
+          acc = fmaf(d, d, acc);
+        }
+      }
+    }
+    if (sse) {
+      acc = wave_sum(acc);
+      if (lane == 0) red[wv] = acc;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+        sse[f] = s;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// slab row layout per block: [K*h*h template | K*3*h*h content | 3*H*W bg]
+template <int K>
+__global__ void __launch_bounds__(256)
+dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
+          float* __restrict__ slab, float* __restrict__ gscratch, int F, int h, int H) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int hh = h * h, HW = H * H;
+  float* T = lds;
+  float* Cn = T + K * hh;
+  float* G = gscratch ? gscratch + (long long)blockIdx.x * K * 4 * HW : Cn + K * 3 * hh;  // [K][4][HW]
+  __shared__ double redd[4][2 * K];
+  __shared__ int skip_s;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  const long long slab_len = (long long)K * hh + (long long)K * 3 * hh + 3LL * HW;
+  float* srow = slab + (long long)blockIdx.x * slab_len;
+  float* s_tm = srow;
+  float* s_ct = srow + K * hh;
+  float* s_bg = s_ct + K * 3 * hh;
+  // zero this block's slab row (each element is owned by exactly one thread below)
+  for (int s = threadIdx.x; s < K * hh; s += blockDim.x) {
+    s_tm[s] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s_ct[(s / hh * 3 + c) * hh + s % hh] = 0.f;
+  }
+  for (int p = threadIdx.x; p < HW; p += blockDim.x)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s_bg[c * HW + p] = 0.f;
+  stage_sources<K>(S, h, T, Cn);
+  __syncthreads();
+
+  for (int f = blockIdx.x; f < F; f += gridDim.x) {
+    const float w_f = dsse ? 2.f * dsse[f] : 0.f;
+    const float* dof = dout.p ? dout.frame(f) : nullptr;
+    if (threadIdx.x == 0) skip_s = (w_f == 0.f && dof == nullptr);
+    __syncthreads();
+    if (skip_s) {
+      if (threadIdx.x < 2 * K) dpos[(long long)f * 2 * K + threadIdx.x] = 0.f;
+      __syncthreads();
+      continue;
+    }
+    const float* pf = pos.at(f);
+    double tx[K], ty[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      tx[k] = (double)(((float)H / 2.f - pf[2 * k]) / (float)h);
+      ty[k] = (double)(((float)H / 2.f - pf[2 * k + 1]) / (float)h);
+    }
+    const float* tf = tgt.frame(f);
+    double sx[K], sy[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) sx[k] = sy[k] = 0.0;
+
+    // ---- pass 1: per-pixel gradients
+    for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+      const int i = p / H, j = p % H;
+      Bil bl[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) bl[k] = bil(src_coord(j, H, tx[k], h), src_coord(i, H, ty[k], h));
+      float o[3], m[K + 1], cs[K][3];
+      composite<K>(T, Cn, S.bg, HW, p, h, bl, o, m, cs);
+      float g[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        g[c] = w_f * (o[c] - tf[c * HW + p]);
+        if (dof) g[c] += dof[c * HW + p];
+        s_bg[c * HW + p] += m[K] * g[c];
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float dT = 0.f;
+        float dC[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          dC[c] = m[k] * g[c];
+          dT = fmaf(g[c], cs[k][c] - o[c], dT);
+        }
+        dT *= m[k];
+        G[(k * 4 + 0) * HW + p] = dT;
+        float v, dx, dy;
+        sample(T + k * hh, h, bl[k], v, dx, dy);
+        float gx = dT * dx, gy = dT * dy;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          G[(k * 4 + 1 + c) * HW + p] = dC[c];
+          sample(Cn + (k * 3 + c) * hh, h, bl[k], v, dx, dy);
+          gx = fmaf(dC[c], dx, gx);
+          gy = fmaf(dC[c], dy, gy);
+        }
+        sx[k] += (double)gx;
+        sy[k] += (double)gy;
+      }
+    }
+    // ---- per-frame dpos reduction (fp64)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      double a = wave_sum_d(sx[k]), b = wave_sum_d(sy[k]);
+      if (lane == 0) {
+        redd[wv][2 * k] = a;
+        redd[wv][2 * k + 1] = b;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * K) {
+      double s = 0.0;
+      for (int w = 0; w < nw; ++w) s += redd[w][threadIdx.x];
+      // d theta = sum_p dgrid = sum_p dix * h/2 ; dloc = -dtheta / h
+      const float dth = (float)(s * (double)h * 0.5);
+      dpos[(long long)f * 2 * K + threadIdx.x] = -dth / (float)h;
+    }
+    // ---- pass 2: gather source gradients from the pixel-gradient image
+    for (int s = threadIdx.x; s < K * hh; s += blockDim.x) {
+      const int k = s / hh, q = s % hh, ys = q / h, xs = q % h;
+      // output index j has ix(j) ~= a + j*h/H; candidates with floor(ix) in {xs-1, xs}
+      const float a0x = src_coord(0, H, tx[k], h), a0y = src_coord(0, H, ty[k], h);
+      const float slope = (float)h / (float)H;
+      int jlo = (int)floorf(((float)xs - 1.f - a0x) / slope) - 1, jhi = (int)ceilf(((float)xs + 1.f - a0x) / slope) + 1;
+      int ilo = (int)floorf(((float)ys - 1.f - a0y) / slope) - 1, ihi = (int)ceilf(((float)ys + 1.f - a0y) / slope) + 1;
+      if (jlo < 0) jlo = 0;
+      if (ilo < 0) ilo = 0;
+      if (jhi > H - 1) jhi = H - 1;
+      if (ihi > H - 1) ihi = H - 1;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = ilo; i <= ihi; ++i) {
+        const float iy = src_coord(i, H, ty[k], h);
+        const float fy0 = floorf(iy);
+        const int y0 = (int)fy0;
+        const float fy = iy - fy0;
+        const float wy = (y0 == ys ? 1.f - fy : 0.f) + (y0 + 1 == ys ? fy : 0.f);
+        if (wy == 0.f) continue;
+        float row[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int j = jlo; j <= jhi; ++j) {
+          const float ix = src_coord(j, H, tx[k], h);
+          const float fx0 = floorf(ix);
+          const int x0 = (int)fx0;
+          const float fx = ix - fx0;
+          const float wx = (x0 == xs ? 1.f - fx : 0.f) + (x0 + 1 == xs ? fx : 0.f);
+          if (wx == 0.f) continue;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) row[c] = fmaf(wx, G[(k * 4 + c) * HW + i * H + j], row[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = fmaf(wy, row[c], acc[c]);
+      }
+      s_tm[s] += acc[0];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) s_ct[(k * 3 + c) * hh + q] += acc[1 + c];
+    }
+    __syncthreads();
+  }
+}
+
+template <int K>
+static int dec_launch_fwd(PosView pv, Src S, FViewW out, FView tgt, float* sse, int F, int h, int H, hipStream_t st) {
+  const int lds = (K * h * h * 4) * 4;
+  int g = F < 2048 ? F : 2048;
+  hipLaunchKernelGGL((dec_fwd_k<K>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F, h, H);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Decoder grid size used by paig_decoder_bwd (the slab has that many rows).
+int paig_decoder_bwd_blocks(int F) {
+  int g = (F + 3) / 4;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  return g;
+}
+
+size_t paig_decoder_slab_len(int K, int h, int H) { return (size_t)K * h * h * 4 + 3 * (size_t)H * H; }
+
+// Global scratch (floats) needed when the per-frame pixel-gradient image does
+// not fit LDS; 0 when it does.
+size_t paig_decoder_bwd_scratch(int F, int K, int h, int H) {
+  size_t lds = ((size_t)K * h * h * 4 + (size_t)K * 4 * H * H) * 4;
+  if (lds <= 120 * 1024) return 0;
+  return (size_t)paig_decoder_bwd_blocks(F) * K * 4 * H * H;
+}
+
+int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                     const float* cont, const float* bg, float* out, long long out_fs, const float* tgt,
+                     long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F, int K, int h, int H,
+                     void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(H == 2 * h, "decoder: H=%d must be 2*tmpl=%d", H, 2 * h);
+  PosView pv{pos, pos_outer, pos_inner, pos_grp};
+  Src S{tmpl, cont, bg};
+  FViewW o{out, out_fs};
+  FView t{tgt, tgt_fs, tgt_gs, tgt_grp};
+  hipStream_t st = (hipStream_t)stream;
+  if (K == 2) return dec_launch_fwd<2>(pv, S, o, t, sse, F, h, H, st);
+  if (K == 3) return dec_launch_fwd<3>(pv, S, o, t, sse, F, h, H, st);
+  paig_set_error("decoder: unsupported n_objs %d", K);
+  return PAIG_E_UNSUPPORTED;
+}
+
+int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                     const float* cont, const float* bg, const float* tgt, long long tgt_fs, int tgt_grp,
+                     long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
+                     float* slab, float* scratch, int F, int K, int h, int H, void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(H == 2 * h, "decoder: H=%d must be 2*tmpl=%d", H, 2 * h);
+  PosView pv{pos, pos_outer, pos_inner, pos_grp};
+  Src S{tmpl, cont, bg};
+  FView t{tgt, tgt_fs, tgt_gs, tgt_grp};
+  FView d{dout, dout_fs, 0, 0};
+  hipStream_t st = (hipStream_t)stream;
+  const int g = paig_decoder_bwd_blocks(F);
+  const bool need_scratch = paig_decoder_bwd_scratch(F, K, h, H) > 0;
+  PAIG_REQUIRE(!need_scratch || scratch, "decoder_bwd: scratch required");
+  const int lds = (K * h * h * 4 + (need_scratch ? 0 : K * 4 * H * H)) * 4;
+  float* gs = need_scratch ? scratch : nullptr;
+  if (K == 2)
+    hipLaunchKernelGGL((dec_bwd_k<2>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);
+  else if (K == 3)
+    hipLaunchKernelGGL((dec_bwd_k<3>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);
+  else {
+    paig_set_error("decoder: unsupported n_objs %d", K);
+    return PAIG_E_UNSUPPORTED;
+  }
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,336 @@
+// Small kernels of the step:
+//   * VariableFromNetwork forward/backward (nn/network/blocks.py:311-322): the
+//     decoder's template/content/background MLPs on a constant ones[1,10] input,
+//     computed ONCE per step (the reference recomputes them on every one of the
+//     R+1 decoder calls -- quirk Q12; the gradient is identical);
+//   * loss reduction from per-frame SSE (nn/network/physics_models.py:119-142)
+//     and its backward (per-frame loss weights, no dense dL/dframe);
+//   * optimizers on the flat parameter buffer (nn/network/base.py:12-17:
+//     RMSprop default, Adam, SGD, SGD+momentum; torch default hyper-params).
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+
+static thread_local char g_err[512];
+
+void paig_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+namespace {
+
+constexpr int VH = 200;  // VariableFromNetwork hidden width (blocks.py:314)
+constexpr int VIN = 10;  // ones[1, 10]
+
+// h = tanh(W1 @ ones + b1) in LDS; one wave per output row afterwards.
+__global__ void __launch_bounds__(256)
+vfn_fwd_k(const float* __restrict__ W1, const float* __restrict__ b1, const float* __restrict__ W2,
+          const float* __restrict__ b2, float* __restrict__ hout, float* __restrict__ y, float* __restrict__ ypost,
+          int P) {
+  __shared__ float h[VH];
+  for (int j = threadIdx.x; j < VH; j += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < VIN; ++i) s += W1[j * VIN + i];  // x = ones
+    const float v = tanhf(s + b1[j]);
+    h[j] = v;
+    if (blockIdx.x == 0) hout[j] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  for (int p = wg; p < P; p += nw) {
+    float s = 0.f;
+    for (int j = lane; j < VH; j += 64) s = fmaf(W2[(long long)p * VH + j], h[j], s);
+    s = wave_sum(s);
+    if (lane == 0) {
+      const float v = s + b2[p];
+      y[p] = v;
+      if (ypost) ypost[p] = 1.f / (1.f + expf(-v));
+    }
+  }
+}
+
+// dy = d (raw) or d * s (1 - s), s = sigmoid(y) ; dW2 = dy h^T ; db2 = dy ;
+// part[blk][j] = sum_{p in blk} W2[p][j] dy[p]
+__global__ void __launch_bounds__(256)
+vfn_bwd1_k(const float* __restrict__ d, const float* __restrict__ y, int sig, const float* __restrict__ h,
+           const float* __restrict__ W2, float* __restrict__ dW2, float* __restrict__ db2, float* __restrict__ part,
+           int P, int rows) {
+  const int j = threadIdx.x;
+  const int p0 = blockIdx.x * rows;
+  int p1 = p0 + rows;
+  if (p1 > P) p1 = P;
+  const float hj = j < VH ? h[j] : 0.f;
+  float acc = 0.f;
+  for (int p = p0; p < p1; ++p) {
+    float g = d[p];
+    if (sig) {
+      const float s = 1.f / (1.f + expf(-y[p]));
+      g = g * (s * (1.f - s));
+    }
+    if (j < VH) {
+      dW2[(long long)p * VH + j] = g * hj;
+      acc = fmaf(W2[(long long)p * VH + j], g, acc);
+    }
+    if (j == 0) db2[p] = g;
+  }
+  if (j < VH) part[blockIdx.x * VH + j] = acc;
+}
+
+__global__ void vfn_bwd2_k(const float* __restrict__ part, int nblk, const float* __restrict__ h,
+                           float* __restrict__ dW1, float* __restrict__ db1) {
+  const int j = threadIdx.x;
+  if (j >= VH) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[b * VH + j];
+  const float hj = h[j];
+  const float g = s * (1.f - hj * hj);
+  for (int i = 0; i < VIN; ++i) dW1[j * VIN + i] = g;
+  db1[j] = g;
+}
+
+// losses: pred, extrap, recons (means of per-frame SSE)
+__global__ void loss_reduce_k(const float* __restrict__ sse_rec, const float* __restrict__ sse_roll, int B, int Te,
+                              int R, int pred, float* __restrict__ o_pred, float* __restrict__ o_ext,
+                              float* __restrict__ o_rec) {
+  __shared__ float red[3][4];
+  float a = 0.f, b = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < B * R; i += blockDim.x) {
+    const int t = i % R;
+    if (t < pred) a += sse_roll[i];
+    else b += sse_roll[i];
+  }
+  for (int i = threadIdx.x; i < B * Te; i += blockDim.x) c += sse_rec[i];
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum(c);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wv] = a;
+    red[1][wv] = b;
+    red[2][wv] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s[3];
+    for (int k = 0; k < 3; ++k) s[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    *o_pred = s[0] / (float)(B * pred);
+    *o_ext = (R - pred) > 0 ? s[1] / (float)(B * (R - pred)) : nanf("");
+    *o_rec = s[2] / (float)(B * Te);
+  }
+}
+
+// per-frame loss weights from the loss adjoints (any may be null = 0)
+__global__ void loss_bwd_k(const float* __restrict__ dpred, const float* __restrict__ dext,
+                           const float* __restrict__ drec, float* __restrict__ wrec, float* __restrict__ wroll, int B,
+                           int Te, int R, int pred) {
+  const float gp = dpred ? *dpred / (float)(B * pred) : 0.f;
+  const float ge = (dext && R > pred) ? *dext / (float)(B * (R - pred)) : 0.f;
+  const float gr = drec ? *drec / (float)(B * Te) : 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * R; i += gridDim.x * blockDim.x)
+    if (wroll) wroll[i] = (i % R) < pred ? gp : ge;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * Te; i += gridDim.x * blockDim.x)
+    if (wrec) wrec[i] = gr;
+}
+
+// per-frame SSE of dense frames vs targets (the unfused path, used when the
+// loss is taken on frames that did not come from the current forward)
+__global__ void __launch_bounds__(256) frame_sse_k(FView a, FView b, float* __restrict__ sse, int F, int n) {
+  __shared__ float red[4];
+  for (int f = blockIdx.x; f < F; f += gridDim.x) {
+    const float* pa = a.frame(f);
+    const float* pb = b.frame(f);
+    float s = 0.f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const float d = pb[i] - pa[i];
+      s = fmaf(d, d, s);
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) sse[f] = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+  }
+}
+
+// dframe[f][i] = 2 * w[f] * (a - b)
+__global__ void frame_sse_bwd_k(FView a, FView b, const float* __restrict__ w, float* __restrict__ da, int F, int n) {
+  const long long tot = (long long)F * n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < tot; i += (long long)gridDim.x * blockDim.x) {
+    const int f = (int)(i / n), e = (int)(i % n);
+    da[i] = 2.f * w[f] * (a.frame(f)[e] - b.frame(f)[e]);
+  }
+}
+
+// ------------------------------------------------------------- optimizers ---
+template <typename T>
+__global__ void rmsprop_k(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ sa, long long n, T lr, T alpha,
+                          T eps) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const T gi = g[i];
+    T s = sa[i] * alpha;
+    s = s + (T(1) - alpha) * gi * gi;
+    sa[i] = s;
+    p[i] = p[i] - lr * gi / (sqrt(s) + eps);
+  }
+}
+
+template <typename T>
+__global__ void adam_k(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ m, T* __restrict__ v, long long n,
+                       T lr, T b1, T b2, T eps, T bc1, T bc2sqrt) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const T gi = g[i];
+    const T mi = m[i] * b1 + (T(1) - b1) * gi;
+    const T vi = v[i] * b2 + (T(1) - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const T denom = sqrt(vi) / bc2sqrt + eps;
+    p[i] = p[i] - (lr / bc1) * mi / denom;
+  }
+}
+
+template <typename T>
+__global__ void sgd_k(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ buf, long long n, T lr, T mom,
+                      int first) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    T d = g[i];
+    if (buf) {
+      const T b = first ? d : buf[i] * mom + d;
+      buf[i] = b;
+      d = b;
+    }
+    p[i] = p[i] - lr * d;
+  }
+}
+
+static inline int grid_for(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* paig_last_error(void) { return g_err; }
+
+int paig_abi_version(void) { return 1; }
+
+// y[P] = W2 tanh(W1 1 + b1) + b2 ; hout[200] ; ypost = sigmoid(y) if non-null
+int paig_vfn_fwd(const float* W1, const float* b1, const float* W2, const float* b2, float* hout, float* y,
+                 float* ypost, int P, void* stream) {
+  int g = (P + 3) / 4;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(vfn_fwd_k, dim3(g), dim3(256), 0, (hipStream_t)stream, W1, b1, W2, b2, hout, y, ypost, P);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_vfn_bwd_blocks(int P) { return cdiv(P, 16); }
+
+// d: adjoint of y (sig = 0) or of sigmoid(y) (sig = 1). part: >= blocks*200 floats.
+int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,
+                 float* dW2, float* db2, float* part, int P, void* stream) {
+  const int rows = 16;
+  const int nblk = cdiv(P, rows);
+  hipLaunchKernelGGL(vfn_bwd1_k, dim3(nblk), dim3(256), 0, (hipStream_t)stream, d, y, sig, h, W2, dW2, db2, part, P,
+                     rows);
+  PAIG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(vfn_bwd2_k, dim3(1), dim3(256), 0, (hipStream_t)stream, part, nblk, h, dW1, db1);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_loss_reduce(const float* sse_rec, const float* sse_roll, int B, int Te, int R, int pred, float* pred_out,
+                     float* extrap_out, float* recons_out, void* stream) {
+  hipLaunchKernelGGL(loss_reduce_k, dim3(1), dim3(256), 0, (hipStream_t)stream, sse_rec, sse_roll, B, Te, R, pred,
+                     pred_out, extrap_out, recons_out);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_loss_bwd(const float* dpred, const float* dext, const float* drec, float* wrec, float* wroll, int B, int Te,
+                  int R, int pred, void* stream) {
+  hipLaunchKernelGGL(loss_bwd_k, dim3(grid_for((long long)B * (R > Te ? R : Te))), dim3(256), 0, (hipStream_t)stream,
+                     dpred, dext, drec, wrec, wroll, B, Te, R, pred);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_frame_sse(const float* a, long long a_fs, int a_grp, long long a_gs, const float* b, long long b_fs, int b_grp,
+                   long long b_gs, float* sse, int F, int n, void* stream) {
+  if (F <= 0) return 0;
+  int g = F < 2048 ? F : 2048;
+  hipLaunchKernelGGL(frame_sse_k, dim3(g), dim3(256), 0, (hipStream_t)stream, FView{a, a_fs, a_gs, a_grp},
+                     FView{b, b_fs, b_gs, b_grp}, sse, F, n);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_frame_sse_bwd(const float* a, long long a_fs, int a_grp, long long a_gs, const float* b, long long b_fs,
+                       int b_grp, long long b_gs, const float* w, float* da, int F, int n, void* stream) {
+  if (F <= 0) return 0;
+  hipLaunchKernelGGL(frame_sse_bwd_k, dim3(grid_for((long long)F * n)), dim3(256), 0, (hipStream_t)stream,
+                     FView{a, a_fs, a_gs, a_grp}, FView{b, b_fs, b_gs, b_grp}, w, da, F, n);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_rmsprop_f32(float* p, const float* g, float* sa, long long n, float lr, float alpha, float eps, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rmsprop_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, sa, n, lr, alpha, eps);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_rmsprop_f64(double* p, const double* g, double* sa, long long n, double lr, double alpha, double eps,
+                     void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rmsprop_k<double>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, sa, n, lr, alpha,
+                     eps);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_adam_f32(float* p, const float* g, float* m, float* v, long long n, float lr, float b1, float b2, float eps,
+                  float bc1, float bc2sqrt, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(adam_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, b1, b2,
+                     eps, bc1, bc2sqrt);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_adam_f64(double* p, const double* g, double* m, double* v, long long n, double lr, double b1, double b2,
+                  double eps, double bc1, double bc2sqrt, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(adam_k<double>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, b1, b2,
+                     eps, bc1, bc2sqrt);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_sgd_f32(float* p, const float* g, float* buf, long long n, float lr, float mom, int first, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(sgd_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, buf, n, lr, mom, first);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_sgd_f64(double* p, const double* g, double* buf, long long n, double lr, double mom, int first, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(sgd_k<double>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, buf, n, lr, mom, first);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,454 @@
+// Memory-bound U-Net glue + encoder head kernels (fp32, NCHW per frame):
+//   maxpool 2x2 fwd/bwd            nn/network/blocks.py:250,254 (aten max_pool2d)
+//   bilinear 2x upsample fwd/bwd   nn/network/blocks.py:260,269 (torchvision Resize,
+//                                  == bilinear align_corners=False; antialias no-op)
+//   mask softmax + masked objects  nn/network/blocks.py:84-93
+//   tanh position head             nn/network/blocks.py:101-102
+//   deterministic slab / column reductions for weight and bias gradients.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- maxpool ----
+__global__ void maxpool_fwd_k(FView x, FViewW y, int F, int C, int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  const long long n = (long long)F * C * Ho * Wo;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    int j = i % Wo;
+    long long t = i / Wo;
+    int ii = t % Ho;
+    t /= Ho;
+    int c = t % C;
+    int f = (int)(t / C);
+    const float* xp = x.frame(f) + ((long long)c * H + 2 * ii) * W + 2 * j;
+    // aten scan order (kh, kw) with "val > max || isnan(val)"
+    float m = xp[0];
+    float v = xp[1];
+    if (v > m || v != v) m = v;
+    v = xp[W];
+    if (v > m || v != v) m = v;
+    v = xp[W + 1];
+    if (v > m || v != v) m = v;
+    y.frame(f)[((long long)c * Ho + ii) * Wo + j] = m;
+  }
+}
+
+// dx = (dx_existing + [argmax] * dy) * (x > 0), one thread per input pixel.
+__global__ void maxpool_bwd_relu_k(FView x, FView dy, FViewW dx, int F, int C, int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  const long long n = (long long)F * C * H * W;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    int xx = i % W;
+    long long t = i / W;
+    int yy = t % H;
+    t /= H;
+    int c = t % C;
+    int f = (int)(t / C);
+    const float* xc = x.frame(f) + (long long)c * H * W;
+    float* dxp = dx.frame(f) + (long long)c * H * W + (long long)yy * W + xx;
+    float g = *dxp;
+    const int pi = yy >> 1, pj = xx >> 1;
+    if (pi < Ho && pj < Wo) {
+      const float* xp = xc + (2 * pi) * W + 2 * pj;
+      int am = 0;
+      float m = xp[0];
+      float v = xp[1];
+      if (v > m || v != v) { m = v; am = 1; }
+      v = xp[W];
+      if (v > m || v != v) { m = v; am = 2; }
+      v = xp[W + 1];
+      if (v > m || v != v) { m = v; am = 3; }
+      const int me = ((yy & 1) << 1) | (xx & 1);
+      if (am == me) g += dy.frame(f)[((long long)c * Ho + pi) * Wo + pj];
+    }
+    *dxp = xc[(long long)yy * W + xx] > 0.f ? g : 0.f;
+  }
+}
+
+// ------------------------------------------------------- bilinear upsample ---
+// 1-D taps of aten's upsample_bilinear2d (align_corners=False, no scale given):
+//   src = max(0, (dst + 0.5) * in/out - 0.5); i0 = floor(src); i1 = min(i0+1, in-1)
+__device__ __forceinline__ void up_taps(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  const float scale = (float)in / (float)out;
+  float s = scale * ((float)dst + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+  l0 = 1.f - l1;
+}
+
+__global__ void upsample_fwd_k(FView s, FViewW u, int F, int C, int Hs, int Ws, int Ho, int Wo) {
+  const long long n = (long long)F * C * Ho * Wo;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    int x = i % Wo;
+    long long t = i / Wo;
+    int y = t % Ho;
+    t /= Ho;
+    int c = t % C;
+    int f = (int)(t / C);
+    int y0, y1, x0, x1;
+    float wy0, wy1, wx0, wx1;
+    up_taps(y, Hs, Ho, y0, y1, wy0, wy1);
+    up_taps(x, Ws, Wo, x0, x1, wx0, wx1);
+    const float* sp = s.frame(f) + (long long)c * Hs * Ws;
+    float v = wy0 * (wx0 * sp[y0 * Ws + x0] + wx1 * sp[y0 * Ws + x1]) +
+              wy1 * (wx0 * sp[y1 * Ws + x0] + wx1 * sp[y1 * Ws + x1]);
+    u.frame(f)[((long long)c * Ho + y) * Wo + x] = v;
+  }
+}
+
+// ds[sy][sx] = sum over outputs using it (gather form, deterministic), then
+// optionally * (s > 0) (ReLU'd source).
+__global__ void upsample_bwd_k(FView du, FView s, FViewW ds, int F, int C, int Hs, int Ws, int Ho, int Wo,
+                               int relu_mask) {
+  const long long n = (long long)F * C * Hs * Ws;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    int sx = i % Ws;
+    long long t = i / Ws;
+    int sy = t % Hs;
+    t /= Hs;
+    int c = t % C;
+    int f = (int)(t / C);
+    const float* dup = du.frame(f) + (long long)c * Ho * Wo;
+    const int ry = Ho / Hs, rx = Wo / Ws;
+    int ylo = sy * ry - 2 * ry, yhi = sy * ry + 2 * ry + 1;
+    int xlo = sx * rx - 2 * rx, xhi = sx * rx + 2 * rx + 1;
+    if (ylo < 0) ylo = 0;
+    if (xlo < 0) xlo = 0;
+    if (yhi > Ho - 1) yhi = Ho - 1;
+    if (xhi > Wo - 1) xhi = Wo - 1;
+    float acc = 0.f;
+    for (int y = ylo; y <= yhi; ++y) {
+      int y0, y1;
+      float wy0, wy1;
+      up_taps(y, Hs, Ho, y0, y1, wy0, wy1);
+      float wy = (y0 == sy ? wy0 : 0.f) + (y1 == sy ? wy1 : 0.f);
+      if (wy == 0.f) continue;
+      float row = 0.f;
+      for (int x = xlo; x <= xhi; ++x) {
+        int x0, x1;
+        float wx0, wx1;
+        up_taps(x, Ws, Wo, x0, x1, wx0, wx1);
+        float wx = (x0 == sx ? wx0 : 0.f) + (x1 == sx ? wx1 : 0.f);
+        if (wx != 0.f) row = fmaf(wx, dup[y * Wo + x], row);
+      }
+      acc = fmaf(wy, row, acc);
+    }
+    if (relu_mask) acc = s.frame(f)[((long long)c * Hs + sy) * Ws + sx] > 0.f ? acc : 0.f;
+    ds.frame(f)[((long long)c * Hs + sy) * Ws + sx] = acc;
+  }
+}
+
+// ------------------------------------------------------------ mask softmax ---
+// logits [F][K][HW] (ReLU'd U-Net output) ++ constant 1 (background) ->
+// masks [F][K+1][HW]; masked objects A[k*F + f][c*HW + p] = mask_k * x[f][c][p].
+__global__ void mask_softmax_fwd_k(const float* __restrict__ lg, FView x, float* __restrict__ masks,
+                                   float* __restrict__ objs, int F, int K, int C, int HW) {
+  const long long n = (long long)F * HW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int p = i % HW;
+    const int f = (int)(i / HW);
+    float l[8];
+    float m = 1.f;
+    for (int k = 0; k < K; ++k) {
+      l[k] = lg[((long long)f * K + k) * HW + p];
+      m = fmaxf(m, l[k]);
+    }
+    float e[9];
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) {
+      e[k] = expf(l[k] - m);
+      s += e[k];
+    }
+    e[K] = expf(1.f - m);
+    s += e[K];
+    const float* xp = x.frame(f);
+    for (int k = 0; k <= K; ++k) {
+      const float mk = e[k] / s;
+      masks[((long long)f * (K + 1) + k) * HW + p] = mk;
+      if (k < K)
+        for (int c = 0; c < C; ++c) objs[((long long)k * F + f) * C * HW + (long long)c * HW + p] = mk * xp[c * HW + p];
+    }
+  }
+}
+
+// dlogits[f][k][p] = relu'(lg) * m_k * (dm_k - sum_j m_j dm_j),
+// dm_k = sum_c dobjs[k*F+f][c][p] * x[f][c][p] (k < K), dm_bg = 0.
+__global__ void mask_softmax_bwd_k(const float* __restrict__ lg, FView x, const float* __restrict__ masks,
+                                   const float* __restrict__ dobjs, float* __restrict__ dlg, int F, int K, int C,
+                                   int HW) {
+  const long long n = (long long)F * HW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int p = i % HW;
+    const int f = (int)(i / HW);
+    const float* xp = x.frame(f);
+    float dm[8], mk[8];
+    float dot = 0.f;
+    for (int k = 0; k < K; ++k) {
+      float a = 0.f;
+      for (int c = 0; c < C; ++c) a = fmaf(dobjs[((long long)k * F + f) * C * HW + (long long)c * HW + p], xp[c * HW + p], a);
+      dm[k] = a;
+      mk[k] = masks[((long long)f * (K + 1) + k) * HW + p];
+      dot = fmaf(mk[k], a, dot);
+    }
+    for (int k = 0; k < K; ++k) {
+      const float g = mk[k] * (dm[k] - dot);
+      dlg[((long long)f * K + k) * HW + p] = lg[((long long)f * K + k) * HW + p] > 0.f ? g : 0.f;
+    }
+  }
+}
+
+// --------------------------------------------------------- position head ----
+// enc_pos[n][2k+j] = tanh(h3[k*N+n][j]) * (H/2) + H/2
+__global__ void pos_head_fwd_k(const float* __restrict__ h3, float* __restrict__ pos, int N, int K, float half) {
+  const int n = N * K * 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int j = i & 1;
+    const int k = (i >> 1) % K;
+    const int r = i / (2 * K);
+    pos[i] = tanhf(h3[((long long)k * N + r) * 2 + j]) * half + half;
+  }
+}
+
+__global__ void pos_head_bwd_k(const float* __restrict__ h3, const float* __restrict__ dpos, float* __restrict__ dh3,
+                               int N, int K, float half) {
+  const int n = N * K * 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int j = i & 1;
+    const int k = (i >> 1) % K;
+    const int r = i / (2 * K);
+    const long long o = ((long long)k * N + r) * 2 + j;
+    const float t = tanhf(h3[o]);
+    dh3[o] = dpos[i] * half * (1.f - t * t);
+  }
+}
+
+// ------------------------------------------------------- velocity packing ----
+// enc_pos [B][Te][D] (D = 2K). Forward (blocks.py:43-45, non-alt):
+//   X[k*B+b][t*2+j] = pos[b][t][2k+j], t < S
+// alt_vel (blocks.py:33-38): X[k*B+b][t*2+j] = pos[b][t+1][2k+j] - pos[b][t][2k+j], t < S-1
+__global__ void vel_pack_k(const float* __restrict__ pos, float* __restrict__ X, int B, int Te, int K, int S,
+                           int alt) {
+  const int cols = (alt ? S - 1 : S) * 2;
+  const int n = K * B * cols;
+  const int D = 2 * K;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int col = i % cols;
+    const int row = i / cols;
+    const int k = row / B, b = row % B;
+    const int t = col >> 1, j = col & 1;
+    const float* pb = pos + (long long)b * Te * D + 2 * k + j;
+    X[i] = alt ? pb[(t + 1) * D] - pb[t * D] : pb[t * D];
+  }
+}
+
+// dpos[b][t][2k+j] += dX (+ dpos0[b][2k+j] at t = S-1 where dpos0 != null).
+// One thread per (b, t, d) of the first S steps: no write conflicts.
+__global__ void vel_unpack_add_k(const float* __restrict__ dX, const float* __restrict__ dpos0, float* __restrict__ dpos,
+                                 int B, int Te, int K, int S, int alt) {
+  const int D = 2 * K;
+  const int cols = (alt ? S - 1 : S) * 2;
+  const int n = B * S * D;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int d = i % D;
+    const int t = (i / D) % S;
+    const int b = i / (D * S);
+    const int k = d >> 1, j = d & 1;
+    const float* xr = dX ? dX + (long long)(k * B + b) * cols : nullptr;
+    float g = 0.f;
+    if (xr) {
+      if (alt) {
+        if (t >= 1) g += xr[(t - 1) * 2 + j];
+        if (t <= S - 2) g -= xr[t * 2 + j];
+      } else {
+        g += xr[t * 2 + j];
+      }
+    }
+    if (dpos0 && t == S - 1) g += dpos0[(long long)b * D + d];
+    dpos[((long long)b * Te + t) * D + d] += g;
+  }
+}
+
+// ------------------------------------------------------------- reductions ---
+// out[i] (+)= sum_b slab[b][i]; 64 columns per block, 4 waves split the rows.
+__global__ void __launch_bounds__(256) slab_reduce_k(const float* __restrict__ slab, int nblk, long long ld, int len,
+                                                     float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (i < len)
+    for (int b = wv; b < nblk; b += 4) s += slab[(long long)b * ld + i];
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && i < len) {
+    float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    out[i] = accumulate ? out[i] + v : v;
+  }
+}
+
+// part[s][n] = sum over rows r in stripe s of X[r][n]
+__global__ void __launch_bounds__(256) colsum_part_k(const float* __restrict__ X, int M, int N, long long ld,
+                                                     float* __restrict__ part, int rows_per) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * rows_per;
+  int r1 = r0 + rows_per;
+  if (r1 > M) r1 = M;
+  float s = 0.f;
+  if (n < N)
+    for (int r = r0 + wv; r < r1; r += 4) s += X[(long long)r * ld + n];
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && n < N) part[(long long)blockIdx.y * N + n] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ void axpby_k(const float* __restrict__ x, float* __restrict__ y, long long n, float a, float b) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = a * x[i] + (b == 0.f ? 0.f : b * y[i]);
+}
+
+static inline int grid_for(long long n, int bs = 256) {
+  long long g = (n + bs - 1) / bs;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,
+                      void* stream) {
+  if (F <= 0) return 0;
+  long long n = (long long)F * C * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(maxpool_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
+                     FViewW{y, y_fs}, F, C, H, W);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_maxpool2_bwd_relu(const float* x, long long x_fs, const float* dy, long long dy_fs, float* dx, long long dx_fs,
+                           int F, int C, int H, int W, void* stream) {
+  if (F <= 0) return 0;
+  long long n = (long long)F * C * H * W;
+  hipLaunchKernelGGL(maxpool_bwd_relu_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
+                     FView{dy, dy_fs, 0, 0}, FViewW{dx, dx_fs}, F, C, H, W);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_upsample2_fwd(const float* s, long long s_fs, float* u, long long u_fs, int F, int C, int Hs, int Ws, int Ho,
+                       int Wo, void* stream) {
+  if (F <= 0) return 0;
+  long long n = (long long)F * C * Ho * Wo;
+  hipLaunchKernelGGL(upsample_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{s, s_fs, 0, 0},
+                     FViewW{u, u_fs}, F, C, Hs, Ws, Ho, Wo);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_upsample2_bwd(const float* du, long long du_fs, const float* s, long long s_fs, float* ds, long long ds_fs,
+                       int F, int C, int Hs, int Ws, int Ho, int Wo, int relu_mask, void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(Ho >= Hs && Wo >= Ws && Ho % Hs == 0 && Wo % Ws == 0, "upsample_bwd: integer upscale only");
+  long long n = (long long)F * C * Hs * Ws;
+  hipLaunchKernelGGL(upsample_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{du, du_fs, 0, 0},
+                     FView{s, s_fs, 0, 0}, FViewW{ds, ds_fs}, F, C, Hs, Ws, Ho, Wo, relu_mask);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_mask_softmax_fwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs,
+                          float* masks, float* objs, int F, int K, int C, int HW, void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(K >= 1 && K <= 7, "mask_softmax: K=%d", K);
+  hipLaunchKernelGGL(mask_softmax_fwd_k, dim3(grid_for((long long)F * HW)), dim3(256), 0, (hipStream_t)stream, logits,
+                     FView{x, x_fs, x_gs, x_grp}, masks, objs, F, K, C, HW);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_mask_softmax_bwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs,
+                          const float* masks, const float* dobjs, float* dlogits, int F, int K, int C, int HW,
+                          void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(K >= 1 && K <= 7, "mask_softmax: K=%d", K);
+  hipLaunchKernelGGL(mask_softmax_bwd_k, dim3(grid_for((long long)F * HW)), dim3(256), 0, (hipStream_t)stream, logits,
+                     FView{x, x_fs, x_gs, x_grp}, masks, dobjs, dlogits, F, K, C, HW);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_pos_head_fwd(const float* h3, float* pos, int N, int K, float half, void* stream) {
+  hipLaunchKernelGGL(pos_head_fwd_k, dim3(grid_for(N * K * 2)), dim3(256), 0, (hipStream_t)stream, h3, pos, N, K, half);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_pos_head_bwd(const float* h3, const float* dpos, float* dh3, int N, int K, float half, void* stream) {
+  hipLaunchKernelGGL(pos_head_bwd_k, dim3(grid_for(N * K * 2)), dim3(256), 0, (hipStream_t)stream, h3, dpos, dh3, N, K,
+                     half);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_vel_pack(const float* pos, float* X, int B, int Te, int K, int S, int alt, void* stream) {
+  hipLaunchKernelGGL(vel_pack_k, dim3(grid_for(K * B * S * 2)), dim3(256), 0, (hipStream_t)stream, pos, X, B, Te, K, S,
+                     alt);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_vel_unpack_add(const float* dX, const float* dpos0, float* dpos, int B, int Te, int K, int S, int alt,
+                        void* stream) {
+  hipLaunchKernelGGL(vel_unpack_add_k, dim3(grid_for(B * S * 2 * K)), dim3(256), 0, (hipStream_t)stream, dX, dpos0,
+                     dpos, B, Te, K, S, alt);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_slab_reduce(const float* slab, int nblk, long long ld, int len, float* out, int accumulate, void* stream) {
+  if (len <= 0) return 0;
+  hipLaunchKernelGGL(slab_reduce_k, dim3(cdiv(len, 64)), dim3(256), 0, (hipStream_t)stream, slab, nblk, ld, len, out,
+                     accumulate);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+// out[n] (+)= sum_r X[r][n]; workspace >= stripes*N floats (stripes = ceil(M/rows_per)).
+size_t paig_colsum_workspace(int M, int N) {
+  int rows_per = 256;
+  int stripes = cdiv(M, rows_per);
+  return (size_t)stripes * N;
+}
+
+int paig_colsum(const float* X, int M, int N, long long ld, float* out, int accumulate, float* ws, void* stream) {
+  if (N <= 0) return 0;
+  int rows_per = 256;
+  int stripes = cdiv(M, rows_per);
+  if (M <= 0) {
+    stripes = 0;
+  } else {
+    hipLaunchKernelGGL(colsum_part_k, dim3(cdiv(N, 64), stripes), dim3(256), 0, (hipStream_t)stream, X, M, N, ld, ws,
+                       rows_per);
+    PAIG_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(slab_reduce_k, dim3(cdiv(N, 64)), dim3(256), 0, (hipStream_t)stream, ws, stripes, (long long)N, N,
+                     out, accumulate);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_axpby(const float* x, float* y, long long n, float a, float b, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(axpby_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, a, b);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,581 @@
+"""Native PhysicsNet step: forward and backward of the reference's training
+path, every FLOP in libpaig_hip.so (include/paig_hip.h), orchestrated here.
+
+Reference path: PhysicsNet.conv_feedforward
+(nn/network/physics_models.py:204-245) -> compute_loss (:119-142) ->
+loss.backward() -> optimizer.step() (nn/network/base.py:141-152).
+
+What is different from the reference, by design (results are the same):
+  * the decoder runs ONCE over all B*(Te+R) frames instead of R+1 calls;
+    the per-frame SSE of the loss is fused into it;
+  * VariableFromNetwork outputs are computed once per step (Q12);
+  * the backward is explicit (no autograd graph of ~2k aten nodes): the
+    whole step is one autograd.Function whose backward calls the kernels in
+    reverse order, writing parameter gradients straight into one flat
+    gradient buffer (ready for a single RCCL all-reduce and a fused
+    optimizer kernel);
+  * the 5-substep physics rollout is one kernel for all R steps.
+Nothing here falls back to PyTorch math: torch is used only for device
+memory (caching allocator), streams and the autograd hook.
+"""
+import ctypes
+
+import torch
+
+from ._lib import lib, ptr, stream_handle, require_device
+
+# --------------------------------------------------------------------------
+# U-Net plans (buffers + ops), forward order.  A buffer is (channels, level),
+# level = spatial divisor.  An op's src/dst are (buffer, channel offset, count).
+# --------------------------------------------------------------------------
+
+
+def _conv(name, src, dst, relu, ks=3):
+    return {"op": "conv", "name": name, "src": src, "dst": dst, "relu": relu, "ks": ks}
+
+
+def _pool(src, dst):
+    return {"op": "pool", "src": src, "dst": dst}
+
+
+def _up(src, dst):
+    return {"op": "up", "src": src, "dst": dst}
+
+
+def shallow_unet_plan(c, K):
+    """ShallowUNet, nn/network/blocks.py:240-308 (hidden c=8; c13 ReLU'd, Q13)."""
+    bufs = {"X0": (3, 1), "A1": (c, 1), "CAT2": (3 * c, 1), "P1": (c, 2), "A3": (2 * c, 2), "CAT1": (4 * c, 2),
+            "P2": (2 * c, 4), "A5": (4 * c, 4), "A6": (4 * c, 4), "U1": (4 * c, 2), "A8": (2 * c, 2),
+            "A9": (2 * c, 2), "U2": (2 * c, 1), "A11": (c, 1), "A12": (c, 1), "LG": (K, 1)}
+    ops = [
+        _conv("c1", ("X0", 0, 3), ("A1", 0, c), True),
+        _conv("c2", ("A1", 0, c), ("CAT2", 2 * c, c), True),
+        _pool(("CAT2", 2 * c, c), ("P1", 0, c)),
+        _conv("c3", ("P1", 0, c), ("A3", 0, 2 * c), True),
+        _conv("c4", ("A3", 0, 2 * c), ("CAT1", 2 * c, 2 * c), True),
+        _pool(("CAT1", 2 * c, 2 * c), ("P2", 0, 2 * c)),
+        _conv("c5", ("P2", 0, 2 * c), ("A5", 0, 4 * c), True),
+        _conv("c6", ("A5", 0, 4 * c), ("A6", 0, 4 * c), True),
+        _up(("A6", 0, 4 * c), ("U1", 0, 4 * c)),
+        _conv("c7", ("U1", 0, 4 * c), ("CAT1", 0, 2 * c), False),
+        _conv("c8", ("CAT1", 0, 4 * c), ("A8", 0, 2 * c), True),
+        _conv("c9", ("A8", 0, 2 * c), ("A9", 0, 2 * c), True),
+        _up(("A9", 0, 2 * c), ("U2", 0, 2 * c)),
+        _conv("c10", ("U2", 0, 2 * c), ("CAT2", 0, 2 * c), False),
+        _conv("c11", ("CAT2", 0, 3 * c), ("A11", 0, c), True),
+        _conv("c12", ("A11", 0, c), ("A12", 0, c), True),
+        _conv("c13", ("A12", 0, c), ("LG", 0, K), True, ks=1),
+    ]
+    return bufs, ops
+
+
+def unet_plan(h, K):
+    """UNet, nn/network/blocks.py:106-237 (hidden h=16; c9/c12/c15/c18 un-ReLU'd)."""
+    bufs = {"X0": (3, 1), "A1": (h, 1), "CAT3": (3 * h, 1), "P1": (h, 2), "A3": (2 * h, 2), "CAT2": (4 * h, 2),
+            "P2": (2 * h, 4), "A5": (4 * h, 4), "CAT1": (6 * h, 4), "P3": (4 * h, 8), "A7": (8 * h, 8),
+            "A8": (8 * h, 8), "U1": (8 * h, 4), "A10": (4 * h, 4), "A11": (4 * h, 4), "U2": (4 * h, 2),
+            "A13": (2 * h, 2), "A14": (2 * h, 2), "U3": (2 * h, 1), "A16": (h, 1), "A17": (h, 1), "LG": (K, 1)}
+    ops = [
+        _conv("c1", ("X0", 0, 3), ("A1", 0, h), True),
+        _conv("c2", ("A1", 0, h), ("CAT3", 2 * h, h), True),
+        _pool(("CAT3", 2 * h, h), ("P1", 0, h)),
+        _conv("c3", ("P1", 0, h), ("A3", 0, 2 * h), True),
+        _conv("c4", ("A3", 0, 2 * h), ("CAT2", 2 * h, 2 * h), True),
+        _pool(("CAT2", 2 * h, 2 * h), ("P2", 0, 2 * h)),
+        _conv("c5", ("P2", 0, 2 * h), ("A5", 0, 4 * h), True),
+        _conv("c6", ("A5", 0, 4 * h), ("CAT1", 2 * h, 4 * h), True),
+        _pool(("CAT1", 2 * h, 4 * h), ("P3", 0, 4 * h)),
+        _conv("c7", ("P3", 0, 4 * h), ("A7", 0, 8 * h), True),
+        _conv("c8", ("A7", 0, 8 * h), ("A8", 0, 8 * h), True),
+        _up(("A8", 0, 8 * h), ("U1", 0, 8 * h)),
+        _conv("c9", ("U1", 0, 8 * h), ("CAT1", 0, 2 * h), False),
+        _conv("c10", ("CAT1", 0, 6 * h), ("A10", 0, 4 * h), True),
+        _conv("c11", ("A10", 0, 4 * h), ("A11", 0, 4 * h), True),
+        _up(("A11", 0, 4 * h), ("U2", 0, 4 * h)),
+        _conv("c12", ("U2", 0, 4 * h), ("CAT2", 0, 2 * h), False),
+        _conv("c13", ("CAT2", 0, 4 * h), ("A13", 0, 2 * h), True),
+        _conv("c14", ("A13", 0, 2 * h), ("A14", 0, 2 * h), True),
+        _up(("A14", 0, 2 * h), ("U3", 0, 2 * h)),
+        _conv("c15", ("U3", 0, 2 * h), ("CAT3", 0, 2 * h), False),
+        _conv("c16", ("CAT3", 0, 3 * h), ("A16", 0, h), True),
+        _conv("c17", ("A16", 0, h), ("A17", 0, h), True),
+        _conv("c18", ("A17", 0, h), ("LG", 0, K), False, ks=1),
+    ]
+    return bufs, ops
+
+
+def _overlap(a, b):
+    return a[0] == b[0] and a[1] < b[1] + b[2] and b[1] < a[1] + a[2]
+
+
+def backward_plan(ops):
+    """For every op, the producer regions of its source that it FINALIZES
+    (it is their earliest consumer in forward order = last in reverse), so a
+    ReLU derivative is applied exactly once, after all contributions."""
+    producers = [(i, op["dst"], op.get("relu", False)) for i, op in enumerate(ops)]
+    fin = {i: [] for i in range(len(ops))}
+    for pi, region, relu in producers:
+        consumers = [i for i, op in enumerate(ops) if i > pi and _overlap(op["src"], region)]
+        if consumers:
+            fin[min(consumers)].append((region, relu))
+    return fin
+
+
+class Layout:
+    """Static shapes of one step (from the PhysicsNet config and batch)."""
+
+    def __init__(self, model, B, T):
+        self.B, self.T = B, T
+        self.K = model.n_objs
+        self.D = model.coord_units // 2
+        self.H = model.conv_input_shape[1]
+        self.h = self.H // 2
+        self.ins, self.pred = model.input_steps, model.pred_steps
+        self.Te = self.ins + self.pred
+        self.R = model.pred_steps + model.extrap_steps
+        assert T == model.seq_len, f"input has {T} frames, model expects seq_len={model.seq_len}"
+        self.F = B * self.Te
+        self.alt_vel = model.alt_vel
+        self.cell = {"spring_ode_cell": 0, "bouncing_ode_cell": 1, "gravity_ode_cell": 2}[model.cell_type]
+        self.unet = self.H >= 40
+        if self.unet:
+            raise NotImplementedError("UNet (H >= 40, mnist_spring_color) encoder is not in this build yet")
+        self.bufs, self.ops = shallow_unet_plan(8, self.K)
+        self.prefix = "encoder.shallow_unet."
+        self.fin = backward_plan(self.ops)
+        self.HW = self.H * self.H
+        self.frame = 3 * self.HW
+
+
+class KernelProbe:
+    """Times every launch of ONE tagged kernel with HIP events recorded on the
+    stream it is launched on (bench.py's roofline numbers)."""
+
+    def __init__(self, tag):
+        self.tag = tag
+        self.events = []
+        self.flops = 0
+
+    def wrap(self, tag, flops):
+        probe = self
+
+        class _Ctx:
+            def __enter__(self):
+                if tag == probe.tag:
+                    self.e0 = torch.cuda.Event(enable_timing=True)
+                    self.e1 = torch.cuda.Event(enable_timing=True)
+                    self.e0.record()
+                return self
+
+            def __exit__(self, *exc):
+                if tag == probe.tag:
+                    self.e1.record()
+                    probe.events.append((self.e0, self.e1))
+                    probe.flops = flops
+                return False
+
+        return _Ctx()
+
+    def summary(self):
+        if not self.events:
+            return None
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in self.events]
+        return {"tag": self.tag, "n": len(ms), "avg_ms": sum(ms) / len(ms), "flops": self.flops}
+
+
+class _NoProbe:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NOPROBE = _NoProbe()
+
+
+def _empty(n, device, dtype=torch.float32):
+    return torch.empty(n, device=device, dtype=dtype)
+
+
+class Engine:
+    """Binds a PhysicsNet's parameters to the HIP kernels."""
+
+    def __init__(self, model):
+        self.model = model
+        self.L = lib()
+        self.probe = None
+        self.last_masked_objs = None
+
+    def _p(self, tag, flops=0):
+        return self.probe.wrap(tag, flops) if self.probe is not None else _NOPROBE
+
+    # -- parameter access ------------------------------------------------
+    def p(self, name):
+        return self.model._param_by_name[name]
+
+    def g(self, name):
+        return self.model._flat.grad_view(name)
+
+    # -- small helpers ---------------------------------------------------
+    def linear(self, x, rows, name, out, act, st, ws):
+        """out[rows, O] = act(x[rows, I] W^T + b) ; W = name.weight [O, I]"""
+        W, b = self.p(name + ".weight"), self.p(name + ".bias")
+        O, I = W.shape
+        self.L.paig_gemm(0, 1, rows, O, I, 1.0, ptr(x), I, ptr(W), I, 0.0, ptr(out), O, ptr(b), act, 0, None, 0,
+                         ptr(ws), ws.numel() if ws is not None else 0, st)
+
+    def linear_bwd(self, x, dy, rows, name, dx, aux, auxm, st, ws, need_dx=True):
+        """dW = dy^T x ; db = colsum(dy) ; dx = (dy W) * act'(aux)"""
+        W = self.p(name + ".weight")
+        O, I = W.shape
+        gW, gb = self.g(name + ".weight"), self.g(name + ".bias")
+        n_ws = ws.numel()
+        self.L.paig_gemm(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
+                         ptr(ws), n_ws, st)
+        self.L.paig_colsum(ptr(dy), rows, O, O, ptr(gb), 0, ptr(ws), st)
+        if need_dx:
+            self.L.paig_gemm(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm, ptr(aux),
+                             I, ptr(ws), n_ws, st)
+
+    def workspace_floats(self, lay):
+        K, F, B = lay.K, lay.F, lay.B
+        need = [self.L.paig_gemm_workspace(K * F, 200, 3 * lay.HW), self.L.paig_gemm_workspace(200, 3 * lay.HW, K * F),
+                self.L.paig_gemm_workspace(K * F, 3 * lay.HW, 200), self.L.paig_gemm_workspace(200, 200, K * F),
+                self.L.paig_colsum_workspace(K * F, 3 * lay.HW), self.L.paig_gemm_workspace(100, 100, K * B),
+                self.L.paig_gemm_workspace(K * B, 100, 100), 1 << 16]
+        return int(max(need))
+
+    # -- forward ---------------------------------------------------------
+    def forward(self, x, need_saved=True):
+        require_device(x)
+        model = self.model
+        model._flat.ensure()
+        B, T = x.shape[0], x.shape[1]
+        lay = Layout(model, B, T)
+        dev = x.device
+        st = stream_handle(dev)
+        L = self.L
+        x = x.contiguous()
+        K, F, HW, H, h, D = lay.K, lay.F, lay.HW, lay.H, lay.h, lay.D
+        ws = _empty(self.workspace_floats(lay), dev)
+        S = {"lay": lay, "x": x, "ws": ws}
+
+        # ---- VariableFromNetwork sources (once per step, Q12)
+        src = {}
+        for nm, P, post in (("var_net_template", K * h * h, False), ("var_net_content", K * 3 * h * h, False),
+                            ("var_net_background", 3 * HW, True)):
+            hv = _empty(200, dev)
+            y = _empty(P, dev)
+            yp = _empty(P, dev) if post else None
+            L.paig_vfn_fwd(ptr(self.p(nm + ".l1.weight")), ptr(self.p(nm + ".l1.bias")), ptr(self.p(nm + ".l2.weight")),
+                           ptr(self.p(nm + ".l2.bias")), ptr(hv), ptr(y), ptr(yp), P, st)
+            src[nm] = (hv, y, yp)
+        S["src"] = src
+        tmpl, cont, bgp = src["var_net_template"][1], src["var_net_content"][1], src["var_net_background"][2]
+
+        # ---- encoder U-Net over the first Te frames of every sequence
+        x_view = (ptr(x), T * lay.frame, lay.Te, lay.frame)   # frame n = b*Te + t, in place
+        acts = {}
+        for name, (C, lvl) in lay.bufs.items():
+            if name != "X0":
+                acts[name] = _empty(F * C * (H // lvl) * (H // lvl), dev)
+        S["acts"] = acts
+
+        def view(region):
+            buf, off, n = region
+            C, lvl = lay.bufs[buf]
+            hw = (H // lvl) ** 2
+            if buf == "X0":
+                return (x_view[0] + off * hw * 4, x_view[1], x_view[2], x_view[3]), lvl
+            t = acts[buf]
+            return (t.data_ptr() + off * hw * 4, C * hw, 0, 0), lvl
+
+        S["view"] = view
+        for op in lay.ops:
+            sv, slvl = view(op["src"])
+            dv, dlvl = view(op["dst"])
+            if op["op"] == "conv":
+                Hl = H // slvl
+                W_ = self.p(lay.prefix + op["name"] + ".weight")
+                b_ = self.p(lay.prefix + op["name"] + ".bias")
+                fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
+                with self._p("conv_fwd:" + op["name"], fl):
+                    L.paig_conv2d_fwd(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
+                                      op["src"][2], op["dst"][2], Hl, Hl, op["ks"], 1 if op["relu"] else 0, st)
+            elif op["op"] == "pool":
+                Hl = H // slvl
+                L.paig_maxpool2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hl, Hl, st)
+            else:
+                Hs, Ho = H // slvl, H // dlvl
+                L.paig_upsample2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hs, Hs, Ho, Ho, st)
+
+        # ---- mask softmax + masked objects + localiser MLP + position head
+        masks = _empty(F * (K + 1) * HW, dev)
+        objs = _empty(K * F * 3 * HW, dev)
+        L.paig_mask_softmax_fwd(ptr(acts["LG"]), *x_view, ptr(masks), ptr(objs), F, K, 3, HW, st)
+        h1 = _empty(K * F * 200, dev)
+        h2 = _empty(K * F * 200, dev)
+        h3 = _empty(K * F * 2, dev)
+        self.linear(objs, K * F, "encoder.l1", h1, 1, st, ws)
+        self.linear(h1, K * F, "encoder.l2", h2, 1, st, ws)
+        self.linear(h2, K * F, "encoder.l3", h3, 0, st, ws)
+        enc_pos = _empty(F * 2 * K, dev)
+        L.paig_pos_head_fwd(ptr(h3), ptr(enc_pos), F, K, float(H / 2), st)
+        S.update(masks=masks, objs=objs, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
+
+        # ---- reconstruction decode (all B*Te frames, SSE vs input fused)
+        recons = _empty(F * lay.frame, dev)
+        sse_rec = _empty(F, dev)
+        L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons), lay.frame,
+                           x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, st)
+
+        # ---- velocity encoder
+        vel0 = None
+        if lay.ins > 1:
+            S_in = lay.ins
+            cols = 2 * (S_in - 1 if lay.alt_vel else S_in)
+            Xv = _empty(K * B * cols, dev)
+            L.paig_vel_pack(ptr(enc_pos), ptr(Xv), B, lay.Te, K, S_in, int(lay.alt_vel), st)
+            vel0 = _empty(K * B * 2, dev)
+            if lay.alt_vel:
+                self.linear(Xv, K * B, "velocity_encoder.init_vel_linear", vel0, 0, st, ws)
+                S.update(Xv=Xv)
+            else:
+                v1 = _empty(K * B * 100, dev)
+                v2 = _empty(K * B * 100, dev)
+                self.linear(Xv, K * B, "velocity_encoder.init_vel_mlp.0", v1, 2, st, ws)
+                self.linear(v1, K * B, "velocity_encoder.init_vel_mlp.2", v2, 2, st, ws)
+                self.linear(v2, K * B, "velocity_encoder.init_vel_mlp.4", vel0, 0, st, ws)
+                S.update(Xv=Xv, v1=v1, v2=v2)
+        S["vel0"] = vel0
+
+        # ---- physics rollout (all R steps in one launch)
+        pvs = _empty(B * (lay.R + 1) * 2 * D, dev)
+        prm = self.cell_params(lay)
+        L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0), ptr(prm[0]),
+                           ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, st)
+        S["pvs"] = pvs
+
+        # ---- rollout decode (all B*R frames in one launch, SSE vs input[:, ins:])
+        out = _empty(B * lay.R * lay.frame, dev)
+        sse_roll = _empty(B * lay.R, dev)
+        tgt_roll = (ptr(x) + lay.ins * lay.frame * 4, T * lay.frame, lay.R, lay.frame)
+        L.paig_decoder_fwd(ptr(pvs) + 2 * D * 4, (lay.R + 1) * 2 * D, 2 * D, lay.R, ptr(tmpl), ptr(cont), ptr(bgp),
+                           ptr(out), lay.frame, *tgt_roll, ptr(sse_roll), B * lay.R, K, h, H, st)
+        S["tgt_roll"] = tgt_roll
+        S["x_view"] = x_view
+
+        res = {
+            "output_seq": out.view(B, lay.R, 3, H, H),
+            "recons_out": recons.view(B, lay.Te, 3, H, H),
+            "enc_pos": enc_pos.view(B, lay.Te, D),
+            "pos_vel_seq": pvs.view(B, lay.R + 1, 2 * D),
+            "enc_masks": masks.view(F, K + 1, H, H),
+            "masked_objs": [objs[k * F * 3 * HW:(k + 1) * F * 3 * HW].view(F, 3, H, H) for k in range(K)],
+            "sse_rec": sse_rec,
+            "sse_roll": sse_roll,
+            "template": tmpl.view(K, 1, h, h),
+            "contents": cont.view(K, 3, h, h),
+            "background_content": bgp.view(1, 3, H, H),
+        }
+        return res, (S if need_saved else None)
+
+    def cell_params(self, lay):
+        m = self.model
+        dt = m.rollout_cell.dt
+        if lay.cell == 0:
+            return dt, m.rollout_cell.k, m.rollout_cell.equil
+        if lay.cell == 2:
+            return dt, m.rollout_cell.g, m.rollout_cell.m
+        return dt, None, None
+
+    # -- backward --------------------------------------------------------
+    def backward(self, S, d_sse_rec=None, d_sse_roll=None, d_out=None, d_recons=None, d_enc_pos=None, d_pvs=None):
+        """Writes every live parameter gradient into the model's flat grad buffer."""
+        lay = S["lay"]
+        L = self.L
+        x = S["x"]
+        dev = x.device
+        st = stream_handle(dev)
+        ws = S["ws"]
+        K, F, HW, H, h, D, B, R = lay.K, lay.F, lay.HW, lay.H, lay.h, lay.D, lay.B, lay.R
+        tmpl = S["src"]["var_net_template"][1]
+        cont = S["src"]["var_net_content"][1]
+        bgp = S["src"]["var_net_background"][2]
+        x_view = S["x_view"]
+        if d_out is not None:
+            d_out = d_out.contiguous()
+        if d_recons is not None:
+            d_recons = d_recons.contiguous()
+
+        # ---- decoder backward (recon + rollout frames), partial source grads
+        slab_len = int(L.paig_decoder_slab_len(K, h, H))
+        nb_rec = L.paig_decoder_bwd_blocks(F)
+        nb_roll = L.paig_decoder_bwd_blocks(B * R)
+        slab = _empty((nb_rec + nb_roll) * slab_len, dev)
+        scr_n = max(L.paig_decoder_bwd_scratch(F, K, h, H), L.paig_decoder_bwd_scratch(B * R, K, h, H))
+        scratch = _empty(scr_n, dev) if scr_n else None
+        denc = _empty(F * D, dev)   # d enc_pos [B][Te][D]
+        L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
+                           ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, K, h, H, st)
+        dpos_roll = _empty(B * R * D, dev)
+        pvs = S["pvs"]
+        L.paig_decoder_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
+                           *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
+                           ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, K, h, H, st)
+        dsrc = _empty(slab_len, dev)
+        L.paig_slab_reduce(ptr(slab), nb_rec + nb_roll, slab_len, slab_len, ptr(dsrc), 0, st)
+        if d_enc_pos is not None:
+            L.paig_axpby(ptr(d_enc_pos.contiguous()), ptr(denc), F * D, 1.0, 1.0, st)
+
+        # ---- VariableFromNetwork backward
+        off = 0
+        for nm, P, sig, raw in (("var_net_template", K * h * h, 0, tmpl), ("var_net_content", K * 3 * h * h, 1, cont),
+                                ("var_net_background", 3 * HW, 1, S["src"]["var_net_background"][1])):
+            hv = S["src"][nm][0]
+            part = _empty(L.paig_vfn_bwd_blocks(P) * 200, dev)
+            L.paig_vfn_bwd(ptr(dsrc) + off * 4, ptr(raw), sig, ptr(hv), ptr(self.p(nm + ".l2.weight")),
+                           ptr(self.g(nm + ".l1.weight")), ptr(self.g(nm + ".l1.bias")), ptr(self.g(nm + ".l2.weight")),
+                           ptr(self.g(nm + ".l2.bias")), ptr(part), P, st)
+            off += P
+
+        # ---- rollout adjoint -> d pos0, d vel0, physics params
+        dpos0 = _empty(B * D, dev)
+        dvel0 = _empty(K * B * 2, dev) if S["vel0"] is not None else None
+        part = _empty(2 * L.paig_rollout_bwd_blocks(B), dev, torch.float64)
+        prm = self.cell_params(lay)
+        gk = gq = None
+        if lay.cell == 0:
+            gk, gq = self.g("rollout_cell.k"), self.g("rollout_cell.equil")
+        elif lay.cell == 2:
+            gk = self.g("rollout_cell.g")
+        L.paig_rollout_bwd(lay.cell, ptr(pvs), ptr(dpos_roll), ptr(d_pvs.contiguous() if d_pvs is not None else None),
+                           ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(dpos0), ptr(dvel0), ptr(part), ptr(gk), ptr(gq),
+                           0, B, D, R, st)
+
+        # ---- velocity encoder backward -> d enc_pos[:, :ins]
+        dXv = None
+        if S["vel0"] is not None:
+            cols = 2 * (lay.ins - 1 if lay.alt_vel else lay.ins)
+            dXv = _empty(K * B * cols, dev)
+            if lay.alt_vel:
+                self.linear_bwd(S["Xv"], dvel0, K * B, "velocity_encoder.init_vel_linear", dXv, None, 0, st, ws)
+            else:
+                dv2 = _empty(K * B * 100, dev)
+                dv1 = _empty(K * B * 100, dev)
+                self.linear_bwd(S["v2"], dvel0, K * B, "velocity_encoder.init_vel_mlp.4", dv2, S["v2"], 2, st, ws)
+                self.linear_bwd(S["v1"], dv2, K * B, "velocity_encoder.init_vel_mlp.2", dv1, S["v1"], 2, st, ws)
+                self.linear_bwd(S["Xv"], dv1, K * B, "velocity_encoder.init_vel_mlp.0", dXv, None, 0, st, ws)
+        L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
+
+        # ---- position head + localiser MLP backward -> d masked objects
+        dh3 = _empty(K * F * 2, dev)
+        L.paig_pos_head_bwd(ptr(S["h3"]), ptr(denc), ptr(dh3), F, K, float(H / 2), st)
+        dh2 = _empty(K * F * 200, dev)
+        dh1 = _empty(K * F * 200, dev)
+        dobjs = _empty(K * F * 3 * HW, dev)
+        self.linear_bwd(S["h2"], dh3, K * F, "encoder.l3", dh2, S["h2"], 1, st, ws)
+        self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws)
+        self.linear_bwd(S["objs"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
+
+        # ---- mask softmax backward (incl. ReLU' of the last U-Net conv: Q13)
+        acts = S["acts"]
+        dacts = {}
+        dLG = _empty(F * K * HW, dev)
+        L.paig_mask_softmax_bwd(ptr(acts["LG"]), x_view[0], x_view[1], x_view[2], x_view[3], ptr(S["masks"]),
+                                ptr(dobjs), ptr(dLG), F, K, 3, HW, st)
+        dacts["LG"] = dLG
+        self._unet_backward(S, dacts, st)
+
+    def _unet_backward(self, S, dacts, st):
+        lay = S["lay"]
+        L = self.L
+        dev = S["x"].device
+        acts = S["acts"]
+        view = S["view"]
+        F, H = lay.F, lay.H
+        written = {"LG": [(0, lay.K)]}
+
+        def dview(region):
+            buf, off, n = region
+            C, lvl = lay.bufs[buf]
+            hw = (H // lvl) ** 2
+            if buf not in dacts:
+                dacts[buf] = _empty(F * C * hw, dev)
+            t = dacts[buf]
+            return (t.data_ptr() + off * hw * 4, C * hw), lvl
+
+        def state(region):
+            buf, off, n = region
+            spans = written.get(buf, [])
+            cov = sum(max(0, min(off + n, a + c) - max(off, a)) for a, c in spans)
+            if cov == 0:
+                return "write"
+            if cov == n:
+                return "accum"
+            raise RuntimeError(f"partially written gradient region {region}")
+
+        def mark(region):
+            written.setdefault(region[0], []).append((region[1], region[2]))
+
+        slabs = []
+        for i in range(len(lay.ops) - 1, -1, -1):
+            op = lay.ops[i]
+            fin = lay.fin[i]
+            relu_fin = [r for r, relu in fin if relu]
+            src, dst = op["src"], op["dst"]
+            sv, slvl = view(src)
+            dyv, dlvl = dview(dst)
+            if op["op"] == "conv":
+                Hl = H // slvl
+                cin, cout, ks = src[2], dst[2], op["ks"]
+                # weight + bias gradient: per-block partials, then one reduction
+                nblk_max = 256
+                slab = _empty(nblk_max * (cout * cin * ks * ks + cout), dev)
+                nb = ctypes.c_int(0)
+                fl = 2 * F * cin * cout * ks * ks * Hl * Hl
+                with self._p("conv_wgrad:" + op["name"], fl):
+                    L.paig_conv2d_wgrad(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], ptr(slab), nblk_max,
+                                        ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, st)
+                gw = self.g(lay.prefix + op["name"] + ".weight")
+                gb = self.g(lay.prefix + op["name"] + ".bias")
+                n_w = cout * cin * ks * ks
+                assert gb.data_ptr() == gw.data_ptr() + n_w * 4, "flat grads: weight and bias must be adjacent"
+                L.paig_slab_reduce(ptr(slab), nb.value, n_w + cout, n_w + cout, ptr(gw), 0, st)
+                slabs.append(slab)
+                if src[0] == "X0":
+                    continue
+                dxv, _ = dview(src)
+                mode = state(src)
+                flags = 8 | (4 if mode == "accum" else 0)
+                aux = (0, 0)
+                if relu_fin:
+                    assert len(fin) == 1 and fin[0][0] == src, f"{op['name']}: mixed ReLU finalization"
+                    a = view(src)[0]
+                    aux = (a[0], a[1])
+                    flags |= 2
+                W_ = self.p(lay.prefix + op["name"] + ".weight")
+                with self._p("conv_dgrad:" + op["name"], fl):
+                    L.paig_conv2d_fwd(dyv[0], dyv[1], 0, 0, dxv[0], dxv[1], aux[0] or None, aux[1], ptr(W_), None, F,
+                                      cout, cin, Hl, Hl, ks, flags, st)
+                mark(src)
+            elif op["op"] == "pool":
+                Hl = H // slvl
+                dxv, _ = dview(src)
+                # the pool kernel accumulates into the concat partner's gradient
+                assert state(src) == "accum", "maxpool backward reached before its concat partner (plan error)"
+                relu = any(relu for r, relu in fin if r == src)
+                assert relu, "pool sources are ReLU'd activations in both U-Nets"
+                L.paig_maxpool2_bwd_relu(sv[0], sv[1], dyv[0], dyv[1], dxv[0], dxv[1], F, src[2], Hl, Hl, st)
+                mark(src)
+            else:
+                Hs, Ho = H // slvl, H // dlvl
+                dxv, _ = dview(src)
+                assert state(src) == "write"
+                relu = any(relu for r, relu in fin if r == src)
+                L.paig_upsample2_bwd(dyv[0], dyv[1], sv[0], sv[1], dxv[0], dxv[1], F, src[2], Hs, Hs, Ho, Ho,
+                                     int(relu), st)
+                mark(src)
+        S["_slabs"] = slabs

@@ -1,0 +1,204 @@
+"""Flat parameter / gradient storage and the fused optimizers.
+
+All live fp32 parameters of a PhysicsNet share ONE contiguous device buffer
+(each nn.Parameter is a view into it, so state_dict keys, shapes and
+load_state_dict are unchanged), and so do their gradients.  This makes the
+data-parallel exchange one RCCL all-reduce of one buffer and the optimizer
+one kernel launch (nn/network/base.py:12-17, :150-152 in the reference run a
+per-parameter torch optimizer).  The 0-dim float64 physics parameters
+(cells.py:28-29, 92-93; quirk Q9) get a tiny flat fp64 buffer of their own.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+from ._lib import lib, ptr, stream_handle
+
+
+class FlatParams:
+    def __init__(self, model, names):
+        self.model = model
+        self.names = list(names)
+        self.index = {}
+        self.p32 = self.p64 = self.g32 = self.g64 = None
+        self.device = None
+        self._redirect = None
+
+    def _params(self):
+        pd = dict(self.model.named_parameters())
+        return [(n, pd[n]) for n in self.names]
+
+    def ensure(self):
+        """(Re)build the flat buffers if any parameter moved (e.g. .to(device))."""
+        if self.p32 is not None:
+            ok = True
+            for n, p in self._params():
+                kind, off, num, _ = self.index[n]
+                base = self.p32 if kind == 32 else self.p64
+                if p.data_ptr() != base.data_ptr() + off * base.element_size() or p.device != base.device:
+                    ok = False
+                    break
+            if ok:
+                return False
+        self.rebuild()
+        return True
+
+    def rebuild(self):
+        params = self._params()
+        dev = params[0][1].device
+        n32 = sum(p.numel() for _, p in params if p.dtype == torch.float32)
+        n64 = sum(p.numel() for _, p in params if p.dtype == torch.float64)
+        self.p32 = torch.empty(n32, device=dev, dtype=torch.float32)
+        self.p64 = torch.empty(max(n64, 1), device=dev, dtype=torch.float64)
+        self.g32 = torch.zeros(n32, device=dev, dtype=torch.float32)
+        self.g64 = torch.zeros(max(n64, 1), device=dev, dtype=torch.float64)
+        o32 = o64 = 0
+        self.index = {}
+        with torch.no_grad():
+            for n, p in params:
+                num = p.numel()
+                if p.dtype == torch.float32:
+                    self.p32[o32:o32 + num].copy_(p.data.reshape(-1))
+                    p.data = self.p32[o32:o32 + num].view(p.shape)
+                    self.index[n] = (32, o32, num, tuple(p.shape))
+                    o32 += num
+                elif p.dtype == torch.float64:
+                    self.p64[o64:o64 + num].copy_(p.data.reshape(-1))
+                    p.data = self.p64[o64:o64 + num].view(p.shape)
+                    self.index[n] = (64, o64, num, tuple(p.shape))
+                    o64 += num
+                else:
+                    raise TypeError(f"{n}: unsupported dtype {p.dtype}")
+        self.n32, self.n64 = n32, n64
+        self.device = dev
+        return True
+
+    def grad_view(self, name):
+        kind, off, num, shape = self.index[name]
+        g = self._redirect if self._redirect is not None else (self.g32, self.g64)
+        base = g[0] if kind == 32 else g[1]
+        return base[off:off + num].view(shape)
+
+    # -- autograd integration ------------------------------------------------
+    def begin_backward(self):
+        """Returns True if gradients must accumulate (grads not zeroed since the
+        last backward, the torch semantics the reference relies on)."""
+        acc = any(p.grad is not None for _, p in self._params())
+        if acc:
+            self._redirect = (torch.empty_like(self.g32), torch.empty_like(self.g64))
+            self._redirect[1].zero_()
+        return acc
+
+    def end_backward(self, accumulated):
+        if accumulated:
+            L = lib()
+            st = stream_handle(self.g32.device)
+            L.paig_axpby(ptr(self._redirect[0]), ptr(self.g32), self.n32, 1.0, 1.0, st)
+            if self.n64:
+                self.g64.add_(self._redirect[1])  # 2 fp64 scalars
+            self._redirect = None
+        self.attach_grads()
+
+    def attach_grads(self):
+        for n, p in self._params():
+            p.grad = self.grad_view(n)
+
+    def allreduce_grads(self, group=None):
+        """Mean of the gradients over the data-parallel group (RCCL over xGMI)."""
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+            return
+        ws = dist.get_world_size(group)
+        dist.all_reduce(self.g32, op=dist.ReduceOp.SUM, group=group)
+        if self.n64:
+            dist.all_reduce(self.g64, op=dist.ReduceOp.SUM, group=group)
+        L = lib()
+        st = stream_handle(self.g32.device)
+        L.paig_axpby(ptr(self.g32), ptr(self.g32), self.n32, 1.0 / ws, 0.0, st)
+        if self.n64:
+            self.g64.mul_(1.0 / ws)
+
+
+class FlatOptimizer:
+    """Drop-in for the reference's torch optimizers (OPTIMIZERS, base.py:12-17)
+    acting on the flat buffers with one fused HIP kernel per dtype.
+
+    Exposes param_groups/zero_grad/step/state_dict like torch.optim, and
+    performs the data-parallel gradient all-reduce before the update when a
+    process group is initialised (the reference is single-GPU)."""
+
+    def __init__(self, model, kind, lr, **hp):
+        self.model = model
+        self.kind = kind
+        self.param_groups = [{"params": [p for _, p in model._flat._params()], "lr": lr, **hp}]
+        self.hp = hp
+        self.state = {}
+        self.steps = 0
+        self._bufs = None
+
+    def _ensure_state(self):
+        flat = self.model._flat
+        if self._bufs is None or self._bufs[0].numel() != flat.n32 or self._bufs[0].device != flat.p32.device:
+            z32 = lambda: torch.zeros(flat.n32, device=flat.p32.device)  # noqa: E731
+            z64 = lambda: torch.zeros(max(flat.n64, 1), device=flat.p32.device, dtype=torch.float64)  # noqa: E731
+            if self.kind == "adam":
+                self._bufs = (z32(), z32(), z64(), z64())
+            else:
+                self._bufs = (z32(), z64())
+            self.steps = 0
+
+    def zero_grad(self, set_to_none=True):
+        for _, p in self.model._flat._params():
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        flat = self.model._flat
+        flat.ensure()
+        self._ensure_state()
+        flat.allreduce_grads()
+        L = lib()
+        st = stream_handle(flat.p32.device)
+        lr = float(self.param_groups[0]["lr"])
+        self.steps += 1
+        n32, n64 = flat.n32, flat.n64
+        if self.kind == "rmsprop":
+            a, eps = self.hp.get("alpha", 0.99), self.hp.get("eps", 1e-8)
+            L.paig_rmsprop_f32(ptr(flat.p32), ptr(flat.g32), ptr(self._bufs[0]), n32, lr, a, eps, st)
+            if n64:
+                L.paig_rmsprop_f64(ptr(flat.p64), ptr(flat.g64), ptr(self._bufs[1]), n64, lr, a, eps, st)
+        elif self.kind == "adam":
+            b1, b2 = self.hp.get("betas", (0.9, 0.999))
+            eps = self.hp.get("eps", 1e-8)
+            bc1 = 1 - b1 ** self.steps
+            bc2s = math.sqrt(1 - b2 ** self.steps)
+            L.paig_adam_f32(ptr(flat.p32), ptr(flat.g32), ptr(self._bufs[0]), ptr(self._bufs[1]), n32, lr, b1, b2,
+                            eps, bc1, bc2s, st)
+            if n64:
+                L.paig_adam_f64(ptr(flat.p64), ptr(flat.g64), ptr(self._bufs[2]), ptr(self._bufs[3]), n64, lr, b1,
+                                b2, eps, bc1, bc2s, st)
+        else:  # sgd / momentum
+            mom = self.hp.get("momentum", 0.0)
+            b32 = self._bufs[0] if mom else None
+            b64 = self._bufs[1] if mom else None
+            first = int(self.steps == 1)
+            L.paig_sgd_f32(ptr(flat.p32), ptr(flat.g32), ptr(b32), n32, lr, mom, first, st)
+            if n64:
+                L.paig_sgd_f64(ptr(flat.p64), ptr(flat.g64), ptr(b64), n64, lr, mom, first, st)
+        return None
+
+    def state_dict(self):
+        return {"kind": self.kind, "steps": self.steps, "param_groups": [
+            {k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
+            "bufs": [b.detach().cpu() for b in (self._bufs or ())]}
+
+    def load_state_dict(self, sd):
+        self.steps = sd["steps"]
+        for g, s in zip(self.param_groups, sd["param_groups"]):
+            g.update(s)
+        if sd.get("bufs"):
+            dev = self.model._flat.p32.device
+            self._bufs = tuple(b.to(dev) for b in sd["bufs"])

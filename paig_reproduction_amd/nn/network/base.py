@@ -1,0 +1,208 @@
+"""BaseNetTorch: the reference's trainer surface (nn/network/base.py:20-218),
+same methods, arguments and side effects, driving the HIP step.
+
+Differences (documented in DESIGN.md):
+  * OPTIMIZERS map to FlatOptimizer (one fused HIP kernel over the flat
+    parameter buffer) with the torch defaults the reference uses;
+  * ``loss_mode`` (default "fresh"): the loss is taken on the CURRENT forward
+    (the north star's combined loss).  "reference" reproduces quirk Q1: the
+    train step's loss reads the stale ``self.output`` of the last eval batch;
+  * when torch.distributed is initialised, the optimizer step first averages
+    the flat gradient over the group (RCCL), and each rank trains on its own
+    shard of every epoch (DataIterator(rank, world)).
+"""
+import logging
+import os
+import shutil
+import sys
+
+import numpy as np
+import torch
+
+from paig_reproduction_amd.flat import FlatOptimizer
+from paig_reproduction_amd.nn.utils.misc import log_metrics, zipdir
+
+logger = logging.getLogger("torch")
+root_path = os.path.join(os.path.dirname(os.path.realpath(__file__)), "..", "..")
+
+OPTIMIZERS = {
+    "adam": lambda model, lr: FlatOptimizer(model, "adam", lr),
+    "rmsprop": lambda model, lr: FlatOptimizer(model, "rmsprop", lr),
+    "momentum": lambda model, lr: FlatOptimizer(model, "sgd", lr, momentum=0.9),
+    "sgd": lambda model, lr: FlatOptimizer(model, "sgd", lr),
+}
+
+
+class BaseNetTorch(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.train_metrics = {}
+        self.eval_metrics = {}
+        self.extra_train_fns = []
+        self.extra_valid_fns = []
+        self.extra_test_fns = []
+
+    def run_extra_fns(self, type):
+        if type == "train":
+            extra_fns = self.extra_train_fns
+        elif type == "valid":
+            extra_fns = self.extra_valid_fns
+        else:
+            extra_fns = self.extra_test_fns
+        for fn, args, kwargs in extra_fns:
+            fn(*args, **kwargs)
+
+    def conv_feedforward(self, inp):
+        raise NotImplementedError
+
+    def compute_loss(self):
+        raise NotImplementedError
+
+    def get_data(self, data_iterators):
+        self.train_iterator, self.valid_iterator, self.test_iterator = data_iterators
+
+    def get_batch(self, batch_size, iterator):
+        batch_x, batch_y = iterator.next_batch(batch_size)
+        if batch_y is None:
+            feed_dict = {"input": batch_x}
+        else:
+            feed_dict = {"input": batch_x, "target": batch_y}
+        return feed_dict, (batch_x, batch_y)
+
+    def initialize_graph(self, save_dir, use_ckpt, ckpt_dir=""):
+        """nn/network/base.py:65-94, including Q14 (an existing save_dir is
+        deleted unless use_ckpt)."""
+        self.save_dir = save_dir
+        if os.path.exists(save_dir):
+            if use_ckpt:
+                restore = True
+                restore_dir = ckpt_dir if ckpt_dir else save_dir
+            else:
+                logger.info("Folder exists, deleting...")
+                shutil.rmtree(save_dir)
+                os.makedirs(save_dir)
+                restore = False
+        else:
+            os.makedirs(save_dir)
+            if use_ckpt:
+                restore = True
+                restore_dir = ckpt_dir
+            else:
+                restore = False
+        if restore:
+            print(f"Loading model from: {restore_dir + '/model.ckpt'}")
+            sd = torch.load(os.path.join(restore_dir, "model.ckpt"), map_location=self.device, weights_only=True)
+            self.load_state_dict(sd)
+
+    def get_iterator(self, type):
+        if type == "train":
+            return self.train_iterator
+        if type == "valid":
+            return self.valid_iterator
+        if type == "test":
+            return self.test_iterator
+
+    def add_train_logger(self):
+        log_path = os.path.join(self.save_dir, "log.txt")
+        fh = logging.FileHandler(log_path)
+        fh.setFormatter(logging.Formatter('%(asctime)s - %(name)s - %(message)s'))
+        logger.addHandler(fh)
+
+    def _to_device(self, batch, requires_grad):
+        t = torch.as_tensor(batch, device=self.device)
+        if t.dtype != torch.float32:
+            t = t.float()
+        # the reference creates the input with requires_grad=True (Q10); its
+        # gradient is never used, so it is not computed here.
+        return t
+
+    def train_model(self, epochs, batch_size, save_every_n_epochs, eval_every_n_epochs, print_interval, debug=False):
+        """nn/network/base.py:112-172."""
+        self.train()
+        self.batch_size = batch_size
+        self.add_train_logger()
+        zipdir(root_path, self.save_dir)
+        logger.info("\n".join(sys.argv))
+        step = 0
+        if not debug and epochs > 0:
+            valid_metrics_results = self.eval_performance(batch_size, type='valid')
+            log_metrics(logger, "valid - epoch=%s" % 0, valid_metrics_results)
+
+        for ep in range(1, epochs + 1):
+            if self.anneal_lr:
+                if ep == int(0.75 * epochs):
+                    self.lr = self.lr / 5          # Q6: never reaches the optimizer
+            while self.train_iterator.epochs_completed < ep:
+                feed_dict, _ = self.get_batch(batch_size, self.train_iterator)
+                inp = self._to_device(feed_dict["input"], True)
+                result_sequence = self.forward(inp)
+                if getattr(self, "loss_mode", "fresh") == "fresh":
+                    self.output = result_sequence
+                self.train_loss, self.eval_losses = self.compute_loss()
+                self.train_metrics["train_loss"] = self.train_loss
+                self.eval_metrics["eval_pred_loss"] = self.eval_losses[0]
+                self.eval_metrics["eval_extrap_loss"] = self.eval_losses[1]
+                self.eval_metrics["eval_recons_loss"] = self.eval_losses[2]
+                self.loss = self.train_loss
+                self.optimizer.zero_grad(set_to_none=True)
+                self.loss.backward()
+                self.optimizer.step()
+                self.run_extra_fns("train")
+                if step % print_interval == 0:
+                    log_metrics(logger, "train - iter=%s" % step, self.train_metrics)
+                step += 1
+
+            if ep % eval_every_n_epochs == 0:
+                print("eval running")
+                valid_metrics_results = self.eval_performance(batch_size, type='valid')
+                log_metrics(logger, "valid - epoch=%s" % ep, valid_metrics_results)
+
+            if ep % save_every_n_epochs == 0:
+                print("saving")
+                if self._is_rank0():
+                    torch.save(self.state_dict(), os.path.join(self.save_dir, "model.ckpt"))
+
+        test_metrics_results = self.eval_performance(batch_size, type='test')
+        log_metrics(logger, "test - epoch=%s" % epochs, test_metrics_results)
+
+    @staticmethod
+    def _is_rank0():
+        import torch.distributed as dist
+        return not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+
+    def eval_performance(self, batch_size, type='valid'):
+        """nn/network/base.py:174-218 (Q15: whole set when it has < 100 examples)."""
+        self.eval()
+        with torch.no_grad():
+            self.eval_metrics["eval_pred_loss"] = torch.tensor([0], device=self.device)
+            self.eval_metrics["eval_extrap_loss"] = torch.tensor([0], device=self.device)
+            self.eval_metrics["eval_recons_loss"] = torch.tensor([0], device=self.device)
+            eval_metrics_results = {k: [] for k in self.eval_metrics.keys()}
+            eval_outputs = {"input": [], "output": []}
+            eval_iterator = self.get_iterator(type)
+            eval_iterator.reset_epoch()
+            while eval_iterator.get_epoch() < 1:
+                if eval_iterator.X.shape[0] < 100:
+                    batch_size = eval_iterator.X.shape[0]
+                feed_dict, _ = self.get_batch(batch_size, eval_iterator)
+                inp = self._to_device(feed_dict["input"], False)
+                self.output = self.conv_feedforward(inp)
+                self.train_loss, self.eval_losses = self.compute_loss()
+                self.train_metrics["train_loss"] = self.train_loss
+                self.eval_metrics["eval_pred_loss"] = self.eval_losses[0]
+                self.eval_metrics["eval_extrap_loss"] = self.eval_losses[1]
+                self.eval_metrics["eval_recons_loss"] = self.eval_losses[2]
+                self.loss = self.train_loss
+                for k in self.eval_metrics.keys():
+                    eval_metrics_results[k].append(self.eval_metrics[k])
+                eval_outputs["input"].append(feed_dict["input"])
+                eval_outputs["output"].append(self.eval_losses)
+            eval_metrics_results = {k: np.mean([i.detach().cpu().numpy() for i in v], axis=0)
+                                    for k, v in eval_metrics_results.items()}
+            if self._is_rank0():
+                np.savez_compressed(os.path.join(self.save_dir, "outputs.npz"),
+                                    input=np.concatenate(eval_outputs["input"], axis=0),
+                                    output=np.array([[o.detach().cpu().numpy() for o in out]
+                                                     for out in eval_outputs["output"]]))
+            self.run_extra_fns(type)
+            return eval_metrics_results

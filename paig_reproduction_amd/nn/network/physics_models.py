@@ -1,0 +1,337 @@
+"""PhysicsNet — the reference's model surface (nn/network/physics_models.py:40-330)
+on the MI355X-native step.
+
+Same constructor signature/positional order, attributes, state_dict keys and
+init RNG stream as the reference, so it is a drop-in for
+runners/torch_run_physics.py.  ``forward``/``conv_feedforward`` run the whole
+step (encoder U-Net -> localiser -> velocity MLP -> physics rollout -> STN
+decoder, fused per-frame SSE) through libpaig_hip.so as ONE autograd node whose
+backward is the explicit HIP backward (paig_reproduction_amd.engine).
+"""
+import inspect
+import logging
+import os
+
+import numpy as np
+import torch
+import torch.nn as pnn
+
+from paig_reproduction_amd._lib import lib, ptr, stream_handle, require_device
+from paig_reproduction_amd.engine import Engine
+from paig_reproduction_amd.flat import FlatParams
+from paig_reproduction_amd.nn.network.base import OPTIMIZERS, BaseNetTorch
+from paig_reproduction_amd.nn.network.blocks import ConvolutionalEncoder, VelocityEncoder, VariableFromNetwork
+from paig_reproduction_amd.nn.network.cells import bouncing_ode_cell, spring_ode_cell, gravity_ode_cell
+
+logger = logging.getLogger("tf")
+
+CELLS = {
+    "bouncing_ode_cell": bouncing_ode_cell,
+    "spring_ode_cell": spring_ode_cell,
+    "gravity_ode_cell": gravity_ode_cell,
+    "lstm": pnn.LSTMCell,
+}
+
+COORD_UNITS = {
+    "bouncing_balls": 8,
+    "spring_color": 8,
+    "spring_color_half": 8,
+    "3bp_color": 12,
+    "mnist_spring_color": 8,
+}
+
+
+class _PhysicsStep(torch.autograd.Function):
+    """The whole forward as one node; backward = engine.backward."""
+
+    @staticmethod
+    def forward(ctx, anchor, x, engine):
+        need = ctx.needs_input_grad[0]
+        res, S = engine.forward(x, need_saved=need)
+        ctx.engine = engine
+        ctx.S = S
+        ctx.set_materialize_grads(False)
+        engine.last_masked_objs = res["masked_objs"]
+        outs = (res["output_seq"], res["recons_out"], res["enc_pos"], res["pos_vel_seq"], res["sse_rec"],
+                res["sse_roll"], res["enc_masks"], res["template"], res["contents"], res["background_content"])
+        ctx.mark_non_differentiable(res["enc_masks"], res["template"], res["contents"], res["background_content"])
+        return outs
+
+    @staticmethod
+    def backward(ctx, d_out, d_rec, d_enc, d_pvs, d_sse_rec, d_sse_roll, *unused):
+        if ctx.S is None:
+            raise RuntimeError("PhysicsNet step was run without saving activations")
+        flat = ctx.engine.model._flat
+        acc = flat.begin_backward()
+        ctx.engine.backward(ctx.S, d_sse_rec, d_sse_roll, d_out, d_rec, d_enc, d_pvs)
+        flat.end_backward(acc)
+        ctx.S = None
+        return None, None, None
+
+
+class _LossReduce(torch.autograd.Function):
+    """Per-frame SSE -> (pred, extrap, recons) means (physics_models.py:119-135)."""
+
+    @staticmethod
+    def forward(ctx, sse_rec, sse_roll, B, Te, R, pred):
+        dev = sse_rec.device
+        o = [torch.empty((), device=dev) for _ in range(3)]
+        lib().paig_loss_reduce(ptr(sse_rec), ptr(sse_roll), B, Te, R, pred, ptr(o[0]), ptr(o[1]), ptr(o[2]),
+                               stream_handle(dev))
+        ctx.shape = (B, Te, R, pred)
+        ctx.dev = dev
+        ctx.set_materialize_grads(False)
+        return o[0], o[1], o[2]
+
+    @staticmethod
+    def backward(ctx, dp, de, dr):
+        B, Te, R, pred = ctx.shape
+        wrec = torch.empty(B * Te, device=ctx.dev)
+        wroll = torch.empty(B * R, device=ctx.dev)
+        lib().paig_loss_bwd(ptr(dp), ptr(de), ptr(dr), ptr(wrec), ptr(wroll), B, Te, R, pred, stream_handle(ctx.dev))
+        return wrec, wroll, None, None, None, None
+
+
+class _FrameSSE(torch.autograd.Function):
+    """Per-frame SSE of dense frames vs input[:, ins:] (the unfused path, for a
+    loss on frames that are not the current forward's, e.g. quirk Q1)."""
+
+    @staticmethod
+    def forward(ctx, frames, x, ins):
+        B, R = frames.shape[0], frames.shape[1]
+        T = x.shape[1]
+        fr = 3 * frames.shape[-1] * frames.shape[-2]
+        frames = frames.contiguous()
+        x = x.contiguous()
+        sse = torch.empty(B * R, device=frames.device)
+        lib().paig_frame_sse(ptr(frames), fr, 0, 0, ptr(x) + ins * fr * 4, T * fr, R, fr, ptr(sse), B * R, fr,
+                             stream_handle(frames.device))
+        ctx.save_for_backward(frames, x)
+        ctx.meta = (ins, B, R, T, fr)
+        return sse
+
+    @staticmethod
+    def backward(ctx, w):
+        frames, x = ctx.saved_tensors
+        ins, B, R, T, fr = ctx.meta
+        d = torch.empty_like(frames)
+        lib().paig_frame_sse_bwd(ptr(frames), fr, 0, 0, ptr(x) + ins * fr * 4, T * fr, R, fr, ptr(w.contiguous()),
+                                 ptr(d), B * R, fr, stream_handle(frames.device))
+        return d, None, None
+
+
+class PhysicsNet(BaseNetTorch):
+    def __init__(self,
+                 task="",
+                 recurrent_units=128,
+                 lstm_layers=1,
+                 cell_type="",
+                 seq_len=20,
+                 input_steps=3,
+                 pred_steps=5,
+                 autoencoder_loss=0.0,
+                 alt_vel=False,
+                 color=False,
+                 input_size=36 * 36,
+                 encoder_type="",
+                 decoder_type="conv_st_decoder",
+                 device=torch.device("cpu")):
+        super().__init__()
+        self.device = device
+        assert task in COORD_UNITS
+        self.task = task
+        self.recurrent_units = recurrent_units
+        self.lstm_layers = lstm_layers
+        self.cell_type = cell_type
+        self.cell = CELLS[self.cell_type]
+        if self.cell is pnn.LSTMCell:
+            raise NotImplementedError("the 'lstm' black-box cell cannot be called by the reference's rollout "
+                                      "(physics_models.py:233 signature mismatch); not supported")
+        self.color = color
+        self.conv_ch = 3 if color else 1
+        if not color:
+            # Q11: the template is tiled to 3 channels regardless of --color, so
+            # grayscale breaks in the reference too.
+            raise ValueError("PhysicsNet requires color=True (reference quirk Q11: grayscale is broken)")
+        self.input_size = input_size
+        self.conv_input_shape = [self.conv_ch] + [int(np.sqrt(input_size))] * 2
+        self.input_shape = [self.conv_ch] + [int(np.sqrt(input_size))] * 2
+        self.decoder = {name: method for name, method in
+                        inspect.getmembers(self, predicate=inspect.ismethod) if "decoder" in name}[decoder_type]
+        self.output_shape = self.conv_input_shape
+        assert seq_len > input_steps + pred_steps
+        assert input_steps >= 1
+        assert pred_steps >= 1
+        self.seq_len = seq_len
+        self.input_steps = input_steps
+        self.pred_steps = pred_steps
+        self.extrap_steps = self.seq_len - self.input_steps - self.pred_steps
+        self.alt_vel = alt_vel
+        self.autoencoder_loss = autoencoder_loss
+        self.coord_units = COORD_UNITS[self.task]
+        self.n_objs = self.coord_units // 4
+        self.extra_valid_fns.append((self.visualize_sequence, [], {}))
+        self.extra_test_fns.append((self.visualize_sequence, [], {}))
+        tmpl_size = self.conv_input_shape[1] // 2
+        self.log_sig = 1.
+        if self.log_sig != 1.:
+            raise NotImplementedError("sigma != 1")
+        # Network subcomponents (creation order = reference order, for init parity)
+        self.var_net_content = VariableFromNetwork([self.n_objs, self.conv_ch, tmpl_size, tmpl_size])
+        self.var_net_background = VariableFromNetwork([1, *self.input_shape])
+        self.var_net_template = VariableFromNetwork([self.n_objs, 1, tmpl_size, tmpl_size])
+        self.encoder = ConvolutionalEncoder(self.conv_input_shape, 200, 2, self.n_objs, self.device)
+        self.velocity_encoder = VelocityEncoder(self.alt_vel, self.input_steps, self.n_objs, self.coord_units,
+                                                self.device)
+        self.rollout_cell = self.cell(self.coord_units // 2, self.coord_units // 2)
+        self.loss_mode = "fresh"
+        self._init_native()
+
+    # ------------------------------------------------------------ native ----
+    def _live_names(self):
+        dead = "encoder.unet." if self.conv_input_shape[1] < 40 else "encoder.shallow_unet."
+        names = []
+        for n, p in self.named_parameters():
+            if n.startswith(dead) or n.startswith("rollout_cell."):
+                continue
+            names.append(n)
+        if self.cell_type == "spring_ode_cell":
+            names += ["rollout_cell.k", "rollout_cell.equil"]
+        elif self.cell_type == "gravity_ode_cell":
+            names += ["rollout_cell.g"]
+        return names
+
+    def _init_native(self):
+        object.__setattr__(self, "_flat", FlatParams(self, self._live_names()))
+        object.__setattr__(self, "_engine", None)
+        object.__setattr__(self, "_anchor", None)
+
+    @property
+    def _param_by_name(self):
+        return dict(self.named_parameters())
+
+    def _native(self):
+        if self._engine is None:
+            object.__setattr__(self, "_engine", Engine(self))
+        self._flat.ensure()
+        if self._anchor is None:
+            object.__setattr__(self, "_anchor", torch.zeros((), requires_grad=True))
+        return self._engine
+
+    # ------------------------------------------------------------- API ----
+    def get_batch(self, batch_size, iterator):
+        batch_x, _ = iterator.next_batch(batch_size)
+        feed_dict = {"input": batch_x}
+        return feed_dict, (batch_x, None)
+
+    def compute_loss(self):
+        """nn/network/physics_models.py:119-142, including the in-place ``+=``
+        that makes pred_loss alias train_loss (Q2)."""
+        B, Te, R = self.input.shape[0], self.input_steps + self.pred_steps, self.pred_steps + self.extrap_steps
+        sse_rec = self._sse_rec
+        if self.output is self._fwd_output:
+            sse_roll = self._sse_roll
+        else:
+            sse_roll = _FrameSSE.apply(self.output, self.input, self.input_steps)
+        pred, extrap, recons = _LossReduce.apply(sse_rec, sse_roll, B, Te, R, self.pred_steps)
+        self.recons_loss = recons
+        self.pred_loss = pred
+        self.extrap_loss = extrap
+        train_loss = self.pred_loss
+        if self.autoencoder_loss > 0.0:
+            train_loss += self.autoencoder_loss * self.recons_loss
+        eval_losses = [self.pred_loss, self.extrap_loss, self.recons_loss]
+        return train_loss, eval_losses
+
+    def build_optimizer(self, base_lr, optimizer="rmsprop", anneal_lr=True):
+        self.base_lr = base_lr
+        self.anneal_lr = anneal_lr
+        self.lr = base_lr
+        self._flat.ensure()
+        self.optimizer = OPTIMIZERS[optimizer](self, self.lr)
+
+    def conv_st_decoder(self, inp):
+        """Decode positions [N, coord_units/2] -> frames [N, C, H, W]
+        (physics_models.py:151-199) with the HIP decoder (no gradient through
+        this standalone call; the training path decodes inside forward)."""
+        require_device(inp)
+        eng = self._native()
+        K, H = self.n_objs, self.conv_input_shape[1]
+        h = H // 2
+        N = inp.shape[0]
+        inp = inp.detach().float().contiguous()
+        dev = inp.device
+        L = lib()
+        st = stream_handle(dev)
+        srcs = {}
+        for nm, P, post in (("var_net_template", K * h * h, False), ("var_net_content", K * 3 * h * h, False),
+                            ("var_net_background", 3 * H * H, True)):
+            hv, y = torch.empty(200, device=dev), torch.empty(P, device=dev)
+            yp = torch.empty(P, device=dev) if post else None
+            L.paig_vfn_fwd(ptr(eng.p(nm + ".l1.weight")), ptr(eng.p(nm + ".l1.bias")), ptr(eng.p(nm + ".l2.weight")),
+                           ptr(eng.p(nm + ".l2.bias")), ptr(hv), ptr(y), ptr(yp), P, st)
+            srcs[nm] = yp if post else y
+        out = torch.empty(N, 3, H, H, device=dev)
+        L.paig_decoder_fwd(ptr(inp), 0, 2 * K, 0, ptr(srcs["var_net_template"]), ptr(srcs["var_net_content"]),
+                           ptr(srcs["var_net_background"]), ptr(out), 3 * H * H, None, 0, 0, 0, None, N, K, h, H, st)
+        self.template = srcs["var_net_template"].view(K, 1, h, h)
+        self.contents = srcs["var_net_content"].view(K, 3, h, h)
+        self.background_content = srcs["var_net_background"].view(1, 3, H, H)
+        return out
+
+    def forward(self, input):
+        return self.conv_feedforward(input)
+
+    def conv_feedforward(self, inp):
+        """nn/network/physics_models.py:204-245 as one fused native step."""
+        require_device(inp)
+        eng = self._native()
+        self.input = inp
+        x = inp.detach()
+        if x.dtype != torch.float32:
+            x = x.float()
+        outs = _PhysicsStep.apply(self._anchor, x, eng)
+        (out, recons, enc_pos, pvs, sse_rec, sse_roll, masks, tmpl, cont, bg) = outs
+        self.recons_out = recons
+        self.enc_pos = enc_pos
+        self.pos_vel_seq = pvs
+        self.enc_masks = masks
+        self.masked_objs = eng.last_masked_objs
+        self.template, self.contents, self.background_content = tmpl, cont, bg
+        self._sse_rec, self._sse_roll = sse_rec, sse_roll
+        self._fwd_output = out
+        return out
+
+    def visualize_sequence(self):
+        """physics_models.py:247-330, reduced to what this image supports:
+        example%d.jpg grids and extra_outputs.npz (the gif needs moviepy,
+        absent here).  Off the hot path."""
+        try:
+            import matplotlib
+            matplotlib.use("agg")
+            import matplotlib.pyplot as plt
+        except Exception:  # pragma: no cover
+            return
+        batch_size = min(self.batch_size, 4)
+        feed_dict, (batch_x, _) = self.get_batch(batch_size, self.test_iterator)
+        if not hasattr(self, "output") or self.output is None:
+            return
+        output_seq = self.output.detach().cpu().numpy()[:batch_size]
+        recons_seq = self.recons_out.detach().cpu().numpy()[:batch_size]
+        n = min(batch_size, output_seq.shape[0], batch_x.shape[0])
+        for i in range(n):
+            seq = np.concatenate([batch_x[i, :self.input_steps], output_seq[i]], 0)
+            rows = [seq, batch_x[i], np.concatenate([recons_seq[i], np.zeros(
+                (self.extrap_steps,) + recons_seq.shape[2:], dtype=recons_seq.dtype)], 0)]
+            grid = np.concatenate([np.concatenate(list(r.reshape(r.shape[0], *self.input_shape[1:],
+                                                                 self.conv_ch)), 1) for r in rows], 0)
+            fig, ax = plt.subplots(figsize=(grid.shape[1] // 32, grid.shape[0] // 32 + 1))
+            ax.imshow(np.clip(grid, 0, 1), interpolation="nearest")
+            ax.axis("off")
+            fig.savefig(os.path.join(self.save_dir, "example%d.jpg" % i))
+            plt.close(fig)
+        np.savez_compressed(os.path.join(self.save_dir, "extra_outputs.npz"),
+                            contents=self.contents.detach().cpu().numpy(),
+                            templates=self.template.detach().cpu().numpy(),
+                            background_content=self.background_content.detach().cpu().numpy(),
+                            enc_masks=self.enc_masks.detach().cpu().numpy())

@@ -33,8 +33,21 @@ def golden_state(shapes, seed=0):
             out[key] = np.array({"rollout_cell.dt": 0.3}.get(key, 0.3), dtype=dt)
             continue
         rng = np.random.default_rng((zlib.crc32(key.encode()) ^ (seed * 7919)) & 0xFFFFFFFF)
+        unet = key.startswith("encoder.shallow_unet.") or key.startswith("encoder.unet.")
+        if unet and key.endswith("bias"):
+            # keep the ReLU U-Net alive (with torch-default scales its ReLU'd
+            # output is identically 0 and every U-Net gradient vanishes)
+            out[key] = rng.uniform(-0.1, 0.2, size=shape).astype(dt)
+            continue
+        if key.startswith("encoder.l3.") and key.endswith("bias"):
+            out[key] = rng.uniform(-1.0, 1.0, size=shape).astype(dt)  # spread positions over the frame
+            continue
         if key.endswith("weight") and len(shape) >= 2:
             b = 1.0 / np.sqrt(fan[key[: -len("weight")]])
+            if unet:
+                b *= np.sqrt(6.0)            # He-uniform gain
+            if key.startswith("encoder.l3."):
+                b *= 4.0
         elif key.endswith("bias"):
             prefix = key[: -len("bias")]
             b = 1.0 / np.sqrt(fan.get(prefix, shape[0] if len(shape) else 1))

@@ -1,0 +1,141 @@
+"""Per-kernel GPU numerics: each HIP kernel vs a plain PyTorch fp32 CPU
+reference of the same op (the aten op the reference calls), at small sizes
+including ragged ones.  Bar: 1e-5 normwise for single ops (fp32, different
+summation order), unless stated."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def L():
+    from paig_reproduction_amd._lib import lib
+    return lib()
+
+
+def st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def p(t):
+    return None if t is None else t.data_ptr()
+
+
+CONV_CASES = [(3, 8, 32, 3, 5), (8, 8, 32, 3, 3), (8, 16, 16, 3, 7), (16, 16, 16, 3, 4), (16, 32, 8, 3, 9),
+              (32, 32, 8, 3, 3), (32, 16, 16, 3, 2), (24, 8, 32, 3, 2), (8, 2, 32, 1, 3), (16, 16, 32, 3, 2),
+              (8, 16, 18, 3, 3), (16, 32, 9, 3, 5), (3, 8, 36, 3, 2)]
+
+
+@pytest.mark.parametrize("cin,cout,hw,ks,F_", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(cin, cout, hw, ks, F_):
+    torch.manual_seed(cin * 100 + cout)
+    x = torch.randn(F_, cin, hw, hw)
+    w = torch.randn(cout, cin, ks, ks) * 0.2
+    b = torch.randn(cout)
+    dy = torch.randn(F_, cout, hw, hw)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, br, padding="same")
+    y.backward(dy)
+    ref_relu = torch.relu(y.detach())
+    xg, wg, bg, dyg = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
+    out = torch.empty(F_, cout, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(xg), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout, hw,
+                        hw, ks, 1, st())
+    torch.cuda.synchronize()
+    assert rel_err(out, ref_relu) <= 1e-5
+    # dgrad with ReLU' mask of an activation aux
+    aux = torch.relu(torch.randn(F_, cin, hw, hw))
+    dx = torch.empty(F_, cin, hw, hw, device=DEV)
+    auxg = aux.to(DEV)
+    L().paig_conv2d_fwd(p(dyg), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, p(auxg), cin * hw * hw, p(wg), None, F_,
+                        cout, cin, hw, hw, ks, 8 | 2, st())
+    torch.cuda.synchronize()
+    assert rel_err(dx, xr.grad * (aux > 0)) <= 1e-5
+    # wgrad
+    nmax = 64
+    slab = torch.empty(nmax * (cout * cin * ks * ks + cout), device=DEV)
+    nb = ctypes.c_int(0)
+    L().paig_conv2d_wgrad(p(xg), cin * hw * hw, 0, 0, p(dyg), cout * hw * hw, p(slab), nmax, ctypes.byref(nb), F_, cin,
+                          cout, hw, hw, ks, st())
+    g = torch.empty(cout * cin * ks * ks + cout, device=DEV)
+    L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
+    torch.cuda.synchronize()
+    n = cout * cin * ks * ks
+    assert rel_err(g[:n].view_as(w), wr.grad) <= 1e-5
+    assert rel_err(g[n:], br.grad) <= 1e-5
+
+
+def test_conv_grouped_input_view():
+    """The first conv reads frames (b, t < Te) of a [B, T, C, H, W] input in place."""
+    B, T, Te, H = 3, 7, 4, 32
+    x = torch.rand(B, T, 3, H, H)
+    w = torch.randn(8, 3, 3, 3) * 0.3
+    b = torch.randn(8)
+    ref = torch.relu(F.conv2d(x[:, :Te].reshape(B * Te, 3, H, H), w, b, padding="same"))
+    xg, wg, bg = x.to(DEV), w.to(DEV), b.to(DEV)   # keep every operand alive until the kernel ran
+    out = torch.empty(B * Te, 8, H, H, device=DEV)
+    L().paig_conv2d_fwd(p(xg), T * 3 * H * H, Te, 3 * H * H, p(out), 8 * H * H, None, 0, p(wg), p(bg),
+                        B * Te, 3, 8, H, H, 3, 1, st())
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) <= 1e-5
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(37, 50, 19), (130, 200, 3072), (200, 3072, 130), (6, 2, 200), (1, 513, 200)])
+def test_gemm(ta, tb, M, N, K):
+    torch.manual_seed(M + N + K)
+    A = (torch.randn(K, M) if ta else torch.randn(M, K)) / K ** 0.5   # O(1) pre-activations
+    Bm = torch.randn(N, K) if tb else torch.randn(K, N)
+    bias = torch.randn(N)
+    ref = (A.t() if ta else A) @ (Bm.t() if tb else Bm) + bias
+    ref = torch.tanh(ref)
+    Ag, Bg, biasg = A.to(DEV), Bm.to(DEV), bias.to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    ws = torch.empty(max(1, L().paig_gemm_workspace(M, N, K)), device=DEV)
+    L().paig_gemm(ta, tb, M, N, K, 1.0, p(Ag), A.shape[1], p(Bg), Bm.shape[1], 0.0, p(C), N, p(biasg), 2, 0,
+                  None, 0, p(ws), ws.numel(), st())
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) <= 2e-5
+
+
+def test_pool_upsample():
+    x = torch.relu(torch.randn(5, 6, 16, 16))
+    xg = x.to(DEV)
+    y = torch.empty(5, 6, 8, 8, device=DEV)
+    L().paig_maxpool2_fwd(p(xg), 6 * 256, p(y), 6 * 64, 5, 6, 16, 16, st())
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, 2)
+    dyy = torch.randn_like(yr)
+    yr.backward(dyy)
+    base = torch.randn(5, 6, 16, 16)
+    dx = base.to(DEV).clone()
+    dyg = dyy.to(DEV)
+    L().paig_maxpool2_bwd_relu(p(xg), 6 * 256, p(dyg), 6 * 64, p(dx), 6 * 256, 5, 6, 16, 16, st())
+    torch.cuda.synchronize()
+    assert rel_err(y, yr.detach()) == 0.0
+    assert rel_err(dx, (base + xr.grad) * (x > 0)) <= 1e-6
+    # upsample 8 -> 16
+    s = torch.relu(torch.randn(4, 5, 8, 8))
+    sr = s.clone().requires_grad_(True)
+    u = F.interpolate(sr, size=(16, 16), mode="bilinear", align_corners=False, antialias=True)
+    du = torch.randn_like(u)
+    u.backward(du)
+    ug = torch.empty(4, 5, 16, 16, device=DEV)
+    sg = s.to(DEV)
+    L().paig_upsample2_fwd(p(sg), 5 * 64, p(ug), 5 * 256, 4, 5, 8, 8, 16, 16, st())
+    ds = torch.empty(4, 5, 8, 8, device=DEV)
+    dug = du.to(DEV)
+    L().paig_upsample2_bwd(p(dug), 5 * 256, p(sg), 5 * 64, p(ds), 5 * 64, 4, 5, 8, 8, 16, 16, 1, st())
+    torch.cuda.synchronize()
+    assert rel_err(ug, u.detach()) <= 1e-6
+    assert rel_err(ds, sr.grad * (s > 0)) <= 1e-6
