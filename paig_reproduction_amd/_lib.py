@@ -38,6 +38,7 @@ SIGNATURES = {
     "paig_colsum_workspace": (SZ, [I, I]),
     "paig_colsum": (I, [P, I, I, LL, P, I, P, P]),
     "paig_slab_reduce": (I, [P, I, LL, I, P, I, P]),
+    "paig_slab_reduce_multi": (I, [I, P, P, P, P, I, P]),
     "paig_axpby": (I, [P, P, LL, F32, F32, P]),
     "paig_vfn_fwd": (I, [P, P, P, P, P, P, P, I, P]),
     "paig_vfn_bwd_blocks": (I, [I]),

@@ -69,3 +69,10 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// MFMA implicit-GEMM convolutions (conv_mfma.hip): return 1 when the shape is
+// instantiated there (launch status in *rc), 0 to fall back to the VALU path.
+int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
+                       int H, int W, int ks, int flags, hipStream_t st, int* rc);
+int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H,
+                         int W, int ks, hipStream_t st, int* rc);

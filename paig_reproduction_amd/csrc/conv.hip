@@ -356,6 +356,8 @@ int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_g
   const bool dgrad = (flags & 8) != 0;
   const int fl = flags & 7;
   if (F <= 0) return 0;
+  int rc = 0;
+  if (!(flags & 16) && paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc)) return rc;
 #define PAIG_CASE(CI, CO, K)                                                                   \
   if (Cin == CI && Cout == CO && ks == K) {                                                   \
     return dgrad ? launch_fwd<CI, CO, K, true>(vin, vout, vaux, w, bias, F, H, W, fl, st)     \
@@ -377,6 +379,10 @@ int paig_conv2d_wgrad(const float* x, long long x_fs, int x_grp, long long x_gs,
   FView vd{dy, dy_fs, 0, 0};
   *nblk_out = 0;
   if (F <= 0) return 0;
+  int rc = 0;
+  if (!(Cin & 0x10000) && paig_conv_mfma_wgrad(vx, vd, slab, nblk_max, nblk_out, F, Cin, Cout, H, W, ks, st, &rc))
+    return rc;
+  Cin &= 0xFFFF;
 #define PAIG_CASE(CI, CO, K) \
   if (Cin == CI && Cout == CO && ks == K) return launch_wgrad<CI, CO, K>(vx, vd, slab, nblk_max, nblk_out, F, H, W, st);
   PAIG_CONV_SHAPES(PAIG_CASE)

@@ -1,0 +1,434 @@
+// U-Net convolutions as implicit GEMMs on CDNA4 matrix cores
+// (v_mfma_f32_16x16x4_f32: exact fp32 FMA chain, one instruction per 16
+// FMAs per lane).  Reference: aten conv2d / convolution_backward behind
+// nn/network/blocks.py:246-276 (ShallowUNet) and :113-170 (UNet).
+//
+// forward / dgrad   D[pixel][co] = im2col(X)[pixel][k] * Wt[k][co]
+//   k = tap * CINP + ci (tap-major, 4 consecutive input channels per MFMA
+//   k-step).  A fragment = one LDS read per lane at (lane pixel base +
+//   compile-time (ci, tap) offset): zero VALU address math per MFMA; the
+//   16 pixels of an M-tile are consecutive in (frame,row,x) order so each
+//   lane's 4 accumulator rows are 4 adjacent x -> one float4 store.
+//   Weights are staged once per block as Wt[tap][ci][co] (dgrad stages the
+//   transposed + flipped kernel, so the same kernel computes dX).
+// wgrad             D[co][n] = dY[co][pixel] * im2col(X)[pixel][n],
+//   n = ci*KK + tap (the weight layout), K = pixels: each block walks many
+//   (frame,rows) tiles accumulating in registers, waves split the pixels (and
+//   the n-tiles when accumulators would not fit), one deterministic
+//   cross-wave reduction, one partial row per block (paig_slab_reduce*).
+// LDS layouts are padded so every fragment read is bank-conflict free
+// (lanes 0-15 and 16-31 of a ds_read_b32 group land on disjoint halves).
+#include "common.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
+constexpr int pad16mod32(int x) { return ((x + 15) / 16 * 16) % 32 == 0 ? (x + 15) / 16 * 16 + 16 : (x + 15) / 16 * 16; }
+// smallest y >= x with y % 32 == r
+constexpr int to_mod32(int x, int r) { return x + ((r - x % 32) + 32) % 32; }
+
+// ============================================================ forward / dgrad
+template <int CIN, int COUT, int H, int W, int KS, bool DG>
+struct FwdCfg {
+  static constexpr int KK = KS * KS, PADL = KS / 2;
+  static constexpr int CINP = ceil_div(CIN, 4) * 4;
+  static constexpr int NT = ceil_div(COUT, 16);
+  static constexpr int COUTP = pad16mod32(COUT);            // weight row stride, = 16 mod 32
+  static constexpr int MW = W >= 32 ? 8 : (W >= 16 ? 4 : 2);  // M-tiles per wave
+  static constexpr int TPX = 4 * MW * 16;                    // pixels per block tile
+  static constexpr int FPT = TPX >= H * W ? TPX / (H * W) : 1;
+  static constexpr int RT = TPX >= H * W ? H : TPX / W;      // rows per tile (per frame)
+  static constexpr int TWP = W + 8;                          // cols: [3]=halo, [4, 4+W)=data, [4+W]=halo
+  static constexpr int ROWS = RT + KS - 1;
+  static constexpr int CHS = to_mod32(ROWS * TWP, 16);        // channel stride in LDS, = 16 mod 32
+  static constexpr int CI0 = CINP < 8 ? CINP : 8;
+  static constexpr int CI = (FPT * CI0 * CHS * 4 > 48 * 1024 && CI0 > 4) ? 4 : CI0;
+  static constexpr int NCH = CINP / CI;
+  static constexpr int LDS_I = FPT * CI * CHS;
+  static constexpr int LDS_W = KK * CINP * COUTP;
+  static constexpr int LDS = (LDS_I + LDS_W) * 4;
+  static_assert(CINP % CI == 0, "chunking");
+  static_assert(W % 4 == 0 && (H * W) % 16 == 0, "MFMA conv needs W % 4 == 0");
+  static_assert(RT * W * FPT == TPX || RT == H, "tile");
+};
+
+template <int CIN, int COUT, int H, int W, int KS, bool DG>
+__global__ void __launch_bounds__(256)
+conv_fwd_mfma_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
+                int flags) {
+  using C = FwdCfg<CIN, COUT, H, W, KS, DG>;
+  constexpr int KK = C::KK, NT = C::NT, MW = C::MW, TWP = C::TWP, CHS = C::CHS, CI = C::CI;
+  constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, COUTP = C::COUTP, CINP = C::CINP;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Il = lds;                 // [FPT][CI][CHS]
+  float* Wl = lds + C::LDS_I;      // [KK][CINP][COUTP]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr int NRB = H / RT;      // row blocks per frame (RT divides H)
+  const int tile = blockIdx.x;
+  const int f0 = (tile / NRB) * FPT;
+  const int y0 = (tile % NRB) * RT;
+
+  // ---- weights -> Wt[tap][ci][co] (zero padded); dgrad: transposed + flipped
+  for (int i = tid; i < KK * CINP * COUTP; i += 256) {
+    const int co = i % COUTP;
+    const int ci = (i / COUTP) % CINP;
+    const int tap = i / (COUTP * CINP);
+    float v = 0.f;
+    if (co < COUT && ci < CIN) {
+      if (DG) v = w[(ci * COUT + co) * KK + (KK - 1 - tap)];
+      else v = w[(co * CIN + ci) * KK + tap];
+    }
+    Wl[i] = v;
+  }
+  // ---- zero the halo columns (never written by the staging below)
+  for (int i = tid; i < FPT * CI * ROWS; i += 256) {
+    Il[(i / ROWS) * CHS + (i % ROWS) * TWP + 3] = 0.f;
+    Il[(i / ROWS) * CHS + (i % ROWS) * TWP + 4 + W] = 0.f;
+  }
+
+  // ---- per-lane pixel bases of this wave's M-tiles
+  int abase[MW];
+#pragma unroll
+  for (int mt = 0; mt < MW; ++mt) {
+    const int pix = (wv * MW + mt) * 16 + (lane & 15);     // pixel index within the tile
+    const int fi = pix / (RT * W);
+    const int rem = pix % (RT * W);
+    const int y = rem / W, x = rem % W;
+    abase[mt] = fi * CI * CHS + (lane >> 4) * CHS + y * TWP + x + 4 - C::PADL;
+  }
+  f32x4 acc[MW][NT];
+#pragma unroll
+  for (int mt = 0; mt < MW; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int Q = W / 4;   // float4 per row
+  for (int ch = 0; ch < C::NCH; ++ch) {
+    const int ci0 = ch * CI;
+    if (ch) __syncthreads();
+    // ---- stage input rows [fi][c][rr] (float4 along x)
+    for (int i = tid; i < FPT * CI * ROWS * Q; i += 256) {
+      const int q = i % Q;
+      const int r = i / Q;
+      const int rr = r % ROWS;
+      const int c = (r / ROWS) % CI;
+      const int fi = r / (ROWS * CI);
+      const int f = f0 + fi, gy = y0 + rr - C::PADL, ci = ci0 + c;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (f < F && gy >= 0 && gy < H && ci < CIN)
+        v = *reinterpret_cast<const f32x4*>(in.frame(f) + ((long long)ci * H + gy) * W + 4 * q);
+      *reinterpret_cast<f32x4*>(&Il[(fi * CI + c) * CHS + rr * TWP + 4 + 4 * q]) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < KK; ++tap) {
+      const int toff = (tap / KS) * TWP + (tap % KS);
+#pragma unroll
+      for (int cg = 0; cg < CI / 4; ++cg) {
+        float b[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          b[nt] = Wl[(tap * CINP + ci0 + cg * 4 + (lane >> 4)) * COUTP + nt * 16 + (lane & 15)];
+#pragma unroll
+        for (int mt = 0; mt < MW; ++mt) {
+          const float a = Il[abase[mt] + cg * 4 * CHS + toff];
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma4(a, b[nt], acc[mt][nt]);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for co = nt*16 + (lane&15)
+  constexpr long long HW = (long long)H * W;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int co = nt * 16 + (lane & 15);
+    if (co >= COUT) continue;
+    const float bv = bias ? bias[co] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MW; ++mt) {
+      const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+      const int fi = pix / (RT * W);
+      const int rem = pix % (RT * W);
+      const int y = y0 + rem / W, x = rem % W;
+      const int f = f0 + fi;
+      if (f >= F || y >= H) continue;
+      float* op = out.frame(f) + co * HW + (long long)y * W + x;
+      f32x4 v = acc[mt][nt];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += bv;
+      if (flags & 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] < 0.f ? 0.f : v[r];
+      }
+      if (flags & 4) {
+        const f32x4 o = *reinterpret_cast<const f32x4*>(op);
+        v += o;
+      }
+      if (flags & 2) {
+        const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(op) = v;
+    }
+  }
+  (void)ROWS;
+}
+
+// ===================================================================== wgrad
+template <int CIN, int COUT, int H, int W, int KS>
+struct WgCfg {
+  static constexpr int KK = KS * KS, PADL = KS / 2;
+  static constexpr int NCOL = CIN * KK;
+  static constexpr int NT = ceil_div(NCOL, 16);
+  static constexpr int MT = ceil_div(COUT, 16);
+  static constexpr int WN = (MT * NT * 4 <= 96) ? 1 : ((MT * ceil_div(NT, 2) * 4 <= 96) ? 2 : 4);
+  static constexpr int WP = 4 / WN;
+  static constexpr int NTW = ceil_div(NT, WN);
+  static constexpr int TWP = W + 8;
+  // rows per tile: as many as fit ~48 KB of LDS
+  static constexpr int COP = pad16mod32(COUT);
+  static constexpr int rows_fit(int rt) {
+    return (CIN * to_mod32((rt + KS - 1) * TWP, 2) + rt * W * COP) * 4 <= 56 * 1024 ? rt : rows_fit(rt / 2);
+  }
+  static constexpr int RT0 = rows_fit(H);
+  static constexpr int FPT = (RT0 == H && H * W < 256) ? 256 / (H * W) : 1;
+  static constexpr int RT = RT0;
+  static constexpr int ROWS = RT + KS - 1;
+  static constexpr int CHS = to_mod32(ROWS * TWP, 2);
+  static constexpr int LDS_X = FPT * CIN * CHS;
+  static constexpr int LDS_D = FPT * RT * W * COP;
+  static constexpr int RED = 4 * 64 * MT * NTW * 4;          // cross-wave reduction buffer
+  static constexpr int LDS = ((LDS_X + LDS_D) > RED ? (LDS_X + LDS_D) : RED) * 4;
+  static constexpr int NG = FPT * RT * W / 4;                // 4-pixel groups per tile
+  static constexpr int SLAB = COUT * NCOL + COUT;
+  static_assert(W % 4 == 0, "W % 4");
+  static_assert(H % RT == 0, "RT divides H");
+};
+
+template <int CIN, int COUT, int H, int W, int KS>
+__global__ void __launch_bounds__(256)
+conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles) {
+  using C = WgCfg<CIN, COUT, H, W, KS>;
+  constexpr int KK = C::KK, NT = C::NT, MT = C::MT, WN = C::WN, WP = C::WP, NTW = C::NTW;
+  constexpr int TWP = C::TWP, CHS = C::CHS, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, COP = C::COP;
+  constexpr int NCOL = C::NCOL;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Xl = lds;                 // [FPT][CIN][CHS]
+  float* Dl = lds + C::LDS_X;      // [FPT*RT*W][COP]  (pixel-major, co fastest)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wn = wv % WN, wp = wv / WN;
+
+  // per-lane column offsets (n = ci*KK + tap) of this wave's n-tiles
+  int coff[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    int n = (wn + j * WN) * 16 + (lane & 15);
+    if (n >= NCOL) n = NCOL - 1;                  // padded columns read valid LDS, never stored
+    const int ci = n / KK, tap = n % KK;
+    coff[j] = ci * CHS + (tap / KS) * TWP + (tap % KS) + 4 - C::PADL;
+  }
+  f32x4 acc[MT][NTW];
+  float bacc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    bacc[m] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // zero halo columns once
+  for (int i = tid; i < FPT * CIN * ROWS; i += 256) {
+    Xl[(i / ROWS) * CHS + (i % ROWS) * TWP + 3] = 0.f;
+    Xl[(i / ROWS) * CHS + (i % ROWS) * TWP + 4 + W] = 0.f;
+  }
+  constexpr int NRB = H / RT;
+  constexpr int Q = W / 4;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
+    __syncthreads();
+    for (int i = tid; i < FPT * CIN * ROWS * Q; i += 256) {
+      const int q = i % Q;
+      const int r = i / Q;
+      const int rr = r % ROWS;
+      const int c = (r / ROWS) % CIN;
+      const int fi = r / (ROWS * CIN);
+      const int f = f0 + fi, gy = y0 + rr - C::PADL;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (f < F && gy >= 0 && gy < H) v = *reinterpret_cast<const f32x4*>(x.frame(f) + ((long long)c * H + gy) * W + 4 * q);
+      *reinterpret_cast<f32x4*>(&Xl[(fi * CIN + c) * CHS + rr * TWP + 4 + 4 * q]) = v;
+    }
+    for (int i = tid; i < FPT * COUT * RT * Q; i += 256) {
+      const int q = i % Q;
+      const int r = i / Q;
+      const int rr = r % RT;
+      const int co = (r / RT) % COUT;
+      const int fi = r / (RT * COUT);
+      const int f = f0 + fi;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (f < F) v = *reinterpret_cast<const f32x4*>(dy.frame(f) + ((long long)co * H + y0 + rr) * W + 4 * q);
+      const int pb = (fi * RT + rr) * W + 4 * q;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Dl[(pb + e) * COP + co] = v[e];
+    }
+    if (COP > COUT) {   // zero padded co columns (read by padded M rows; never stored)
+      for (int i = tid; i < FPT * RT * W * (COP - COUT); i += 256)
+        Dl[(i / (COP - COUT)) * COP + COUT + i % (COP - COUT)] = 0.f;
+    }
+    __syncthreads();
+    for (int g = wp; g < C::NG; g += WP) {
+      const int fi = g / (RT * Q);
+      const int rem = g % (RT * Q);
+      const int y = rem / Q, x0 = (rem % Q) * 4;
+      const int pix = (fi * RT + y) * W + x0 + (lane >> 4);
+      float a[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        a[m] = Dl[pix * COP + m * 16 + (lane & 15)];
+        bacc[m] += a[m];
+      }
+      const int xb = fi * CIN * CHS + y * TWP + x0 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        if (wn + j * WN < NT) {
+          const float b = Xl[coff[j] + xb];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) acc[m][j] = mfma4(a[m], b, acc[m][j]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- cross-wave reduction (waves with equal wn, different wp) through LDS
+  float* R = lds;   // [4 waves][MT][NTW][4][64]
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) R[(((wv * MT + m) * NTW + j) * 4 + r) * 64 + lane] = acc[m][j][r];
+  // bias: lane (l&15) co partial over its (l>>4) pixel lanes, then across waves
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    float v = bacc[m];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    bacc[m] = v;
+  }
+  __syncthreads();
+  float* s = slab + (long long)blockIdx.x * C::SLAB;
+  if (wp == 0) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int nt = wn + j * WN;
+        if (nt >= NT) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = 0.f;
+          for (int p = 0; p < WP; ++p) v += R[((((p * WN + wn) * MT + m) * NTW + j) * 4 + r) * 64 + lane];
+          const int co = m * 16 + (lane >> 4) * 4 + r;
+          const int n = nt * 16 + (lane & 15);
+          if (co < COUT && n < NCOL) s[co * NCOL + n] = v;
+        }
+      }
+  }
+  __syncthreads();
+  // bias partials: every wave with wn == 0 holds a full-pixel-subset partial
+  if (wn == 0 && lane < 16) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) R[(wp * MT + m) * 16 + lane] = bacc[m];
+  }
+  __syncthreads();
+  if (tid < COUT) {
+    const int m = tid / 16, l = tid % 16;
+    float v = 0.f;
+    for (int p = 0; p < WP; ++p) v += R[(p * MT + m) * 16 + l];
+    s[COUT * NCOL + tid] = v;
+  }
+}
+
+template <int CIN, int COUT, int H, int W, int KS, bool DG>
+static int fwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
+                      hipStream_t st) {
+  using C = FwdCfg<CIN, COUT, H, W, KS, DG>;
+  constexpr int NRB = H / C::RT;
+  const int ntiles = cdiv(F, C::FPT) * NRB;
+  auto k = conv_fwd_mfma_k<CIN, COUT, H, W, KS, DG>;
+  static bool attr = false;
+  if (!attr && C::LDS > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(ntiles), dim3(256), C::LDS, st, in, out, aux, w, b, F, flags);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int CIN, int COUT, int H, int W, int KS>
+static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st) {
+  using C = WgCfg<CIN, COUT, H, W, KS>;
+  const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
+  int nb = ntiles < nblk_max ? ntiles : nblk_max;
+  if (nb < 1) nb = 1;
+  *nblk_out = nb;
+  auto k = conv_wgrad_mfma_k<CIN, COUT, H, W, KS>;
+  static bool attr = false;
+  if (!attr && C::LDS > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), C::LDS, st, x, dy, slab, F, ntiles);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+// (CIN, COUT, H, KS): ShallowUNet(hidden 8) at 32x32 — forward and dgrad
+// shapes (dgrad kernel shapes are (layer Cout, layer Cin)).
+#define PAIG_MFMA_FWD(X)                                                                                  \
+  X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
+  X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1) X(16, 8, 16, 3) X(8, 24, 32, 3)       \
+  X(2, 8, 32, 1) X(32, 16, 8, 3) X(16, 32, 16, 3)
+#define PAIG_MFMA_WG(X)                                                                                   \
+  X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
+  X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1)
+
+}  // namespace
+
+// Returns 1 if handled (rc in *rc), 0 if the shape has no MFMA instantiation.
+int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
+                       int H, int W, int ks, int flags, hipStream_t st, int* rc) {
+  const bool dg = (flags & 8) != 0;
+  const int fl = flags & 7;
+  if (H != W) return 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                                      \
+  if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                \
+    *rc = dg ? fwd_launch<CI, CO, HH, HH, K, true>(in, out, aux, w, b, F, fl, st)                     \
+             : fwd_launch<CI, CO, HH, HH, K, false>(in, out, aux, w, b, F, fl, st);                   \
+    return 1;                                                                                         \
+  }
+  PAIG_MFMA_FWD(PAIG_CASE)
+#undef PAIG_CASE
+  return 0;
+}
+
+int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H,
+                         int W, int ks, hipStream_t st, int* rc) {
+  if (H != W) return 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                         \
+  if (Cin == CI && Cout == CO && H == HH && ks == K) {                                   \
+    *rc = wgrad_launch<CI, CO, HH, HH, K>(x, dy, slab, nblk_max, nblk_out, F, st);       \
+    return 1;                                                                            \
+  }
+  PAIG_MFMA_WG(PAIG_CASE)
+#undef PAIG_CASE
+  return 0;
+}

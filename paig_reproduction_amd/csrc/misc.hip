@@ -235,12 +235,12 @@ int paig_vfn_fwd(const float* W1, const float* b1, const float* W2, const float*
   return 0;
 }
 
-int paig_vfn_bwd_blocks(int P) { return cdiv(P, 16); }
+int paig_vfn_bwd_blocks(int P) { return cdiv(P, 64); }
 
 // d: adjoint of y (sig = 0) or of sigmoid(y) (sig = 1). part: >= blocks*200 floats.
 int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,
                  float* dW2, float* db2, float* part, int P, void* stream) {
-  const int rows = 16;
+  const int rows = 64;
   const int nblk = cdiv(P, rows);
   hipLaunchKernelGGL(vfn_bwd1_k, dim3(nblk), dim3(256), 0, (hipStream_t)stream, d, y, sig, h, W2, dW2, db2, part, P,
                      rows);

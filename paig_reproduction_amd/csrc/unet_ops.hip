@@ -7,6 +7,8 @@
 //   deterministic slab / column reductions for weight and bias gradients.
 #include "common.h"
 
+#define PAIG_MAX_SLAB_TASKS 32
+
 namespace {
 
 // ---------------------------------------------------------------- maxpool ----
@@ -113,8 +115,8 @@ __global__ void upsample_bwd_k(FView du, FView s, FViewW ds, int F, int C, int H
     int f = (int)(t / C);
     const float* dup = du.frame(f) + (long long)c * Ho * Wo;
     const int ry = Ho / Hs, rx = Wo / Ws;
-    int ylo = sy * ry - 2 * ry, yhi = sy * ry + 2 * ry + 1;
-    int xlo = sx * rx - 2 * rx, xhi = sx * rx + 2 * rx + 1;
+    int ylo = sy * ry - ry, yhi = sy * ry + 2 * ry - 1;
+    int xlo = sx * rx - rx, xhi = sx * rx + 2 * rx - 1;
     if (ylo < 0) ylo = 0;
     if (xlo < 0) xlo = 0;
     if (yhi > Ho - 1) yhi = Ho - 1;
@@ -289,6 +291,43 @@ __global__ void __launch_bounds__(256) slab_reduce_k(const float* __restrict__ s
   }
 }
 
+// Many reductions in one launch: task t sums nblk[t] rows of len[t] floats
+// (row stride len[t]) into dst[t]; blocks [start[t], start[t+1]) serve task t.
+struct SlabTasks {
+  const float* src[PAIG_MAX_SLAB_TASKS];
+  float* dst[PAIG_MAX_SLAB_TASKS];
+  int nblk[PAIG_MAX_SLAB_TASKS];
+  int len[PAIG_MAX_SLAB_TASKS];
+  int start[PAIG_MAX_SLAB_TASKS + 1];
+  int ntask;
+  int accumulate;
+};
+
+__global__ void __launch_bounds__(256) slab_reduce_multi_k(SlabTasks T) {
+  __shared__ float red[4][64];
+  int t = 0;
+  while (t + 1 < T.ntask && (int)blockIdx.x >= T.start[t + 1]) ++t;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int len = T.len[t], nblk = T.nblk[t];
+  const int i = (blockIdx.x - T.start[t]) * 64 + lane;
+  const float* src = T.src[t];
+  float s0 = 0.f, s1 = 0.f;
+  if (i < len) {
+    int b = wv;
+    for (; b + 4 < nblk; b += 8) {
+      s0 += src[(long long)b * len + i];
+      s1 += src[(long long)(b + 4) * len + i];
+    }
+    for (; b < nblk; b += 4) s0 += src[(long long)b * len + i];
+  }
+  red[wv][lane] = s0 + s1;
+  __syncthreads();
+  if (wv == 0 && i < len) {
+    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    T.dst[t][i] = T.accumulate ? T.dst[t][i] + v : v;
+  }
+}
+
 // part[s][n] = sum over rows r in stripe s of X[r][n]
 __global__ void __launch_bounds__(256) colsum_part_k(const float* __restrict__ X, int M, int N, long long ld,
                                                      float* __restrict__ part, int rows_per) {
@@ -408,6 +447,28 @@ int paig_vel_unpack_add(const float* dX, const float* dpos0, float* dpos, int B,
                         void* stream) {
   hipLaunchKernelGGL(vel_unpack_add_k, dim3(grid_for(B * S * 2 * K)), dim3(256), 0, (hipStream_t)stream, dX, dpos0,
                      dpos, B, Te, K, S, alt);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_slab_reduce_multi(int ntask, const float* const* src, const int* nblk, const int* len, float* const* dst,
+                           int accumulate, void* stream) {
+  PAIG_REQUIRE(ntask >= 0 && ntask <= PAIG_MAX_SLAB_TASKS, "slab_reduce_multi: %d tasks", ntask);
+  if (ntask == 0) return 0;
+  SlabTasks T;
+  int blocks = 0;
+  for (int t = 0; t < ntask; ++t) {
+    T.src[t] = src[t];
+    T.dst[t] = dst[t];
+    T.nblk[t] = nblk[t];
+    T.len[t] = len[t];
+    T.start[t] = blocks;
+    blocks += cdiv(len[t], 64);
+  }
+  T.start[ntask] = blocks;
+  T.ntask = ntask;
+  T.accumulate = accumulate;
+  hipLaunchKernelGGL(slab_reduce_multi_k, dim3(blocks), dim3(256), 0, (hipStream_t)stream, T);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

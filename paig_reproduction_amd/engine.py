@@ -543,8 +543,7 @@ class Engine:
                 gb = self.g(lay.prefix + op["name"] + ".bias")
                 n_w = cout * cin * ks * ks
                 assert gb.data_ptr() == gw.data_ptr() + n_w * 4, "flat grads: weight and bias must be adjacent"
-                L.paig_slab_reduce(ptr(slab), nb.value, n_w + cout, n_w + cout, ptr(gw), 0, st)
-                slabs.append(slab)
+                slabs.append((slab, nb.value, n_w + cout, gw))
                 if src[0] == "X0":
                     continue
                 dxv, _ = dview(src)
@@ -578,4 +577,11 @@ class Engine:
                 L.paig_upsample2_bwd(dyv[0], dyv[1], sv[0], sv[1], dxv[0], dxv[1], F, src[2], Hs, Hs, Ho, Ho,
                                      int(relu), st)
                 mark(src)
+        # all conv weight/bias gradients: one batched deterministic reduction
+        n = len(slabs)
+        srcs = (ctypes.c_void_p * n)(*[ptr(s[0]) for s in slabs])
+        nbs = (ctypes.c_int * n)(*[s[1] for s in slabs])
+        lens = (ctypes.c_int * n)(*[s[2] for s in slabs])
+        dsts = (ctypes.c_void_p * n)(*[ptr(s[3]) for s in slabs])
+        L.paig_slab_reduce_multi(n, srcs, nbs, lens, dsts, 0, st)
         S["_slabs"] = slabs
