@@ -36,14 +36,17 @@ int paig_abi_version(void);
  * (nn/network/blocks.py:246-276 and :113-170, forward :278-308, :172-237).
  * flags: 1 ReLU, 2 multiply by (aux > 0) [ReLU' of the layer input],
  *        4 accumulate into out, 8 dgrad (in = dY, weight read transposed and
- *        flipped, Cin/Cout are the DGRAD kernel's in/out channel counts).  */
+ *        flipped, Cin/Cout are the DGRAD kernel's in/out channel counts),
+ *        16 force the VALU path (tests), 32 the input is the 2x bilinear
+ *        upsample of the given (H/2 x W/2) planes, formed while staging
+ *        (torchvision Resize of blocks.py:260,269 fused, never materialised). */
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                     const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin, int Cout,
                     int H, int W, int ks, int flags, void* stream);
 /* per-block partial [Cout*Cin*ks*ks | Cout] weight+bias grads into slab rows */
 int paig_conv2d_wgrad(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
                       float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
-                      void* stream);
+                      int flags, void* stream);
 
 /* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,
@@ -69,11 +72,12 @@ int paig_pos_head_bwd(const float* h3, const float* dpos, float* dh3, int N, int
 /* ---- dense layers on MFMA (l1/l2/l3 blocks.py:71-75,98-100; velocity MLP
  *      blocks.py:23-29,43-48; VariableFromNetwork blocks.py:311-322)
  * C = alpha op(A) op(B) (+beta C) (+bias[n]) -> act (0 none,1 relu,2 tanh,3 sigmoid)
- *     -> * aux' (auxm 0 none, 1 relu'(aux), 2 tanh'(aux)=1-aux^2)          */
+ *     -> * aux' (auxm 0 none, 1 relu'(aux), 2 tanh'(aux)=1-aux^2)
+ * rowsum (optional) = alpha * sum_k op(A)[m][k]: the bias gradient of dW = dY^T X */
 size_t paig_gemm_workspace(int M, int N, int K);
 int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
               long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
-              const float* aux, long long ldaux, float* ws, size_t ws_floats, void* stream);
+              const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, void* stream);
 size_t paig_colsum_workspace(int M, int N);
 int paig_colsum(const float* X, int M, int N, long long ld, float* out, int accumulate, float* ws, void* stream);
 int paig_slab_reduce(const float* slab, int nblk, long long ld, int len, float* out, int accumulate, void* stream);

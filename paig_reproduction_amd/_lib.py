@@ -24,7 +24,7 @@ SIGNATURES = {
     "paig_last_error": (ctypes.c_char_p, []),
     "paig_abi_version": (I, []),
     "paig_conv2d_fwd": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P]),
-    "paig_conv2d_wgrad": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, P]),
+    "paig_conv2d_wgrad": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P]),
     "paig_maxpool2_fwd": (I, [P, LL, P, LL, I, I, I, I, P]),
     "paig_maxpool2_bwd_relu": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
     "paig_upsample2_fwd": (I, [P, LL, P, LL, I, I, I, I, I, I, P]),
@@ -34,7 +34,7 @@ SIGNATURES = {
     "paig_pos_head_fwd": (I, [P, P, I, I, F32, P]),
     "paig_pos_head_bwd": (I, [P, P, P, I, I, F32, P]),
     "paig_gemm_workspace": (SZ, [I, I, I]),
-    "paig_gemm": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, SZ, P]),
+    "paig_gemm": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, P]),
     "paig_colsum_workspace": (SZ, [I, I]),
     "paig_colsum": (I, [P, I, I, LL, P, I, P, P]),
     "paig_slab_reduce": (I, [P, I, LL, I, P, I, P]),

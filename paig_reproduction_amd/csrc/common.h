@@ -75,4 +75,4 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
                        int H, int W, int ks, int flags, hipStream_t st, int* rc);
 int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H,
-                         int W, int ks, hipStream_t st, int* rc);
+                         int W, int ks, int flags, hipStream_t st, int* rc);

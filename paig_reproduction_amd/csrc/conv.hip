@@ -358,6 +358,10 @@ int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_g
   if (F <= 0) return 0;
   int rc = 0;
   if (!(flags & 16) && paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc)) return rc;
+  if (flags & 32) {
+    paig_set_error("paig_conv2d_fwd: fused-upsample input has no instantiation for Cin=%d Cout=%d H=%d", Cin, Cout, H);
+    return PAIG_E_UNSUPPORTED;
+  }
 #define PAIG_CASE(CI, CO, K)                                                                   \
   if (Cin == CI && Cout == CO && ks == K) {                                                   \
     return dgrad ? launch_fwd<CI, CO, K, true>(vin, vout, vaux, w, bias, F, H, W, fl, st)     \
@@ -373,16 +377,19 @@ int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_g
 // *nblk_out receives the number of partial rows written (<= nblk_max).
 int paig_conv2d_wgrad(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
                       float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
-                      void* stream) {
+                      int flags, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   FView vx{x, x_fs, x_gs, x_grp};
   FView vd{dy, dy_fs, 0, 0};
   *nblk_out = 0;
   if (F <= 0) return 0;
   int rc = 0;
-  if (!(Cin & 0x10000) && paig_conv_mfma_wgrad(vx, vd, slab, nblk_max, nblk_out, F, Cin, Cout, H, W, ks, st, &rc))
+  if (!(flags & 16) && paig_conv_mfma_wgrad(vx, vd, slab, nblk_max, nblk_out, F, Cin, Cout, H, W, ks, flags, st, &rc))
     return rc;
-  Cin &= 0xFFFF;
+  if (flags & 32) {
+    paig_set_error("paig_conv2d_wgrad: fused-upsample input has no instantiation for Cin=%d Cout=%d H=%d", Cin, Cout, H);
+    return PAIG_E_UNSUPPORTED;
+  }
 #define PAIG_CASE(CI, CO, K) \
   if (Cin == CI && Cout == CO && ks == K) return launch_wgrad<CI, CO, K>(vx, vd, slab, nblk_max, nblk_out, F, H, W, st);
   PAIG_CONV_SHAPES(PAIG_CASE)

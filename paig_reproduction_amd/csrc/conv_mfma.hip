@@ -33,6 +33,42 @@ constexpr int pad16mod32(int x) { return ((x + 15) / 16 * 16) % 32 == 0 ? (x + 1
 // smallest y >= x with y % 32 == r
 constexpr int to_mod32(int x, int r) { return x + ((r - x % 32) + 32) % 32; }
 
+// aten upsample_bilinear2d taps for an exact 2x upscale (scale 0.5, align_corners=False)
+__device__ __forceinline__ void up2_taps(int d, int n, int& i0, int& i1, float& l0, float& l1) {
+  float s = 0.5f * ((float)d + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  if (i0 > n - 1) i0 = n - 1;
+  i1 = i0 + (i0 < n - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+  l0 = 1.f - l1;
+}
+
+// 4 consecutive pixels (row gy, x = 4q..4q+3) of a conv input plane of size
+// H x W: read directly (UPS = false) or formed on the fly as the 2x bilinear
+// upsample of a (H/2 x W/2) source plane (UPS = true: the reference's
+// torchvision Resize feeding c7/c10, blocks.py:289-290,298-299, never
+// materialised).
+template <bool UPS, int H, int W>
+__device__ __forceinline__ f32x4 load_row4(const float* __restrict__ plane, int gy, int q) {
+  if (!UPS) return *reinterpret_cast<const f32x4*>(plane + (long long)gy * W + 4 * q);
+  constexpr int HS = H / 2, WS = W / 2;
+  int y0, y1;
+  float wy0, wy1;
+  up2_taps(gy, HS, y0, y1, wy0, wy1);
+  const float* r0 = plane + y0 * WS;
+  const float* r1 = plane + y1 * WS;
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    int x0, x1;
+    float wx0, wx1;
+    up2_taps(4 * q + e, WS, x0, x1, wx0, wx1);
+    v[e] = wy0 * (wx0 * r0[x0] + wx1 * r0[x1]) + wy1 * (wx0 * r1[x0] + wx1 * r1[x1]);
+  }
+  return v;
+}
+
 // ============================================================ forward / dgrad
 template <int CIN, int COUT, int H, int W, int KS, bool DG>
 struct FwdCfg {
@@ -58,10 +94,11 @@ struct FwdCfg {
   static_assert(RT * W * FPT == TPX || RT == H, "tile");
 };
 
-template <int CIN, int COUT, int H, int W, int KS, bool DG>
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS>
 __global__ void __launch_bounds__(256)
 conv_fwd_mfma_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
                 int flags) {
+  constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   using C = FwdCfg<CIN, COUT, H, W, KS, DG>;
   constexpr int KK = C::KK, NT = C::NT, MW = C::MW, TWP = C::TWP, CHS = C::CHS, CI = C::CI;
   constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, COUTP = C::COUTP, CINP = C::CINP;
@@ -121,8 +158,7 @@ conv_fwd_mfma_k(FView in, FViewW out, FView aux, const float* __restrict__ w, co
       const int fi = r / (ROWS * CI);
       const int f = f0 + fi, gy = y0 + rr - C::PADL, ci = ci0 + c;
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (f < F && gy >= 0 && gy < H && ci < CIN)
-        v = *reinterpret_cast<const f32x4*>(in.frame(f) + ((long long)ci * H + gy) * W + 4 * q);
+      if (f < F && gy >= 0 && gy < H && ci < CIN) v = load_row4<UPS, H, W>(in.frame(f) + ci * PLANE, gy, q);
       *reinterpret_cast<f32x4*>(&Il[(fi * CI + c) * CHS + rr * TWP + 4 + 4 * q]) = v;
     }
     __syncthreads();
@@ -214,10 +250,11 @@ struct WgCfg {
   static_assert(H % RT == 0, "RT divides H");
 };
 
-template <int CIN, int COUT, int H, int W, int KS>
+template <int CIN, int COUT, int H, int W, int KS, bool UPS>
 __global__ void __launch_bounds__(256)
 conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles) {
   using C = WgCfg<CIN, COUT, H, W, KS>;
+  constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   constexpr int KK = C::KK, NT = C::NT, MT = C::MT, WN = C::WN, WP = C::WP, NTW = C::NTW;
   constexpr int TWP = C::TWP, CHS = C::CHS, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, COP = C::COP;
   constexpr int NCOL = C::NCOL;
@@ -262,15 +299,17 @@ conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles
       const int fi = r / (ROWS * CIN);
       const int f = f0 + fi, gy = y0 + rr - C::PADL;
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (f < F && gy >= 0 && gy < H) v = *reinterpret_cast<const f32x4*>(x.frame(f) + ((long long)c * H + gy) * W + 4 * q);
+      if (f < F && gy >= 0 && gy < H) v = load_row4<UPS, H, W>(x.frame(f) + c * PLANE, gy, q);
       *reinterpret_cast<f32x4*>(&Xl[(fi * CIN + c) * CHS + rr * TWP + 4 + 4 * q]) = v;
     }
+    // dY -> [pixel][co]: co varies fastest across lanes so the transposed LDS
+    // writes of one float4 (4 pixels) are conflict free
     for (int i = tid; i < FPT * COUT * RT * Q; i += 256) {
-      const int q = i % Q;
-      const int r = i / Q;
-      const int rr = r % RT;
-      const int co = (r / RT) % COUT;
-      const int fi = r / (RT * COUT);
+      const int co = i % COUT;
+      const int r = i / COUT;
+      const int q = r % Q;
+      const int rr = (r / Q) % RT;
+      const int fi = r / (Q * RT);
       const int f = f0 + fi;
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
       if (f < F) v = *reinterpret_cast<const f32x4*>(dy.frame(f) + ((long long)co * H + y0 + rr) * W + 4 * q);
@@ -356,13 +395,13 @@ conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles
   }
 }
 
-template <int CIN, int COUT, int H, int W, int KS, bool DG>
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS>
 static int fwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
                       hipStream_t st) {
   using C = FwdCfg<CIN, COUT, H, W, KS, DG>;
   constexpr int NRB = H / C::RT;
   const int ntiles = cdiv(F, C::FPT) * NRB;
-  auto k = conv_fwd_mfma_k<CIN, COUT, H, W, KS, DG>;
+  auto k = conv_fwd_mfma_k<CIN, COUT, H, W, KS, DG, UPS>;
   static bool attr = false;
   if (!attr && C::LDS > 64 * 1024) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
@@ -373,14 +412,14 @@ static int fwd_launch(FView in, FViewW out, FView aux, const float* w, const flo
   return 0;
 }
 
-template <int CIN, int COUT, int H, int W, int KS>
+template <int CIN, int COUT, int H, int W, int KS, bool UPS>
 static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st) {
   using C = WgCfg<CIN, COUT, H, W, KS>;
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   int nb = ntiles < nblk_max ? ntiles : nblk_max;
   if (nb < 1) nb = 1;
   *nblk_out = nb;
-  auto k = conv_wgrad_mfma_k<CIN, COUT, H, W, KS>;
+  auto k = conv_wgrad_mfma_k<CIN, COUT, H, W, KS, UPS>;
   static bool attr = false;
   if (!attr && C::LDS > 64 * 1024) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
@@ -391,8 +430,9 @@ static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_
   return 0;
 }
 
-// (CIN, COUT, H, KS): ShallowUNet(hidden 8) at 32x32 — forward and dgrad
-// shapes (dgrad kernel shapes are (layer Cout, layer Cin)).
+// (CIN, COUT, H, KS): ShallowUNet(hidden 8) at 32x32 -- forward and dgrad
+// shapes (dgrad kernel shapes are (layer Cout, layer Cin)); *_UP: convs whose
+// input is the fused 2x upsample (c7, c10).
 #define PAIG_MFMA_FWD(X)                                                                                  \
   X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1) X(16, 8, 16, 3) X(8, 24, 32, 3)       \
@@ -400,19 +440,33 @@ static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_
 #define PAIG_MFMA_WG(X)                                                                                   \
   X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1)
+#define PAIG_MFMA_UP(X) X(32, 16, 16, 3) X(16, 16, 32, 3)
 
 }  // namespace
 
 // Returns 1 if handled (rc in *rc), 0 if the shape has no MFMA instantiation.
+// flags: 1 relu, 2 mask(aux>0), 4 accumulate, 8 dgrad, 32 input = 2x upsample of (H/2 x W/2)
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
                        int H, int W, int ks, int flags, hipStream_t st, int* rc) {
   const bool dg = (flags & 8) != 0;
+  const bool up = (flags & 32) != 0;
   const int fl = flags & 7;
   if (H != W) return 0;
+  if (up) {
+    if (dg) return 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                              \
+    if (Cin == CI && Cout == CO && H == HH && ks == K) {                                      \
+      *rc = fwd_launch<CI, CO, HH, HH, K, false, true>(in, out, aux, w, b, F, fl, st);        \
+      return 1;                                                                               \
+    }
+    PAIG_MFMA_UP(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
 #define PAIG_CASE(CI, CO, HH, K)                                                                      \
   if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                \
-    *rc = dg ? fwd_launch<CI, CO, HH, HH, K, true>(in, out, aux, w, b, F, fl, st)                     \
-             : fwd_launch<CI, CO, HH, HH, K, false>(in, out, aux, w, b, F, fl, st);                   \
+    *rc = dg ? fwd_launch<CI, CO, HH, HH, K, true, false>(in, out, aux, w, b, F, fl, st)              \
+             : fwd_launch<CI, CO, HH, HH, K, false, false>(in, out, aux, w, b, F, fl, st);            \
     return 1;                                                                                         \
   }
   PAIG_MFMA_FWD(PAIG_CASE)
@@ -421,11 +475,21 @@ int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const fl
 }
 
 int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H,
-                         int W, int ks, hipStream_t st, int* rc) {
+                         int W, int ks, int flags, hipStream_t st, int* rc) {
   if (H != W) return 0;
+  if (flags & 32) {
+#define PAIG_CASE(CI, CO, HH, K)                                                                 \
+    if (Cin == CI && Cout == CO && H == HH && ks == K) {                                         \
+      *rc = wgrad_launch<CI, CO, HH, HH, K, true>(x, dy, slab, nblk_max, nblk_out, F, st);       \
+      return 1;                                                                                  \
+    }
+    PAIG_MFMA_UP(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
 #define PAIG_CASE(CI, CO, HH, K)                                                         \
   if (Cin == CI && Cout == CO && H == HH && ks == K) {                                   \
-    *rc = wgrad_launch<CI, CO, HH, HH, K>(x, dy, slab, nblk_max, nblk_out, F, st);       \
+    *rc = wgrad_launch<CI, CO, HH, HH, K, false>(x, dy, slab, nblk_max, nblk_out, F, st); \
     return 1;                                                                            \
   }
   PAIG_MFMA_WG(PAIG_CASE)

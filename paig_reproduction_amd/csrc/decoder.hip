@@ -81,6 +81,21 @@ __device__ __forceinline__ void sample(const float* s, int h, const Bil& b, floa
   dy = (sw - nw) * ex + (se - ne) * b.fx;
 }
 
+// Per-frame sampling coordinate tables: cx[k][j] = ix of output column j,
+// cy[k][i] = iy of output row i (the warp is separable).  fp64 grid math once
+// per (frame, object, row/col) instead of per pixel.  Caller syncs.
+constexpr int MAXH = 64;
+template <int K>
+__device__ __forceinline__ void coord_tables(const float* pf, int H, int h, float (*cx)[MAXH], float (*cy)[MAXH]) {
+  for (int t = threadIdx.x; t < K * 2 * H; t += blockDim.x) {
+    const int k = t / (2 * H), r = t % (2 * H);
+    const float l = r < H ? pf[2 * k] : pf[2 * k + 1];
+    const double tt = (double)(((float)H / 2.f - l) / (float)h);
+    if (r < H) cx[k][r] = src_coord(r, H, tt, h);
+    else cy[k][r - H] = src_coord(r - H, H, tt, h);
+  }
+}
+
 template <int K>
 __device__ __forceinline__ void stage_sources(const Src& S, int h, float* T, float* Cn) {
   const int hh = h * h;
@@ -133,17 +148,13 @@ dec_fwd_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse, in
   float* T = lds;
   float* Cn = T + K * hh;
   __shared__ float red[4];
+  __shared__ float cx[K][MAXH], cy[K][MAXH];
   stage_sources<K>(S, h, T, Cn);
-  __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int f = blockIdx.x; f < F; f += gridDim.x) {
-    const float* pf = pos.at(f);
-    double tx[K], ty[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      tx[k] = (double)(((float)H / 2.f - pf[2 * k]) / (float)h);
-      ty[k] = (double)(((float)H / 2.f - pf[2 * k + 1]) / (float)h);
-    }
+    __syncthreads();   // previous frame done with the tables
+    coord_tables<K>(pos.at(f), H, h, cx, cy);
+    __syncthreads();
     float* of = out.frame(f);
     const float* tf = sse ? tgt.frame(f) : nullptr;
     float acc = 0.f;
@@ -151,7 +162,7 @@ dec_fwd_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse, in
       const int i = p / H, j = p % H;
       Bil bl[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) bl[k] = bil(src_coord(j, H, tx[k], h), src_coord(i, H, ty[k], h));
+      for (int k = 0; k < K; ++k) bl[k] = bil(cx[k][j], cy[k][i]);
       float o[3], m[K + 1], cs[K][3];
       composite<K>(T, Cn, S.bg, HW, p, h, bl, o, m, cs);
 #pragma unroll
@@ -189,6 +200,7 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
   float* G = gscratch ? gscratch + (long long)blockIdx.x * K * 4 * HW : Cn + K * 3 * hh;  // [K][4][HW]
   __shared__ double redd[4][2 * K];
   __shared__ int skip_s;
+  __shared__ float cx[K][MAXH], cy[K][MAXH];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nw = blockDim.x >> 6;
   const long long slab_len = (long long)K * hh + (long long)K * 3 * hh + 3LL * HW;
@@ -218,13 +230,8 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
       __syncthreads();
       continue;
     }
-    const float* pf = pos.at(f);
-    double tx[K], ty[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      tx[k] = (double)(((float)H / 2.f - pf[2 * k]) / (float)h);
-      ty[k] = (double)(((float)H / 2.f - pf[2 * k + 1]) / (float)h);
-    }
+    coord_tables<K>(pos.at(f), H, h, cx, cy);
+    __syncthreads();
     const float* tf = tgt.frame(f);
     double sx[K], sy[K];
 #pragma unroll
@@ -235,7 +242,7 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
       const int i = p / H, j = p % H;
       Bil bl[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) bl[k] = bil(src_coord(j, H, tx[k], h), src_coord(i, H, ty[k], h));
+      for (int k = 0; k < K; ++k) bl[k] = bil(cx[k][j], cy[k][i]);
       float o[3], m[K + 1], cs[K][3];
       composite<K>(T, Cn, S.bg, HW, p, h, bl, o, m, cs);
       float g[3];
@@ -291,7 +298,7 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
     for (int s = threadIdx.x; s < K * hh; s += blockDim.x) {
       const int k = s / hh, q = s % hh, ys = q / h, xs = q % h;
       // output index j has ix(j) ~= a + j*h/H; candidates with floor(ix) in {xs-1, xs}
-      const float a0x = src_coord(0, H, tx[k], h), a0y = src_coord(0, H, ty[k], h);
+      const float a0x = cx[k][0], a0y = cy[k][0];
       const float slope = (float)h / (float)H;
       int jlo = (int)floorf(((float)xs - 1.f - a0x) / slope) - 1, jhi = (int)ceilf(((float)xs + 1.f - a0x) / slope) + 1;
       int ilo = (int)floorf(((float)ys - 1.f - a0y) / slope) - 1, ihi = (int)ceilf(((float)ys + 1.f - a0y) / slope) + 1;
@@ -301,7 +308,7 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
       if (ihi > H - 1) ihi = H - 1;
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
       for (int i = ilo; i <= ihi; ++i) {
-        const float iy = src_coord(i, H, ty[k], h);
+        const float iy = cy[k][i];
         const float fy0 = floorf(iy);
         const int y0 = (int)fy0;
         const float fy = iy - fy0;
@@ -309,7 +316,7 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
         if (wy == 0.f) continue;
         float row[4] = {0.f, 0.f, 0.f, 0.f};
         for (int j = jlo; j <= jhi; ++j) {
-          const float ix = src_coord(j, H, tx[k], h);
+          const float ix = cx[k][j];
           const float fx0 = floorf(ix);
           const int x0 = (int)fx0;
           const float fx = ix - fx0;
@@ -344,8 +351,8 @@ extern "C" {
 
 // Decoder grid size used by paig_decoder_bwd (the slab has that many rows).
 int paig_decoder_bwd_blocks(int F) {
-  int g = (F + 3) / 4;
-  if (g > 1024) g = 1024;
+  int g = (F + 1) / 2;
+  if (g > 768) g = 768;   // ~3 blocks per CU: latency hiding for the per-frame passes
   if (g < 1) g = 1;
   return g;
 }

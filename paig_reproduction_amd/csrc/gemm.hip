@@ -3,24 +3,31 @@
 //
 // Used for every dense layer of the path: the encoder's projection to latent
 // coordinates (nn/network/blocks.py:71-75,98-100; K = 3072 -> 200, the one
-// MFMA-shaped op the north star names), its MLP tail, the velocity MLP
-// (blocks.py:23-29) and VariableFromNetwork (blocks.py:311-322), forward and
-// backward (dX = dY W, dW = dY^T X).
+// MFMA-shaped op the north star names), its MLP tail and the velocity MLP
+// (blocks.py:23-29), forward and backward (dX = dY W, dW = dY^T X, and the
+// bias gradient db = colsum(dY) fused into the dW GEMM as row sums of op(A)).
 //
 //   C[M,N] = alpha * op(A)[M,K] op(B)[K,N]  (+ beta*C) (+ bias[n]) -> act -> *aux'
 //   op(A)[m][k] = TA ? A[k*lda+m] : A[m*lda+k]
 //   op(B)[k][n] = TB ? B[n*ldb+k] : B[k*ldb+n]
+//   rowsum[m] = sum_k op(A)[m][k]            (optional)
 //
-// Tile 64x64x16, 256 threads = 4 waves in 2x2, each wave 32x32 = 2x2 MFMA
-// tiles. LDS holds A as [k][m] and B as [k][n] with a 16-float pad so the
-// fragment reads (lanes 0-15 one k-row, lanes 16-31 the next) are
-// bank-conflict free. Optional split-K writes fp32 partial slabs reduced by
-// gemm_splitk_epilogue_k (deterministic).
+// Tile 64x64x32, 256 threads = 4 waves in 2x2, each wave 32x32 = 2x2 MFMA
+// tiles.  Global loads are float4 along each operand's contiguous dimension;
+// the LDS image keeps that orientation ([row][k] with pitch 34 = 2 mod 32, or
+// [k][row] with pitch 80 = 16 mod 32) so the 16B loads land with wide LDS
+// writes AND every MFMA fragment read is bank-conflict free.  The next K
+// tile is prefetched into registers while the current one is multiplied.
+// Split-K writes fp32 partial slabs reduced by gemm_splitk_epilogue_k
+// (deterministic).
 #include "common.h"
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 16, LDP = 64 + 16;
+constexpr int BM = 64, BN = 64, BK = 32;
+constexpr int LDRK = BK + 2;    // [row][k] image pitch
+constexpr int LDKR = 64 + 16;   // [k][row] image pitch
+constexpr int IMG = (BK * LDKR > 64 * LDRK ? BK * LDKR : 64 * LDRK);
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_SIGMOID = 3 };
 enum { AUX_NONE = 0, AUX_RELU = 1, AUX_TANH = 2 };
@@ -36,14 +43,69 @@ __device__ __forceinline__ float epi(float v, int act, int auxm, const float* au
   return v;
 }
 
+// One operand tile (64 rows x BK k) as 2 float4 per thread.
+//  KCONTIG: element (r, k) at p[(r0 + r) * ld + k0 + k]   -> image [r][k]
+// !KCONTIG: element (r, k) at p[(k0 + k) * ld + r0 + r]   -> image [k][r]
+template <bool KCONTIG>
+struct Tile {
+  f32x4 v[2];
+  __device__ __forceinline__ void load(const float* __restrict__ p, long long ld, int r0, int k0, int R, int K,
+                                       bool vec, int tid) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      int r, k;
+      if (KCONTIG) { r = (tid >> 3) + 32 * e; k = (tid & 7) * 4; }
+      else { k = (tid >> 4) + 16 * e; r = (tid & 15) * 4; }
+      const int gr = r0 + r, gk = k0 + k;
+      f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (KCONTIG) {
+        if (gr < R) {
+          const float* q = p + (long long)gr * ld + gk;
+          if (vec && gk + 3 < K) x = *reinterpret_cast<const f32x4*>(q);
+          else
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = (gk + i < K) ? q[i] : 0.f;
+        }
+      } else {
+        if (gk < K) {
+          const float* q = p + (long long)gk * ld + gr;
+          if (vec && gr + 3 < R) x = *reinterpret_cast<const f32x4*>(q);
+          else
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = (gr + i < R) ? q[i] : 0.f;
+        }
+      }
+      v[e] = x;
+    }
+  }
+  __device__ __forceinline__ void store(float* img, int tid) const {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      if (KCONTIG) {
+        const int r = (tid >> 3) + 32 * e, k = (tid & 7) * 4;
+        float* q = img + r * LDRK + k;
+        *reinterpret_cast<float2*>(q) = make_float2(v[e][0], v[e][1]);
+        *reinterpret_cast<float2*>(q + 2) = make_float2(v[e][2], v[e][3]);
+      } else {
+        const int k = (tid >> 4) + 16 * e, r = (tid & 15) * 4;
+        *reinterpret_cast<f32x4*>(img + k * LDKR + r) = v[e];
+      }
+    }
+  }
+  // fragment element (row, k) of the image
+  static __device__ __forceinline__ float at(const float* img, int r, int k) {
+    return KCONTIG ? img[r * LDRK + k] : img[k * LDKR + r];
+  }
+};
+
 template <bool TA, bool TB>
 __global__ void __launch_bounds__(256)
-gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda,
-       const float* __restrict__ B, long long ldb, float* __restrict__ C, long long ldc, float beta,
+gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
+       const float* __restrict__ B, long long ldb, int vecb, float* __restrict__ C, long long ldc, float beta,
        const float* __restrict__ bias, int act, int auxm, const float* __restrict__ aux, long long ldaux,
-       float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float As[BK][LDP];
-  __shared__ __attribute__((aligned(16))) float Bs[BK][LDP];
+       float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart) {
+  __shared__ __attribute__((aligned(16))) float As[IMG];
+  __shared__ __attribute__((aligned(16))) float Bs[IMG];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
@@ -51,53 +113,51 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
   const int kbeg = blockIdx.z * kchunk;
   int kend = kbeg + kchunk;
   if (kend > K) kend = K;
+  const bool do_rs = rowsum != nullptr && blockIdx.x == 0;
 
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rs = 0.f;
 
+  Tile<!TA> ta;  // A is k-contiguous unless transposed
+  Tile<TB> tb;   // B is k-contiguous when transposed
+  if (kbeg < kend) {
+    ta.load(A, lda, m0, kbeg, M, kend, veca, tid);
+    tb.load(B, ldb, n0, kbeg, N, kend, vecb, tid);
+  }
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    // ---- stage A (BM x BK) into As[k][m]
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid * 4 + e;  // 0..1023
-      int mm, kk;
-      if (TA) { kk = idx >> 6; mm = idx & 63; }   // m contiguous in memory
-      else { mm = idx >> 4; kk = idx & 15; }      // k contiguous in memory
-      const int gm = m0 + mm, gk = k0 + kk;
-      float v = 0.f;
-      if (gm < M && gk < kend) v = TA ? A[(long long)gk * lda + gm] : A[(long long)gm * lda + gk];
-      As[kk][mm] = v;
-    }
-    // ---- stage B (BK x BN) into Bs[k][n]
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid * 4 + e;
-      int nn, kk;
-      if (TB) { nn = idx >> 4; kk = idx & 15; }   // k contiguous
-      else { kk = idx >> 6; nn = idx & 63; }      // n contiguous
-      const int gn = n0 + nn, gk = k0 + kk;
-      float v = 0.f;
-      if (gn < N && gk < kend) v = TB ? B[(long long)gn * ldb + gk] : B[(long long)gk * ldb + gn];
-      Bs[kk][nn] = v;
-    }
     __syncthreads();
+    ta.store(As, tid);
+    tb.store(Bs, tid);
+    __syncthreads();
+    if (k0 + BK < kend) {   // prefetch the next K tile into registers
+      ta.load(A, lda, m0, k0 + BK, M, kend, veca, tid);
+      tb.load(B, ldb, n0, k0 + BK, N, kend, vecb, tid);
+    }
+    if (do_rs && tid < BM) {
+#pragma unroll 8
+      for (int k = 0; k < BK; ++k) rs += Tile<!TA>::at(As, tid, k);
+    }
 #pragma unroll
     for (int ks = 0; ks < BK; ks += 4) {
       const int kr = ks + (lane >> 4);
       float a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = As[kr][wm * 32 + i * 16 + (lane & 15)];
+      for (int i = 0; i < 2; ++i) a[i] = Tile<!TA>::at(As, wm * 32 + i * 16 + (lane & 15), kr);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = Bs[kr][wn * 32 + j * 16 + (lane & 15)];
+      for (int j = 0; j < 2; ++j) b[j] = Tile<TB>::at(Bs, wn * 32 + j * 16 + (lane & 15), kr);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
+  }
+  if (do_rs && tid < BM && m0 + tid < M) {
+    if (rowpart) rowpart[(long long)blockIdx.z * M + m0 + tid] = alpha * rs;
+    else rowsum[m0 + tid] = alpha * rs;
   }
 
   // C/D layout: row = (lane>>4)*4 + r, col = lane & 15
@@ -124,9 +184,18 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
 
 __global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restrict__ part, float* __restrict__ C,
                                        long long ldc, float beta, const float* __restrict__ bias, int act, int auxm,
-                                       const float* __restrict__ aux, long long ldaux) {
+                                       const float* __restrict__ aux, long long ldaux, const float* __restrict__ rowpart,
+                                       float* __restrict__ rowsum) {
   const long long n_el = (long long)M * N;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n_el; i += (long long)gridDim.x * blockDim.x) {
+  const long long tot = n_el + (rowsum ? M : 0);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < tot; i += (long long)gridDim.x * blockDim.x) {
+    if (i >= n_el) {
+      const int m = (int)(i - n_el);
+      float v = 0.f;
+      for (int s = 0; s < S; ++s) v += rowpart[(long long)s * M + m];
+      rowsum[m] = v;
+      continue;
+    }
     const int m = (int)(i / N), n = (int)(i % N);
     float v = 0.f;
     for (int s = 0; s < S; ++s) v += part[(long long)s * n_el + i];
@@ -143,29 +212,35 @@ static int choose_split(int M, int N, int K) {
   return s;
 }
 
+static inline bool vec_ok(const float* p, long long ld) {
+  return ((uintptr_t)p % 16 == 0) && (ld % 4 == 0);
+}
+
 }  // namespace
 
 extern "C" {
 
 size_t paig_gemm_workspace(int M, int N, int K) {
   int s = choose_split(M, N, K);
-  return s > 1 ? (size_t)s * M * N : 0;
+  return s > 1 ? (size_t)s * M * N + (size_t)s * M : 0;
 }
 
 int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
               long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
-              const float* aux, long long ldaux, float* ws, size_t ws_floats, void* stream) {
+              const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M <= 0 || N <= 0) return 0;
   int S = K > 0 ? choose_split(M, N, K) : 1;
-  if (S > 1 && (ws == nullptr || ws_floats < (size_t)S * M * N)) S = 1;
+  if (S > 1 && (ws == nullptr || ws_floats < (size_t)S * M * N + (size_t)S * M)) S = 1;
   const int kchunk = S > 1 ? cdiv(cdiv(K, S), BK) * BK : (K > 0 ? K : 1);
   S = K > 0 ? cdiv(K, kchunk) : 1;
   dim3 grid(cdiv(N, BN), cdiv(M, BM), S);
   float* part = S > 1 ? ws : nullptr;
-#define PAIG_G(TA_, TB_)                                                                                       \
-  hipLaunchKernelGGL((gemm_k<TA_, TB_>), grid, dim3(256), 0, st, M, N, K, kchunk, alpha, A, lda, B, ldb, C, ldc, \
-                     beta, bias, act, auxm, aux, ldaux, part)
+  float* rowpart = (S > 1 && rowsum) ? ws + (size_t)S * M * N : nullptr;
+  const int va = vec_ok(A, lda), vb = vec_ok(B, ldb);
+#define PAIG_G(TA_, TB_)                                                                                          \
+  hipLaunchKernelGGL((gemm_k<TA_, TB_>), grid, dim3(256), 0, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, \
+                     ldc, beta, bias, act, auxm, aux, ldaux, part, rowsum, rowpart)
   if (ta && tb) PAIG_G(true, true);
   else if (ta) PAIG_G(true, false);
   else if (tb) PAIG_G(false, true);
@@ -173,11 +248,11 @@ int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, 
 #undef PAIG_G
   PAIG_CHECK_LAUNCH();
   if (S > 1) {
-    long long n_el = (long long)M * N;
+    long long n_el = (long long)M * N + (rowsum ? M : 0);
     int g = cdiv(n_el, 256);
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(gemm_splitk_epilogue_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, ldc, beta, bias, act, auxm,
-                       aux, ldaux);
+                       aux, ldaux, rowpart, rowsum);
     PAIG_CHECK_LAUNCH();
   }
   return 0;

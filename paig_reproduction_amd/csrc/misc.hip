@@ -83,16 +83,18 @@ vfn_bwd1_k(const float* __restrict__ d, const float* __restrict__ y, int sig, co
   if (j < VH) part[blockIdx.x * VH + j] = acc;
 }
 
+// one 64-lane block per hidden unit j: dh[j] = sum of the partials, then the
+// tanh' and the first layer's grads (input = ones)
 __global__ void vfn_bwd2_k(const float* __restrict__ part, int nblk, const float* __restrict__ h,
                            float* __restrict__ dW1, float* __restrict__ db1) {
-  const int j = threadIdx.x;
-  if (j >= VH) return;
+  const int j = blockIdx.x;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[b * VH + j];
+  for (int b = threadIdx.x; b < nblk; b += 64) s += part[b * VH + j];
+  s = wave_sum(s);
   const float hj = h[j];
   const float g = s * (1.f - hj * hj);
-  for (int i = 0; i < VIN; ++i) dW1[j * VIN + i] = g;
-  db1[j] = g;
+  if (threadIdx.x < VIN) dW1[j * VIN + threadIdx.x] = g;
+  if (threadIdx.x == 0) db1[j] = g;
 }
 
 // losses: pred, extrap, recons (means of per-frame SSE)
@@ -235,17 +237,17 @@ int paig_vfn_fwd(const float* W1, const float* b1, const float* W2, const float*
   return 0;
 }
 
-int paig_vfn_bwd_blocks(int P) { return cdiv(P, 64); }
+int paig_vfn_bwd_blocks(int P) { return cdiv(P, 8); }
 
 // d: adjoint of y (sig = 0) or of sigmoid(y) (sig = 1). part: >= blocks*200 floats.
 int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,
                  float* dW2, float* db2, float* part, int P, void* stream) {
-  const int rows = 64;
+  const int rows = 8;
   const int nblk = cdiv(P, rows);
   hipLaunchKernelGGL(vfn_bwd1_k, dim3(nblk), dim3(256), 0, (hipStream_t)stream, d, y, sig, h, W2, dW2, db2, part, P,
                      rows);
   PAIG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(vfn_bwd2_k, dim3(1), dim3(256), 0, (hipStream_t)stream, part, nblk, h, dW1, db1);
+  hipLaunchKernelGGL(vfn_bwd2_k, dim3(VH), dim3(64), 0, (hipStream_t)stream, part, nblk, h, dW1, db1);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

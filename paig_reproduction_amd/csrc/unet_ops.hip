@@ -114,29 +114,31 @@ __global__ void upsample_bwd_k(FView du, FView s, FViewW ds, int F, int C, int H
     int c = t % C;
     int f = (int)(t / C);
     const float* dup = du.frame(f) + (long long)c * Ho * Wo;
-    const int ry = Ho / Hs, rx = Wo / Ws;
-    int ylo = sy * ry - ry, yhi = sy * ry + 2 * ry - 1;
-    int xlo = sx * rx - rx, xhi = sx * rx + 2 * rx - 1;
-    if (ylo < 0) ylo = 0;
-    if (xlo < 0) xlo = 0;
-    if (yhi > Ho - 1) yhi = Ho - 1;
-    if (xhi > Wo - 1) xhi = Wo - 1;
+    // exact 2x: source s receives from outputs 2s-1 .. 2s+2 with weights
+    // 1/4, 3/4, 3/4, 1/4 (the clamped edges give 1 to s = 0 from 0 and to
+    // s = n-1 from 2n-1) -- the same, exactly representable taps as up_taps
+    float wy[4], wx[4];
+    wy[0] = sy >= 1 ? 0.25f : 0.f;
+    wy[1] = sy == 0 ? 1.f : 0.75f;
+    wy[2] = sy == Hs - 1 ? 1.f : 0.75f;
+    wy[3] = sy <= Hs - 2 ? 0.25f : 0.f;
+    wx[0] = sx >= 1 ? 0.25f : 0.f;
+    wx[1] = sx == 0 ? 1.f : 0.75f;
+    wx[2] = sx == Ws - 1 ? 1.f : 0.75f;
+    wx[3] = sx <= Ws - 2 ? 0.25f : 0.f;
     float acc = 0.f;
-    for (int y = ylo; y <= yhi; ++y) {
-      int y0, y1;
-      float wy0, wy1;
-      up_taps(y, Hs, Ho, y0, y1, wy0, wy1);
-      float wy = (y0 == sy ? wy0 : 0.f) + (y1 == sy ? wy1 : 0.f);
-      if (wy == 0.f) continue;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int y = 2 * sy - 1 + a;
+      if (wy[a] == 0.f) continue;
+      const float* rp = dup + y * Wo;
       float row = 0.f;
-      for (int x = xlo; x <= xhi; ++x) {
-        int x0, x1;
-        float wx0, wx1;
-        up_taps(x, Ws, Wo, x0, x1, wx0, wx1);
-        float wx = (x0 == sx ? wx0 : 0.f) + (x1 == sx ? wx1 : 0.f);
-        if (wx != 0.f) row = fmaf(wx, dup[y * Wo + x], row);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int x = 2 * sx - 1 + b;
+        if (wx[b] != 0.f) row = fmaf(wx[b], rp[x], row);
       }
-      acc = fmaf(wy, row, acc);
+      acc = fmaf(wy[a], row, acc);
     }
     if (relu_mask) acc = s.frame(f)[((long long)c * Hs + sy) * Ws + sx] > 0.f ? acc : 0.f;
     ds.frame(f)[((long long)c * Hs + sy) * Ws + sx] = acc;
@@ -303,27 +305,34 @@ struct SlabTasks {
   int accumulate;
 };
 
-__global__ void __launch_bounds__(256) slab_reduce_multi_k(SlabTasks T) {
-  __shared__ float red[4][64];
+// 16 waves per block: each lane owns one column, the waves stride the rows
+// (4 independent accumulators each), then a fixed-order combine.
+__global__ void __launch_bounds__(1024) slab_reduce_multi_k(SlabTasks T) {
+  constexpr int NW = 16;
+  __shared__ float red[NW][64];
   int t = 0;
   while (t + 1 < T.ntask && (int)blockIdx.x >= T.start[t + 1]) ++t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int len = T.len[t], nblk = T.nblk[t];
   const int i = (blockIdx.x - T.start[t]) * 64 + lane;
   const float* src = T.src[t];
-  float s0 = 0.f, s1 = 0.f;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (i < len) {
     int b = wv;
-    for (; b + 4 < nblk; b += 8) {
+    for (; b + 3 * NW < nblk; b += 4 * NW) {
       s0 += src[(long long)b * len + i];
-      s1 += src[(long long)(b + 4) * len + i];
+      s1 += src[(long long)(b + NW) * len + i];
+      s2 += src[(long long)(b + 2 * NW) * len + i];
+      s3 += src[(long long)(b + 3 * NW) * len + i];
     }
-    for (; b < nblk; b += 4) s0 += src[(long long)b * len + i];
+    for (; b < nblk; b += NW) s0 += src[(long long)b * len + i];
   }
-  red[wv][lane] = s0 + s1;
+  red[wv][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (wv == 0 && i < len) {
-    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][lane];
     T.dst[t][i] = T.accumulate ? T.dst[t][i] + v : v;
   }
 }
@@ -394,7 +403,7 @@ int paig_upsample2_fwd(const float* s, long long s_fs, float* u, long long u_fs,
 int paig_upsample2_bwd(const float* du, long long du_fs, const float* s, long long s_fs, float* ds, long long ds_fs,
                        int F, int C, int Hs, int Ws, int Ho, int Wo, int relu_mask, void* stream) {
   if (F <= 0) return 0;
-  PAIG_REQUIRE(Ho >= Hs && Wo >= Ws && Ho % Hs == 0 && Wo % Ws == 0, "upsample_bwd: integer upscale only");
+  PAIG_REQUIRE(Ho == 2 * Hs && Wo == 2 * Ws, "upsample_bwd: exact 2x upscale only (Resize(H/2 -> H))");
   long long n = (long long)F * C * Hs * Ws;
   hipLaunchKernelGGL(upsample_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{du, du_fs, 0, 0},
                      FView{s, s_fs, 0, 0}, FViewW{ds, ds_fs}, F, C, Hs, Ws, Ho, Wo, relu_mask);
@@ -468,7 +477,7 @@ int paig_slab_reduce_multi(int ntask, const float* const* src, const int* nblk, 
   T.start[ntask] = blocks;
   T.ntask = ntask;
   T.accumulate = accumulate;
-  hipLaunchKernelGGL(slab_reduce_multi_k, dim3(blocks), dim3(256), 0, (hipStream_t)stream, T);
+  hipLaunchKernelGGL(slab_reduce_multi_k, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, T);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

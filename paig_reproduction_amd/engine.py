@@ -143,6 +143,21 @@ class Layout:
         self.bufs, self.ops = shallow_unet_plan(8, self.K)
         self.prefix = "encoder.shallow_unet."
         self.fin = backward_plan(self.ops)
+        # upsamples consumed by exactly one conv (c7, c10) are fused into that
+        # conv's input staging (fwd and wgrad); only the gradient buffer of the
+        # upsampled tensor remains (dgrad output -> upsample backward)
+        self.fused_up, self.fused_bufs = {}, set()
+        for i, op in enumerate(self.ops):
+            if op["op"] != "up":
+                continue
+            consumers = [j for j, o in enumerate(self.ops) if o["src"][0] == op["dst"][0]]
+            if len(consumers) != 1 or self.ops[consumers[0]]["op"] != "conv":
+                continue
+            c = self.ops[consumers[0]]
+            lvl = self.bufs[op["dst"][0]][1]
+            if (c["src"][2], c["dst"][2], self.H // lvl) in {(32, 16, 16), (16, 16, 32)}:
+                self.fused_up[consumers[0]] = op
+                self.fused_bufs.add(op["dst"][0])
         self.HW = self.H * self.H
         self.frame = 3 * self.HW
 
@@ -223,21 +238,23 @@ class Engine:
         """out[rows, O] = act(x[rows, I] W^T + b) ; W = name.weight [O, I]"""
         W, b = self.p(name + ".weight"), self.p(name + ".bias")
         O, I = W.shape
-        self.L.paig_gemm(0, 1, rows, O, I, 1.0, ptr(x), I, ptr(W), I, 0.0, ptr(out), O, ptr(b), act, 0, None, 0,
-                         ptr(ws), ws.numel() if ws is not None else 0, st)
+        with self._p("gemm_fwd:" + name, 2 * rows * O * I):
+            self.L.paig_gemm(0, 1, rows, O, I, 1.0, ptr(x), I, ptr(W), I, 0.0, ptr(out), O, ptr(b), act, 0, None, 0,
+                             None, ptr(ws), ws.numel() if ws is not None else 0, st)
 
     def linear_bwd(self, x, dy, rows, name, dx, aux, auxm, st, ws, need_dx=True):
-        """dW = dy^T x ; db = colsum(dy) ; dx = (dy W) * act'(aux)"""
+        """dW = dy^T x and db = colsum(dy) (one GEMM, fused row sums) ; dx = (dy W) * act'(aux)"""
         W = self.p(name + ".weight")
         O, I = W.shape
         gW, gb = self.g(name + ".weight"), self.g(name + ".bias")
         n_ws = ws.numel()
-        self.L.paig_gemm(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
-                         ptr(ws), n_ws, st)
-        self.L.paig_colsum(ptr(dy), rows, O, O, ptr(gb), 0, ptr(ws), st)
+        with self._p("gemm_wgrad:" + name, 2 * rows * O * I):
+            self.L.paig_gemm(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
+                             ptr(gb), ptr(ws), n_ws, st)
         if need_dx:
-            self.L.paig_gemm(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm, ptr(aux),
-                             I, ptr(ws), n_ws, st)
+            with self._p("gemm_dgrad:" + name, 2 * rows * O * I):
+                self.L.paig_gemm(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm,
+                                 ptr(aux), I, None, ptr(ws), n_ws, st)
 
     def workspace_floats(self, lay):
         K, F, B = lay.K, lay.F, lay.B
@@ -279,7 +296,7 @@ class Engine:
         x_view = (ptr(x), T * lay.frame, lay.Te, lay.frame)   # frame n = b*Te + t, in place
         acts = {}
         for name, (C, lvl) in lay.bufs.items():
-            if name != "X0":
+            if name != "X0" and name not in lay.fused_bufs:
                 acts[name] = _empty(F * C * (H // lvl) * (H // lvl), dev)
         S["acts"] = acts
 
@@ -292,22 +309,37 @@ class Engine:
             t = acts[buf]
             return (t.data_ptr() + off * hw * 4, C * hw, 0, 0), lvl
 
+        def conv_input(i, op):
+            """(view, level of the conv, extra flags): a fused upsample reads its
+            half-resolution source and forms the 2x bilinear rows while staging."""
+            up = lay.fused_up.get(i)
+            if up is None:
+                v, lvl = view(op["src"])
+                return v, lvl, 0
+            v, lvl = view(up["src"])
+            return v, lvl // 2, 32
+
         S["view"] = view
-        for op in lay.ops:
-            sv, slvl = view(op["src"])
+        S["conv_input"] = conv_input
+        for i, op in enumerate(lay.ops):
+            if op["op"] == "up" and op["dst"][0] in lay.fused_bufs:
+                continue   # formed inside the consuming conv's staging
             dv, dlvl = view(op["dst"])
             if op["op"] == "conv":
-                Hl = H // slvl
+                sv, clvl, xfl = conv_input(i, op)
+                Hl = H // clvl
                 W_ = self.p(lay.prefix + op["name"] + ".weight")
                 b_ = self.p(lay.prefix + op["name"] + ".bias")
                 fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
                 with self._p("conv_fwd:" + op["name"], fl):
                     L.paig_conv2d_fwd(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
-                                      op["src"][2], op["dst"][2], Hl, Hl, op["ks"], 1 if op["relu"] else 0, st)
+                                      op["src"][2], op["dst"][2], Hl, Hl, op["ks"], (1 if op["relu"] else 0) | xfl, st)
             elif op["op"] == "pool":
+                sv, slvl = view(op["src"])
                 Hl = H // slvl
                 L.paig_maxpool2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hl, Hl, st)
             else:
+                sv, slvl = view(op["src"])
                 Hs, Ho = H // slvl, H // dlvl
                 L.paig_upsample2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hs, Hs, Ho, Ho, st)
 
@@ -426,7 +458,8 @@ class Engine:
                            *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
                            ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, K, h, H, st)
         dsrc = _empty(slab_len, dev)
-        L.paig_slab_reduce(ptr(slab), nb_rec + nb_roll, slab_len, slab_len, ptr(dsrc), 0, st)
+        L.paig_slab_reduce_multi(1, (ctypes.c_void_p * 1)(ptr(slab)), (ctypes.c_int * 1)(nb_rec + nb_roll),
+                                 (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, st)
         if d_enc_pos is not None:
             L.paig_axpby(ptr(d_enc_pos.contiguous()), ptr(denc), F * D, 1.0, 1.0, st)
 
@@ -526,19 +559,19 @@ class Engine:
             fin = lay.fin[i]
             relu_fin = [r for r, relu in fin if relu]
             src, dst = op["src"], op["dst"]
-            sv, slvl = view(src)
             dyv, dlvl = dview(dst)
             if op["op"] == "conv":
+                sv, slvl, xfl = S["conv_input"](i, op)
                 Hl = H // slvl
                 cin, cout, ks = src[2], dst[2], op["ks"]
                 # weight + bias gradient: per-block partials, then one reduction
-                nblk_max = 256
+                nblk_max = 768
                 slab = _empty(nblk_max * (cout * cin * ks * ks + cout), dev)
                 nb = ctypes.c_int(0)
                 fl = 2 * F * cin * cout * ks * ks * Hl * Hl
                 with self._p("conv_wgrad:" + op["name"], fl):
                     L.paig_conv2d_wgrad(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], ptr(slab), nblk_max,
-                                        ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, st)
+                                        ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, xfl, st)
                 gw = self.g(lay.prefix + op["name"] + ".weight")
                 gb = self.g(lay.prefix + op["name"] + ".bias")
                 n_w = cout * cin * ks * ks
@@ -561,6 +594,7 @@ class Engine:
                                       cout, cin, Hl, Hl, ks, flags, st)
                 mark(src)
             elif op["op"] == "pool":
+                sv, slvl = view(src)
                 Hl = H // slvl
                 dxv, _ = dview(src)
                 # the pool kernel accumulates into the concat partner's gradient
@@ -570,6 +604,7 @@ class Engine:
                 L.paig_maxpool2_bwd_relu(sv[0], sv[1], dyv[0], dyv[1], dxv[0], dxv[1], F, src[2], Hl, Hl, st)
                 mark(src)
             else:
+                sv, slvl = view(src)
                 Hs, Ho = H // slvl, H // dlvl
                 dxv, _ = dview(src)
                 assert state(src) == "write"

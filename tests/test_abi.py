@@ -51,7 +51,7 @@ def test_library_loads_and_exports_every_symbol():
     # size queries are host-only and safe without a GPU
     assert L.paig_decoder_slab_len(2, 16, 32) == 2 * 16 * 16 * 4 + 3 * 32 * 32
     assert L.paig_decoder_bwd_blocks(1600) >= 1
-    assert L.paig_vfn_bwd_blocks(3072) == 48
+    assert L.paig_vfn_bwd_blocks(3072) == 384
 
 
 def test_product_path_refuses_cpu_tensors():

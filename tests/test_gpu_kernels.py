@@ -66,7 +66,7 @@ def test_conv_fwd_dgrad_wgrad(cin, cout, hw, ks, F_):
     slab = torch.empty(nmax * (cout * cin * ks * ks + cout), device=DEV)
     nb = ctypes.c_int(0)
     L().paig_conv2d_wgrad(p(xg), cin * hw * hw, 0, 0, p(dyg), cout * hw * hw, p(slab), nmax, ctypes.byref(nb), F_, cin,
-                          cout, hw, hw, ks, st())
+                          cout, hw, hw, ks, 0, st())
     g = torch.empty(cout * cin * ks * ks + cout, device=DEV)
     L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
     torch.cuda.synchronize()
@@ -102,10 +102,12 @@ def test_gemm(ta, tb, M, N, K):
     Ag, Bg, biasg = A.to(DEV), Bm.to(DEV), bias.to(DEV)
     C = torch.empty(M, N, device=DEV)
     ws = torch.empty(max(1, L().paig_gemm_workspace(M, N, K)), device=DEV)
+    rs = torch.empty(M, device=DEV)
     L().paig_gemm(ta, tb, M, N, K, 1.0, p(Ag), A.shape[1], p(Bg), Bm.shape[1], 0.0, p(C), N, p(biasg), 2, 0,
-                  None, 0, p(ws), ws.numel(), st())
+                  None, 0, p(rs), p(ws), ws.numel(), st())
     torch.cuda.synchronize()
     assert rel_err(C, ref) <= 2e-5
+    assert rel_err(rs, (A.t() if ta else A).sum(1)) <= 2e-5
 
 
 def test_pool_upsample():
