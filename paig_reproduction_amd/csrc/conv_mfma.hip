@@ -56,16 +56,20 @@ __device__ __forceinline__ f32x4 load_row4(const float* __restrict__ plane, int 
   int y0, y1;
   float wy0, wy1;
   up2_taps(gy, HS, y0, y1, wy0, wy1);
+  // x = 4q..4q+3 read source columns 2q-1 .. 2q+2 (clamped): 4 loads per row;
+  // the horizontal weights are the constants up2_taps yields for 2x
+  const int c0 = q > 0 ? 2 * q - 1 : 0, c3 = 2 * q + 2 < WS ? 2 * q + 2 : WS - 1;
   const float* r0 = plane + y0 * WS;
   const float* r1 = plane + y1 * WS;
+  const float2 m0 = *reinterpret_cast<const float2*>(r0 + 2 * q);
+  const float2 m1 = *reinterpret_cast<const float2*>(r1 + 2 * q);
+  const float a0 = r0[c0], a3 = r0[c3], b0 = r1[c0], b3 = r1[c3];
+  const float w0 = q > 0 ? 0.25f : 0.f, w1 = q > 0 ? 0.75f : 1.f;
   f32x4 v;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    int x0, x1;
-    float wx0, wx1;
-    up2_taps(4 * q + e, WS, x0, x1, wx0, wx1);
-    v[e] = wy0 * (wx0 * r0[x0] + wx1 * r0[x1]) + wy1 * (wx0 * r1[x0] + wx1 * r1[x1]);
-  }
+  v[0] = wy0 * (w0 * a0 + w1 * m0.x) + wy1 * (w0 * b0 + w1 * m1.x);
+  v[1] = wy0 * (0.75f * m0.x + 0.25f * m0.y) + wy1 * (0.75f * m1.x + 0.25f * m1.y);
+  v[2] = wy0 * (0.25f * m0.x + 0.75f * m0.y) + wy1 * (0.25f * m1.x + 0.75f * m1.y);
+  v[3] = wy0 * (0.75f * m0.y + 0.25f * a3) + wy1 * (0.75f * m1.y + 0.25f * b3);
   return v;
 }
 

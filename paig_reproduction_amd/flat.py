@@ -109,14 +109,18 @@ class FlatParams:
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
             return
         ws = dist.get_world_size(group)
-        dist.all_reduce(self.g32, op=dist.ReduceOp.SUM, group=group)
-        if self.n64:
-            dist.all_reduce(self.g64, op=dist.ReduceOp.SUM, group=group)
-        L = lib()
-        st = stream_handle(self.g32.device)
-        L.paig_axpby(ptr(self.g32), ptr(self.g32), self.n32, 1.0 / ws, 0.0, st)
-        if self.n64:
-            self.g64.mul_(1.0 / ws)
+        if dist.get_backend(group) == "nccl":
+            # RCCL over xGMI: one in-place AVG all-reduce per dtype buffer
+            dist.all_reduce(self.g32, op=dist.ReduceOp.AVG, group=group)
+            if self.n64:
+                dist.all_reduce(self.g64, op=dist.ReduceOp.AVG, group=group)
+        else:
+            # gloo (the CPU test harness of the DP path): no AVG op
+            dist.all_reduce(self.g32, op=dist.ReduceOp.SUM, group=group)
+            self.g32.div_(ws)
+            if self.n64:
+                dist.all_reduce(self.g64, op=dist.ReduceOp.SUM, group=group)
+                self.g64.div_(ws)
 
 
 class FlatOptimizer:
