@@ -28,20 +28,40 @@ sys.path.insert(0, REPO)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 (vector == f32 MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
+METRIC = "video-seqs/sec (train step) spring_color B=100 @ 1/2/4/8 MI355X"   # BASELINE.json
+DOMINANT = "conv_wgrad:c11"   # largest kernel in profiles/r01_summary_eager.txt
+
+
+def pmc_traffic(path, tag, cfg):
+    """(bytes per launch of the probed kernel, memory-side bytes per step) from
+    the committed PMC summary of the same workload, or (None, None)."""
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if d.get("config") != cfg:
+        return None, None
+    kern = d.get("probe_kernels", {}).get(tag)
+    per = d["kernels"].get(kern, {}).get("traffic_bytes") if kern else None
+    step = sum(v["traffic_bytes"] * v["launches"] for v in d["kernels"].values()) / d.get("steps_profiled", 1)
+    return per, step
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=100, help="sequences per rank")
     ap.add_argument("--task", default="spring_color")
     ap.add_argument("--seq_len", type=int, default=50, help="4 in / 6 pred / 40 extrap")
     ap.add_argument("--ae", type=float, default=3.0)
     ap.add_argument("--lr", type=float, default=6e-4)
     ap.add_argument("--nbatches", type=int, default=4, help="distinct resident batches cycled through")
-    ap.add_argument("--probe", default="auto", help="kernel tag timed with HIP events for the roofline")
+    ap.add_argument("--probe", default="auto", help="kernel tag timed with HIP events for the roofline "
+                    "(auto: the dominant kernel of the committed rocprof profile)")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"),
+                    help="committed rocprofv3 FETCH_SIZE/WRITE_SIZE summary (tools/pmc_traffic.py)")
     ap.add_argument("--graph", type=int, default=1, help="capture fwd+loss+bwd in a HIP graph per resident batch")
     ap.add_argument("--probe_steps", type=int, default=5, help="eager steps timing the probed kernel")
     ap.add_argument("--cpu_baseline", type=int, default=1)
@@ -108,7 +128,7 @@ def main():
     data = [torch.from_numpy(as_model_input(render_sequences(a.task, a.batch, a.seq_len, seed=1000 * rank + i)))
             .to(dev) for i in range(a.nbatches)]
 
-    probe = E.KernelProbe(a.probe if a.probe != "auto" else "conv_wgrad:c10")
+    probe = E.KernelProbe(a.probe if a.probe != "auto" else DOMINANT)
     eng = m._native()
 
     def body(x):
@@ -174,17 +194,19 @@ def main():
     value = seqs / el
     kd = probe.summary()
     roof = None
+    traffic, step_bytes = pmc_traffic(a.traffic, probe.tag, {"task": a.task, "batch": a.batch, "seq_len": a.seq_len})
     if kd is not None:
         achieved = kd["flops"] / (kd["avg_ms"] * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": kd["tag"], "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (PMC, fetch x2)",
                 "avg_us": round(kd["avg_ms"] * 1e3, 2), "launches": kd["n"], "algorithmic_flops": kd["flops"]}
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:
         cpu = cpu_baseline(a.task, a.seq_len, a.ae, a.cpu_seconds)
     if rank == 0:
         line = {
-            "metric": "video-seqs/sec (train step) spring_color B=100",
+            "metric": METRIC,
             "value": round(value, 2), "unit": "video-seqs/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
@@ -193,6 +215,10 @@ def main():
                                    f"({ins} in / {pred} pred / {a.seq_len - ins - pred} extrap)",
                        "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "final_loss": round(lossv, 4),
+            # whole-step memory-side traffic (committed PMC profile) at this run's step time
+            "hbm_step": None if step_bytes is None else {
+                "bytes_per_step": round(step_bytes), "achieved_GBs": round(step_bytes / (el / a.steps) / 1e9, 1),
+                "peak_GBs": PEAK_HBM_GBS, "frac": round(step_bytes / (el / a.steps) / 1e9 / PEAK_HBM_GBS, 4)},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
