@@ -73,6 +73,76 @@ __device__ __forceinline__ f32x4 load_row4(const float* __restrict__ plane, int 
   return v;
 }
 
+// The same 4-pixel row segment split in two halves for software pipelining:
+// issue() only starts the global loads (into registers, for the NEXT tile or
+// channel chunk), finish() -- after the current tile's MFMAs -- forms the
+// values (the 2x interpolation when UPS).  Out-of-range segments are zeros.
+template <bool UPS, int H, int W>
+struct Seg {
+  f32x4 v;
+  __device__ __forceinline__ void issue(const float* __restrict__ plane, int gy, int q, bool ok) {
+    v = ok ? *reinterpret_cast<const f32x4*>(plane + (long long)gy * W + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __device__ __forceinline__ f32x4 finish(int, int) const { return v; }
+};
+
+template <int H, int W>
+struct Seg<true, H, W> {
+  static constexpr int HS = H / 2, WS = W / 2;
+  float2 m0, m1;
+  float a0, a3, b0, b3;
+  __device__ __forceinline__ void issue(const float* __restrict__ plane, int gy, int q, bool ok) {
+    if (!ok) {
+      m0 = m1 = make_float2(0.f, 0.f);
+      a0 = a3 = b0 = b3 = 0.f;
+      return;
+    }
+    int y0, y1;
+    float wy0, wy1;
+    up2_taps(gy, HS, y0, y1, wy0, wy1);
+    const int c0 = q > 0 ? 2 * q - 1 : 0, c3 = 2 * q + 2 < WS ? 2 * q + 2 : WS - 1;
+    const float* r0 = plane + y0 * WS;
+    const float* r1 = plane + y1 * WS;
+    m0 = *reinterpret_cast<const float2*>(r0 + 2 * q);
+    m1 = *reinterpret_cast<const float2*>(r1 + 2 * q);
+    a0 = r0[c0];
+    a3 = r0[c3];
+    b0 = r1[c0];
+    b3 = r1[c3];
+  }
+  __device__ __forceinline__ f32x4 finish(int gy, int q) const {
+    int y0, y1;
+    float wy0, wy1;
+    up2_taps(gy, HS, y0, y1, wy0, wy1);
+    const float w0 = q > 0 ? 0.25f : 0.f, w1 = q > 0 ? 0.75f : 1.f;
+    f32x4 v;
+    v[0] = wy0 * (w0 * a0 + w1 * m0.x) + wy1 * (w0 * b0 + w1 * m1.x);
+    v[1] = wy0 * (0.75f * m0.x + 0.25f * m0.y) + wy1 * (0.75f * m1.x + 0.25f * m1.y);
+    v[2] = wy0 * (0.25f * m0.x + 0.75f * m0.y) + wy1 * (0.25f * m1.x + 0.75f * m1.y);
+    v[3] = wy0 * (0.75f * m0.y + 0.25f * a3) + wy1 * (0.75f * m1.y + 0.25f * b3);
+    return v;
+  }
+};
+
+// A value the compiler cannot prove loop-invariant: keeps the staging index
+// math of persistent kernels from being hoisted out of the tile loop (where
+// it would hold ~5 VGPRs per staged segment across all the MFMAs).  Used only
+// by the full-resolution upsampling convs, whose occupancy it restores; the
+// other shapes measured faster with the hoisted (recompute-free) form.
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// resident blocks per CU x CUs for a persistent launch of kernel k
+static int persistent_grid(const void* k, int lds_bytes) {
+  int dev = 0, cus = 256, per = 1;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, lds_bytes) != hipSuccess || per < 1) per = 1;
+  return per * cus;
+}
+
 // ============================================================ forward / dgrad
 template <int CIN, int COUT, int H, int W, int KS, bool DG>
 struct FwdCfg {
@@ -101,21 +171,22 @@ struct FwdCfg {
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS>
 __global__ void __launch_bounds__(256)
 conv_fwd_mfma_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
-                int flags) {
+                int flags, int ntiles) {
   constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   using C = FwdCfg<CIN, COUT, H, W, KS, DG>;
   constexpr int KK = C::KK, NT = C::NT, MW = C::MW, TWP = C::TWP, CHS = C::CHS, CI = C::CI;
-  constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, COUTP = C::COUTP, CINP = C::CINP;
+  constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, COUTP = C::COUTP, CINP = C::CINP, NCH = C::NCH;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* Il = lds;                 // [FPT][CI][CHS]
   float* Wl = lds + C::LDS_I;      // [KK][CINP][COUTP]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NRB = H / RT;      // row blocks per frame (RT divides H)
-  const int tile = blockIdx.x;
-  const int f0 = (tile / NRB) * FPT;
-  const int y0 = (tile % NRB) * RT;
+  constexpr int Q = W / 4;         // float4 per row
+  constexpr int NI = FPT * CI * ROWS * Q;   // staged 4-pixel segments per (tile, chunk)
+  constexpr int NL = (NI + 255) / 256;
 
-  // ---- weights -> Wt[tap][ci][co] (zero padded); dgrad: transposed + flipped
+  // ---- weights -> Wt[tap][ci][co] (zero padded); dgrad: transposed + flipped.
+  // Staged once: the block is persistent over tiles.
   for (int i = tid; i < KK * CINP * COUTP; i += 256) {
     const int co = i % COUTP;
     const int ci = (i / COUTP) % CINP;
@@ -143,84 +214,117 @@ conv_fwd_mfma_k(FView in, FViewW out, FView aux, const float* __restrict__ w, co
     const int y = rem / W, x = rem % W;
     abase[mt] = fi * CI * CHS + (lane >> 4) * CHS + y * TWP + x + 4 - C::PADL;
   }
-  f32x4 acc[MW][NT];
-#pragma unroll
-  for (int mt = 0; mt < MW; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int Q = W / 4;   // float4 per row
-  for (int ch = 0; ch < C::NCH; ++ch) {
-    const int ci0 = ch * CI;
-    if (ch) __syncthreads();
-    // ---- stage input rows [fi][c][rr] (float4 along x)
-    for (int i = tid; i < FPT * CI * ROWS * Q; i += 256) {
-      const int q = i % Q;
-      const int r = i / Q;
-      const int rr = r % ROWS;
-      const int c = (r / ROWS) % CI;
-      const int fi = r / (ROWS * CI);
-      const int f = f0 + fi, gy = y0 + rr - C::PADL, ci = ci0 + c;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (f < F && gy >= 0 && gy < H && ci < CIN) v = load_row4<UPS, H, W>(in.frame(f) + ci * PLANE, gy, q);
-      *reinterpret_cast<f32x4*>(&Il[(fi * CI + c) * CHS + rr * TWP + 4 + 4 * q]) = v;
+  // ---- software pipeline: the global loads of (tile, chunk + 1) -- or of the
+  // block's next tile -- are in flight while the current chunk is multiplied
+  Seg<UPS, H, W> seg[NL];
+  auto issue = [&](int t, int ch) {
+    const int tt = (UPS && H >= 32) ? opaque(tid) : tid;
+    const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tt + l * 256;
+      const int q = i % Q, r = i / Q;
+      const int rr = r % ROWS, c = (r / ROWS) % CI, fi = r / (ROWS * CI);
+      const int f = f0 + fi, gy = y0 + rr - C::PADL, ci = ch * CI + c;
+      const bool ok = i < NI && f < F && gy >= 0 && gy < H && ci < CIN;
+      seg[l].issue(ok ? in.frame(f) + ci * PLANE : in.p, gy, q, ok);
     }
-    __syncthreads();
+  };
+  auto commit = [&](int t) {
+    const int tt = (UPS && H >= 32) ? opaque(tid) : tid;
+    const int y0 = (t % NRB) * RT;
 #pragma unroll
-    for (int tap = 0; tap < KK; ++tap) {
-      const int toff = (tap / KS) * TWP + (tap % KS);
+    for (int l = 0; l < NL; ++l) {
+      const int i = tt + l * 256;
+      if (NI % 256 != 0 && i >= NI) break;
+      const int q = i % Q, r = i / Q;
+      const int rr = r % ROWS, c = (r / ROWS) % CI, fi = r / (ROWS * CI);
+      *reinterpret_cast<f32x4*>(&Il[(fi * CI + c) * CHS + rr * TWP + 4 + 4 * q]) =
+          seg[l].finish(y0 + rr - C::PADL, q);
+    }
+  };
+
+  constexpr long long HW = (long long)H * W;
+  // the full-resolution upsampling convs hold 8 raw floats per segment: their
+  // prefetch would cost the occupancy it is meant to replace (measured), so
+  // they load synchronously
+  constexpr bool PIPE = !(UPS && H >= 32);
+  int tile = blockIdx.x;
+  if (PIPE && tile < ntiles) issue(tile, 0);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int f0 = (tile / NRB) * FPT;
+    const int y0 = (tile % NRB) * RT;
+    f32x4 acc[MW][NT];
 #pragma unroll
-      for (int cg = 0; cg < CI / 4; ++cg) {
-        float b[NT];
+    for (int mt = 0; mt < MW; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          b[nt] = Wl[(tap * CINP + ci0 + cg * 4 + (lane >> 4)) * COUTP + nt * 16 + (lane & 15)];
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int ci0 = ch * CI;
+      __syncthreads();           // previous chunk's fragment reads are done
+      if (!PIPE) issue(tile, ch);
+      commit(tile);
+      __syncthreads();
+      if (PIPE) {
+        if (ch + 1 < NCH) issue(tile, ch + 1);
+        else if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x, 0);
+      }
 #pragma unroll
-        for (int mt = 0; mt < MW; ++mt) {
-          const float a = Il[abase[mt] + cg * 4 * CHS + toff];
+      for (int tap = 0; tap < KK; ++tap) {
+        const int toff = (tap / KS) * TWP + (tap % KS);
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma4(a, b[nt], acc[mt][nt]);
+        for (int cg = 0; cg < CI / 4; ++cg) {
+          float b[NT];
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            b[nt] = Wl[(tap * CINP + ci0 + cg * 4 + (lane >> 4)) * COUTP + nt * 16 + (lane & 15)];
+#pragma unroll
+          for (int mt = 0; mt < MW; ++mt) {
+            const float a = Il[abase[mt] + cg * 4 * CHS + toff];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma4(a, b[nt], acc[mt][nt]);
+          }
         }
       }
     }
-  }
 
-  // ---- epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for co = nt*16 + (lane&15)
-  constexpr long long HW = (long long)H * W;
+    // ---- epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for co = nt*16 + (lane&15)
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int co = nt * 16 + (lane & 15);
-    if (co >= COUT) continue;
-    const float bv = bias ? bias[co] : 0.f;
+    for (int nt = 0; nt < NT; ++nt) {
+      const int co = nt * 16 + (lane & 15);
+      if (co >= COUT) continue;
+      const float bv = bias ? bias[co] : 0.f;
 #pragma unroll
-    for (int mt = 0; mt < MW; ++mt) {
-      const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
-      const int fi = pix / (RT * W);
-      const int rem = pix % (RT * W);
-      const int y = y0 + rem / W, x = rem % W;
-      const int f = f0 + fi;
-      if (f >= F || y >= H) continue;
-      float* op = out.frame(f) + co * HW + (long long)y * W + x;
-      f32x4 v = acc[mt][nt];
+      for (int mt = 0; mt < MW; ++mt) {
+        const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+        const int fi = pix / (RT * W);
+        const int rem = pix % (RT * W);
+        const int y = y0 + rem / W, x = rem % W;
+        const int f = f0 + fi;
+        if (f >= F || y >= H) continue;
+        float* op = out.frame(f) + co * HW + (long long)y * W + x;
+        f32x4 v = acc[mt][nt];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += bv;
-      if (flags & 1) {
+        for (int r = 0; r < 4; ++r) v[r] += bv;
+        if (flags & 1) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = v[r] < 0.f ? 0.f : v[r];
+          for (int r = 0; r < 4; ++r) v[r] = v[r] < 0.f ? 0.f : v[r];
+        }
+        if (flags & 4) {
+          const f32x4 o = *reinterpret_cast<const f32x4*>(op);
+          v += o;
+        }
+        if (flags & 2) {
+          const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(op) = v;
       }
-      if (flags & 4) {
-        const f32x4 o = *reinterpret_cast<const f32x4*>(op);
-        v += o;
-      }
-      if (flags & 2) {
-        const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
-      }
-      *reinterpret_cast<f32x4*>(op) = v;
     }
   }
-  (void)ROWS;
 }
 
 // ===================================================================== wgrad
@@ -290,42 +394,74 @@ conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles
     Xl[(i / ROWS) * CHS + (i % ROWS) * TWP + 3] = 0.f;
     Xl[(i / ROWS) * CHS + (i % ROWS) * TWP + 4 + W] = 0.f;
   }
+  if (COP > COUT) {   // zero padded co columns once (read by padded M rows; never stored)
+    for (int i = tid; i < FPT * RT * W * (COP - COUT); i += 256)
+      Dl[(i / (COP - COUT)) * COP + COUT + i % (COP - COUT)] = 0.f;
+  }
   constexpr int NRB = H / RT;
   constexpr int Q = W / 4;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
-    __syncthreads();
-    for (int i = tid; i < FPT * CIN * ROWS * Q; i += 256) {
-      const int q = i % Q;
-      const int r = i / Q;
-      const int rr = r % ROWS;
-      const int c = (r / ROWS) % CIN;
-      const int fi = r / (ROWS * CIN);
+  constexpr int NIX = FPT * CIN * ROWS * Q, NLX = (NIX + 255) / 256;   // X row segments per tile
+  constexpr int NID = FPT * COUT * RT * Q, NLD = (NID + 255) / 256;    // dY segments per tile
+  // software pipeline: the next tile's global loads are in flight while the
+  // current tile is multiplied
+  Seg<UPS, H, W> sx[NLX];
+  f32x4 sd[NLD];
+  auto issue = [&](int t) {
+    const int tt = (UPS && H >= 32) ? opaque(tid) : tid;
+    const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NLX; ++l) {
+      const int i = tt + l * 256;
+      const int q = i % Q, r = i / Q;
+      const int rr = r % ROWS, c = (r / ROWS) % CIN, fi = r / (ROWS * CIN);
       const int f = f0 + fi, gy = y0 + rr - C::PADL;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (f < F && gy >= 0 && gy < H) v = load_row4<UPS, H, W>(x.frame(f) + c * PLANE, gy, q);
-      *reinterpret_cast<f32x4*>(&Xl[(fi * CIN + c) * CHS + rr * TWP + 4 + 4 * q]) = v;
+      const bool ok = i < NIX && f < F && gy >= 0 && gy < H;
+      sx[l].issue(ok ? x.frame(f) + c * PLANE : x.p, gy, q, ok);
+    }
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int i = tt + l * 256;
+      const int co = i % COUT, r = i / COUT;
+      const int q = r % Q, rr = (r / Q) % RT, fi = r / (Q * RT);
+      const int f = f0 + fi;
+      sd[l] = (i < NID && f < F)
+                  ? *reinterpret_cast<const f32x4*>(dy.frame(f) + ((long long)co * H + y0 + rr) * W + 4 * q)
+                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto commit = [&](int t) {
+    const int tt = (UPS && H >= 32) ? opaque(tid) : tid;
+    const int y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NLX; ++l) {
+      const int i = tt + l * 256;
+      if (NIX % 256 != 0 && i >= NIX) break;
+      const int q = i % Q, r = i / Q;
+      const int rr = r % ROWS, c = (r / ROWS) % CIN, fi = r / (ROWS * CIN);
+      *reinterpret_cast<f32x4*>(&Xl[(fi * CIN + c) * CHS + rr * TWP + 4 + 4 * q]) =
+          sx[l].finish(y0 + rr - C::PADL, q);
     }
     // dY -> [pixel][co]: co varies fastest across lanes so the transposed LDS
     // writes of one float4 (4 pixels) are conflict free
-    for (int i = tid; i < FPT * COUT * RT * Q; i += 256) {
-      const int co = i % COUT;
-      const int r = i / COUT;
-      const int q = r % Q;
-      const int rr = (r / Q) % RT;
-      const int fi = r / (Q * RT);
-      const int f = f0 + fi;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (f < F) v = *reinterpret_cast<const f32x4*>(dy.frame(f) + ((long long)co * H + y0 + rr) * W + 4 * q);
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int i = tt + l * 256;
+      if (NID % 256 != 0 && i >= NID) break;
+      const int co = i % COUT, r = i / COUT;
+      const int q = r % Q, rr = (r / Q) % RT, fi = r / (Q * RT);
       const int pb = (fi * RT + rr) * W + 4 * q;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Dl[(pb + e) * COP + co] = v[e];
+      for (int e = 0; e < 4; ++e) Dl[(pb + e) * COP + co] = sd[l][e];
     }
-    if (COP > COUT) {   // zero padded co columns (read by padded M rows; never stored)
-      for (int i = tid; i < FPT * RT * W * (COP - COUT); i += 256)
-        Dl[(i / (COP - COUT)) * COP + COUT + i % (COP - COUT)] = 0.f;
-    }
+  };
+  constexpr bool PIPE = true;
+  if (PIPE && (int)blockIdx.x < ntiles) issue(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();            // previous tile's fragment reads are done
+    if (!PIPE) issue(tile);
+    commit(tile);
     __syncthreads();
+    if (PIPE && tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
     for (int g = wp; g < C::NG; g += WP) {
       const int fi = g / (RT * Q);
       const int rem = g % (RT * Q);
@@ -406,12 +542,14 @@ static int fwd_launch(FView in, FViewW out, FView aux, const float* w, const flo
   constexpr int NRB = H / C::RT;
   const int ntiles = cdiv(F, C::FPT) * NRB;
   auto k = conv_fwd_mfma_k<CIN, COUT, H, W, KS, DG, UPS>;
-  static bool attr = false;
-  if (!attr && C::LDS > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr = true;
+  static int resident = 0;
+  if (!resident) {
+    if (C::LDS > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    resident = persistent_grid((const void*)k, C::LDS);
   }
-  hipLaunchKernelGGL(k, dim3(ntiles), dim3(256), C::LDS, st, in, out, aux, w, b, F, flags);
+  const int nb = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), C::LDS, st, in, out, aux, w, b, F, flags, ntiles);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

@@ -33,8 +33,20 @@ def test_cli_flags_match_reference():
     assert R.TASKS["mnist_spring_color"][2:] == ("spring_ode_cell", 12, 30, 3, 7, 64 * 64)
 
 
+@pytest.fixture
+def torch_logger():
+    import logging
+    lg = logging.getLogger("torch")     # the reference logs to the "torch" logger (runner :38-44)
+    handlers, level = list(lg.handlers), lg.level
+    yield lg
+    for h in list(lg.handlers):
+        if h not in handlers:
+            lg.removeHandler(h)
+    lg.setLevel(level)
+
+
 @pytest.mark.gpu
-def test_cli_train_then_test(tmp_path):
+def test_cli_train_then_test(tmp_path, torch_logger):
     import torch_run_physics as R
     save = str(tmp_path / "run")
     data = str(tmp_path / "data")
