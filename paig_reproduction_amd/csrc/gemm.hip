@@ -182,6 +182,22 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
       }
 }
 
+// sum_{s<S} p[s*ld] in order s = 0..S-1 (deterministic), loads issued 8 at a
+// time so the partial slabs stream instead of one dependent load per split
+__device__ __forceinline__ float sum_strided(const float* __restrict__ p, long long ld, int S) {
+  float v = 0.f;
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = p[(long long)(s + j) * ld];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v += t[j];
+  }
+  for (; s < S; ++s) v += p[(long long)s * ld];
+  return v;
+}
+
 __global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restrict__ part, float* __restrict__ C,
                                        long long ldc, float beta, const float* __restrict__ bias, int act, int auxm,
                                        const float* __restrict__ aux, long long ldaux, const float* __restrict__ rowpart,
@@ -191,24 +207,24 @@ __global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restr
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < tot; i += (long long)gridDim.x * blockDim.x) {
     if (i >= n_el) {
       const int m = (int)(i - n_el);
-      float v = 0.f;
-      for (int s = 0; s < S; ++s) v += rowpart[(long long)s * M + m];
-      rowsum[m] = v;
+      rowsum[m] = sum_strided(rowpart + m, M, S);
       continue;
     }
     const int m = (int)(i / N), n = (int)(i % N);
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += part[(long long)s * n_el + i];
+    float v = sum_strided(part + i, n_el, S);
     if (beta != 0.f) v += beta * C[(long long)m * ldc + n];
     if (bias) v += bias[n];
     C[(long long)m * ldc + n] = epi(v, act, auxm, aux, (long long)m * ldaux + n);
   }
 }
 
+// Split-K factor: the dense layers here are small (M, N <= a few thousand)
+// and latency-bound, so split until ~4 blocks per CU are in flight, keeping
+// >= 1 BK step per split and the partial slabs <= 16 MB.
 static int choose_split(int M, int N, int K) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
   int s = 1;
-  while (tiles * s < 512 && K / (s * 2) >= 256) s *= 2;
+  while (tiles * s < 1024 && cdiv(K, 2 * s) >= BK && (long long)(2 * s) * M * N <= (4ll << 20)) s *= 2;
   return s;
 }
 
