@@ -43,6 +43,9 @@ int paig_abi_version(void);
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                     const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin, int Cout,
                     int H, int W, int ks, int flags, void* stream);
+/* 1 if the shape runs on the MFMA path for fwd/dgrad (what 0) or wgrad (what 1)
+ * with these flags; flag 32 (fused upsample input) is available only there */
+int paig_conv2d_mfma_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags);
 /* per-block partial [Cout*Cin*ks*ks | Cout] weight+bias grads into slab rows */
 int paig_conv2d_wgrad(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
                       float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
@@ -60,12 +63,16 @@ int paig_upsample2_bwd(const float* du, long long du_fs, const float* s, long lo
                        int F, int C, int Hs, int Ws, int Ho, int Wo, int relu_mask, void* stream);
 
 /* ---- encoder head: cat(ones)+softmax+mask*image (blocks.py:84-93),
- *      tanh position head (blocks.py:101-102) */
+ *      tanh position head (blocks.py:101-102).
+ * fwd: pobjs (nullable) also receives AvgPool2d(2) of the masked objects
+ *      (UNet / H >= 40, blocks.py:94-96), the l1 input in that case.
+ * bwd flags: 1 the logits are ReLU'd (ShallowUNet c13, Q13),
+ *            2 dobjs is the gradient of the pooled objects [K*F][C][H/2][W/2]. */
 int paig_mask_softmax_fwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs, float* masks,
-                          float* objs, int F, int K, int C, int HW, void* stream);
+                          float* objs, float* pobjs, int F, int K, int C, int H, int W, void* stream);
 int paig_mask_softmax_bwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs,
-                          const float* masks, const float* dobjs, float* dlogits, int F, int K, int C, int HW,
-                          void* stream);
+                          const float* masks, const float* dobjs, float* dlogits, int F, int K, int C, int H, int W,
+                          int flags, void* stream);
 int paig_pos_head_fwd(const float* h3, float* pos, int N, int K, float half, void* stream);
 int paig_pos_head_bwd(const float* h3, const float* dpos, float* dh3, int N, int K, float half, void* stream);
 
@@ -133,6 +140,11 @@ int paig_frame_sse(const float* a, long long a_fs, int a_grp, long long a_gs, co
                    long long b_gs, float* sse, int F, int n, void* stream);
 int paig_frame_sse_bwd(const float* a, long long a_fs, int a_grp, long long a_gs, const float* b, long long b_fs,
                        int b_grp, long long b_gs, const float* w, float* da, int F, int n, void* stream);
+
+/* ---- device-resident dataset (nn/datasets/iterators.py:26-40,60-67, Q5):
+ * out[b][:] = float(src[idx[b]][:]) / 255 for a uint8 dataset of `row`-byte
+ * sequences (T*H*W*C; multiple of 16); idx: device int64[B] */
+int paig_gather_u8_f32(const unsigned char* src, const long long* idx, float* out, int B, long long row, void* stream);
 
 /* ---- optimizers over the flat parameter buffer (base.py:12-17, torch defaults) */
 int paig_rmsprop_f32(float* p, const float* g, float* sa, long long n, float lr, float alpha, float eps, void* stream);

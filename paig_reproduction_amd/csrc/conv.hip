@@ -143,7 +143,8 @@ conv_wgrad_k(FView x, FView dy, float* __restrict__ slab, int F, int H, int W, i
   const int TR = RPB + HALO;
   const int tid = threadIdx.x;
   const int nthreads = blockDim.x;
-  const int combo = tid / PP, pp = tid % PP;
+  // (cout group, ci) combos: blockIdx.y selects this block's slice of them
+  const int combo = blockIdx.y * (nthreads / PP) + tid / PP, pp = tid % PP;
   const int cob = combo / CIN, ci = combo % CIN;
   float* xs = lds;
   float* ds = lds + FPB * CIN * TR * TWP;
@@ -254,7 +255,7 @@ static FwdGeom fwd_geom(int F, int H, int W, int CIN, int COUT, int CO, int KS) 
   FwdGeom g;
   const int CIC = CIN < 8 ? CIN : 8;
   g.G = COUT / CO;
-  g.GB = g.G > 4 ? 4 : g.G;
+  g.GB = g.G % 4 == 0 ? 4 : (g.G % 2 == 0 ? 2 : 1);   // cout groups per block: a divisor of G
   int target = (256 / g.GB) / 64 * 64;  // slots per cout group (multiple of 64)
   if (target < 64) target = 64;
   const int CGR = (W + PX - 1) / PX;
@@ -288,7 +289,7 @@ static int launch_fwd(FView in, FViewW out, FView aux, const float* w, const flo
     paig_set_error("conv: cout groups %d not a multiple of %d", g.G, g.GB);
     return PAIG_E_UNSUPPORTED;
   }
-  if (g.threads > 1024 || g.lds_bytes > 64 * 1024) {
+  if (g.threads > 256 || g.lds_bytes > 64 * 1024) {   // __launch_bounds__(256)
     paig_set_error("conv: geometry too large (threads %d, lds %d)", g.threads, g.lds_bytes);
     return PAIG_E_UNSUPPORTED;
   }
@@ -305,9 +306,15 @@ static int launch_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_
   constexpr int NCOMBO = (COUT / CO) * CIN;
   int PP = 1;
   while (PP * 2 * NCOMBO <= 256 && PP < 64) PP *= 2;
-  const int threads = NCOMBO * PP;
-  if (threads > 1024) {
-    paig_set_error("wgrad: %d combos too many", NCOMBO);
+  // more combos than one 256-thread block holds (UNet): split them over gridDim.y
+  int CPB = NCOMBO, GY = 1;
+  while (CPB * PP > 256 && CPB % 2 == 0) {
+    CPB /= 2;
+    GY *= 2;
+  }
+  const int threads = CPB * PP;
+  if (threads > 256 || threads % 64 != 0) {
+    paig_set_error("wgrad: %d combos cannot be split into blocks", NCOMBO);
     return PAIG_E_UNSUPPORTED;
   }
   const int CGR = (W + PX - 1) / PX;
@@ -324,7 +331,7 @@ static int launch_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_
   int nblk = ntiles < nblk_max ? ntiles : nblk_max;
   if (nblk < 1) nblk = 1;
   *nblk_out = nblk;
-  hipLaunchKernelGGL((conv_wgrad_k<CIN, COUT, CO, KS>), dim3(nblk), dim3(threads), lds, st, x, dy, slab, F, H, W,
+  hipLaunchKernelGGL((conv_wgrad_k<CIN, COUT, CO, KS>), dim3(nblk, GY), dim3(threads), lds, st, x, dy, slab, F, H, W,
                      FPB, RPB, PP, ntiles);
   PAIG_CHECK_LAUNCH();
   return 0;

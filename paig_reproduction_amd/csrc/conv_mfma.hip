@@ -638,3 +638,26 @@ int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk
 #undef PAIG_CASE
   return 0;
 }
+
+// Query (see include/paig_hip.h): does paig_conv2d_fwd (what = 0) or
+// paig_conv2d_wgrad (what = 1) run this shape on the MFMA path with these
+// flags?  flags & 32 (fused 2x upsample input) exists ONLY on that path, so
+// the host uses this to decide which upsamples it may fuse.
+extern "C" int paig_conv2d_mfma_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags) {
+  if (H != W) return 0;
+  const bool up = (flags & 32) != 0, dg = (flags & 8) != 0;
+#define PAIG_CASE(CI, CO, HH, K) \
+  if (Cin == CI && Cout == CO && H == HH && ks == K) return 1;
+  if (up) {
+    if (dg) return 0;
+    PAIG_MFMA_UP(PAIG_CASE)
+    return 0;
+  }
+  if (what == 0) {
+    PAIG_MFMA_FWD(PAIG_CASE)
+  } else {
+    PAIG_MFMA_WG(PAIG_CASE)
+  }
+#undef PAIG_CASE
+  return 0;
+}

@@ -178,28 +178,87 @@ __global__ void mask_softmax_fwd_k(const float* __restrict__ lg, FView x, float*
   }
 }
 
-// dlogits[f][k][p] = relu'(lg) * m_k * (dm_k - sum_j m_j dm_j),
+// UNet (H >= 40): the same softmax over 2x2 quads, also writing the
+// AvgPool2d(2) of the masked objects that feeds l1 (blocks.py:94-96); window
+// sum in aten's (0,0),(0,1),(1,0),(1,1) order, then * 1/4 (exact).
+__global__ void mask_softmax_pool_fwd_k(const float* __restrict__ lg, FView x, float* __restrict__ masks,
+                                        float* __restrict__ objs, float* __restrict__ pobjs, int F, int K, int C,
+                                        int H, int W) {
+  const int H2 = H / 2, W2 = W / 2, HW = H * W, HW4 = H2 * W2;
+  const long long n = (long long)F * HW4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % HW4);
+    const int f = (int)(i / HW4);
+    const int qy = q / W2, qx = q % W2;
+    const float* xp = x.frame(f);
+    float acc[7][3];
+    for (int k = 0; k < K; ++k)
+      for (int c = 0; c < 3; ++c) acc[k][c] = 0.f;
+    for (int d = 0; d < 4; ++d) {
+      const int p = (2 * qy + (d >> 1)) * W + 2 * qx + (d & 1);
+      float l[8];
+      float m = 1.f;
+      for (int k = 0; k < K; ++k) {
+        l[k] = lg[((long long)f * K + k) * HW + p];
+        m = fmaxf(m, l[k]);
+      }
+      float e[9];
+      float s = 0.f;
+      for (int k = 0; k < K; ++k) {
+        e[k] = expf(l[k] - m);
+        s += e[k];
+      }
+      e[K] = expf(1.f - m);
+      s += e[K];
+      for (int k = 0; k <= K; ++k) {
+        const float mk = e[k] / s;
+        masks[((long long)f * (K + 1) + k) * HW + p] = mk;
+        if (k < K)
+          for (int c = 0; c < C; ++c) {
+            const float o = mk * xp[c * HW + p];
+            objs[((long long)k * F + f) * C * HW + (long long)c * HW + p] = o;
+            acc[k][c] += o;
+          }
+      }
+    }
+    for (int k = 0; k < K; ++k)
+      for (int c = 0; c < C; ++c) pobjs[((long long)k * F + f) * C * HW4 + (long long)c * HW4 + q] = acc[k][c] * 0.25f;
+  }
+}
+
+// dlogits[f][k][p] = [relu'(lg)] * m_k * (dm_k - sum_j m_j dm_j),
 // dm_k = sum_c dobjs[k*F+f][c][p] * x[f][c][p] (k < K), dm_bg = 0.
+// flags: 1 the logits are ReLU'd (ShallowUNet c13, Q13), 2 dobjs is the
+// gradient of the 2x2-average-pooled objects (UNet: d = dpooled / 4).
 __global__ void mask_softmax_bwd_k(const float* __restrict__ lg, FView x, const float* __restrict__ masks,
                                    const float* __restrict__ dobjs, float* __restrict__ dlg, int F, int K, int C,
-                                   int HW) {
+                                   int H, int W, int flags) {
+  const int HW = H * W;
+  const bool pooled = (flags & 2) != 0;
+  const int W2 = W / 2, HW4 = (H / 2) * W2;
   const long long n = (long long)F * HW;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const int p = i % HW;
     const int f = (int)(i / HW);
     const float* xp = x.frame(f);
+    const int pq = pooled ? ((p / W) >> 1) * W2 + ((p % W) >> 1) : p;
+    const int DHW = pooled ? HW4 : HW;
     float dm[8], mk[8];
     float dot = 0.f;
     for (int k = 0; k < K; ++k) {
       float a = 0.f;
-      for (int c = 0; c < C; ++c) a = fmaf(dobjs[((long long)k * F + f) * C * HW + (long long)c * HW + p], xp[c * HW + p], a);
+      for (int c = 0; c < C; ++c) {
+        float d = dobjs[((long long)k * F + f) * C * DHW + (long long)c * DHW + pq];
+        if (pooled) d *= 0.25f;
+        a = fmaf(d, xp[c * HW + p], a);
+      }
       dm[k] = a;
       mk[k] = masks[((long long)f * (K + 1) + k) * HW + p];
       dot = fmaf(mk[k], a, dot);
     }
     for (int k = 0; k < K; ++k) {
       const float g = mk[k] * (dm[k] - dot);
-      dlg[((long long)f * K + k) * HW + p] = lg[((long long)f * K + k) * HW + p] > 0.f ? g : 0.f;
+      dlg[((long long)f * K + k) * HW + p] = ((flags & 1) && !(lg[((long long)f * K + k) * HW + p] > 0.f)) ? 0.f : g;
     }
   }
 }
@@ -412,22 +471,28 @@ int paig_upsample2_bwd(const float* du, long long du_fs, const float* s, long lo
 }
 
 int paig_mask_softmax_fwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs,
-                          float* masks, float* objs, int F, int K, int C, int HW, void* stream) {
+                          float* masks, float* objs, float* pobjs, int F, int K, int C, int H, int W, void* stream) {
   if (F <= 0) return 0;
   PAIG_REQUIRE(K >= 1 && K <= 7, "mask_softmax: K=%d", K);
-  hipLaunchKernelGGL(mask_softmax_fwd_k, dim3(grid_for((long long)F * HW)), dim3(256), 0, (hipStream_t)stream, logits,
-                     FView{x, x_fs, x_gs, x_grp}, masks, objs, F, K, C, HW);
+  if (pobjs) {
+    PAIG_REQUIRE(C <= 3 && H % 2 == 0 && W % 2 == 0, "mask_softmax pooled: C=%d H=%d W=%d", C, H, W);
+    hipLaunchKernelGGL(mask_softmax_pool_fwd_k, dim3(grid_for((long long)F * (H / 2) * (W / 2))), dim3(256), 0,
+                       (hipStream_t)stream, logits, FView{x, x_fs, x_gs, x_grp}, masks, objs, pobjs, F, K, C, H, W);
+  } else {
+    hipLaunchKernelGGL(mask_softmax_fwd_k, dim3(grid_for((long long)F * H * W)), dim3(256), 0, (hipStream_t)stream,
+                       logits, FView{x, x_fs, x_gs, x_grp}, masks, objs, F, K, C, H * W);
+  }
   PAIG_CHECK_LAUNCH();
   return 0;
 }
 
 int paig_mask_softmax_bwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs,
-                          const float* masks, const float* dobjs, float* dlogits, int F, int K, int C, int HW,
-                          void* stream) {
+                          const float* masks, const float* dobjs, float* dlogits, int F, int K, int C, int H, int W,
+                          int flags, void* stream) {
   if (F <= 0) return 0;
   PAIG_REQUIRE(K >= 1 && K <= 7, "mask_softmax: K=%d", K);
-  hipLaunchKernelGGL(mask_softmax_bwd_k, dim3(grid_for((long long)F * HW)), dim3(256), 0, (hipStream_t)stream, logits,
-                     FView{x, x_fs, x_gs, x_grp}, masks, dobjs, dlogits, F, K, C, HW);
+  hipLaunchKernelGGL(mask_softmax_bwd_k, dim3(grid_for((long long)F * H * W)), dim3(256), 0, (hipStream_t)stream,
+                     logits, FView{x, x_fs, x_gs, x_grp}, masks, dobjs, dlogits, F, K, C, H, W, flags);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

@@ -138,14 +138,21 @@ class Layout:
         self.alt_vel = model.alt_vel
         self.cell = {"spring_ode_cell": 0, "bouncing_ode_cell": 1, "gravity_ode_cell": 2}[model.cell_type]
         self.unet = self.H >= 40
-        if self.unet:
-            raise NotImplementedError("UNet (H >= 40, mnist_spring_color) encoder is not in this build yet")
-        self.bufs, self.ops = shallow_unet_plan(8, self.K)
-        self.prefix = "encoder.shallow_unet."
+        if self.unet:       # UNet(hidden 16), blocks.py:106-237; c18 not ReLU'd
+            self.bufs, self.ops = unet_plan(16, self.K)
+            self.prefix = "encoder.unet."
+        else:               # ShallowUNet(hidden 8), blocks.py:240-308; c13 ReLU'd (Q13)
+            self.bufs, self.ops = shallow_unet_plan(8, self.K)
+            self.prefix = "encoder.shallow_unet."
+        self.lg_relu = not self.unet
+        # l1 input: the masked objects, AvgPool2d(2)'d first for H >= 40 (blocks.py:92-96)
+        self.l1_in = 3 * (self.H // 2) ** 2 if self.unet else 3 * self.H * self.H
         self.fin = backward_plan(self.ops)
-        # upsamples consumed by exactly one conv (c7, c10) are fused into that
-        # conv's input staging (fwd and wgrad); only the gradient buffer of the
-        # upsampled tensor remains (dgrad output -> upsample backward)
+        # an upsample consumed by exactly one conv is fused into that conv's
+        # input staging (fwd and wgrad) when the MFMA path has the shape; only
+        # the gradient buffer of the upsampled tensor remains (dgrad output ->
+        # upsample backward)
+        L = lib()
         self.fused_up, self.fused_bufs = {}, set()
         for i, op in enumerate(self.ops):
             if op["op"] != "up":
@@ -154,8 +161,8 @@ class Layout:
             if len(consumers) != 1 or self.ops[consumers[0]]["op"] != "conv":
                 continue
             c = self.ops[consumers[0]]
-            lvl = self.bufs[op["dst"][0]][1]
-            if (c["src"][2], c["dst"][2], self.H // lvl) in {(32, 16, 16), (16, 16, 32)}:
+            Hc = self.H // self.bufs[op["dst"][0]][1]
+            if all(L.paig_conv2d_mfma_supported(w, c["src"][2], c["dst"][2], Hc, Hc, c["ks"], 32) for w in (0, 1)):
                 self.fused_up[consumers[0]] = op
                 self.fused_bufs.add(op["dst"][0])
         self.HW = self.H * self.H
@@ -258,9 +265,10 @@ class Engine:
 
     def workspace_floats(self, lay):
         K, F, B = lay.K, lay.F, lay.B
-        need = [self.L.paig_gemm_workspace(K * F, 200, 3 * lay.HW), self.L.paig_gemm_workspace(200, 3 * lay.HW, K * F),
-                self.L.paig_gemm_workspace(K * F, 3 * lay.HW, 200), self.L.paig_gemm_workspace(200, 200, K * F),
-                self.L.paig_colsum_workspace(K * F, 3 * lay.HW), self.L.paig_gemm_workspace(100, 100, K * B),
+        n1 = lay.l1_in
+        need = [self.L.paig_gemm_workspace(K * F, 200, n1), self.L.paig_gemm_workspace(200, n1, K * F),
+                self.L.paig_gemm_workspace(K * F, n1, 200), self.L.paig_gemm_workspace(200, 200, K * F),
+                self.L.paig_gemm_workspace(2, 200, K * F), self.L.paig_gemm_workspace(100, 100, K * B),
                 self.L.paig_gemm_workspace(K * B, 100, 100), 1 << 16]
         return int(max(need))
 
@@ -346,16 +354,18 @@ class Engine:
         # ---- mask softmax + masked objects + localiser MLP + position head
         masks = _empty(F * (K + 1) * HW, dev)
         objs = _empty(K * F * 3 * HW, dev)
-        L.paig_mask_softmax_fwd(ptr(acts["LG"]), *x_view, ptr(masks), ptr(objs), F, K, 3, HW, st)
+        pobjs = _empty(K * F * lay.l1_in, dev) if lay.unet else None
+        L.paig_mask_softmax_fwd(ptr(acts["LG"]), *x_view, ptr(masks), ptr(objs), ptr(pobjs), F, K, 3, H, H, st)
+        l1_x = pobjs if lay.unet else objs
         h1 = _empty(K * F * 200, dev)
         h2 = _empty(K * F * 200, dev)
         h3 = _empty(K * F * 2, dev)
-        self.linear(objs, K * F, "encoder.l1", h1, 1, st, ws)
+        self.linear(l1_x, K * F, "encoder.l1", h1, 1, st, ws)
         self.linear(h1, K * F, "encoder.l2", h2, 1, st, ws)
         self.linear(h2, K * F, "encoder.l3", h3, 0, st, ws)
         enc_pos = _empty(F * 2 * K, dev)
         L.paig_pos_head_fwd(ptr(h3), ptr(enc_pos), F, K, float(H / 2), st)
-        S.update(masks=masks, objs=objs, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
+        S.update(masks=masks, objs=objs, l1_x=l1_x, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
 
         # ---- reconstruction decode (all B*Te frames, SSE vs input fused)
         recons = _empty(F * lay.frame, dev)
@@ -508,17 +518,19 @@ class Engine:
         L.paig_pos_head_bwd(ptr(S["h3"]), ptr(denc), ptr(dh3), F, K, float(H / 2), st)
         dh2 = _empty(K * F * 200, dev)
         dh1 = _empty(K * F * 200, dev)
-        dobjs = _empty(K * F * 3 * HW, dev)
+        dobjs = _empty(K * F * lay.l1_in, dev)
         self.linear_bwd(S["h2"], dh3, K * F, "encoder.l3", dh2, S["h2"], 1, st, ws)
         self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws)
-        self.linear_bwd(S["objs"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
+        self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
 
-        # ---- mask softmax backward (incl. ReLU' of the last U-Net conv: Q13)
+        # ---- mask softmax backward (incl. ReLU' of ShallowUNet's c13, Q13, and
+        # the AvgPool2d backward of the UNet path)
         acts = S["acts"]
         dacts = {}
         dLG = _empty(F * K * HW, dev)
         L.paig_mask_softmax_bwd(ptr(acts["LG"]), x_view[0], x_view[1], x_view[2], x_view[3], ptr(S["masks"]),
-                                ptr(dobjs), ptr(dLG), F, K, 3, HW, st)
+                                ptr(dobjs), ptr(dLG), F, K, 3, H, H, (1 if lay.lg_relu else 0) | (2 if lay.unet else 0),
+                                st)
         dacts["LG"] = dLG
         self._unet_backward(S, dacts, st)
 

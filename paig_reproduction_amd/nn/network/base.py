@@ -195,7 +195,8 @@ class BaseNetTorch(torch.nn.Module):
                 self.loss = self.train_loss
                 for k in self.eval_metrics.keys():
                     eval_metrics_results[k].append(self.eval_metrics[k])
-                eval_outputs["input"].append(feed_dict["input"])
+                fi = feed_dict["input"]
+                eval_outputs["input"].append(fi.detach().cpu().numpy() if torch.is_tensor(fi) else fi)
                 eval_outputs["output"].append(self.eval_losses)
             eval_metrics_results = {k: np.mean([i.detach().cpu().numpy() for i in v], axis=0)
                                     for k, v in eval_metrics_results.items()}

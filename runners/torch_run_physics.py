@@ -12,6 +12,8 @@ Additive flags only:
   --synthetic N                  if the task's npz is missing, render one with
         N training sequences (N//10 valid/test) with nn/datasets/synth.py.
   --seed S                       shared shuffle seed (required for DDP sharding).
+  --device_data {1,0}            1 (default): uint8 dataset resident in HBM, each
+        batch gathered on the GPU; 0: the reference's host path.
 
 Data-parallel training: launch with torchrun (one process per GPU, RCCL);
 --batch_size is per rank, every rank draws a disjoint shard of each epoch.
@@ -86,6 +88,8 @@ def build_parser():
     p.add_argument("--data_dir", type=str, default=os.path.join(REPO, "data", "datasets"))
     p.add_argument("--synthetic", type=int, default=0)
     p.add_argument("--seed", type=int, default=None)
+    p.add_argument("--device_data", type=int, default=1,
+                   help="1: dataset resident in HBM as uint8, batches gathered on the GPU (F2); 0: host iterators")
     return p
 
 
@@ -148,7 +152,7 @@ def main(argv=None):
     if not args.test_mode:
         network = make(seq_len)
         its = get_iterators(dataset_path(args, data_file, seq_len), conv=True, datapoints=args.datapoints,
-                            seed=args.seed, rank=rank, world=world)
+                            seed=args.seed, rank=rank, world=world, device=device if args.device_data else None)
         network.get_data(its)
         network.build_optimizer(args.base_lr, args.optimizer, args.anneal_lr)
         network.initialize_graph(args.save_dir, args.use_ckpt, args.ckpt_dir)
@@ -159,7 +163,7 @@ def main(argv=None):
     network.build_optimizer(args.base_lr, args.optimizer, args.anneal_lr)
     network.initialize_graph(args.save_dir, True, args.ckpt_dir)
     its = get_iterators(dataset_path(args, test_data_file, test_seq_len), conv=True, datapoints=args.datapoints,
-                        seed=args.seed, rank=rank, world=world)
+                        seed=args.seed, rank=rank, world=world, device=device if args.device_data else None)
     network.get_data(its)
     network.train_model(0, args.batch_size, args.save_every_n_epochs, args.eval_every_n_epochs,
                         args.print_interval, args.debug)

@@ -1,0 +1,38 @@
+"""the device-resident dataset yields exactly the batches of the
+reference-semantics host iterator (same seed -> same permutation, drop-last,
+rank sharding, uint8/255 with the Q5 reshape), bit for bit."""
+import numpy as np
+import pytest
+import torch
+
+from paig_reproduction_amd.nn.datasets.iterators import DataIterator, DeviceDataIterator
+
+
+def _data(n=23, T=5, H=8, C=3, seed=0):
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 256, size=(n, T, H, H, C), dtype=np.uint8)
+
+
+def test_take_is_drop_last_and_sharded():
+    X = np.zeros((10, 1), np.float32)
+    it = DataIterator(X, seed=1, rank=1, world=2)
+    seen = []
+    while it.get_epoch() < 1:
+        seen.append(it._take(2))
+    assert len(seen) == 2 and all(len(s) == 2 for s in seen)   # 10 // (2*2) = 2 global batches
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rank,world", [(0, 1), (1, 2)])
+def test_device_batches_match_host(rank, world):
+    u8 = _data()
+    N, T, H, W, C = u8.shape
+    host = DataIterator(u8.astype(np.float32).reshape(N, T, C, H, W) / 255, seed=5, rank=rank, world=world)
+    dev = DeviceDataIterator(u8, (T, C, H, W), "cuda:0", seed=5, rank=rank, world=world)
+    for _ in range(12):                    # crosses epoch boundaries
+        hx, _ = host.next_batch(3)
+        dx, _ = dev.next_batch(3)
+        torch.cuda.synchronize()
+        assert dx.dtype == torch.float32 and tuple(dx.shape) == (3, T, C, H, W)
+        assert np.array_equal(dx.cpu().numpy(), hx.astype(np.float32))
+        assert host.get_epoch() == dev.get_epoch()

@@ -31,7 +31,10 @@ def p(t):
 
 CONV_CASES = [(3, 8, 32, 3, 5), (8, 8, 32, 3, 3), (8, 16, 16, 3, 7), (16, 16, 16, 3, 4), (16, 32, 8, 3, 9),
               (32, 32, 8, 3, 3), (32, 16, 16, 3, 2), (24, 8, 32, 3, 2), (8, 2, 32, 1, 3), (16, 16, 32, 3, 2),
-              (8, 16, 18, 3, 3), (16, 32, 9, 3, 5), (3, 8, 36, 3, 2)]
+              (8, 16, 18, 3, 3), (16, 32, 9, 3, 5), (3, 8, 36, 3, 2),
+              # UNet (mnist, 64x64, hidden 16): wide layers, VALU path, combos split over blocks
+              (16, 16, 64, 3, 2), (48, 16, 64, 3, 2), (96, 64, 16, 3, 2), (64, 128, 8, 3, 3), (128, 128, 8, 3, 2),
+              (16, 2, 64, 1, 2)]
 
 
 @pytest.mark.parametrize("cin,cout,hw,ks,F_", CONV_CASES)

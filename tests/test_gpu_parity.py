@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 GRAD_RTOL = 1e-3
 ROLLOUT_RTOL_3BP = 2e-3
-SUPPORTED = [n for n in GOLDEN if not n.startswith("mnist")]
+SUPPORTED = list(GOLDEN)
 
 
 def _model(z, device):
