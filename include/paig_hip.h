@@ -100,6 +100,28 @@ int paig_vfn_bwd_blocks(int P);
 int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,
                  float* dW2, float* db2, float* part, int P, void* stream);
 
+/* ---- velocity encoder MLP fused (blocks.py:22-29, forward :43-48): rows
+ * K*B of [2S] packed from pos [B][Te][2K] -> 100 tanh -> 100 tanh -> 2.
+ * X/h1/h2 are saved for the backward, which writes per-block partial
+ * [W0|b0|W2|b2|W4|b4] rows (paig_velmlp_bwd_blocks x paig_velmlp_slab_len)
+ * and dX [K*B][2S] (then paig_vel_unpack_add). */
+int paig_velmlp_fwd(const float* pos, int B, int Te, int K, int S, const float* W0, const float* b0, const float* W2,
+                    const float* b2, const float* W4, const float* b4, float* X, float* h1, float* h2, float* vel,
+                    void* stream);
+int paig_velmlp_bwd_blocks(int rows);
+int paig_velmlp_slab_len(int S);
+int paig_velmlp_bwd(const float* dvel, const float* X, const float* h1, const float* h2, const float* W0,
+                    const float* W2, const float* W4, float* dX, float* slab, int rows, int S, void* stream);
+
+/* ---- encoder position head fused: l3 Linear(IN, 2) + split/cat + tanh*H/2+H/2
+ * (blocks.py:100-102) over rows k*F+f of h2 [K*F][IN]; the backward writes
+ * dh2 (with l2's ReLU') and per-block [W3 | b3] partial rows of 2*IN+2. */
+int paig_head_fwd(const float* h2, const float* W3, const float* b3, float* h3, float* pos, int F, int K, int IN,
+                  float half, void* stream);
+int paig_head_bwd_blocks(int rows);
+int paig_head_bwd(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab, int F,
+                  int K, int IN, float half, void* stream);
+
 /* ---- velocity encoder input packing (blocks.py:33-45) */
 int paig_vel_pack(const float* pos, float* X, int B, int Te, int K, int S, int alt, void* stream);
 int paig_vel_unpack_add(const float* dX, const float* dpos0, float* dpos, int B, int Te, int K, int S, int alt,

@@ -27,6 +27,13 @@ SIGNATURES = {
     "paig_conv2d_wgrad": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
     "paig_gather_u8_f32": (I, [P, P, P, I, LL, P]),
+    "paig_velmlp_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
+    "paig_velmlp_bwd_blocks": (I, [I]),
+    "paig_velmlp_slab_len": (I, [I]),
+    "paig_velmlp_bwd": (I, [P, P, P, P, P, P, P, P, P, I, I, P]),
+    "paig_head_fwd": (I, [P, P, P, P, P, I, I, I, F32, P]),
+    "paig_head_bwd_blocks": (I, [I]),
+    "paig_head_bwd": (I, [P, P, P, P, P, P, I, I, I, F32, P]),
     "paig_maxpool2_fwd": (I, [P, LL, P, LL, I, I, I, I, P]),
     "paig_maxpool2_bwd_relu": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
     "paig_upsample2_fwd": (I, [P, LL, P, LL, I, I, I, I, I, I, P]),
@@ -67,7 +74,8 @@ SIGNATURES = {
     "paig_sgd_f64": (I, [P, P, P, LL, F64, F64, I, P]),
 }
 
-_QUERY = {"paig_last_error", "paig_abi_version", "paig_conv2d_mfma_supported", "paig_gemm_workspace", "paig_colsum_workspace",
+_QUERY = {"paig_last_error", "paig_abi_version", "paig_conv2d_mfma_supported", "paig_velmlp_bwd_blocks",
+          "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_gemm_workspace", "paig_colsum_workspace",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
           "paig_decoder_bwd_scratch"}
 

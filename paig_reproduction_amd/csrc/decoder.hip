@@ -336,11 +336,318 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
   }
 }
 
+// ---------------------------------------------------------------------------
+// Register-resident variants for the small frames of the headline workloads
+// ((K, H) = (2, 32) spring/bouncing; the forward also (3, 36) 3bp).  Every thread owns the
+// same PPT pixels and SPT source texels in every frame, so
+//   * the background values it composites are loaded once per block,
+//   * its background / template / content gradients accumulate in registers
+//     and are written to the slab row once at the end (no per-frame global
+//     read-modify-write),
+//   * the next frame's target pixels are prefetched behind the current frame.
+// The generic kernels above remain for the large (mnist 64x64) frames.
+template <int K>
+__device__ __forceinline__ void composite_v(const float* T, const float* Cn, const float* bgv, int h, const Bil* bl,
+                                            float* out, float* m, float (*cs)[3]) {
+  const int hh = h * h;
+  float lg[K + 1];
+  float mx = 1.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float v, dx, dy;
+    sample(T + k * hh, h, bl[k], v, dx, dy);
+    lg[k] = v - 5.f;
+    mx = fmaxf(mx, lg[k]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      sample(Cn + (k * 3 + c) * hh, h, bl[k], v, dx, dy);
+      cs[k][c] = v;
+    }
+  }
+  lg[K] = 1.f;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k <= K; ++k) {
+    m[k] = expf(lg[k] - mx);
+    s += m[k];
+  }
+#pragma unroll
+  for (int k = 0; k <= K; ++k) m[k] = m[k] / s;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float o = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) o += m[k] * cs[k][c];
+    out[c] = o + m[K] * bgv[c];
+  }
+}
+
+template <int K, int H>
+__global__ void __launch_bounds__(256)
+dec_fwd_reg_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse, int F) {
+  constexpr int h = H / 2, hh = h * h, HW = H * H, PPT = (HW + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* T = lds;
+  float* Cn = T + K * hh;
+  __shared__ float red[4];
+  __shared__ float cx[K][MAXH], cy[K][MAXH];
+  stage_sources<K>(S, h, T, Cn);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float bgv[PPT][3], tn[PPT][3];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    const int p = tid + 256 * j;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) bgv[j][c] = (p < HW) ? S.bg[c * HW + p] : 0.f;
+  }
+  auto fetch = [&](int f) {
+    const float* tf = tgt.frame(f);
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = tid + 256 * j;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) tn[j][c] = (p < HW) ? tf[c * HW + p] : 0.f;
+    }
+  };
+  if (sse && (int)blockIdx.x < F) fetch(blockIdx.x);
+  for (int f = blockIdx.x; f < F; f += gridDim.x) {
+    __syncthreads();   // previous frame done with the tables
+    coord_tables<K>(pos.at(f), H, h, cx, cy);
+    __syncthreads();
+    float tc[PPT][3];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) tc[j][c] = tn[j][c];
+    if (sse && f + (int)gridDim.x < F) fetch(f + gridDim.x);
+    float* of = out.frame(f);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = tid + 256 * j;
+      if (p >= HW) break;
+      const int i = p / H, jj = p % H;
+      Bil bl[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) bl[k] = bil(cx[k][jj], cy[k][i]);
+      float o[3], m[K + 1], cs[K][3];
+      composite_v<K>(T, Cn, bgv[j], h, bl, o, m, cs);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        of[c * HW + p] = o[c];
+        const float d = tc[j][c] - o[c];
+        acc = fmaf(d, d, acc);
+      }
+    }
+    if (sse) {
+      acc = wave_sum(acc);
+      if (lane == 0) red[wv] = acc;
+      __syncthreads();
+      if (tid == 0) sse[f] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
+  }
+}
+
+template <int K, int H>
+__global__ void __launch_bounds__(256)
+dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
+              float* __restrict__ slab, int F) {
+  constexpr int h = H / 2, hh = h * h, HW = H * H, PPT = (HW + 255) / 256, SPT = (K * hh + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* T = lds;
+  float* Cn = T + K * hh;
+  float* G = Cn + K * 3 * hh;   // [K][4][HW] per-frame pixel-gradient image
+  __shared__ double redd[4][2 * K];
+  __shared__ float cx[K][MAXH], cy[K][MAXH];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  stage_sources<K>(S, h, T, Cn);
+  float bgv[PPT][3], gbg[PPT][3], tn[PPT][3], gsrc[SPT][4];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    const int p = tid + 256 * j;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      bgv[j][c] = (p < HW) ? S.bg[c * HW + p] : 0.f;
+      gbg[j][c] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < SPT; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) gsrc[j][c] = 0.f;
+  auto fetch = [&](int f) {
+    const float* tf = tgt.frame(f);
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = tid + 256 * j;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) tn[j][c] = (p < HW) ? tf[c * HW + p] : 0.f;
+    }
+  };
+  // frames with no loss weight and no dense gradient contribute nothing (the
+  // extrapolation frames of the rollout decode): walk only the live ones
+  auto live = [&](int f) { return (dsse && dsse[f] != 0.f) || dout.p != nullptr; };
+  if ((int)blockIdx.x < F) fetch(blockIdx.x);
+  for (int f = blockIdx.x; f < F; f += gridDim.x) {
+    float tc[PPT][3];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) tc[j][c] = tn[j][c];
+    if (f + (int)gridDim.x < F) fetch(f + gridDim.x);
+    const float w_f = dsse ? 2.f * dsse[f] : 0.f;
+    if (!live(f)) {   // uniform across the block
+      if (tid < 2 * K) dpos[(long long)f * 2 * K + tid] = 0.f;
+      continue;
+    }
+    const float* dof = dout.p ? dout.frame(f) : nullptr;
+    __syncthreads();   // previous frame's pass 2 done with G and the tables
+    coord_tables<K>(pos.at(f), H, h, cx, cy);
+    __syncthreads();
+    double sx[K], sy[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) sx[k] = sy[k] = 0.0;
+    // ---- pass 1: per-pixel gradients
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = tid + 256 * j;
+      if (p >= HW) break;
+      const int i = p / H, jj = p % H;
+      Bil bl[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) bl[k] = bil(cx[k][jj], cy[k][i]);
+      float o[3], m[K + 1], cs[K][3];
+      composite_v<K>(T, Cn, bgv[j], h, bl, o, m, cs);
+      float g[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        g[c] = w_f * (o[c] - tc[j][c]);
+        if (dof) g[c] += dof[c * HW + p];
+        gbg[j][c] = fmaf(m[K], g[c], gbg[j][c]);
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float dT = 0.f;
+        float dC[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          dC[c] = m[k] * g[c];
+          dT = fmaf(g[c], cs[k][c] - o[c], dT);
+        }
+        dT *= m[k];
+        G[(k * 4 + 0) * HW + p] = dT;
+        float v, dx, dy;
+        sample(T + k * hh, h, bl[k], v, dx, dy);
+        float gx = dT * dx, gy = dT * dy;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          G[(k * 4 + 1 + c) * HW + p] = dC[c];
+          sample(Cn + (k * 3 + c) * hh, h, bl[k], v, dx, dy);
+          gx = fmaf(dC[c], dx, gx);
+          gy = fmaf(dC[c], dy, gy);
+        }
+        sx[k] += (double)gx;
+        sy[k] += (double)gy;
+      }
+    }
+    // ---- per-frame dpos reduction (fp64)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double a = wave_sum_d(sx[k]), b = wave_sum_d(sy[k]);
+      if (lane == 0) {
+        redd[wv][2 * k] = a;
+        redd[wv][2 * k + 1] = b;
+      }
+    }
+    __syncthreads();   // G complete, redd complete
+    if (tid < 2 * K) {
+      const double s = (redd[0][tid] + redd[1][tid]) + (redd[2][tid] + redd[3][tid]);
+      const float dth = (float)(s * (double)h * 0.5);
+      dpos[(long long)f * 2 * K + tid] = -dth / (float)h;
+    }
+    // ---- pass 2: gather this thread's source texels from the pixel-gradient image
+    constexpr float slope = (float)h / (float)H;
+#pragma unroll
+    for (int jt = 0; jt < SPT; ++jt) {
+      const int s = tid + 256 * jt;
+      if (s >= K * hh) break;
+      const int k = s / hh, q = s % hh, ys = q / h, xs = q % h;
+      const float a0x = cx[k][0], a0y = cy[k][0];
+      int jlo = (int)floorf(((float)xs - 1.f - a0x) / slope) - 1, jhi = (int)ceilf(((float)xs + 1.f - a0x) / slope) + 1;
+      int ilo = (int)floorf(((float)ys - 1.f - a0y) / slope) - 1, ihi = (int)ceilf(((float)ys + 1.f - a0y) / slope) + 1;
+      if (jlo < 0) jlo = 0;
+      if (ilo < 0) ilo = 0;
+      if (jhi > H - 1) jhi = H - 1;
+      if (ihi > H - 1) ihi = H - 1;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = ilo; i <= ihi; ++i) {
+        const float iy = cy[k][i];
+        const float fy0 = floorf(iy);
+        const int y0 = (int)fy0;
+        const float fy = iy - fy0;
+        const float wy = (y0 == ys ? 1.f - fy : 0.f) + (y0 + 1 == ys ? fy : 0.f);
+        if (wy == 0.f) continue;
+        float row[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int j = jlo; j <= jhi; ++j) {
+          const float ix = cx[k][j];
+          const float fx0 = floorf(ix);
+          const int x0 = (int)fx0;
+          const float fx = ix - fx0;
+          const float wx = (x0 == xs ? 1.f - fx : 0.f) + (x0 + 1 == xs ? fx : 0.f);
+          if (wx == 0.f) continue;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) row[c] = fmaf(wx, G[(k * 4 + c) * HW + i * H + j], row[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = fmaf(wy, row[c], acc[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) gsrc[jt][c] += acc[c];
+    }
+  }
+  // ---- this block's partial source gradients -> its slab row (every element
+  // owned by exactly one thread; written once)
+  float* srow = slab + (long long)blockIdx.x * ((long long)K * hh * 4 + 3LL * HW);
+  float* s_tm = srow;
+  float* s_ct = srow + K * hh;
+  float* s_bg = s_ct + K * 3 * hh;
+#pragma unroll
+  for (int jt = 0; jt < SPT; ++jt) {
+    const int s = tid + 256 * jt;
+    if (s >= K * hh) break;
+    const int k = s / hh, q = s % hh;
+    s_tm[s] = gsrc[jt][0];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s_ct[(k * 3 + c) * hh + q] = gsrc[jt][1 + c];
+  }
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    const int p = tid + 256 * j;
+    if (p >= HW) break;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s_bg[c * HW + p] = gbg[j][c];
+  }
+}
+
 template <int K>
 static int dec_launch_fwd(PosView pv, Src S, FViewW out, FView tgt, float* sse, int F, int h, int H, hipStream_t st) {
   const int lds = (K * h * h * 4) * 4;
   int g = F < 2048 ? F : 2048;
-  hipLaunchKernelGGL((dec_fwd_k<K>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F, h, H);
+  if constexpr (K == 2) {
+    if (H == 32) {
+      hipLaunchKernelGGL((dec_fwd_reg_k<2, 32>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F);
+      PAIG_CHECK_LAUNCH();
+      return 0;
+    }
+  }
+  if constexpr (K == 3) {
+    if (H == 36) {
+      hipLaunchKernelGGL((dec_fwd_reg_k<3, 36>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F);
+      PAIG_CHECK_LAUNCH();
+      return 0;
+    }
+  }
+    hipLaunchKernelGGL((dec_fwd_k<K>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F, h, H);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -400,7 +707,9 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
   PAIG_REQUIRE(!need_scratch || scratch, "decoder_bwd: scratch required");
   const int lds = (K * h * h * 4 + (need_scratch ? 0 : K * 4 * H * H)) * 4;
   float* gs = need_scratch ? scratch : nullptr;
-  if (K == 2)
+  if (K == 2 && H == 32 && !need_scratch)
+    hipLaunchKernelGGL((dec_bwd_reg_k<2, 32>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, F);
+  else if (K == 2)
     hipLaunchKernelGGL((dec_bwd_k<2>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);
   else if (K == 3)
     hipLaunchKernelGGL((dec_bwd_k<3>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);

@@ -260,9 +260,20 @@ rollout_bwd_k(const float* __restrict__ pvs, const float* __restrict__ dpos_roll
     float gp[D], gv[D];
     for (int d = 0; d < D; ++d) gp[d] = gv[d] = 0.f;
     const float* st = pvs + (long long)b * (R + 1) * 2 * D;
+    // the serial reverse sweep would wait one global-load latency per step for
+    // its inputs: they are prefetched one step ahead, behind the substep math
+    float nd[D], ns[2 * D];
+    for (int d = 0; d < D; ++d) nd[d] = dpos_roll ? dpos_roll[((long long)b * R + (R - 1)) * D + d] : 0.f;
+    for (int d = 0; d < 2 * D; ++d) ns[d] = st[(R - 1) * 2 * D + d];
     for (int t = R; t >= 1; --t) {
-      if (dpos_roll)
-        for (int d = 0; d < D; ++d) gp[d] += dpos_roll[((long long)b * R + (t - 1)) * D + d];
+      float cd[D], cs[2 * D];
+      for (int d = 0; d < D; ++d) cd[d] = nd[d];
+      for (int d = 0; d < 2 * D; ++d) cs[d] = ns[d];
+      if (t > 1) {
+        for (int d = 0; d < D; ++d) nd[d] = dpos_roll ? dpos_roll[((long long)b * R + (t - 2)) * D + d] : 0.f;
+        for (int d = 0; d < 2 * D; ++d) ns[d] = st[(t - 2) * 2 * D + d];
+      }
+      for (int d = 0; d < D; ++d) gp[d] += cd[d];
       if (dpvs)
         for (int d = 0; d < D; ++d) {
           gp[d] += dpvs[((long long)b * (R + 1) + t) * 2 * D + d];
@@ -273,8 +284,8 @@ rollout_bwd_k(const float* __restrict__ pvs, const float* __restrict__ dpos_roll
       unsigned fl[5];
       float p[D], v[D];
       for (int d = 0; d < D; ++d) {
-        p[d] = st[(t - 1) * 2 * D + d];
-        v[d] = st[(t - 1) * 2 * D + D + d];
+        p[d] = cs[d];
+        v[d] = cs[D + d];
       }
 #pragma unroll
       for (int s = 0; s < 5; ++s) {

@@ -1,0 +1,305 @@
+// Velocity encoder MLP, fused (reference VelocityEncoder, nn/network/blocks.py:
+// 22-29 and forward :43-48: object-split rows [K*B, 2*S] -> Linear(2S,100)
+// -> tanh -> Linear(100,100) -> tanh -> Linear(100,2)).
+//
+// 200 rows x 100 hidden units: six dependent GEMM launches of a few
+// microseconds each are pure latency, so the whole forward is ONE launch (row
+// blocks; the input packing of blocks.py:43-45 fused in), and the whole
+// backward is ONE launch writing per-block partial [W0|b0|W2|b2|W4|b4]
+// gradients (the parameters' flat-buffer order) for the step's batched
+// deterministic slab reduction.
+#include "common.h"
+
+namespace {
+
+constexpr int HID = 100, OUT = 2, RB = 8, MAXIN = 16;
+
+// X[r][2t+j] = pos[b][t][2k+j], r = k*B + b (the chunk/cat of blocks.py:43-45)
+__device__ __forceinline__ float packed_in(const float* pos, int B, int Te, int K, int r, int col) {
+  const int k = r / B, b = r % B, t = col >> 1, j = col & 1;
+  return pos[((long long)b * Te + t) * 2 * K + 2 * k + j];
+}
+
+__global__ void __launch_bounds__(128)
+velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const float* __restrict__ W0,
+             const float* __restrict__ b0, const float* __restrict__ W2, const float* __restrict__ b2,
+             const float* __restrict__ W4, const float* __restrict__ b4, float* __restrict__ X,
+             float* __restrict__ h1, float* __restrict__ h2, float* __restrict__ vel) {
+  __shared__ float Xs[RB][MAXIN];
+  __shared__ float H1[RB][HID + 1], H2[RB][HID + 1];
+  const int rows = K * B, r0 = blockIdx.x * RB, tid = threadIdx.x;
+  const int nr = rows - r0 < RB ? rows - r0 : RB;
+  for (int e = tid; e < nr * IN; e += blockDim.x) {
+    const int r = e / IN, c = e % IN;
+    const float v = packed_in(pos, B, Te, K, r0 + r, c);
+    Xs[r][c] = v;
+    X[(long long)(r0 + r) * IN + c] = v;
+  }
+  __syncthreads();
+  if (tid < HID) {
+    float w[MAXIN];
+    for (int i = 0; i < IN; ++i) w[i] = W0[tid * IN + i];
+    for (int r = 0; r < nr; ++r) {
+      float a = b0[tid];
+      for (int i = 0; i < IN; ++i) a = fmaf(Xs[r][i], w[i], a);
+      a = tanhf(a);
+      H1[r][tid] = a;
+      h1[(long long)(r0 + r) * HID + tid] = a;
+    }
+    for (int r = nr; r < RB; ++r) H1[r][tid] = 0.f;   // ragged last block
+  }
+  __syncthreads();
+  if (tid < HID) {
+    float a[RB];
+    for (int r = 0; r < RB; ++r) a[r] = b2[tid];
+    const float* wr = W2 + tid * HID;
+    for (int u = 0; u < HID; ++u) {
+      const float w = wr[u];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) a[r] = fmaf(H1[r][u], w, a[r]);
+    }
+    for (int r = 0; r < nr; ++r) {
+      const float v = tanhf(a[r]);
+      H2[r][tid] = v;
+      h2[(long long)(r0 + r) * HID + tid] = v;
+    }
+  }
+  __syncthreads();
+  // vel[r][j]: one wave per output, lanes split the hidden units
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int o = wv; o < nr * OUT; o += blockDim.x >> 6) {
+    const int r = o / OUT, j = o % OUT;
+    float a = 0.f;
+    for (int t = lane; t < HID; t += 64) a = fmaf(H2[r][t], W4[j * HID + t], a);
+    a = wave_sum(a);
+    if (lane == 0) vel[(long long)(r0 + r) * OUT + j] = a + b4[j];
+  }
+}
+
+// slab row (per block): [W0 (HID*IN) | b0 (HID) | W2 (HID*HID) | b2 (HID) | W4 (OUT*HID) | b4 (OUT)]
+__global__ void __launch_bounds__(256)
+velmlp_bwd_k(const float* __restrict__ dvel, const float* __restrict__ X, const float* __restrict__ h1,
+             const float* __restrict__ h2, const float* __restrict__ W0, const float* __restrict__ W2,
+             const float* __restrict__ W4, float* __restrict__ dX, float* __restrict__ slab, int rows, int IN) {
+  __shared__ float Xs[RB][MAXIN], DV[RB][OUT];
+  __shared__ float H1[RB][HID + 1], DZ2[RB][HID + 1], DZ1[RB][HID + 1];
+  const int r0 = blockIdx.x * RB, tid = threadIdx.x;
+  const int nr = rows - r0 < RB ? rows - r0 : RB;
+  const long long len = (long long)HID * IN + HID + HID * HID + HID + OUT * HID + OUT;
+  float* s = slab + blockIdx.x * len;
+  float* sW0 = s;
+  float* sb0 = sW0 + HID * IN;
+  float* sW2 = sb0 + HID;
+  float* sb2 = sW2 + HID * HID;
+  float* sW4 = sb2 + HID;
+  float* sb4 = sW4 + OUT * HID;
+  for (int e = tid; e < RB * IN; e += blockDim.x) {
+    const int r = e / IN, c = e % IN;
+    Xs[r][c] = r < nr ? X[(long long)(r0 + r) * IN + c] : 0.f;
+  }
+  for (int e = tid; e < RB * HID; e += blockDim.x) {
+    const int r = e / HID, u = e % HID;
+    H1[r][u] = r < nr ? h1[(long long)(r0 + r) * HID + u] : 0.f;
+  }
+  if (tid < RB * OUT) DV[tid / OUT][tid % OUT] = tid / OUT < nr ? dvel[(long long)(r0 + tid / OUT) * OUT + tid % OUT] : 0.f;
+  __syncthreads();
+  // ---- layer 4 (linear): dz2 = (dvel W4) * tanh'(h2);  gW4 = dvel^T h2, gb4 = sum dvel
+  if (tid < HID) {
+    float g4[OUT] = {0.f, 0.f};
+    for (int r = 0; r < RB; ++r) {
+      const float hv = r < nr ? h2[(long long)(r0 + r) * HID + tid] : 0.f;
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < OUT; ++j) {
+        d = fmaf(DV[r][j], W4[j * HID + tid], d);
+        g4[j] = fmaf(DV[r][j], hv, g4[j]);
+      }
+      DZ2[r][tid] = d * (1.f - hv * hv);
+    }
+#pragma unroll
+    for (int j = 0; j < OUT; ++j) sW4[j * HID + tid] = g4[j];
+  }
+  if (tid < OUT) {
+    float a = 0.f;
+    for (int r = 0; r < RB; ++r) a += DV[r][tid];
+    sb4[tid] = a;
+  }
+  __syncthreads();
+  // ---- layer 2: gW2[t][u] = sum_r dz2[r][t] h1[r][u], gb2 = sum dz2
+  for (int e = tid; e < HID * HID; e += blockDim.x) {
+    const int t = e / HID, u = e % HID;
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) a = fmaf(DZ2[r][t], H1[r][u], a);
+    sW2[e] = a;
+  }
+  if (tid < HID) {
+    float a = 0.f;
+    for (int r = 0; r < RB; ++r) a += DZ2[r][tid];
+    sb2[tid] = a;
+    // dz1[r][u = tid] = (sum_t dz2[r][t] W2[t][u]) * tanh'(h1)
+    float d[RB];
+    for (int r = 0; r < RB; ++r) d[r] = 0.f;
+    for (int t = 0; t < HID; ++t) {
+      const float w = W2[t * HID + tid];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) d[r] = fmaf(DZ2[r][t], w, d[r]);
+    }
+    for (int r = 0; r < RB; ++r) DZ1[r][tid] = d[r] * (1.f - H1[r][tid] * H1[r][tid]);
+  }
+  __syncthreads();
+  // ---- layer 0: gW0[u][i] = sum_r dz1[r][u] X[r][i], gb0 = sum dz1, dX = dz1 W0
+  for (int e = tid; e < HID * IN; e += blockDim.x) {
+    const int u = e / IN, i = e % IN;
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) a = fmaf(DZ1[r][u], Xs[r][i], a);
+    sW0[e] = a;
+  }
+  if (tid < HID) {
+    float a = 0.f;
+    for (int r = 0; r < RB; ++r) a += DZ1[r][tid];
+    sb0[tid] = a;
+  }
+  for (int e = tid; e < nr * IN; e += blockDim.x) {
+    const int r = e / IN, i = e % IN;
+    float a = 0.f;
+    for (int u = 0; u < HID; ++u) a = fmaf(DZ1[r][u], W0[u * IN + i], a);
+    dX[(long long)(r0 + r) * IN + i] = a;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int paig_velmlp_fwd(const float* pos, int B, int Te, int K, int S, const float* W0, const float* b0, const float* W2,
+                    const float* b2, const float* W4, const float* b4, float* X, float* h1, float* h2, float* vel,
+                    void* stream) {
+  const int IN = 2 * S, rows = K * B;
+  if (rows <= 0) return 0;
+  PAIG_REQUIRE(IN <= MAXIN && S <= Te, "velmlp: input_steps %d unsupported (max %d)", S, MAXIN / 2);
+  hipLaunchKernelGGL(velmlp_fwd_k, dim3(cdiv(rows, RB)), dim3(128), 0, (hipStream_t)stream, pos, B, Te, K, IN, W0, b0,
+                     W2, b2, W4, b4, X, h1, h2, vel);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_velmlp_bwd_blocks(int rows) { return cdiv(rows, RB); }
+
+int paig_velmlp_slab_len(int S) { return HID * 2 * S + HID + HID * HID + HID + OUT * HID + OUT; }
+
+int paig_velmlp_bwd(const float* dvel, const float* X, const float* h1, const float* h2, const float* W0,
+                    const float* W2, const float* W4, float* dX, float* slab, int rows, int S, void* stream) {
+  const int IN = 2 * S;
+  if (rows <= 0) return 0;
+  PAIG_REQUIRE(IN <= MAXIN, "velmlp: input_steps %d unsupported", S);
+  hipLaunchKernelGGL(velmlp_bwd_k, dim3(cdiv(rows, RB)), dim3(256), 0, (hipStream_t)stream, dvel, X, h1, h2, W0, W2,
+                     W4, dX, slab, rows, IN);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Encoder position head, fused: l3 (Linear(IN=200, 2)) + split/cat + tanh
+// (nn/network/blocks.py:100-102).  Rows n = k*F + f of h2 [K*F][IN]:
+//   h3[n][j] = b3[j] + h2[n] . W3[j],   pos[f][2k+j] = tanh(h3[n][j]) * half + half
+// and its backward (dpos -> dh3 -> dW3/db3 partials + dh2 * relu'(h2)).
+namespace {
+
+constexpr int HEAD_RB = 16;   // rows per backward block
+
+__global__ void __launch_bounds__(256)
+head_fwd_k(const float* __restrict__ h2, const float* __restrict__ W3, const float* __restrict__ b3,
+           float* __restrict__ h3, float* __restrict__ pos, int F, int K, int IN, float half) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   // one wave per row
+  if (n >= K * F) return;
+  const float* x = h2 + (long long)n * IN;
+  float a0 = 0.f, a1 = 0.f;
+  for (int u = lane; u < IN; u += 64) {
+    const float v = x[u];
+    a0 = fmaf(v, W3[u], a0);
+    a1 = fmaf(v, W3[IN + u], a1);
+  }
+  a0 = wave_sum(a0) + b3[0];
+  a1 = wave_sum(a1) + b3[1];
+  if (lane == 0) {
+    const int k = n / F, f = n % F;
+    h3[(long long)n * 2] = a0;
+    h3[(long long)n * 2 + 1] = a1;
+    pos[(long long)f * 2 * K + 2 * k] = tanhf(a0) * half + half;
+    pos[(long long)f * 2 * K + 2 * k + 1] = tanhf(a1) * half + half;
+  }
+}
+
+// slab row per block: [W3 (2*IN) | b3 (2)]
+__global__ void __launch_bounds__(256)
+head_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const float* __restrict__ dpos,
+           const float* __restrict__ W3, float* __restrict__ dh2, float* __restrict__ slab, int F, int K, int IN,
+           float half) {
+  __shared__ float D3[HEAD_RB][2];
+  const int n0 = blockIdx.x * HEAD_RB, rows = K * F, tid = threadIdx.x;
+  const int nr = rows - n0 < HEAD_RB ? rows - n0 : HEAD_RB;
+  if (tid < HEAD_RB * 2) {
+    const int r = tid >> 1, j = tid & 1;
+    float d = 0.f;
+    if (r < nr) {
+      const int n = n0 + r, k = n / F, f = n % F;
+      const float t = tanhf(h3[(long long)n * 2 + j]);
+      d = dpos[(long long)f * 2 * K + 2 * k + j] * half * (1.f - t * t);
+    }
+    D3[r][j] = d;
+  }
+  __syncthreads();
+  float* s = slab + (long long)blockIdx.x * (2 * IN + 2);
+  for (int u = tid; u < IN; u += blockDim.x) {
+    const float w0 = W3[u], w1 = W3[IN + u];
+    float g0 = 0.f, g1 = 0.f;
+    for (int r = 0; r < nr; ++r) {
+      const long long o = (long long)(n0 + r) * IN + u;
+      const float x = h2[o];
+      g0 = fmaf(D3[r][0], x, g0);
+      g1 = fmaf(D3[r][1], x, g1);
+      const float g = fmaf(D3[r][0], w0, D3[r][1] * w1);
+      dh2[o] = x > 0.f ? g : 0.f;                     // relu' of l2's output (blocks.py:99)
+    }
+    s[u] = g0;
+    s[IN + u] = g1;
+  }
+  if (tid < 2) {
+    float a = 0.f;
+    for (int r = 0; r < nr; ++r) a += D3[r][tid];
+    s[2 * IN + tid] = a;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int paig_head_fwd(const float* h2, const float* W3, const float* b3, float* h3, float* pos, int F, int K, int IN,
+                  float half, void* stream) {
+  const int rows = K * F;
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(head_fwd_k, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, h2, W3, b3, h3, pos, F, K, IN,
+                     half);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_head_bwd_blocks(int rows) { return cdiv(rows, HEAD_RB); }
+
+int paig_head_bwd(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab, int F,
+                  int K, int IN, float half, void* stream) {
+  const int rows = K * F;
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(head_bwd_k, dim3(cdiv(rows, HEAD_RB)), dim3(256), 0, (hipStream_t)stream, h2, h3, dpos, W3, dh2,
+                     slab, F, K, IN, half);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -229,6 +229,7 @@ class Engine:
         self.L = lib()
         self.probe = None
         self.last_masked_objs = None
+        self._side = None   # second stream (see _fork)
 
     def _p(self, tag, flops=0):
         return self.probe.wrap(tag, flops) if self.probe is not None else _NOPROBE
@@ -362,43 +363,54 @@ class Engine:
         h3 = _empty(K * F * 2, dev)
         self.linear(l1_x, K * F, "encoder.l1", h1, 1, st, ws)
         self.linear(h1, K * F, "encoder.l2", h2, 1, st, ws)
-        self.linear(h2, K * F, "encoder.l3", h3, 0, st, ws)
         enc_pos = _empty(F * 2 * K, dev)
-        L.paig_pos_head_fwd(ptr(h3), ptr(enc_pos), F, K, float(H / 2), st)
+        L.paig_head_fwd(ptr(h2), ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
+                        ptr(enc_pos), F, K, 200, float(H / 2), st)
         S.update(masks=masks, objs=objs, l1_x=l1_x, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
 
-        # ---- reconstruction decode (all B*Te frames, SSE vs input fused)
+        # Two independent chains follow the position head; they run concurrently:
+        #   side stream: velocity MLP -> physics rollout (one thread per
+        #                sequence: latency-bound, a few blocks)
+        #   main stream: reconstruction decode of all B*Te frames
+        # Everything the side chain touches is allocated before the fork.
         recons = _empty(F * lay.frame, dev)
         sse_rec = _empty(F, dev)
-        L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons), lay.frame,
-                           x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, st)
-
-        # ---- velocity encoder
         vel0 = None
+        vel_args = None
         if lay.ins > 1:
             S_in = lay.ins
             cols = 2 * (S_in - 1 if lay.alt_vel else S_in)
             Xv = _empty(K * B * cols, dev)
-            L.paig_vel_pack(ptr(enc_pos), ptr(Xv), B, lay.Te, K, S_in, int(lay.alt_vel), st)
             vel0 = _empty(K * B * 2, dev)
             if lay.alt_vel:
-                self.linear(Xv, K * B, "velocity_encoder.init_vel_linear", vel0, 0, st, ws)
                 S.update(Xv=Xv)
             else:
                 v1 = _empty(K * B * 100, dev)
                 v2 = _empty(K * B * 100, dev)
-                self.linear(Xv, K * B, "velocity_encoder.init_vel_mlp.0", v1, 2, st, ws)
-                self.linear(v1, K * B, "velocity_encoder.init_vel_mlp.2", v2, 2, st, ws)
-                self.linear(v2, K * B, "velocity_encoder.init_vel_mlp.4", vel0, 0, st, ws)
                 S.update(Xv=Xv, v1=v1, v2=v2)
         S["vel0"] = vel0
-
-        # ---- physics rollout (all R steps in one launch)
         pvs = _empty(B * (lay.R + 1) * 2 * D, dev)
         prm = self.cell_params(lay)
-        L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0), ptr(prm[0]),
-                           ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, st)
         S["pvs"] = pvs
+
+        sst = self._fork(dev)
+        # ---- (side) velocity encoder
+        if vel0 is not None:
+            if lay.alt_vel:
+                L.paig_vel_pack(ptr(enc_pos), ptr(S["Xv"]), B, lay.Te, K, lay.ins, 1, sst)
+                self.linear(S["Xv"], K * B, "velocity_encoder.init_vel_linear", vel0, 0, sst, ws)
+            else:   # the whole MLP (packing fused) in one launch
+                pm = "velocity_encoder.init_vel_mlp."
+                L.paig_velmlp_fwd(ptr(enc_pos), B, lay.Te, K, lay.ins, *[ptr(self.p(pm + n)) for n in (
+                    "0.weight", "0.bias", "2.weight", "2.bias", "4.weight", "4.bias")], ptr(S["Xv"]), ptr(S["v1"]),
+                    ptr(S["v2"]), ptr(vel0), sst)
+        # ---- (side) physics rollout (all R steps in one launch)
+        L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0), ptr(prm[0]),
+                           ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, sst)
+        # ---- (main) reconstruction decode (all B*Te frames, SSE vs input fused)
+        L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons), lay.frame,
+                           x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, st)
+        self._join(dev)
 
         # ---- rollout decode (all B*R frames in one launch, SSE vs input[:, ins:])
         out = _empty(B * lay.R * lay.frame, dev)
@@ -424,6 +436,22 @@ class Engine:
         }
         return res, (S if need_saved else None)
 
+    # -- a second stream for the latency-bound per-sequence chains ---------
+    def _fork(self, dev):
+        """Side stream ordered after everything issued so far on the current
+        stream; graph capture records the fork as a branch."""
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(dev)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        self._side.wait_event(ev)
+        return self._side.cuda_stream
+
+    def _join(self, dev):
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        torch.cuda.current_stream(dev).wait_event(ev)
+
     def cell_params(self, lay):
         m = self.model
         dt = m.rollout_cell.dt
@@ -442,6 +470,7 @@ class Engine:
         dev = x.device
         st = stream_handle(dev)
         ws = S["ws"]
+        S["extra_slabs"] = []   # partial-gradient slabs reduced with the U-Net's at the end
         K, F, HW, H, h, D, B, R = lay.K, lay.F, lay.HW, lay.H, lay.h, lay.D, lay.B, lay.R
         tmpl = S["src"]["var_net_template"][1]
         cont = S["src"]["var_net_content"][1]
@@ -452,7 +481,8 @@ class Engine:
         if d_recons is not None:
             d_recons = d_recons.contiguous()
 
-        # ---- decoder backward (recon + rollout frames), partial source grads
+        # ---- buffers of the whole decoder / rollout / velocity backward (all
+        # allocated on the main stream before the fork below)
         slab_len = int(L.paig_decoder_slab_len(K, h, H))
         nb_rec = L.paig_decoder_bwd_blocks(F)
         nb_roll = L.paig_decoder_bwd_blocks(B * R)
@@ -460,34 +490,29 @@ class Engine:
         scr_n = max(L.paig_decoder_bwd_scratch(F, K, h, H), L.paig_decoder_bwd_scratch(B * R, K, h, H))
         scratch = _empty(scr_n, dev) if scr_n else None
         denc = _empty(F * D, dev)   # d enc_pos [B][Te][D]
-        L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
-                           ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, K, h, H, st)
         dpos_roll = _empty(B * R * D, dev)
+        dsrc = _empty(slab_len, dev)
         pvs = S["pvs"]
+        dpos0 = _empty(B * D, dev)
+        dvel0 = _empty(K * B * 2, dev) if S["vel0"] is not None else None
+        rpart = _empty(2 * L.paig_rollout_bwd_blocks(B), dev, torch.float64)
+        dXv = vslab = None
+        if S["vel0"] is not None:
+            dXv = _empty(K * B * 2 * (lay.ins - 1 if lay.alt_vel else lay.ins), dev)
+            if not lay.alt_vel:
+                vblk, vlen = L.paig_velmlp_bwd_blocks(K * B), L.paig_velmlp_slab_len(lay.ins)
+                vslab = _empty(vblk * vlen, dev)
+        vfn = (("var_net_template", K * h * h, 0, tmpl), ("var_net_content", K * 3 * h * h, 1, cont),
+               ("var_net_background", 3 * HW, 1, S["src"]["var_net_background"][1]))
+        vparts = [_empty(L.paig_vfn_bwd_blocks(P) * 200, dev) for _, P, _, _ in vfn]
+
+        # ---- (main) rollout-frame decoder backward: d rollout positions + partial source grads
         L.paig_decoder_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
                            *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
                            ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, K, h, H, st)
-        dsrc = _empty(slab_len, dev)
-        L.paig_slab_reduce_multi(1, (ctypes.c_void_p * 1)(ptr(slab)), (ctypes.c_int * 1)(nb_rec + nb_roll),
-                                 (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, st)
-        if d_enc_pos is not None:
-            L.paig_axpby(ptr(d_enc_pos.contiguous()), ptr(denc), F * D, 1.0, 1.0, st)
 
-        # ---- VariableFromNetwork backward
-        off = 0
-        for nm, P, sig, raw in (("var_net_template", K * h * h, 0, tmpl), ("var_net_content", K * 3 * h * h, 1, cont),
-                                ("var_net_background", 3 * HW, 1, S["src"]["var_net_background"][1])):
-            hv = S["src"][nm][0]
-            part = _empty(L.paig_vfn_bwd_blocks(P) * 200, dev)
-            L.paig_vfn_bwd(ptr(dsrc) + off * 4, ptr(raw), sig, ptr(hv), ptr(self.p(nm + ".l2.weight")),
-                           ptr(self.g(nm + ".l1.weight")), ptr(self.g(nm + ".l1.bias")), ptr(self.g(nm + ".l2.weight")),
-                           ptr(self.g(nm + ".l2.bias")), ptr(part), P, st)
-            off += P
-
-        # ---- rollout adjoint -> d pos0, d vel0, physics params
-        dpos0 = _empty(B * D, dev)
-        dvel0 = _empty(K * B * 2, dev) if S["vel0"] is not None else None
-        part = _empty(2 * L.paig_rollout_bwd_blocks(B), dev, torch.float64)
+        sst = self._fork(dev)
+        # ---- (side) rollout adjoint -> d pos0, d vel0, physics params
         prm = self.cell_params(lay)
         gk = gq = None
         if lay.cell == 0:
@@ -495,31 +520,50 @@ class Engine:
         elif lay.cell == 2:
             gk = self.g("rollout_cell.g")
         L.paig_rollout_bwd(lay.cell, ptr(pvs), ptr(dpos_roll), ptr(d_pvs.contiguous() if d_pvs is not None else None),
-                           ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(dpos0), ptr(dvel0), ptr(part), ptr(gk), ptr(gq),
-                           0, B, D, R, st)
-
-        # ---- velocity encoder backward -> d enc_pos[:, :ins]
-        dXv = None
+                           ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(dpos0), ptr(dvel0), ptr(rpart), ptr(gk), ptr(gq),
+                           0, B, D, R, sst)
+        # ---- (side) velocity encoder backward -> d packed inputs
         if S["vel0"] is not None:
-            cols = 2 * (lay.ins - 1 if lay.alt_vel else lay.ins)
-            dXv = _empty(K * B * cols, dev)
             if lay.alt_vel:
-                self.linear_bwd(S["Xv"], dvel0, K * B, "velocity_encoder.init_vel_linear", dXv, None, 0, st, ws)
-            else:
-                dv2 = _empty(K * B * 100, dev)
-                dv1 = _empty(K * B * 100, dev)
-                self.linear_bwd(S["v2"], dvel0, K * B, "velocity_encoder.init_vel_mlp.4", dv2, S["v2"], 2, st, ws)
-                self.linear_bwd(S["v1"], dv2, K * B, "velocity_encoder.init_vel_mlp.2", dv1, S["v1"], 2, st, ws)
-                self.linear_bwd(S["Xv"], dv1, K * B, "velocity_encoder.init_vel_mlp.0", dXv, None, 0, st, ws)
+                self.linear_bwd(S["Xv"], dvel0, K * B, "velocity_encoder.init_vel_linear", dXv, None, 0, sst, ws)
+            else:   # one launch; its partial weight grads join the U-Net's batched slab reduction
+                pm = "velocity_encoder.init_vel_mlp."
+                L.paig_velmlp_bwd(ptr(dvel0), ptr(S["Xv"]), ptr(S["v1"]), ptr(S["v2"]), ptr(self.p(pm + "0.weight")),
+                                  ptr(self.p(pm + "2.weight")), ptr(self.p(pm + "4.weight")), ptr(dXv), ptr(vslab),
+                                  K * B, lay.ins, sst)
+                g0 = self.g(pm + "0.weight")
+                assert self.g(pm + "4.bias").data_ptr() == g0.data_ptr() + (vlen - 2) * 4, "velocity MLP grads not contiguous"
+                S["extra_slabs"].append((vslab, vblk, vlen, g0))
+
+        # ---- (main) reconstruction decoder backward, source-grad reduction, VFN backward
+        L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
+                           ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, K, h, H, st)
+        L.paig_slab_reduce_multi(1, (ctypes.c_void_p * 1)(ptr(slab)), (ctypes.c_int * 1)(nb_rec + nb_roll),
+                                 (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, st)
+        if d_enc_pos is not None:
+            L.paig_axpby(ptr(d_enc_pos.contiguous()), ptr(denc), F * D, 1.0, 1.0, st)
+        off = 0
+        for (nm, P, sig, raw), part in zip(vfn, vparts):
+            hv = S["src"][nm][0]
+            L.paig_vfn_bwd(ptr(dsrc) + off * 4, ptr(raw), sig, ptr(hv), ptr(self.p(nm + ".l2.weight")),
+                           ptr(self.g(nm + ".l1.weight")), ptr(self.g(nm + ".l1.bias")), ptr(self.g(nm + ".l2.weight")),
+                           ptr(self.g(nm + ".l2.bias")), ptr(part), P, st)
+            off += P
+        self._join(dev)
+
         L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
 
         # ---- position head + localiser MLP backward -> d masked objects
-        dh3 = _empty(K * F * 2, dev)
-        L.paig_pos_head_bwd(ptr(S["h3"]), ptr(denc), ptr(dh3), F, K, float(H / 2), st)
         dh2 = _empty(K * F * 200, dev)
+        hblk = L.paig_head_bwd_blocks(K * F)
+        hslab = _empty(hblk * (2 * 200 + 2), dev)
+        L.paig_head_bwd(ptr(S["h2"]), ptr(S["h3"]), ptr(denc), ptr(self.p("encoder.l3.weight")), ptr(dh2), ptr(hslab),
+                        F, K, 200, float(H / 2), st)
+        g3 = self.g("encoder.l3.weight")
+        assert self.g("encoder.l3.bias").data_ptr() == g3.data_ptr() + 400 * 4, "l3 grads not contiguous"
+        S["extra_slabs"].append((hslab, hblk, 402, g3))
         dh1 = _empty(K * F * 200, dev)
         dobjs = _empty(K * F * lay.l1_in, dev)
-        self.linear_bwd(S["h2"], dh3, K * F, "encoder.l3", dh2, S["h2"], 1, st, ws)
         self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws)
         self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
 
@@ -624,7 +668,9 @@ class Engine:
                 L.paig_upsample2_bwd(dyv[0], dyv[1], sv[0], sv[1], dxv[0], dxv[1], F, src[2], Hs, Hs, Ho, Ho,
                                      int(relu), st)
                 mark(src)
-        # all conv weight/bias gradients: one batched deterministic reduction
+        # all conv weight/bias gradients (+ the velocity MLP's): one batched
+        # deterministic reduction
+        slabs = slabs + S.get("extra_slabs", [])
         n = len(slabs)
         srcs = (ctypes.c_void_p * n)(*[ptr(s[0]) for s in slabs])
         nbs = (ctypes.c_int * n)(*[s[1] for s in slabs])

@@ -314,6 +314,8 @@ class PhysicsNet(BaseNetTorch):
             return
         batch_size = min(self.batch_size, 4)
         feed_dict, (batch_x, _) = self.get_batch(batch_size, self.test_iterator)
+        if torch.is_tensor(batch_x):   # device-resident dataset (F2)
+            batch_x = batch_x.detach().cpu().numpy()
         if not hasattr(self, "output") or self.output is None:
             return
         output_seq = self.output.detach().cpu().numpy()[:batch_size]
