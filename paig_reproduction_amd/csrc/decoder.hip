@@ -338,31 +338,80 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
 
 // ---------------------------------------------------------------------------
 // Register-resident variants for the small frames of the headline workloads
-// ((K, H) = (2, 32) spring/bouncing; the forward also (3, 36) 3bp).  Every thread owns the
-// same PPT pixels and SPT source texels in every frame, so
+// ((K, H) = (2, 32) spring/bouncing; the forward also (3, 36) 3bp).  Every
+// thread owns the same PPT pixels and SPT source texels in every frame, so
 //   * the background values it composites are loaded once per block,
 //   * its background / template / content gradients accumulate in registers
 //     and are written to the slab row once at the end (no per-frame global
 //     read-modify-write),
-//   * the next frame's target pixels are prefetched behind the current frame.
+//   * the next frame's target pixels are prefetched behind the current frame,
+//   * the bilinear tap weights (and their d/dix, d/diy) are formed once per
+//     (pixel, object) and shared by the template and the 3 content planes,
+//   * the backward's source-gradient gather walks per-frame weight tables
+//     (at most 5 contributing output rows / columns per texel).
 // The generic kernels above remain for the large (mnist 64x64) frames.
+struct Taps {
+  int o[4];      // offsets of nw, ne, sw, se in an h x h plane (0 when out of range)
+  float w[4];    // bilinear weights (0 for out-of-range taps: zero padding)
+  float wx[4];   // d weight / d ix
+  float wy[4];   // d weight / d iy
+};
+
+__device__ __forceinline__ Taps make_taps(const Bil& b, int h) {
+  Taps t;
+  const bool x0 = b.x0 >= 0 && b.x0 < h, x1 = b.x0 + 1 >= 0 && b.x0 + 1 < h;
+  const bool y0 = b.y0 >= 0 && b.y0 < h, y1 = b.y0 + 1 >= 0 && b.y0 + 1 < h;
+  const bool v[4] = {x0 && y0, x1 && y0, x0 && y1, x1 && y1};
+  const int xs[4] = {b.x0, b.x0 + 1, b.x0, b.x0 + 1}, ys[4] = {b.y0, b.y0, b.y0 + 1, b.y0 + 1};
+  const float ex = 1.f - b.fx, ey = 1.f - b.fy;
+  const float w[4] = {ex * ey, b.fx * ey, ex * b.fy, b.fx * b.fy};
+  const float wx[4] = {-ey, ey, -b.fy, b.fy};
+  const float wy[4] = {-ex, -b.fx, ex, b.fx};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    t.o[q] = v[q] ? ys[q] * h + xs[q] : 0;
+    t.w[q] = v[q] ? w[q] : 0.f;
+    t.wx[q] = v[q] ? wx[q] : 0.f;
+    t.wy[q] = v[q] ? wy[q] : 0.f;
+  }
+  return t;
+}
+
+// template (plane 0) and content (planes 1..3) of object k at one pixel:
+// values, and (BWD) their d/dix, d/diy
+template <bool BWD>
+__device__ __forceinline__ void sample4(const float* Tk, const float* Ck, int hh, const Taps& t, float* v, float* dx,
+                                        float* dy) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float* s = c == 0 ? Tk : Ck + (c - 1) * hh;
+    float a = 0.f, gx = 0.f, gy = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float x = s[t.o[q]];
+      a = fmaf(x, t.w[q], a);
+      if (BWD) {
+        gx = fmaf(x, t.wx[q], gx);
+        gy = fmaf(x, t.wy[q], gy);
+      }
+    }
+    v[c] = a;
+    if (BWD) {
+      dx[c] = gx;
+      dy[c] = gy;
+    }
+  }
+}
+
+// softmax compositing of K objects + background from sampled planes sv[k][0..3]
 template <int K>
-__device__ __forceinline__ void composite_v(const float* T, const float* Cn, const float* bgv, int h, const Bil* bl,
-                                            float* out, float* m, float (*cs)[3]) {
-  const int hh = h * h;
+__device__ __forceinline__ void blend(const float (*sv)[4], const float* bgv, float* out, float* m) {
   float lg[K + 1];
   float mx = 1.f;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    float v, dx, dy;
-    sample(T + k * hh, h, bl[k], v, dx, dy);
-    lg[k] = v - 5.f;
+    lg[k] = sv[k][0] - 5.f;
     mx = fmaxf(mx, lg[k]);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      sample(Cn + (k * 3 + c) * hh, h, bl[k], v, dx, dy);
-      cs[k][c] = v;
-    }
   }
   lg[K] = 1.f;
   float s = 0.f;
@@ -377,7 +426,7 @@ __device__ __forceinline__ void composite_v(const float* T, const float* Cn, con
   for (int c = 0; c < 3; ++c) {
     float o = 0.f;
 #pragma unroll
-    for (int k = 0; k < K; ++k) o += m[k] * cs[k][c];
+    for (int k = 0; k < K; ++k) o += m[k] * sv[k][1 + c];
     out[c] = o + m[K] * bgv[c];
   }
 }
@@ -427,11 +476,13 @@ dec_fwd_reg_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse
       const int p = tid + 256 * j;
       if (p >= HW) break;
       const int i = p / H, jj = p % H;
-      Bil bl[K];
+      float sv[K][4], o[3], m[K + 1];
 #pragma unroll
-      for (int k = 0; k < K; ++k) bl[k] = bil(cx[k][jj], cy[k][i]);
-      float o[3], m[K + 1], cs[K][3];
-      composite_v<K>(T, Cn, bgv[j], h, bl, o, m, cs);
+      for (int k = 0; k < K; ++k) {
+        const Taps t = make_taps(bil(cx[k][jj], cy[k][i]), h);
+        sample4<false>(T + k * hh, Cn + k * 3 * hh, hh, t, sv[k], nullptr, nullptr);
+      }
+      blend<K>(sv, bgv[j], o, m);
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         of[c * HW + p] = o[c];
@@ -448,6 +499,38 @@ dec_fwd_reg_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse
   }
 }
 
+// Per-frame gather tables of the backward: for source column xs (row ys) of
+// object k, the output columns (rows) j0 .. j0+4 and their bilinear weights
+// (nonzero where floor(c[j]) == s: 1 - frac, or floor(c[j]) + 1 == s: frac).
+// With the 2x upsampling warp at most 4 output indices contribute.
+constexpr int GW = 5;
+template <int K, int H>
+__device__ __forceinline__ void gather_tables(const float (*cx)[MAXH], const float (*cy)[MAXH], int (*j0)[2][H / 2],
+                                              float (*wt)[2][H / 2][GW]) {
+  constexpr int h = H / 2;
+  for (int t = threadIdx.x; t < K * 2 * h; t += blockDim.x) {
+    const int k = t / (2 * h), ax = (t / h) & 1, s = t % h;
+    const float* c = ax ? cy[k] : cx[k];
+    // first output index whose sample lies at or right of s-1
+    int j = (int)floorf(2.f * ((float)s - 1.f - c[0])) - 2;
+    if (j < 0) j = 0;
+    while (j < H && floorf(c[j]) < (float)(s - 1)) ++j;
+    j0[k][ax][s] = j;
+#pragma unroll
+    for (int b = 0; b < GW; ++b) {
+      const int jj = j + b;
+      float w = 0.f;
+      if (jj < H) {
+        const float v = c[jj], f0 = floorf(v);
+        const int x0 = (int)f0;
+        const float fr = v - f0;
+        w = (x0 == s ? 1.f - fr : 0.f) + (x0 + 1 == s ? fr : 0.f);
+      }
+      wt[k][ax][s][b] = w;
+    }
+  }
+}
+
 template <int K, int H>
 __global__ void __launch_bounds__(256)
 dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
@@ -459,6 +542,8 @@ dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVi
   float* G = Cn + K * 3 * hh;   // [K][4][HW] per-frame pixel-gradient image
   __shared__ double redd[4][2 * K];
   __shared__ float cx[K][MAXH], cy[K][MAXH];
+  __shared__ int j0[K][2][h];
+  __shared__ float wt[K][2][h][GW];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   stage_sources<K>(S, h, T, Cn);
   float bgv[PPT][3], gbg[PPT][3], tn[PPT][3], gsrc[SPT][4];
@@ -504,6 +589,7 @@ dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVi
     __syncthreads();   // previous frame's pass 2 done with G and the tables
     coord_tables<K>(pos.at(f), H, h, cx, cy);
     __syncthreads();
+    gather_tables<K, H>(cx, cy, j0, wt);   // read only after the barrier below
     double sx[K], sy[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) sx[k] = sy[k] = 0.0;
@@ -513,11 +599,14 @@ dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVi
       const int p = tid + 256 * j;
       if (p >= HW) break;
       const int i = p / H, jj = p % H;
-      Bil bl[K];
+      Taps tp[K];
+      float sv[K][4], sdx[K][4], sdy[K][4], o[3], m[K + 1];
 #pragma unroll
-      for (int k = 0; k < K; ++k) bl[k] = bil(cx[k][jj], cy[k][i]);
-      float o[3], m[K + 1], cs[K][3];
-      composite_v<K>(T, Cn, bgv[j], h, bl, o, m, cs);
+      for (int k = 0; k < K; ++k) {
+        tp[k] = make_taps(bil(cx[k][jj], cy[k][i]), h);
+        sample4<true>(T + k * hh, Cn + k * 3 * hh, hh, tp[k], sv[k], sdx[k], sdy[k]);
+      }
+      blend<K>(sv, bgv[j], o, m);
       float g[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -532,19 +621,16 @@ dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVi
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           dC[c] = m[k] * g[c];
-          dT = fmaf(g[c], cs[k][c] - o[c], dT);
+          dT = fmaf(g[c], sv[k][1 + c] - o[c], dT);
         }
         dT *= m[k];
         G[(k * 4 + 0) * HW + p] = dT;
-        float v, dx, dy;
-        sample(T + k * hh, h, bl[k], v, dx, dy);
-        float gx = dT * dx, gy = dT * dy;
+        float gx = dT * sdx[k][0], gy = dT * sdy[k][0];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           G[(k * 4 + 1 + c) * HW + p] = dC[c];
-          sample(Cn + (k * 3 + c) * hh, h, bl[k], v, dx, dy);
-          gx = fmaf(dC[c], dx, gx);
-          gy = fmaf(dC[c], dy, gy);
+          gx = fmaf(dC[c], sdx[k][1 + c], gx);
+          gy = fmaf(dC[c], sdy[k][1 + c], gy);
         }
         sx[k] += (double)gx;
         sy[k] += (double)gy;
@@ -559,47 +645,35 @@ dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVi
         redd[wv][2 * k + 1] = b;
       }
     }
-    __syncthreads();   // G complete, redd complete
+    __syncthreads();   // G, redd and the gather tables complete
     if (tid < 2 * K) {
       const double s = (redd[0][tid] + redd[1][tid]) + (redd[2][tid] + redd[3][tid]);
       const float dth = (float)(s * (double)h * 0.5);
       dpos[(long long)f * 2 * K + tid] = -dth / (float)h;
     }
     // ---- pass 2: gather this thread's source texels from the pixel-gradient image
-    constexpr float slope = (float)h / (float)H;
 #pragma unroll
     for (int jt = 0; jt < SPT; ++jt) {
       const int s = tid + 256 * jt;
       if (s >= K * hh) break;
       const int k = s / hh, q = s % hh, ys = q / h, xs = q % h;
-      const float a0x = cx[k][0], a0y = cy[k][0];
-      int jlo = (int)floorf(((float)xs - 1.f - a0x) / slope) - 1, jhi = (int)ceilf(((float)xs + 1.f - a0x) / slope) + 1;
-      int ilo = (int)floorf(((float)ys - 1.f - a0y) / slope) - 1, ihi = (int)ceilf(((float)ys + 1.f - a0y) / slope) + 1;
-      if (jlo < 0) jlo = 0;
-      if (ilo < 0) ilo = 0;
-      if (jhi > H - 1) jhi = H - 1;
-      if (ihi > H - 1) ihi = H - 1;
+      const int i0 = j0[k][1][ys], c0 = j0[k][0][xs];
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int i = ilo; i <= ihi; ++i) {
-        const float iy = cy[k][i];
-        const float fy0 = floorf(iy);
-        const int y0 = (int)fy0;
-        const float fy = iy - fy0;
-        const float wy = (y0 == ys ? 1.f - fy : 0.f) + (y0 + 1 == ys ? fy : 0.f);
-        if (wy == 0.f) continue;
-        float row[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int j = jlo; j <= jhi; ++j) {
-          const float ix = cx[k][j];
-          const float fx0 = floorf(ix);
-          const int x0 = (int)fx0;
-          const float fx = ix - fx0;
-          const float wx = (x0 == xs ? 1.f - fx : 0.f) + (x0 + 1 == xs ? fx : 0.f);
-          if (wx == 0.f) continue;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) row[c] = fmaf(wx, G[(k * 4 + c) * HW + i * H + j], row[c]);
+      for (int a = 0; a < GW; ++a) {
+        const float wy = wt[k][1][ys][a];
+        if (wy == 0.f) continue;
+        const int row = (i0 + a) * H;
+        float r4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < GW; ++b) {
+          const float wx = wt[k][0][xs][b];
+          const int col = c0 + b < H ? c0 + b : H - 1;   // weight is 0 past the edge
+#pragma unroll
+          for (int c = 0; c < 4; ++c) r4[c] = fmaf(wx, G[(k * 4 + c) * HW + row + col], r4[c]);
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = fmaf(wy, row[c], acc[c]);
+        for (int c = 0; c < 4; ++c) acc[c] = fmaf(wy, r4[c], acc[c]);
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) gsrc[jt][c] += acc[c];
