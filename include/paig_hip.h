@@ -154,10 +154,13 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
 
 /* ---- losses (physics_models.py:119-142): means of the per-frame SSE;
  *      extrap is NaN when there are no extrapolation steps (mean of empty) */
-int paig_loss_reduce(const float* sse_rec, const float* sse_roll, int B, int Te, int R, int pred, float* pred_out,
-                     float* extrap_out, float* recons_out, void* stream);
-int paig_loss_bwd(const float* dpred, const float* dext, const float* drec, float* wrec, float* wroll, int B, int Te,
-                  int R, int pred, void* stream);
+/* pred_out receives train = pred + ae * recons (ae > 0; the reference's
+ * in-place += that also makes pred_loss alias train_loss, Q2); loss_bwd's
+ * dpred is that output's adjoint. */
+int paig_loss_reduce(const float* sse_rec, const float* sse_roll, int B, int Te, int R, int pred, float ae,
+                     float* pred_out, float* extrap_out, float* recons_out, void* stream);
+int paig_loss_bwd(const float* dpred, const float* dext, const float* drec, float ae, float* wrec, float* wroll, int B,
+                  int Te, int R, int pred, void* stream);
 int paig_frame_sse(const float* a, long long a_fs, int a_grp, long long a_gs, const float* b, long long b_fs, int b_grp,
                    long long b_gs, float* sse, int F, int n, void* stream);
 int paig_frame_sse_bwd(const float* a, long long a_fs, int a_grp, long long a_gs, const float* b, long long b_fs,

@@ -62,8 +62,8 @@ SIGNATURES = {
     "paig_decoder_slab_len": (SZ, [I, I, I]),
     "paig_decoder_bwd_scratch": (SZ, [I, I, I, I]),
     "paig_decoder_bwd": (I, [P, LL, LL, I, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, P]),
-    "paig_loss_reduce": (I, [P, P, I, I, I, I, P, P, P, P]),
-    "paig_loss_bwd": (I, [P, P, P, P, P, I, I, I, I, P]),
+    "paig_loss_reduce": (I, [P, P, I, I, I, I, F32, P, P, P, P]),
+    "paig_loss_bwd": (I, [P, P, P, F32, P, P, I, I, I, I, P]),
     "paig_frame_sse": (I, [P, LL, I, LL, P, LL, I, LL, P, I, I, P]),
     "paig_frame_sse_bwd": (I, [P, LL, I, LL, P, LL, I, LL, P, P, I, I, P]),
     "paig_rmsprop_f32": (I, [P, P, P, LL, F32, F32, F32, P]),

@@ -224,6 +224,7 @@ __global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restr
 static int choose_split(int M, int N, int K) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
   int s = 1;
+  if (K < 512) return 1;   // a short K loop costs less than the split-K epilogue launch
   while (tiles * s < 1024 && cdiv(K, 2 * s) >= BK && (long long)(2 * s) * M * N <= (4ll << 20)) s *= 2;
   return s;
 }

@@ -99,7 +99,7 @@ __global__ void vfn_bwd2_k(const float* __restrict__ part, int nblk, const float
 
 // losses: pred, extrap, recons (means of per-frame SSE)
 __global__ void loss_reduce_k(const float* __restrict__ sse_rec, const float* __restrict__ sse_roll, int B, int Te,
-                              int R, int pred, float* __restrict__ o_pred, float* __restrict__ o_ext,
+                              int R, int pred, float ae, float* __restrict__ o_pred, float* __restrict__ o_ext,
                               float* __restrict__ o_rec) {
   __shared__ float red[3][4];
   float a = 0.f, b = 0.f, c = 0.f;
@@ -122,19 +122,25 @@ __global__ void loss_reduce_k(const float* __restrict__ sse_rec, const float* __
   if (threadIdx.x == 0) {
     float s[3];
     for (int k = 0; k < 3; ++k) s[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
-    *o_pred = s[0] / (float)(B * pred);
+    const float pl = s[0] / (float)(B * pred), rl = s[2] / (float)(B * Te);
+    // train = pred (+= ae * recons, physics_models.py:137-141: a separate fp32
+    // multiply then add, never contracted into an FMA)
+    *o_pred = ae > 0.f ? __fadd_rn(pl, __fmul_rn(ae, rl)) : pl;
     *o_ext = (R - pred) > 0 ? s[1] / (float)(B * (R - pred)) : nanf("");
-    *o_rec = s[2] / (float)(B * Te);
+    *o_rec = rl;
   }
 }
 
-// per-frame loss weights from the loss adjoints (any may be null = 0)
+// per-frame loss weights from the loss adjoints (any may be null = 0);
+// dpred is the adjoint of train = pred + ae * recons
 __global__ void loss_bwd_k(const float* __restrict__ dpred, const float* __restrict__ dext,
-                           const float* __restrict__ drec, float* __restrict__ wrec, float* __restrict__ wroll, int B,
-                           int Te, int R, int pred) {
-  const float gp = dpred ? *dpred / (float)(B * pred) : 0.f;
+                           const float* __restrict__ drec, float ae, float* __restrict__ wrec,
+                           float* __restrict__ wroll, int B, int Te, int R, int pred) {
+  const float dt = dpred ? *dpred : 0.f;
+  const float gp = dt / (float)(B * pred);
   const float ge = (dext && R > pred) ? *dext / (float)(B * (R - pred)) : 0.f;
-  const float gr = drec ? *drec / (float)(B * Te) : 0.f;
+  const float dr = (ae > 0.f ? ae * dt : 0.f) + (drec ? *drec : 0.f);
+  const float gr = dr / (float)(B * Te);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * R; i += gridDim.x * blockDim.x)
     if (wroll) wroll[i] = (i % R) < pred ? gp : ge;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * Te; i += gridDim.x * blockDim.x)
@@ -252,18 +258,18 @@ int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const 
   return 0;
 }
 
-int paig_loss_reduce(const float* sse_rec, const float* sse_roll, int B, int Te, int R, int pred, float* pred_out,
+int paig_loss_reduce(const float* sse_rec, const float* sse_roll, int B, int Te, int R, int pred, float ae, float* pred_out,
                      float* extrap_out, float* recons_out, void* stream) {
   hipLaunchKernelGGL(loss_reduce_k, dim3(1), dim3(256), 0, (hipStream_t)stream, sse_rec, sse_roll, B, Te, R, pred,
-                     pred_out, extrap_out, recons_out);
+                     ae, pred_out, extrap_out, recons_out);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
 
-int paig_loss_bwd(const float* dpred, const float* dext, const float* drec, float* wrec, float* wroll, int B, int Te,
-                  int R, int pred, void* stream) {
+int paig_loss_bwd(const float* dpred, const float* dext, const float* drec, float ae, float* wrec, float* wroll, int B,
+                  int Te, int R, int pred, void* stream) {
   hipLaunchKernelGGL(loss_bwd_k, dim3(grid_for((long long)B * (R > Te ? R : Te))), dim3(256), 0, (hipStream_t)stream,
-                     dpred, dext, drec, wrec, wroll, B, Te, R, pred);
+                     dpred, dext, drec, ae, wrec, wroll, B, Te, R, pred);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

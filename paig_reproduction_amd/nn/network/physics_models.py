@@ -70,26 +70,29 @@ class _PhysicsStep(torch.autograd.Function):
 
 
 class _LossReduce(torch.autograd.Function):
-    """Per-frame SSE -> (pred, extrap, recons) means (physics_models.py:119-135)."""
+    """Per-frame SSE -> (train, extrap, recons) (physics_models.py:119-141):
+    train = pred + ae * recons formed in the kernel -- the value the
+    reference's in-place ``+=`` leaves in BOTH train_loss and pred_loss (Q2)."""
 
     @staticmethod
-    def forward(ctx, sse_rec, sse_roll, B, Te, R, pred):
+    def forward(ctx, sse_rec, sse_roll, B, Te, R, pred, ae):
         dev = sse_rec.device
         o = [torch.empty((), device=dev) for _ in range(3)]
-        lib().paig_loss_reduce(ptr(sse_rec), ptr(sse_roll), B, Te, R, pred, ptr(o[0]), ptr(o[1]), ptr(o[2]),
-                               stream_handle(dev))
-        ctx.shape = (B, Te, R, pred)
+        lib().paig_loss_reduce(ptr(sse_rec), ptr(sse_roll), B, Te, R, pred, float(ae), ptr(o[0]), ptr(o[1]),
+                               ptr(o[2]), stream_handle(dev))
+        ctx.shape = (B, Te, R, pred, float(ae))
         ctx.dev = dev
         ctx.set_materialize_grads(False)
         return o[0], o[1], o[2]
 
     @staticmethod
-    def backward(ctx, dp, de, dr):
-        B, Te, R, pred = ctx.shape
+    def backward(ctx, dt, de, dr):
+        B, Te, R, pred, ae = ctx.shape
         wrec = torch.empty(B * Te, device=ctx.dev)
         wroll = torch.empty(B * R, device=ctx.dev)
-        lib().paig_loss_bwd(ptr(dp), ptr(de), ptr(dr), ptr(wrec), ptr(wroll), B, Te, R, pred, stream_handle(ctx.dev))
-        return wrec, wroll, None, None, None, None
+        lib().paig_loss_bwd(ptr(dt), ptr(de), ptr(dr), ae, ptr(wrec), ptr(wroll), B, Te, R, pred,
+                            stream_handle(ctx.dev))
+        return wrec, wroll, None, None, None, None, None
 
 
 class _FrameSSE(torch.autograd.Function):
@@ -233,13 +236,14 @@ class PhysicsNet(BaseNetTorch):
             sse_roll = self._sse_roll
         else:
             sse_roll = _FrameSSE.apply(self.output, self.input, self.input_steps)
-        pred, extrap, recons = _LossReduce.apply(sse_rec, sse_roll, B, Te, R, self.pred_steps)
+        # train = pred + ae * recons in one kernel; pred_loss IS train_loss, as
+        # after the reference's in-place ``train_loss += ae * recons`` (Q2)
+        train, extrap, recons = _LossReduce.apply(sse_rec, sse_roll, B, Te, R, self.pred_steps,
+                                                  self.autoencoder_loss)
         self.recons_loss = recons
-        self.pred_loss = pred
+        self.pred_loss = train
         self.extrap_loss = extrap
         train_loss = self.pred_loss
-        if self.autoencoder_loss > 0.0:
-            train_loss += self.autoencoder_loss * self.recons_loss
         eval_losses = [self.pred_loss, self.extrap_loss, self.recons_loss]
         return train_loss, eval_losses
 
