@@ -362,6 +362,9 @@ template <int CIN, int COUT, int H, int W, int KS, bool UPS>
 __global__ void __launch_bounds__(256)
 conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles) {
   using C = WgCfg<CIN, COUT, H, W, KS>;
+  // staging index math recomputed (opaque) rather than hoisted where that
+  // buys a wave of occupancy -- measured per shape (r01 profiles)
+  constexpr bool WG_OPQ = (H == 16 && (CIN == 16 || UPS)) || (UPS && H >= 32);
   constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   constexpr int KK = C::KK, NT = C::NT, MT = C::MT, WN = C::WN, WP = C::WP, NTW = C::NTW;
   constexpr int TWP = C::TWP, CHS = C::CHS, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, COP = C::COP;
@@ -407,7 +410,7 @@ conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles
   Seg<UPS, H, W> sx[NLX];
   f32x4 sd[NLD];
   auto issue = [&](int t) {
-    const int tt = (UPS && H >= 32) ? opaque(tid) : tid;
+    const int tt = WG_OPQ ? opaque(tid) : tid;
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
 #pragma unroll
     for (int l = 0; l < NLX; ++l) {
@@ -430,7 +433,7 @@ conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles
     }
   };
   auto commit = [&](int t) {
-    const int tt = (UPS && H >= 32) ? opaque(tid) : tid;
+    const int tt = WG_OPQ ? opaque(tid) : tid;
     const int y0 = (t % NRB) * RT;
 #pragma unroll
     for (int l = 0; l < NLX; ++l) {
@@ -462,24 +465,33 @@ conv_wgrad_mfma_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles
     commit(tile);
     __syncthreads();
     if (PIPE && tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
-    for (int g = wp; g < C::NG; g += WP) {
-      const int fi = g / (RT * Q);
-      const int rem = g % (RT * Q);
-      const int y = rem / Q, x0 = (rem % Q) * 4;
-      const int pix = (fi * RT + y) * W + x0 + (lane >> 4);
-      float a[MT];
+    // a wave takes whole rows (FPT*RT rows per tile, split over the WP pixel
+    // waves); the Q 4-pixel groups of a row are unrolled so the fragment
+    // reads of later groups are in flight behind the MFMAs of earlier ones
+    // (waves holding 18+ accumulator tiles keep the row loop rolled: the
+    // unrolled form's in-flight fragments would cost them occupancy)
+    constexpr int UNQ = Q;
+#pragma unroll 1
+    for (int rr = wp; rr < FPT * RT; rr += WP) {
+      const int pixrow = rr * W + (lane >> 4);   // (fi*RT + y)*W
+      const int xrow = (rr / RT) * CIN * CHS + (rr % RT) * TWP + (lane >> 4);
+#pragma unroll UNQ
+      for (int q = 0; q < Q; ++q) {
+        const int pix = pixrow + 4 * q;
+        float a[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        a[m] = Dl[pix * COP + m * 16 + (lane & 15)];
-        bacc[m] += a[m];
-      }
-      const int xb = fi * CIN * CHS + y * TWP + x0 + (lane >> 4);
+        for (int m = 0; m < MT; ++m) {
+          a[m] = Dl[pix * COP + m * 16 + (lane & 15)];
+          bacc[m] += a[m];
+        }
+        const int xb = xrow + 4 * q;
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        if (wn + j * WN < NT) {
-          const float b = Xl[coff[j] + xb];
+        for (int j = 0; j < NTW; ++j) {
+          if (wn + j * WN < NT) {
+            const float b = Xl[coff[j] + xb];
 #pragma unroll
-          for (int m = 0; m < MT; ++m) acc[m][j] = mfma4(a[m], b, acc[m][j]);
+            for (int m = 0; m < MT; ++m) acc[m][j] = mfma4(a[m], b, acc[m][j]);
+          }
         }
       }
     }
