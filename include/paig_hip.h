@@ -37,7 +37,8 @@ int paig_abi_version(void);
  * flags: 1 ReLU, 2 multiply by (aux > 0) [ReLU' of the layer input],
  *        4 accumulate into out, 8 dgrad (in = dY, weight read transposed and
  *        flipped, Cin/Cout are the DGRAD kernel's in/out channel counts),
- *        16 force the VALU path (tests), 32 the input is the 2x bilinear
+ *        16 force the VALU path (tests), 64 skip the Cout=8 pixel-pair
+ *        MFMA kernel (tests), 32 the input is the 2x bilinear
  *        upsample of the given (H/2 x W/2) planes, formed while staging
  *        (torchvision Resize of blocks.py:260,269 fused, never materialised). */
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,

@@ -566,6 +566,201 @@ static int fwd_launch(FView in, FViewW out, FView aux, const float* w, const flo
   return 0;
 }
 
+// ====================================== forward / dgrad, Cout = 8: pixel pairs
+// A 16x16 MFMA tile with only 8 output channels idles half its columns.  Here
+// a D row is a PAIR of horizontally adjacent output pixels (x = 2p, 2p+1) and
+// the 16 columns are (s, co), s = which pixel of the pair:
+//   D[p][(s,co)] = sum_{ci,dy,dx'} X[ci][y+dy-1][2p+dx'] * B[(ci,dy,dx')][(s,co)],
+//   dx' in {-1,0,1,2},  B = w[co][ci][dy][dx'-s]  (0 where dx'-s is outside -1..1)
+// K per input channel is 3 rows x 4 columns (12 instead of 9) for twice the
+// output per MFMA: 2/3 of the MFMAs of the plain layout.  One MFMA k-step is
+// (ci, dy); its 4 k-values are the 4 dx', i.e. lane group g = lane>>4 reads
+// x = 2p + g - 1: lanes 0-31 and 32-63 each read 32 CONSECUTIVE floats of one
+// LDS row (conflict-free for any pitch).  The weights of all k-steps live in
+// VGPRs for the whole (persistent) block.  Epilogue: lanes (s=0,co) and
+// (s=1,co) trade values (xor 8) so each stores one float4 of 4 adjacent pixels.
+template <int CIN, int H, int W, bool DG>
+struct PairCfg {
+  static constexpr int COUT = 8, KS = 3, PADL = 1, KK = 9;
+  static constexpr int PPR = W / 2;                       // pairs per row
+  static_assert(W % 8 == 0 && (PPR % 16 == 0 || 16 % PPR == 0), "pair tiling");
+  static constexpr int RPM = 16 / PPR > 0 ? 16 / PPR : 1; // rows per M-tile (16 pairs)
+  static constexpr int MTR = PPR / 16 > 0 ? PPR / 16 : 1; // M-tiles per row
+  static constexpr int MW = 4;                            // M-tiles per wave
+  static constexpr int TPAIRS = 4 * MW * 16;              // pairs per block tile
+  static constexpr int TPX = 2 * TPAIRS;
+  static constexpr int FPT = TPX >= H * W ? TPX / (H * W) : 1;
+  static constexpr int RT = TPX >= H * W ? H : TPX / W;
+  static constexpr int ROWS = RT + 2;
+  // row pitch: >= W + 5 (x from -1 to W), 16B-aligned rows; rows of one M-tile
+  // (W < 32) land on disjoint bank ranges: pitch = 16 (mod 32) for 2 rows,
+  // 8 (mod 32) for 4 rows
+  static constexpr int TWP = RPM == 1 ? W + 8 : (RPM == 2 ? to_mod32(W + 8, 16) : to_mod32(W + 8, 8));
+  static constexpr int CHS = ROWS * TWP;
+  static constexpr int CI = CIN < 8 ? CIN : 8;            // channels per staged chunk
+  static constexpr int NCH = (CIN + CI - 1) / CI;
+  static constexpr int LDS = FPT * CI * CHS * 4;
+  static_assert(RT * W * FPT == TPX || RT == H, "tile");
+  static_assert(H % RT == 0, "RT divides H");
+};
+
+template <int CIN, int H, int W, bool DG>
+__global__ void __launch_bounds__(256)
+conv_fwd_pair_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
+                int flags, int ntiles) {
+  using C = PairCfg<CIN, H, W, DG>;
+  constexpr int COUT = 8, MW = C::MW, TWP = C::TWP, CHS = C::CHS, CI = C::CI, NCH = C::NCH;
+  constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PPR = C::PPR, RPM = C::RPM, MTR = C::MTR;
+  constexpr long long HW = (long long)H * W, PLANE = HW;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Il = lds;   // [FPT][CI][ROWS][TWP], data at column 4 + x
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4;   // dx' = g - 1
+  const int col = lane & 15, s = col >> 3, co = col & 7;
+  constexpr int NRB = H / RT;
+  constexpr int Q = W / 4;
+
+  // ---- B fragments of every k-step (ci, dy) in registers
+  float breg[CIN * 3];
+#pragma unroll
+  for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int dx = g - 1 - s;   // tap column in -1..1, else no contribution
+      float v = 0.f;
+      if (dx >= -1 && dx <= 1) {
+        const int tap = dy * 3 + dx + 1;
+        v = DG ? w[(ci * COUT + co) * 9 + (8 - tap)] : w[(co * CIN + ci) * 9 + tap];
+      }
+      breg[ci * 3 + dy] = v;
+    }
+  // ---- zero the halo columns (x = -1 and x = W .. W+3 are never staged)
+  for (int i = tid; i < FPT * CI * ROWS; i += 256) {
+    float* r = Il + (i / ROWS) * CHS + (i % ROWS) * TWP;
+    r[3] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[4 + W + e] = 0.f;
+  }
+  // ---- per-lane A base (pair p of M-tile mt -> row, x = 2*(p % PPR) + dx')
+  int abase[MW];
+#pragma unroll
+  for (int mt = 0; mt < MW; ++mt) {
+    const int tile_m = wv * MW + mt;                 // M-tile index within the block tile
+    const int p = (tile_m % MTR) * 16 + col;         // pair within its row group
+    const int rowg = (tile_m / MTR) * RPM + p / PPR; // row within the block tile (all frames)
+    const int fi = rowg / RT, y = rowg % RT;
+    abase[mt] = fi * CI * CHS + y * TWP + 2 * (p % PPR) + g + 3;   // 4 + x + dx', dx' = g - 1
+  }
+
+  constexpr int NI = FPT * CI * ROWS * Q, NL = (NI + 255) / 256;
+  Seg<false, H, W> seg[NL];
+  auto issue = [&](int t, int ch) {
+    const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * 256;
+      const int q = i % Q, r = i / Q;
+      const int rr = r % ROWS, c = (r / ROWS) % CI, fi = r / (ROWS * CI);
+      const int f = f0 + fi, gy = y0 + rr - 1, ci = ch * CI + c;
+      const bool ok = i < NI && f < F && gy >= 0 && gy < H && ci < CIN;
+      seg[l].issue(ok ? in.frame(f) + ci * PLANE : in.p, gy, q, ok);
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * 256;
+      if (NI % 256 != 0 && i >= NI) break;
+      const int q = i % Q, r = i / Q;
+      const int rr = r % ROWS, c = (r / ROWS) % CI, fi = r / (ROWS * CI);
+      *reinterpret_cast<f32x4*>(&Il[(fi * CI + c) * CHS + rr * TWP + 4 + 4 * q]) = seg[l].finish(0, q);
+    }
+  };
+
+  int tile = blockIdx.x;
+  if (tile < ntiles) issue(tile, 0);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
+    f32x4 acc[MW];
+#pragma unroll
+    for (int mt = 0; mt < MW; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      __syncthreads();
+      commit();
+      __syncthreads();
+      if (ch + 1 < NCH) issue(tile, ch + 1);
+      else if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x, 0);
+#pragma unroll
+      for (int c = 0; c < CI; ++c) {
+        if (ch * CI + c >= CIN) break;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const float b = breg[(ch * CI + c) * 3 + dy];
+#pragma unroll
+          for (int mt = 0; mt < MW; ++mt)
+            acc[mt] = mfma4(Il[abase[mt] + c * CHS + dy * TWP], b, acc[mt]);
+        }
+      }
+    }
+    // ---- epilogue: lane holds pairs p = (lane>>4)*4 + r of each M-tile for (s, co)
+    const float bv = bias ? bias[co] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MW; ++mt) {
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mine = acc[mt][r];
+        const float other = __shfl_xor(mine, 8, 64);
+        o[r] = mine;
+        acc[mt][r] = other;   // partner's value for the same pair
+      }
+      // s = 0: pixels 2p0 .. 2p0+3 ; s = 1: pixels 2p0+4 .. 2p0+7
+      f32x4 v;
+      if (s == 0) v = f32x4{o[0], acc[mt][0], o[1], acc[mt][1]};
+      else v = f32x4{acc[mt][2], o[2], acc[mt][3], o[3]};
+      const int tile_m = wv * MW + mt;
+      const int p0 = (tile_m % MTR) * 16 + (lane >> 4) * 4;
+      const int rowg = (tile_m / MTR) * RPM + p0 / PPR;
+      const int fi = rowg / RT, y = y0 + rowg % RT, x = 2 * (p0 % PPR) + 4 * s;
+      const int f = f0 + fi;
+      if (f >= F) continue;
+      float* op = out.frame(f) + co * HW + (long long)y * W + x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += bv;
+      if (flags & 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] < 0.f ? 0.f : v[e];
+      }
+      if (flags & 4) v += *reinterpret_cast<const f32x4*>(op);
+      if (flags & 2) {
+        const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(op) = v;
+    }
+  }
+}
+
+template <int CIN, int H, int W, bool DG>
+static int pair_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
+                       hipStream_t st) {
+  using C = PairCfg<CIN, H, W, DG>;
+  const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
+  auto k = conv_fwd_pair_k<CIN, H, W, DG>;
+  static int resident = 0;
+  if (!resident) {
+    if (C::LDS > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    resident = persistent_grid((const void*)k, C::LDS);
+  }
+  const int nb = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), C::LDS, st, in, out, aux, w, b, F, flags, ntiles);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int CIN, int COUT, int H, int W, int KS, bool UPS>
 static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st) {
   using C = WgCfg<CIN, COUT, H, W, KS>;
@@ -595,6 +790,9 @@ static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_
   X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1)
 #define PAIG_MFMA_UP(X) X(32, 16, 16, 3) X(16, 16, 32, 3)
+// (CIN, H) of the Cout = 8, 3x3 shapes on the pixel-pair kernel (fwd: c1, c2,
+// c11, c12; dgrad: c2/c12 (8 -> 8 at 32) and c3 (16 -> 8 at 16))
+#define PAIG_MFMA_PAIR(X) X(3, 32) X(8, 32) X(24, 32) X(16, 16)
 
 }  // namespace
 
@@ -616,6 +814,16 @@ int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const fl
     PAIG_MFMA_UP(PAIG_CASE)
 #undef PAIG_CASE
     return 0;
+  }
+  if (Cout == 8 && ks == 3 && !(flags & 64)) {
+#define PAIG_PCASE(CI, HH)                                                                   \
+    if (Cin == CI && H == HH) {                                                              \
+      *rc = dg ? pair_launch<CI, HH, HH, true>(in, out, aux, w, b, F, fl, st)                \
+               : pair_launch<CI, HH, HH, false>(in, out, aux, w, b, F, fl, st);              \
+      return 1;                                                                              \
+    }
+    PAIG_MFMA_PAIR(PAIG_PCASE)
+#undef PAIG_PCASE
   }
 #define PAIG_CASE(CI, CO, HH, K)                                                                      \
   if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                \
