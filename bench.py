@@ -64,6 +64,10 @@ def parse():
                     help="committed rocprofv3 FETCH_SIZE/WRITE_SIZE summary (tools/pmc_traffic.py)")
     ap.add_argument("--graph", type=int, default=1, help="capture fwd+loss+bwd in a HIP graph per resident batch")
     ap.add_argument("--probe_steps", type=int, default=5, help="eager steps timing the probed kernel")
+    ap.add_argument("--conv_math", default="split", choices=["split", "fp32", "bf16"],
+                    help="U-Net conv arithmetic: split = f16/bf16 hi+lo operands on the 16-bit matrix cores, "
+                         "fp32-accurate (meets the 1e-4 parity bar; default); fp32 = f32-input MFMA; "
+                         "bf16 = bf16 operands (config #2)")
     ap.add_argument("--cpu_baseline", type=int, default=1)
     ap.add_argument("--cpu_seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -122,6 +126,7 @@ def main():
     torch.manual_seed(0)
     m = PhysicsNet(a.task, 100, 1, cell, a.seq_len, ins, pred, a.ae, False, True, size * size,
                    "conv_encoder", "conv_st_decoder", device=dev).to(dev)
+    m.conv_math = a.conv_math
     m.build_optimizer(a.lr, "rmsprop", True)
     if world > 1:
         for t in m.state_dict().values():
@@ -212,11 +217,13 @@ def main():
             f"video-seqs/sec (train step) {a.task} B={a.batch}",
             "value": round(value, 2), "unit": "video-seqs/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "vs_baseline": None, "dtype": "bf16" if a.conv_math == "bf16" else "fp32",
+            "data": "synthetic",
             "config": {"workload": f"{a.task} PhysicsNet train step (fwd+loss+bwd+allreduce+RMSprop), "
                                    f"B={a.batch}/rank, {size}x{size}x3, seq_len {a.seq_len} "
                                    f"({ins} in / {pred} pred / {a.seq_len - ins - pred} extrap)",
-                       "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}"},
+                       "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}",
+                       "conv_math": a.conv_math},
             "roofline": roof, "cpu_baseline": cpu, "final_loss": round(lossv, 4),
             # whole-step memory-side traffic (committed PMC profile) at this run's step time
             "hbm_step": None if step_bytes is None else {

@@ -1,0 +1,666 @@
+// U-Net convolutions on the gfx950 16-bit matrix cores with split-precision
+// operands (v_mfma_f32_16x16x32_{f16,bf16}, fp32 accumulate).  Reference:
+// aten conv2d / convolution_backward behind nn/network/blocks.py:246-276
+// (ShallowUNet) and :113-170 (UNet).
+//
+// Every fp32 operand v is split as v = hi + lo with hi = rn16(v) and
+// lo = rn16(v - hi) (the subtraction is exact in fp32), and a product is
+// formed from three MFMAs: hi*hi + hi*lo + lo*hi (the lo*lo term and the
+// residual of lo are below fp32 accumulation noise for f16 pieces).  Per K
+// element a 16x16x32 MFMA costs 1/16 of the f32-input v_mfma_f32_16x16x4_f32,
+// so the three-term product does fp32-accurate convolutions at ~5x the f32
+// matrix rate; these layers (3..32 channels) then run at the HBM/LDS
+// roofline instead of the MFMA one.  Precision modes (PM):
+//   0  f16 hi/lo   (22 significant bits: forward activations and weights,
+//                  whose range |v| < 65504 this mode requires)
+//   1  bf16 hi/lo  (16 significant bits, fp32 range: dgrad and wgrad, whose
+//                  gradients have no useful range bound)
+//   2  bf16 hi only (one MFMA: the bf16 configuration, BASELINE config #2)
+// Measured against the reference's golden vectors (tests/golden): outputs
+// within 1e-6 and gradients within fp32 noise with PM 0 forward + PM 1
+// backward.
+//
+// forward / dgrad  D[pixel][co] = im2col(X)[pixel][k] * Wt[k][co], with
+//   k = (tap, ci) in 8-channel chunks: the block stages its input tile as an
+//   NHWC image (8 channels = one 16-byte slot per pixel, pixel pitch an odd
+//   number of slots so the 16 rows of an A fragment read conflict-free), so
+//   an A fragment is ONE ds_read_b128 per lane (pixel, tap, 8 channels).
+//   Weights are staged once per (persistent) block in fragment order.
+// wgrad            D[co][n] = dY[co][pixel] * im2col(X)[pixel][n], K = pixels:
+//   dY staged [co][pixel] (A: one ds_read_b128 of 8 consecutive pixels), X
+//   staged NHWC and read with ds_read_b64_tr_b16, whose per-lane row address
+//   absorbs the tap shift (any pixel offset, no misaligned vector reads); the
+//   16 columns of an N-tile are 4 (tap, 4-channel) quads.  Bias gradients
+//   are summed exactly in fp32 from the staging registers.
+#include "conv_tile.h"
+
+namespace {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int rup(int a, int b) { return ceil_div(a, b) * b; }
+// smallest y >= x with y % 16 == r
+constexpr int to_mod16(int x, int r) { return x + ((r - x % 16) + 16) % 16; }
+
+template <int PM>
+__device__ __forceinline__ void split(float v, short& h, short& l) {
+  if constexpr (PM == 0) {
+    const _Float16 a = (_Float16)v;
+    const _Float16 b = (_Float16)(v - (float)a);
+    h = __builtin_bit_cast(short, a);
+    l = __builtin_bit_cast(short, b);
+  } else {
+    const __bf16 a = (__bf16)v;
+    h = __builtin_bit_cast(short, a);
+    if constexpr (PM == 1) {
+      const __bf16 b = (__bf16)(v - (float)a);
+      l = __builtin_bit_cast(short, b);
+    } else {
+      l = 0;
+    }
+  }
+}
+
+template <int PM>
+__device__ __forceinline__ f32x4 mma(s16x8 a, s16x8 b, f32x4 c) {
+  if constexpr (PM == 0)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+
+// acc += a*b with both operands split (hi, lo); PM 2 uses the hi parts only
+template <int PM>
+__device__ __forceinline__ f32x4 mma3(s16x8 ah, s16x8 al, s16x8 bh, s16x8 bl, f32x4 c) {
+  if constexpr (PM != 2) {
+    c = mma<PM>(al, bh, c);
+    c = mma<PM>(ah, bl, c);
+  }
+  return mma<PM>(ah, bh, c);
+}
+
+__device__ __forceinline__ s16x4 tr_read(const short* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+}
+
+// ============================================================ forward / dgrad
+template <int CIN, int COUT, int H, int W, int KS, int PM>
+struct SFwdCfg {
+  static constexpr int KK = KS * KS, PADL = KS / 2;
+  static constexpr int NIMG = PM == 2 ? 1 : 2;               // hi (+ lo) images
+  static constexpr int CINP = rup(CIN, 8), CC = CINP / 8;    // 8-channel chunks per pixel
+  static constexpr int KC = KK * CC, NS = ceil_div(KC, 4);   // k-chunks, MFMA k-steps (4 chunks each)
+  static constexpr int NT = ceil_div(COUT, 16);
+  static constexpr int MW = W >= 16 ? 4 : 2;                 // M-tiles per wave
+  static constexpr int TPX = 4 * MW * 16;
+  static constexpr int FPT = TPX >= H * W ? TPX / (H * W) : 1;
+  static constexpr int RT = TPX >= H * W ? H : TPX / W;
+  static constexpr int ROWS = RT + KS - 1;
+  static constexpr int TWPX = W + 2 * PADL;                  // pixel columns incl. halo
+  // 16-B slots per pixel: odd, so 16 consecutive pixels hit 16 distinct
+  // bank groups; an M-tile spanning two rows (W = 8) needs the row pitch
+  // = 8 (mod 16) slots so the second row lands on the other 8 groups
+  static constexpr int PS = CC % 2 == 0 ? CC + 1 : CC;
+  static constexpr int RP = W >= 16 ? TWPX * PS : to_mod16(TWPX * PS, 8);
+  static constexpr int IMG = FPT * ROWS * RP * 8;            // 16-bit elements per image
+  static constexpr int WIMG = NS * NT * 64 * 8;
+  static constexpr int LDS = (IMG + WIMG) * 2 * NIMG;
+  static constexpr int Q = W / 4;
+  static constexpr int NI = FPT * ROWS * Q * CC;             // staging units (4 px x 8 ch)
+  static constexpr int NL = (NI + 255) / 256;
+  static_assert(W % 8 == 0 && (W >= 16 || 16 % W == 0), "M-tile rows");
+  static_assert(RT * W * FPT == TPX || RT == H, "tile");
+  static_assert(H % RT == 0, "RT divides H");
+};
+
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
+__global__ void __launch_bounds__(256)
+conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
+                 int flags, int ntiles) {
+  using C = SFwdCfg<CIN, COUT, H, W, KS, PM>;
+  constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
+  constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP, Q = C::Q;
+  constexpr int NI = C::NI, NL = C::NL, PADL = C::PADL;
+  constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
+  constexpr long long HW = (long long)H * W;
+  extern __shared__ __attribute__((aligned(16))) short lds16[];
+  short* Xh = lds16;
+  short* Xl = Xh + (C::NIMG == 2 ? C::IMG : 0);
+  short* Wh = lds16 + C::NIMG * C::IMG;
+  short* Wl = Wh + (C::NIMG == 2 ? C::WIMG : 0);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
+  constexpr int NRB = H / RT;
+
+  // ---- weights in fragment order: [s][nt][lane][8]; dgrad: transposed + flipped
+  for (int idx = tid; idx < NS * NT * 64; idx += 256) {
+    const int ln = idx & 63, snt = idx >> 6, nt = snt % NT, s = snt / NT;
+    const int kc = 4 * s + (ln >> 4), co = nt * 16 + (ln & 15);
+    s16x8 vh, vl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = 0.f;
+      if (kc < KC && co < COUT) {
+        const int tap = kc / CC, ci = (kc % CC) * 8 + j;
+        if (ci < CIN) v = DG ? w[(ci * COUT + co) * KK + (KK - 1 - tap)] : w[(co * CIN + ci) * KK + tap];
+      }
+      short h, l;
+      split<PM>(v, h, l);
+      vh[j] = h;
+      vl[j] = l;
+    }
+    *reinterpret_cast<s16x8*>(Wh + idx * 8) = vh;
+    if (PM != 2) *reinterpret_cast<s16x8*>(Wl + idx * 8) = vl;
+  }
+  // ---- zero the halo columns (never written by the staging)
+  if (PADL > 0) {
+    for (int i = tid; i < FPT * ROWS * 2 * PADL * CC; i += 256) {
+      const int cc = i % CC, hc = (i / CC) % (2 * PADL), r = i / (CC * 2 * PADL);
+      const int xc = hc < PADL ? hc : W + hc;
+      const int o = (r * RP + xc * PS + cc) * 8;
+      *reinterpret_cast<s16x8*>(Xh + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  // ---- per-lane fragment slot offsets: pixel base per M-tile, (tap, chunk) per k-step
+  int pbase[MW];
+#pragma unroll
+  for (int mt = 0; mt < MW; ++mt) {
+    const int pix = (wv * MW + mt) * 16 + (lane & 15);
+    const int fi = pix / (RT * W), rem = pix % (RT * W);
+    pbase[mt] = (fi * ROWS + rem / W) * RP + (rem % W) * PS;
+  }
+  int soff[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int kc = 4 * s + g;
+    if (kc >= KC) kc = 0;   // zero weights there; read any finite slot
+    const int tap = kc / CC, cc = kc % CC;
+    soff[s] = (tap / KS) * RP + (tap % KS) * PS + cc;
+  }
+
+  // ---- staging: unit = 4 pixels (row, x = 4q..4q+3) x 8 channels, loads in
+  // flight during the previous tile's MFMAs (PIPE)
+  Seg<UPS, H, W> seg[NL][8];
+  auto issue = [&](int t) {
+    const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * 256;
+      const int q = i % Q, r = (i / Q) % ROWS, cc = (i / (Q * ROWS)) % CC, fi = i / (Q * ROWS * CC);
+      const int f = f0 + fi, gy = y0 + r - PADL;
+      const bool ok = i < NI && f < F && gy >= 0 && gy < H;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int ci = cc * 8 + c;
+        const bool okc = ok && ci < CIN;
+        seg[l][c].issue(okc ? in.frame(f) + ci * PLANE : in.p, gy, q, okc);
+      }
+    }
+  };
+  auto commit = [&](int t) {
+    const int y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * 256;
+      if (NI % 256 != 0 && i >= NI) break;
+      const int q = i % Q, r = (i / Q) % ROWS, cc = (i / (Q * ROWS)) % CC, fi = i / (Q * ROWS * CC);
+      f32x4 v[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = seg[l][c].finish(y0 + r - PADL, q);
+      const int o0 = ((fi * ROWS + r) * RP + (4 * q + PADL) * PS + cc) * 8;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s16x8 hv, lv;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          short h, lo;
+          split<PM>(v[c][e], h, lo);
+          hv[c] = h;
+          lv[c] = lo;
+        }
+        *reinterpret_cast<s16x8*>(Xh + o0 + e * PS * 8) = hv;
+        if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o0 + e * PS * 8) = lv;
+      }
+    }
+  };
+
+  constexpr bool PIPE = !(UPS && H >= 32);
+  int tile = blockIdx.x;
+  if (PIPE && tile < ntiles) issue(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
+    __syncthreads();   // previous tile's fragment reads are done
+    if (!PIPE) issue(tile);
+    commit(tile);
+    __syncthreads();
+    if (PIPE && tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
+    f32x4 acc[MW][NT];
+#pragma unroll
+    for (int mt = 0; mt < MW; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      s16x8 bh[NT], bl[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int o = ((s * NT + nt) * 64 + lane) * 8;
+        bh[nt] = *reinterpret_cast<const s16x8*>(Wh + o);
+        bl[nt] = PM != 2 ? *reinterpret_cast<const s16x8*>(Wl + o) : bh[nt];
+      }
+#pragma unroll
+      for (int mt = 0; mt < MW; ++mt) {
+        const int o = (pbase[mt] + soff[s]) * 8;
+        const s16x8 ah = *reinterpret_cast<const s16x8*>(Xh + o);
+        const s16x8 al = PM != 2 ? *reinterpret_cast<const s16x8*>(Xl + o) : ah;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mma3<PM>(ah, al, bh[nt], bl[nt], acc[mt][nt]);
+      }
+    }
+    // ---- epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for co = nt*16 + (lane&15)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int co = nt * 16 + (lane & 15);
+      if (co >= COUT) continue;
+      const float bv = bias ? bias[co] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < MW; ++mt) {
+        const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+        const int fi = pix / (RT * W), rem = pix % (RT * W);
+        const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
+        if (f >= F) continue;
+        float* op = out.frame(f) + co * HW + (long long)y * W + x;
+        f32x4 v = acc[mt][nt];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bv;
+        if (flags & 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = v[r] < 0.f ? 0.f : v[r];
+        }
+        if (flags & 4) v += *reinterpret_cast<const f32x4*>(op);
+        if (flags & 2) {
+          const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(op) = v;
+      }
+    }
+  }
+}
+
+// ===================================================================== wgrad
+template <int CIN, int COUT, int H, int W, int KS, int PM>
+struct SWgCfg {
+  static constexpr int KK = KS * KS, PADL = KS / 2;
+  static constexpr int NIMG = PM == 2 ? 1 : 2;
+  static constexpr int CINQ = rup(CIN, 4), CQ = CINQ / 4;     // 4-channel quads per pixel
+  static constexpr int NQ = KK * CQ;                          // (tap, quad) column quads
+  static constexpr int NT = ceil_div(NQ, 4);                  // N-tiles of 16 columns
+  static constexpr int NCOL = CIN * KK;
+  static constexpr int MT = ceil_div(COUT, 16), COP = MT * 16;
+  static constexpr int WN = (MT * NT * 4 <= 72) ? 1 : ((MT * ceil_div(NT, 2) * 4 <= 72) ? 2 : 4);
+  static constexpr int WP = 4 / WN, NTW = ceil_div(NT, WN);
+  static constexpr int TPX = 256;                             // pixels per tile
+  static constexpr int FPT = H * W >= TPX ? 1 : TPX / (H * W);
+  static constexpr int RT = H * W >= TPX ? TPX / W : H;
+  static constexpr int ROWS = RT + KS - 1;
+  static constexpr int TWPX = W + 2 * PADL;
+  static constexpr int PSX = CINQ;                            // 16-bit elements per staged pixel
+  static constexpr int XIMG = FPT * ROWS * TWPX * PSX;
+  static constexpr int DP = TPX + 8;                          // dY row pitch: 16 rows -> 16 bank groups
+  static constexpr int DIMG = COP * DP;
+  static constexpr int KB = TPX / 32;                         // k-blocks of 32 pixels per tile
+  static constexpr int STG = (XIMG + DIMG) * 2 * NIMG;
+  static constexpr int RED = 4 * MT * NTW * 4 * 64 * 4;
+  static constexpr int LDS = STG > RED ? STG : RED;
+  static constexpr int Q = W / 4;
+  static constexpr int NIX = FPT * ROWS * Q * CQ, NLX = (NIX + 255) / 256;   // X units: 4 px x 4 ch
+  static constexpr int NID = COUT * TPX / 4, NLD = (NID + 255) / 256;         // dY units: 4 px x 1 ch
+  static constexpr int SLAB = COUT * NCOL + COUT;
+  static_assert(FPT * RT * W == TPX, "tile = 256 pixels");
+  static_assert((RT * W) % 32 == 0 && (W % 32 == 0 || 32 % W == 0), "k-blocks stay in one frame");
+  static_assert(H % RT == 0, "RT divides H");
+};
+
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
+__global__ void __launch_bounds__(256)
+conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles) {
+  using C = SWgCfg<CIN, COUT, H, W, KS, PM>;
+  constexpr int KK = C::KK, CQ = C::CQ, NQ = C::NQ, NT = C::NT, NCOL = C::NCOL, MT = C::MT, COP = C::COP;
+  constexpr int WN = C::WN, WP = C::WP, NTW = C::NTW, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS;
+  constexpr int TWPX = C::TWPX, PSX = C::PSX, DP = C::DP, KB = C::KB, Q = C::Q, PADL = C::PADL;
+  constexpr int NIX = C::NIX, NLX = C::NLX, NID = C::NID, NLD = C::NLD;
+  constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
+  constexpr long long HW = (long long)H * W;
+  extern __shared__ __attribute__((aligned(16))) short lds16[];
+  short* Xh = lds16;
+  short* Xl = Xh + (C::NIMG == 2 ? C::XIMG : 0);
+  short* Dh = lds16 + C::NIMG * C::XIMG;
+  short* Dl = Dh + (C::NIMG == 2 ? C::DIMG : 0);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
+  const int wn = wv % WN, wp = wv / WN;
+  constexpr int NRB = H / RT;
+
+  // ---- zero the halo columns of X and the padded co rows of dY (never staged)
+  if (PADL > 0) {
+    for (int i = tid; i < FPT * ROWS * 2 * PADL; i += 256) {
+      const int hc = i % (2 * PADL), r = i / (2 * PADL);
+      const int xc = hc < PADL ? hc : W + hc;
+      for (int e = 0; e < PSX; e += 4) {
+        *reinterpret_cast<s16x4*>(Xh + (r * TWPX + xc) * PSX + e) = s16x4{0, 0, 0, 0};
+        if (PM != 2) *reinterpret_cast<s16x4*>(Xl + (r * TWPX + xc) * PSX + e) = s16x4{0, 0, 0, 0};
+      }
+    }
+  }
+  if (COP > COUT) {
+    for (int i = tid; i < (COP - COUT) * DP / 4; i += 256) {
+      *reinterpret_cast<s16x4*>(Dh + COUT * DP + 4 * i) = s16x4{0, 0, 0, 0};
+      if (PM != 2) *reinterpret_cast<s16x4*>(Dl + COUT * DP + 4 * i) = s16x4{0, 0, 0, 0};
+    }
+  }
+  // ---- per-lane transposed-read addressing. Lane 4q+p of its 16-lane group
+  // supplies row q (pixel 8g + 4h + q of the k-block) of column quad p.
+  const int qq = (lane >> 2) & 3, pp = lane & 3;
+  int roff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = 8 * g + 4 * h + qq;
+    roff[h] = (j / W) * TWPX + j % W;
+  }
+  int colt[NTW];
+#pragma unroll
+  for (int jn = 0; jn < NTW; ++jn) {
+    int cq = (wn + jn * WN) * 4 + pp;
+    if (cq >= NQ) cq = 0;   // padded columns: any finite data, never stored
+    const int tap = cq / CQ, ciq = cq % CQ;
+    colt[jn] = ((tap / KS) * TWPX + tap % KS) * PSX + ciq * 4;
+  }
+  f32x4 acc[MT][NTW];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[NLD];
+#pragma unroll
+  for (int l = 0; l < NLD; ++l) bacc[l] = 0.f;
+
+  Seg<UPS, H, W> sx[NLX][4];
+  f32x4 sd[NLD];
+  auto issue = [&](int t) {
+    const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NLX; ++l) {
+      const int i = tid + l * 256;
+      const int q = i % Q, r = (i / Q) % ROWS, cq = (i / (Q * ROWS)) % CQ, fi = i / (Q * ROWS * CQ);
+      const int f = f0 + fi, gy = y0 + r - PADL;
+      const bool ok = i < NIX && f < F && gy >= 0 && gy < H;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int ci = cq * 4 + c;
+        const bool okc = ok && ci < CIN;
+        sx[l][c].issue(okc ? x.frame(f) + ci * PLANE : x.p, gy, q, okc);
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int i = tid + l * 256;
+      const int co = i / (C::TPX / 4), pt = 4 * (i % (C::TPX / 4));
+      const int fi = pt / (RT * W), y = (pt / W) % RT, xx = pt % W;
+      const int f = f0 + fi;
+      sd[l] = (i < NID && f < F)
+                  ? *reinterpret_cast<const f32x4*>(dy.frame(f) + co * HW + (long long)(y0 + y) * W + xx)
+                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto commit = [&](int t) {
+    const int y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NLX; ++l) {
+      const int i = tid + l * 256;
+      if (NIX % 256 != 0 && i >= NIX) break;
+      const int q = i % Q, r = (i / Q) % ROWS, cq = (i / (Q * ROWS)) % CQ, fi = i / (Q * ROWS * CQ);
+      f32x4 v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = sx[l][c].finish(y0 + r - PADL, q);
+      const int o0 = ((fi * ROWS + r) * TWPX + 4 * q + PADL) * PSX + cq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s16x4 hv, lv;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          short h, lo;
+          split<PM>(v[c][e], h, lo);
+          hv[c] = h;
+          lv[c] = lo;
+        }
+        *reinterpret_cast<s16x4*>(Xh + o0 + e * PSX) = hv;
+        if (PM != 2) *reinterpret_cast<s16x4*>(Xl + o0 + e * PSX) = lv;
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int i = tid + l * 256;
+      if (NID % 256 != 0 && i >= NID) break;
+      const int co = i / (C::TPX / 4), pt = 4 * (i % (C::TPX / 4));
+      s16x4 hv, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        short h, lo;
+        split<PM>(sd[l][e], h, lo);
+        hv[e] = h;
+        lv[e] = lo;
+      }
+      bacc[l] += (sd[l][0] + sd[l][1]) + (sd[l][2] + sd[l][3]);
+      *reinterpret_cast<s16x4*>(Dh + co * DP + pt) = hv;
+      if (PM != 2) *reinterpret_cast<s16x4*>(Dl + co * DP + pt) = lv;
+    }
+  };
+
+  if ((int)blockIdx.x < ntiles) issue(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();   // previous tile's fragment reads are done
+    commit(tile);
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
+#pragma unroll
+    for (int kb = wp; kb < KB; kb += WP) {
+      // k-block kb: 32 consecutive tile pixels, all in one frame
+      const int p0 = kb * 32, fi = p0 / (RT * W), pr = p0 % (RT * W);
+      const int base = (fi * ROWS + pr / W) * TWPX + pr % W;
+      s16x8 ah[MT], al[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int o = (m * 16 + (lane & 15)) * DP + p0 + 8 * g;
+        ah[m] = *reinterpret_cast<const s16x8*>(Dh + o);
+        al[m] = PM != 2 ? *reinterpret_cast<const s16x8*>(Dl + o) : ah[m];
+      }
+      const int r0 = (base + roff[0]) * PSX, r1 = (base + roff[1]) * PSX;
+#pragma unroll
+      for (int jn = 0; jn < NTW; ++jn) {
+        if (wn + jn * WN < NT) {
+          const s16x8 bh = __builtin_shufflevector(tr_read(Xh + r0 + colt[jn]), tr_read(Xh + r1 + colt[jn]), 0, 1,
+                                                   2, 3, 4, 5, 6, 7);
+          s16x8 bl = bh;
+          if (PM != 2)
+            bl = __builtin_shufflevector(tr_read(Xl + r0 + colt[jn]), tr_read(Xl + r1 + colt[jn]), 0, 1, 2, 3, 4, 5,
+                                         6, 7);
+#pragma unroll
+          for (int m = 0; m < MT; ++m) acc[m][jn] = mma3<PM>(ah[m], al[m], bh, bl, acc[m][jn]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- cross-wave reduction (waves with equal wn, different wp) through LDS
+  float* R = reinterpret_cast<float*>(lds16);   // [4 waves][MT][NTW][4][64]
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) R[(((wv * MT + m) * NTW + j) * 4 + r) * 64 + lane] = acc[m][j][r];
+  __syncthreads();
+  float* s = slab + (long long)blockIdx.x * C::SLAB;
+  if (wp == 0) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int nt = wn + j * WN;
+        if (nt >= NT) continue;
+        const int col = nt * 16 + (lane & 15), cq = col >> 2;
+        const int tap = cq / CQ, ci = (cq % CQ) * 4 + (col & 3);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = 0.f;
+          for (int p = 0; p < WP; ++p) v += R[((((p * WN + wn) * MT + m) * NTW + j) * 4 + r) * 64 + lane];
+          const int co = m * 16 + (lane >> 4) * 4 + r;
+          if (co < COUT && cq < NQ && ci < CIN) s[co * NCOL + ci * KK + tap] = v;
+        }
+      }
+  }
+  // bias: dY unit i covers channel i / 64, i.e. one channel per (wave, l)
+#pragma unroll
+  for (int l = 0; l < NLD; ++l) {
+    const float v = wave_sum(bacc[l]);
+    const int i = tid + l * 256;
+    if (lane == 0 && i < NID) s[COUT * NCOL + i / (C::TPX / 4)] = v;
+  }
+}
+
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
+static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
+                       hipStream_t st) {
+  using C = SFwdCfg<CIN, COUT, H, W, KS, PM>;
+  const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
+  auto k = conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM>;
+  static int resident = 0;
+  if (!resident) {
+    if (C::LDS > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    resident = persistent_grid((const void*)k, C::LDS);
+  }
+  const int nb = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), C::LDS, st, in, out, aux, w, b, F, flags, ntiles);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
+static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st) {
+  using C = SWgCfg<CIN, COUT, H, W, KS, PM>;
+  const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
+  int nb = ntiles < nblk_max ? ntiles : nblk_max;
+  if (nb < 1) nb = 1;
+  *nblk_out = nb;
+  auto k = conv_wgrad_split_k<CIN, COUT, H, W, KS, UPS, PM>;
+  static bool attr = false;
+  if (!attr && C::LDS > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), C::LDS, st, x, dy, slab, F, ntiles);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+// (CIN, COUT, H, KS) of the ShallowUNet(hidden 8) shapes at 32x32: forward
+// and dgrad kernel shapes (dgrad shapes are (layer Cout, layer Cin)); *_UP:
+// the convs whose input is the fused 2x upsample (c7, c10)
+#define PAIG_SPLIT_FWD(X)                                                                                 \
+  X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
+  X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1) X(16, 8, 16, 3) X(8, 24, 32, 3)       \
+  X(2, 8, 32, 1) X(32, 16, 8, 3) X(16, 32, 16, 3)
+#define PAIG_SPLIT_WG(X)                                                                                  \
+  X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
+  X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1)
+#define PAIG_SPLIT_UP(X) X(32, 16, 16, 3) X(16, 16, 32, 3)
+
+}  // namespace
+
+// flags & 128: split precision (f16 x3 forward, bf16 x3 dgrad), flags & 256:
+// bf16 hi only.  Returns 1 if the shape is instantiated here (rc in *rc).
+int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
+                        int H, int W, int ks, int flags, hipStream_t st, int* rc) {
+  const bool dg = (flags & 8) != 0, up = (flags & 32) != 0, b16 = (flags & 256) != 0;
+  const int fl = flags & 7;
+  if (H != W || !(flags & (128 | 256))) return 0;
+  if (up) {
+    if (dg) return 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                                          \
+    if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
+      *rc = b16 ? sfwd_launch<CI, CO, HH, HH, K, false, true, 2>(in, out, aux, w, b, F, fl, st)           \
+                : sfwd_launch<CI, CO, HH, HH, K, false, true, 0>(in, out, aux, w, b, F, fl, st);          \
+      return 1;                                                                                           \
+    }
+    PAIG_SPLIT_UP(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
+#define PAIG_CASE(CI, CO, HH, K)                                                                            \
+  if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                      \
+    if (b16)                                                                                                \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 2>(in, out, aux, w, b, F, fl, st)              \
+               : sfwd_launch<CI, CO, HH, HH, K, false, false, 2>(in, out, aux, w, b, F, fl, st);            \
+    else                                                                                                    \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 1>(in, out, aux, w, b, F, fl, st)              \
+               : sfwd_launch<CI, CO, HH, HH, K, false, false, 0>(in, out, aux, w, b, F, fl, st);            \
+    return 1;                                                                                               \
+  }
+  PAIG_SPLIT_FWD(PAIG_CASE)
+#undef PAIG_CASE
+  return 0;
+}
+
+int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout,
+                          int H, int W, int ks, int flags, hipStream_t st, int* rc) {
+  const bool up = (flags & 32) != 0, b16 = (flags & 256) != 0;
+  if (H != W || !(flags & (128 | 256))) return 0;
+  if (up) {
+#define PAIG_CASE(CI, CO, HH, K)                                                                          \
+    if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
+      *rc = b16 ? swg_launch<CI, CO, HH, HH, K, true, 2>(x, dy, slab, nblk_max, nblk_out, F, st)          \
+                : swg_launch<CI, CO, HH, HH, K, true, 1>(x, dy, slab, nblk_max, nblk_out, F, st);         \
+      return 1;                                                                                           \
+    }
+    PAIG_SPLIT_UP(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
+#define PAIG_CASE(CI, CO, HH, K)                                                                          \
+  if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                    \
+    *rc = b16 ? swg_launch<CI, CO, HH, HH, K, false, 2>(x, dy, slab, nblk_max, nblk_out, F, st)           \
+              : swg_launch<CI, CO, HH, HH, K, false, 1>(x, dy, slab, nblk_max, nblk_out, F, st);          \
+    return 1;                                                                                             \
+  }
+  PAIG_SPLIT_WG(PAIG_CASE)
+#undef PAIG_CASE
+  return 0;
+}
+
+// 1 if paig_conv_split_fwd (what 0) / paig_conv_split_wgrad (what 1) has the shape
+int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags) {
+  if (H != W) return 0;
+  const bool up = (flags & 32) != 0, dg = (flags & 8) != 0;
+#define PAIG_CASE(CI, CO, HH, K) \
+  if (Cin == CI && Cout == CO && H == HH && ks == K) return 1;
+  if (up) {
+    if (dg) return 0;
+    PAIG_SPLIT_UP(PAIG_CASE)
+    return 0;
+  }
+  if (what == 0) {
+    PAIG_SPLIT_FWD(PAIG_CASE)
+  } else {
+    PAIG_SPLIT_WG(PAIG_CASE)
+  }
+#undef PAIG_CASE
+  return 0;
+}

@@ -231,6 +231,18 @@ class Engine:
         self.last_masked_objs = None
         self._side = None   # second stream (see _fork)
 
+    # conv arithmetic (include/paig_hip.h flags): "split" = f16 hi/lo forward and
+    # bf16 hi/lo dgrad/wgrad on the 16-bit matrix cores (fp32-accurate: the
+    # north-star 1e-4 bar), "fp32" = f32-input MFMA, "bf16" = bf16 operands
+    # (BASELINE config #2)
+    CONV_MATH = {"split": 128, "fp32": 0, "bf16": 256}
+
+    def conv_flags(self):
+        m = getattr(self.model, "conv_math", "split")
+        if m not in self.CONV_MATH:
+            raise ValueError(f"conv_math must be one of {sorted(self.CONV_MATH)}, got {m!r}")
+        return self.CONV_MATH[m]
+
     def _p(self, tag, flops=0):
         return self.probe.wrap(tag, flops) if self.probe is not None else _NOPROBE
 
@@ -287,6 +299,8 @@ class Engine:
         K, F, HW, H, h, D = lay.K, lay.F, lay.HW, lay.H, lay.h, lay.D
         ws = _empty(self.workspace_floats(lay), dev)
         S = {"lay": lay, "x": x, "ws": ws}
+        cm = self.conv_flags()
+        S["cm"] = cm
 
         # ---- VariableFromNetwork sources (once per step, Q12)
         src = {}
@@ -342,7 +356,8 @@ class Engine:
                 fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
                 with self._p("conv_fwd:" + op["name"], fl):
                     L.paig_conv2d_fwd(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
-                                      op["src"][2], op["dst"][2], Hl, Hl, op["ks"], (1 if op["relu"] else 0) | xfl, st)
+                                      op["src"][2], op["dst"][2], Hl, Hl, op["ks"], (1 if op["relu"] else 0) | xfl | cm,
+                                      st)
             elif op["op"] == "pool":
                 sv, slvl = view(op["src"])
                 Hl = H // slvl
@@ -586,6 +601,7 @@ class Engine:
         view = S["view"]
         F, H = lay.F, lay.H
         written = {"LG": [(0, lay.K)]}
+        cm = S["cm"]
 
         def dview(region):
             buf, off, n = region
@@ -627,7 +643,7 @@ class Engine:
                 fl = 2 * F * cin * cout * ks * ks * Hl * Hl
                 with self._p("conv_wgrad:" + op["name"], fl):
                     L.paig_conv2d_wgrad(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], ptr(slab), nblk_max,
-                                        ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, xfl, st)
+                                        ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, xfl | cm, st)
                 gw = self.g(lay.prefix + op["name"] + ".weight")
                 gb = self.g(lay.prefix + op["name"] + ".bias")
                 n_w = cout * cin * ks * ks
@@ -647,7 +663,7 @@ class Engine:
                 W_ = self.p(lay.prefix + op["name"] + ".weight")
                 with self._p("conv_dgrad:" + op["name"], fl):
                     L.paig_conv2d_fwd(dyv[0], dyv[1], 0, 0, dxv[0], dxv[1], aux[0] or None, aux[1], ptr(W_), None, F,
-                                      cout, cin, Hl, Hl, ks, flags, st)
+                                      cout, cin, Hl, Hl, ks, flags | cm, st)
                 mark(src)
             elif op["op"] == "pool":
                 sv, slvl = view(src)

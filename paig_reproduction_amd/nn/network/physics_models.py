@@ -188,6 +188,9 @@ class PhysicsNet(BaseNetTorch):
                                                 self.device)
         self.rollout_cell = self.cell(self.coord_units // 2, self.coord_units // 2)
         self.loss_mode = "fresh"
+        # conv arithmetic of the HIP path: "split" (fp32-accurate split-precision
+        # 16-bit MFMA, default), "fp32" (f32-input MFMA) or "bf16"
+        self.conv_math = os.environ.get("PAIG_CONV_MATH", "split")
         self._init_native()
 
     # ------------------------------------------------------------ native ----

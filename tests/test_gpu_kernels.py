@@ -78,6 +78,90 @@ def test_conv_fwd_dgrad_wgrad(cin, cout, hw, ks, F_):
     assert rel_err(g[n:], br.grad) <= 1e-5
 
 
+SPLIT_CASES = [(3, 8, 32, 3, 5), (8, 8, 32, 3, 3), (8, 16, 16, 3, 7), (16, 16, 16, 3, 4), (16, 32, 8, 3, 9),
+               (32, 32, 8, 3, 3), (32, 16, 16, 3, 2), (24, 8, 32, 3, 2), (8, 2, 32, 1, 3), (16, 16, 32, 3, 2),
+               (16, 8, 16, 3, 3), (8, 24, 32, 3, 2), (2, 8, 32, 1, 3), (32, 16, 8, 3, 3), (16, 32, 16, 3, 2)]
+# normwise bars: f16 hi/lo forward ~2^-22 per product (fp32-level); bf16 hi/lo
+# dgrad/wgrad ~2^-17; bf16 (hi only) ~2^-9
+SPLIT_TOL = {128: (1e-5, 3e-5), 256: (8e-3, 8e-3)}
+
+
+@pytest.mark.parametrize("mode", [128, 256])
+@pytest.mark.parametrize("cin,cout,hw,ks,F_", SPLIT_CASES)
+def test_conv_split(cin, cout, hw, ks, F_, mode):
+    """Split-precision 16-bit MFMA convs (conv_split.hip) vs torch fp32."""
+    tf, tb = SPLIT_TOL[mode]
+    torch.manual_seed(cin * 100 + cout + mode)
+    x = torch.randn(F_, cin, hw, hw)
+    w = torch.randn(cout, cin, ks, ks) * 0.2
+    b = torch.randn(cout)
+    dy = torch.randn(F_, cout, hw, hw)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, br, padding="same")
+    y.backward(dy)
+    xg, wg, bg, dyg = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
+    assert L().paig_conv2d_mfma_supported(0, cin, cout, hw, hw, ks, mode) == 1
+    out = torch.empty(F_, cout, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(xg), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout, hw,
+                        hw, ks, 1 | mode, st())
+    torch.cuda.synchronize()
+    assert rel_err(out, torch.relu(y.detach())) <= tf
+    if L().paig_conv2d_mfma_supported(0, cout, cin, hw, hw, ks, mode | 8):
+        aux = torch.relu(torch.randn(F_, cin, hw, hw))
+        auxg = aux.to(DEV)
+        dx = torch.full((F_, cin, hw, hw), 0.5, device=DEV)
+        L().paig_conv2d_fwd(p(dyg), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, p(auxg), cin * hw * hw, p(wg), None,
+                            F_, cout, cin, hw, hw, ks, 8 | 4 | 2 | mode, st())
+        torch.cuda.synchronize()
+        assert rel_err(dx, (xr.grad + 0.5) * (aux > 0)) <= tb
+    if L().paig_conv2d_mfma_supported(1, cin, cout, hw, hw, ks, mode):
+        nmax = 64
+        slab = torch.empty(nmax * (cout * cin * ks * ks + cout), device=DEV)
+        nb = ctypes.c_int(0)
+        L().paig_conv2d_wgrad(p(xg), cin * hw * hw, 0, 0, p(dyg), cout * hw * hw, p(slab), nmax, ctypes.byref(nb), F_,
+                              cin, cout, hw, hw, ks, mode, st())
+        g = torch.empty(cout * cin * ks * ks + cout, device=DEV)
+        L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
+        torch.cuda.synchronize()
+        n = cout * cin * ks * ks
+        assert rel_err(g[:n].view_as(w), wr.grad) <= tb
+        assert rel_err(g[n:], br.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("mode", [128, 256])
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32)])
+def test_conv_split_fused_upsample(cin, cout, hw, mode):
+    """c7/c10: the conv input is the 2x bilinear upsample, formed while staging."""
+    tf, tb = SPLIT_TOL[mode]
+    torch.manual_seed(cin + cout + hw)
+    F_ = 3
+    xs = torch.randn(F_, cin, hw // 2, hw // 2)
+    xu = F.interpolate(xs, size=(hw, hw), mode="bilinear", align_corners=False, antialias=True)
+    w = torch.randn(cout, cin, 3, 3) * 0.2
+    b = torch.randn(cout)
+    dy = torch.randn(F_, cout, hw, hw)
+    xr = xu.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, b, padding="same")
+    y.backward(dy)
+    xg, wg, bg, dyg = xs.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
+    out = torch.empty(F_, cout, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(xg), cin * hw * hw // 4, 0, 0, p(out), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout,
+                        hw, hw, 3, 32 | mode, st())
+    nmax = 64
+    slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+    nb = ctypes.c_int(0)
+    L().paig_conv2d_wgrad(p(xg), cin * hw * hw // 4, 0, 0, p(dyg), cout * hw * hw, p(slab), nmax, ctypes.byref(nb),
+                          F_, cin, cout, hw, hw, 3, 32 | mode, st())
+    g = torch.empty(cout * cin * 9 + cout, device=DEV)
+    L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
+    torch.cuda.synchronize()
+    assert rel_err(out, y.detach()) <= tf
+    assert rel_err(g[:cout * cin * 9].view_as(w), wr.grad) <= tb
+
+
 def test_conv_grouped_input_view():
     """The first conv reads frames (b, t < Te) of a [B, T, C, H, W] input in place."""
     B, T, Te, H = 3, 7, 4, 32

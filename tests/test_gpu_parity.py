@@ -40,11 +40,15 @@ def _input(z, device):
     return torch.from_numpy(x).to(device)
 
 
+# conv arithmetic: "split" (default: f16 hi/lo forward, bf16 hi/lo backward on
+# the 16-bit matrix cores) and "fp32" (f32-input MFMA) both meet the fp32 bar
+@pytest.mark.parametrize("conv_math", ["split", "fp32"])
 @pytest.mark.parametrize("name", SUPPORTED)
-def test_step_matches_reference(name):
+def test_step_matches_reference(name, conv_math):
     dev = torch.device("cuda:0")
     z = load_golden(name)
     m = _model(z, dev)
+    m.conv_math = conv_math
     x = _input(z, dev)
     m.output = m(x)
     train_loss, (pred, extrap, recons) = m.compute_loss()
@@ -108,3 +112,29 @@ def test_two_steps_accumulate_and_rmsprop():
     pd = dict(m.named_parameters())
     for rp, k in zip(refp, ref):
         assert rel_err(pd[k].detach(), rp.detach()) <= 1e-6, k
+
+
+# bf16 configuration (BASELINE config #2): bf16 conv operands, fp32 accumulate.
+# Not an fp32-parity mode: bars sized to bf16's 8-bit significand (measured
+# in emulation on the golden inputs: masks 5e-3, frames 2e-4, grads 9e-2).
+BF16_RTOL = {"out": 2e-2, "loss": 2e-3, "grad": 0.25}
+
+
+@pytest.mark.parametrize("name", ["spring_s12", "spring_s50"])
+def test_step_bf16_config(name):
+    dev = torch.device("cuda:0")
+    z = load_golden(name)
+    m = _model(z, dev)
+    m.conv_math = "bf16"
+    x = _input(z, dev)
+    m.output = m(x)
+    train_loss, (pred, extrap, recons) = m.compute_loss()
+    m.zero_grad(set_to_none=True)
+    train_loss.backward()
+    torch.cuda.synchronize()
+    for k, a in (("enc_pos", m.enc_pos), ("enc_masks", m.enc_masks), ("recons_out", m.recons_out),
+                 ("output_seq", m.output), ("pos_vel_seq", m.pos_vel_seq)):
+        assert rel_err(a, z[k]) <= BF16_RTOL["out"], k
+    assert rel_err(train_loss.reshape(()), z["loss_train"]) <= BF16_RTOL["loss"]
+    grads = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
+    grad_checks(z, grads, BF16_RTOL["grad"], prefix=name + " bf16: ")
