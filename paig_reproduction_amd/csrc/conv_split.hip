@@ -89,6 +89,71 @@ __device__ __forceinline__ s16x4 tr_read(const short* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
 }
 
+// Fused 2x bilinear upsample input (c7, c10: the reference's torchvision
+// Resize feeding a conv, blocks.py:260,269): a tile's half-resolution source
+// window (rows y0/2 - 1 .. y0/2 + RT/2, all columns, fp32) is prefetched a
+// tile ahead into registers, parked in LDS, and the upsampled rows are formed
+// from LDS while building the 16-bit operand image.
+template <int CIN, int H, int W, int FPT, int RT>
+struct UpStage {
+  static constexpr int HS = H / 2, WS = W / 2, SRN = RT / 2 + 2, QS = WS / 4;
+  static constexpr int NSU = FPT * CIN * SRN * QS, NLS = (NSU + 255) / 256;
+  static constexpr int SL = FPT * CIN * SRN * WS;   // floats of LDS
+  static_assert(WS % 4 == 0 && RT % 2 == 0, "upsample window");
+  f32x4 v[NLS];
+  __device__ __forceinline__ void issue(const FView& x, int F, int f0, int y0, int tid) {
+#pragma unroll
+    for (int l = 0; l < NLS; ++l) {
+      const int i = tid + l * 256;
+      const int q = i % QS, sr = (i / QS) % SRN, c = (i / (QS * SRN)) % CIN, fi = i / (QS * SRN * CIN);
+      const int srow = y0 / 2 - 1 + sr;
+      const bool ok = i < NSU && f0 + fi < F && srow >= 0 && srow < HS;
+      v[l] = ok ? *reinterpret_cast<const f32x4*>(x.frame(f0 + fi) + (long long)c * HS * WS + srow * WS + 4 * q)
+                : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ __forceinline__ void commit(float* Sl, int tid) const {
+#pragma unroll
+    for (int l = 0; l < NLS; ++l) {
+      const int i = tid + l * 256;   // Sl is [fi][c][sr][WS]: unit i sits at 4*i
+      if (NSU % 256 != 0 && i >= NSU) break;
+      *reinterpret_cast<f32x4*>(Sl + 4 * i) = v[l];
+    }
+  }
+  // output pixel (row gy, column x) of channel c of frame fi (0 <= gy < H), in
+  // aten's upsample_bilinear2d operation order
+  static __device__ __forceinline__ float px1(const float* Sl, int fi, int c, int gy, int y0, int x) {
+    int ya, yb, xa, xb;
+    float wa, wb, ua, ub;
+    up2_taps(gy, HS, ya, yb, wa, wb);
+    up2_taps(x, WS, xa, xb, ua, ub);
+    const float* p = Sl + (fi * CIN + c) * SRN * WS;
+    const float* r0 = p + (ya - (y0 / 2 - 1)) * WS;
+    const float* r1 = p + (yb - (y0 / 2 - 1)) * WS;
+    return wa * (ua * r0[xa] + ub * r0[xb]) + wb * (ua * r1[xa] + ub * r1[xb]);
+  }
+  // output pixels (row gy, x = 4q..4q+3) of channel c of frame fi (0 <= gy < H)
+  static __device__ __forceinline__ f32x4 row4(const float* Sl, int fi, int c, int gy, int y0, int q) {
+    int ya, yb;
+    float wa, wb;
+    up2_taps(gy, HS, ya, yb, wa, wb);
+    const float* p = Sl + (fi * CIN + c) * SRN * WS;
+    const float* r0 = p + (ya - (y0 / 2 - 1)) * WS;
+    const float* r1 = p + (yb - (y0 / 2 - 1)) * WS;
+    const int c0 = q > 0 ? 2 * q - 1 : 0, c3 = 2 * q + 2 < WS ? 2 * q + 2 : WS - 1;
+    const float2 m0 = *reinterpret_cast<const float2*>(r0 + 2 * q);
+    const float2 m1 = *reinterpret_cast<const float2*>(r1 + 2 * q);
+    const float a0 = r0[c0], a3 = r0[c3], b0 = r1[c0], b3 = r1[c3];
+    const float w0 = q > 0 ? 0.25f : 0.f, w1 = q > 0 ? 0.75f : 1.f;
+    f32x4 o;
+    o[0] = wa * (w0 * a0 + w1 * m0.x) + wb * (w0 * b0 + w1 * m1.x);
+    o[1] = wa * (0.75f * m0.x + 0.25f * m0.y) + wb * (0.75f * m1.x + 0.25f * m1.y);
+    o[2] = wa * (0.25f * m0.x + 0.75f * m0.y) + wb * (0.25f * m1.x + 0.75f * m1.y);
+    o[3] = wa * (0.75f * m0.y + 0.25f * a3) + wb * (0.75f * m1.y + 0.25f * b3);
+    return o;
+  }
+};
+
 // ============================================================ forward / dgrad
 template <int CIN, int COUT, int H, int W, int KS, int PM>
 struct SFwdCfg {
@@ -111,8 +176,9 @@ struct SFwdCfg {
   static constexpr int IMG = FPT * ROWS * RP * 8;            // 16-bit elements per image
   static constexpr int WIMG = NS * NT * 64 * 8;
   static constexpr int LDS = (IMG + WIMG) * 2 * NIMG;
-  static constexpr int Q = W / 4;
-  static constexpr int NI = FPT * ROWS * Q * CC;             // staging units (4 px x 8 ch)
+  // staging unit = one pixel x 8 channels: consecutive lanes take consecutive
+  // pixels (coalesced loads, b128 LDS writes PS slots apart: conflict-free)
+  static constexpr int NI = FPT * ROWS * W * CC;
   static constexpr int NL = (NI + 255) / 256;
   static_assert(W % 8 == 0 && (W >= 16 || 16 % W == 0), "M-tile rows");
   static_assert(RT * W * FPT == TPX || RT == H, "tile");
@@ -120,12 +186,12 @@ struct SFwdCfg {
 };
 
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 2)
 conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
                  int flags, int ntiles) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, PM>;
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
-  constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP, Q = C::Q;
+  constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP;
   constexpr int NI = C::NI, NL = C::NL, PADL = C::PADL;
   constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   constexpr long long HW = (long long)H * W;
@@ -184,62 +250,79 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     soff[s] = (tap / KS) * RP + (tap % KS) * PS + cc;
   }
 
-  // ---- staging: unit = 4 pixels (row, x = 4q..4q+3) x 8 channels, loads in
-  // flight during the previous tile's MFMAs (PIPE)
-  Seg<UPS, H, W> seg[NL][8];
+  // ---- staging: unit i = (frame fi, row r, chunk cc, pixel xp), xp fastest;
+  // the next tile's loads are in flight during this tile's MFMAs
+  using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
+  float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::IMG + C::WIMG));
+  auto put_px = [&](int i, const float* v) {
+    const int xp = i % W, r = (i / W) % ROWS, cc = (i / (W * ROWS)) % CC, fi = i / (W * ROWS * CC);
+    const int o = ((fi * ROWS + r) * RP + (xp + PADL) * PS + cc) * 8;
+    s16x8 hv, lv;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      short h, lo;
+      split<PM>(v[c], h, lo);
+      hv[c] = h;
+      lv[c] = lo;
+    }
+    *reinterpret_cast<s16x8*>(Xh + o) = hv;
+    if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = lv;
+  };
+  float pre[UPS ? 1 : NL][8];
+  UP up;
   auto issue = [&](int t) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+    if constexpr (UPS) {
+      up.issue(in, F, f0, y0, tid);
+    } else {
 #pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      const int i = tid + l * 256;
-      const int q = i % Q, r = (i / Q) % ROWS, cc = (i / (Q * ROWS)) % CC, fi = i / (Q * ROWS * CC);
-      const int f = f0 + fi, gy = y0 + r - PADL;
-      const bool ok = i < NI && f < F && gy >= 0 && gy < H;
+      for (int l = 0; l < NL; ++l) {
+        const int i = tid + l * 256;
+        const int xp = i % W, r = (i / W) % ROWS, cc = (i / (W * ROWS)) % CC, fi = i / (W * ROWS * CC);
+        const int f = f0 + fi, gy = y0 + r - PADL;
+        const bool ok = i < NI && f < F && gy >= 0 && gy < H;
+        const float* src = in.frame(ok ? f : 0) + (long long)(ok ? gy : 0) * W + xp;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const int ci = cc * 8 + c;
-        const bool okc = ok && ci < CIN;
-        seg[l][c].issue(okc ? in.frame(f) + ci * PLANE : in.p, gy, q, okc);
+        for (int c = 0; c < 8; ++c) {
+          const int ci = cc * 8 + c;
+          pre[l][c] = (ok && ci < CIN) ? src[ci * PLANE] : 0.f;
+        }
       }
     }
   };
   auto commit = [&](int t) {
-    const int y0 = (t % NRB) * RT;
+    if constexpr (UPS) {
+      const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+      up.commit(Sl, tid);
+      __syncthreads();
+#pragma unroll 1
+      for (int i = tid; i < NI; i += 256) {
+        const int xp = i % W, r = (i / W) % ROWS, cc = (i / (W * ROWS)) % CC, fi = i / (W * ROWS * CC);
+        const int gy = y0 + r - PADL;
+        const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+        float v[8];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      const int i = tid + l * 256;
-      if (NI % 256 != 0 && i >= NI) break;
-      const int q = i % Q, r = (i / Q) % ROWS, cc = (i / (Q * ROWS)) % CC, fi = i / (Q * ROWS * CC);
-      f32x4 v[8];
+        for (int c = 0; c < 8; ++c) v[c] = (ok && cc * 8 + c < CIN) ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp) : 0.f;
+        put_px(i, v);
+      }
+    } else {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) v[c] = seg[l][c].finish(y0 + r - PADL, q);
-      const int o0 = ((fi * ROWS + r) * RP + (4 * q + PADL) * PS + cc) * 8;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s16x8 hv, lv;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          short h, lo;
-          split<PM>(v[c][e], h, lo);
-          hv[c] = h;
-          lv[c] = lo;
-        }
-        *reinterpret_cast<s16x8*>(Xh + o0 + e * PS * 8) = hv;
-        if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o0 + e * PS * 8) = lv;
+      for (int l = 0; l < NL; ++l) {
+        const int i = tid + l * 256;
+        if (NI % 256 != 0 && i >= NI) break;
+        put_px(i, pre[l]);
       }
     }
   };
 
-  constexpr bool PIPE = !(UPS && H >= 32);
   int tile = blockIdx.x;
-  if (PIPE && tile < ntiles) issue(tile);
+  if (tile < ntiles) issue(tile);
   for (; tile < ntiles; tile += gridDim.x) {
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
     __syncthreads();   // previous tile's fragment reads are done
-    if (!PIPE) issue(tile);
     commit(tile);
     __syncthreads();
-    if (PIPE && tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
+    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
     f32x4 acc[MW][NT];
 #pragma unroll
     for (int mt = 0; mt < MW; ++mt)
@@ -305,15 +388,19 @@ struct SWgCfg {
   static constexpr int NT = ceil_div(NQ, 4);                  // N-tiles of 16 columns
   static constexpr int NCOL = CIN * KK;
   static constexpr int MT = ceil_div(COUT, 16), COP = MT * 16;
-  static constexpr int WN = (MT * NT * 4 <= 72) ? 1 : ((MT * ceil_div(NT, 2) * 4 <= 72) ? 2 : 4);
+  static constexpr int WN = (MT * NT * 4 <= 40) ? 1 : ((MT * ceil_div(NT, 2) * 4 <= 40) ? 2 : 4);
   static constexpr int WP = 4 / WN, NTW = ceil_div(NT, WN);
   static constexpr int TPX = 256;                             // pixels per tile
   static constexpr int FPT = H * W >= TPX ? 1 : TPX / (H * W);
   static constexpr int RT = H * W >= TPX ? TPX / W : H;
   static constexpr int ROWS = RT + KS - 1;
   static constexpr int TWPX = W + 2 * PADL;
-  static constexpr int PSX = CINQ;                            // 16-bit elements per staged pixel
-  static constexpr int XIMG = FPT * ROWS * TWPX * PSX;
+  // X image: one plane per 4-channel quad, [pixel position][4] (8 B per pixel)
+  // so the staging writes of consecutive pixels are consecutive; plane bases
+  // are 256-B aligned plus {0, 32, 128, 160} B so the transposed reads of an
+  // N-tile's 4 quads (4 pixels x 2 lane groups each) fill distinct banks
+  static constexpr int XPL = rup(FPT * ROWS * TWPX * 4 + 80, 128);   // room for the <= 80-element offset
+  static constexpr int XIMG = CQ * XPL;
   static constexpr int DP = TPX + 8;                          // dY row pitch: 16 rows -> 16 bank groups
   static constexpr int DIMG = COP * DP;
   static constexpr int KB = TPX / 32;                         // k-blocks of 32 pixels per tile
@@ -321,21 +408,22 @@ struct SWgCfg {
   static constexpr int RED = 4 * MT * NTW * 4 * 64 * 4;
   static constexpr int LDS = STG > RED ? STG : RED;
   static constexpr int Q = W / 4;
-  static constexpr int NIX = FPT * ROWS * Q * CQ, NLX = (NIX + 255) / 256;   // X units: 4 px x 4 ch
+  static constexpr int NIX = FPT * ROWS * W * CQ, NLX = (NIX + 255) / 256;   // X units: 1 px x 4 ch
   static constexpr int NID = COUT * TPX / 4, NLD = (NID + 255) / 256;         // dY units: 4 px x 1 ch
   static constexpr int SLAB = COUT * NCOL + COUT;
+  static constexpr int MINW = 2;                              // waves per SIMD the registers must allow
   static_assert(FPT * RT * W == TPX, "tile = 256 pixels");
   static_assert((RT * W) % 32 == 0 && (W % 32 == 0 || 32 % W == 0), "k-blocks stay in one frame");
   static_assert(H % RT == 0, "RT divides H");
 };
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, (SWgCfg<CIN, COUT, H, W, KS, PM>::MINW))
 conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles) {
   using C = SWgCfg<CIN, COUT, H, W, KS, PM>;
   constexpr int KK = C::KK, CQ = C::CQ, NQ = C::NQ, NT = C::NT, NCOL = C::NCOL, MT = C::MT, COP = C::COP;
   constexpr int WN = C::WN, WP = C::WP, NTW = C::NTW, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS;
-  constexpr int TWPX = C::TWPX, PSX = C::PSX, DP = C::DP, KB = C::KB, Q = C::Q, PADL = C::PADL;
+  constexpr int TWPX = C::TWPX, XPL = C::XPL, DP = C::DP, KB = C::KB, PADL = C::PADL;
   constexpr int NIX = C::NIX, NLX = C::NLX, NID = C::NID, NLD = C::NLD;
   constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   constexpr long long HW = (long long)H * W;
@@ -348,14 +436,15 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   const int wn = wv % WN, wp = wv / WN;
   constexpr int NRB = H / RT;
 
+  auto xplane = [](int cq) { return cq * XPL + ((cq & 1) ? 16 : 0) + ((cq & 2) ? 64 : 0); };
   // ---- zero the halo columns of X and the padded co rows of dY (never staged)
   if (PADL > 0) {
     for (int i = tid; i < FPT * ROWS * 2 * PADL; i += 256) {
       const int hc = i % (2 * PADL), r = i / (2 * PADL);
       const int xc = hc < PADL ? hc : W + hc;
-      for (int e = 0; e < PSX; e += 4) {
-        *reinterpret_cast<s16x4*>(Xh + (r * TWPX + xc) * PSX + e) = s16x4{0, 0, 0, 0};
-        if (PM != 2) *reinterpret_cast<s16x4*>(Xl + (r * TWPX + xc) * PSX + e) = s16x4{0, 0, 0, 0};
+      for (int cq = 0; cq < CQ; ++cq) {
+        *reinterpret_cast<s16x4*>(Xh + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
+        if (PM != 2) *reinterpret_cast<s16x4*>(Xl + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
       }
     }
   }
@@ -380,7 +469,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
     int cq = (wn + jn * WN) * 4 + pp;
     if (cq >= NQ) cq = 0;   // padded columns: any finite data, never stored
     const int tap = cq / CQ, ciq = cq % CQ;
-    colt[jn] = ((tap / KS) * TWPX + tap % KS) * PSX + ciq * 4;
+    colt[jn] = xplane(ciq) + ((tap / KS) * TWPX + tap % KS) * 4;
   }
   f32x4 acc[MT][NTW];
 #pragma unroll
@@ -391,57 +480,88 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
 #pragma unroll
   for (int l = 0; l < NLD; ++l) bacc[l] = 0.f;
 
-  Seg<UPS, H, W> sx[NLX][4];
-  f32x4 sd[NLD];
-  auto issue = [&](int t) {
+  // X units (1 pixel x 4 channels, pixel fastest) are prefetched a tile
+  // ahead where their registers are cheap, else loaded synchronously; fused-
+  // upsample inputs go through UpStage (half-resolution window, prefetched).
+  using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
+  float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::XIMG + C::DIMG));
+  constexpr bool XPIPE = !UPS && NLX * 4 + NLD * 4 <= 48;
+  auto load_x = [&](int t, int i, float* v) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+    const int xp = i % W, r = (i / W) % ROWS, cq = (i / (W * ROWS)) % CQ, fi = i / (W * ROWS * CQ);
+    const int f = f0 + fi, gy = y0 + r - PADL;
+    const bool ok = i < NIX && f < F && gy >= 0 && gy < H;
+    const float* src = x.frame(ok ? f : 0) + (long long)(ok ? gy : 0) * W + xp;
 #pragma unroll
-    for (int l = 0; l < NLX; ++l) {
-      const int i = tid + l * 256;
-      const int q = i % Q, r = (i / Q) % ROWS, cq = (i / (Q * ROWS)) % CQ, fi = i / (Q * ROWS * CQ);
-      const int f = f0 + fi, gy = y0 + r - PADL;
-      const bool ok = i < NIX && f < F && gy >= 0 && gy < H;
+    for (int c = 0; c < 4; ++c) v[c] = (ok && cq * 4 + c < CIN) ? src[(cq * 4 + c) * PLANE] : 0.f;
+  };
+  auto put_x = [&](int i, const float* v) {
+    const int xp = i % W, r = (i / W) % ROWS, cq = (i / (W * ROWS)) % CQ, fi = i / (W * ROWS * CQ);
+    const int o = xplane(cq) + ((fi * ROWS + r) * TWPX + xp + PADL) * 4;
+    s16x4 hv, lv;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int ci = cq * 4 + c;
-        const bool okc = ok && ci < CIN;
-        sx[l][c].issue(okc ? x.frame(f) + ci * PLANE : x.p, gy, q, okc);
-      }
+    for (int c = 0; c < 4; ++c) {
+      short h, lo;
+      split<PM>(v[c], h, lo);
+      hv[c] = h;
+      lv[c] = lo;
     }
+    *reinterpret_cast<s16x4*>(Xh + o) = hv;
+    if (PM != 2) *reinterpret_cast<s16x4*>(Xl + o) = lv;
+  };
+  UP up;
+  float sx[XPIPE ? NLX : 1][4];
+  auto load_d = [&](int t, int l) {
+    const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+    const int i = tid + l * 256;
+    const int co = i / (C::TPX / 4), pt = 4 * (i % (C::TPX / 4));
+    const int fi = pt / (RT * W), y = (pt / W) % RT, xx = pt % W;
+    const int f = f0 + fi;
+    return (i < NID && f < F) ? *reinterpret_cast<const f32x4*>(dy.frame(f) + co * HW + (long long)(y0 + y) * W + xx)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  constexpr bool DPIPE = XPIPE || UPS;
+  f32x4 sd[DPIPE ? NLD : 1];
+  auto issue = [&](int t) {
+    if constexpr (UPS) {
+      up.issue(x, F, (t / NRB) * FPT, (t % NRB) * RT, tid);
+    } else if constexpr (XPIPE) {
 #pragma unroll
-    for (int l = 0; l < NLD; ++l) {
-      const int i = tid + l * 256;
-      const int co = i / (C::TPX / 4), pt = 4 * (i % (C::TPX / 4));
-      const int fi = pt / (RT * W), y = (pt / W) % RT, xx = pt % W;
-      const int f = f0 + fi;
-      sd[l] = (i < NID && f < F)
-                  ? *reinterpret_cast<const f32x4*>(dy.frame(f) + co * HW + (long long)(y0 + y) * W + xx)
-                  : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int l = 0; l < NLX; ++l) load_x(t, tid + l * 256, sx[l]);
+    }
+    if constexpr (DPIPE) {
+#pragma unroll
+      for (int l = 0; l < NLD; ++l) sd[l] = load_d(t, l);
     }
   };
   auto commit = [&](int t) {
-    const int y0 = (t % NRB) * RT;
+    if constexpr (UPS) {
+      const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+      up.commit(Sl, tid);
+      __syncthreads();
+#pragma unroll 1
+      for (int i = tid; i < NIX; i += 256) {
+        const int xp = i % W, r = (i / W) % ROWS, cq = (i / (W * ROWS)) % CQ, fi = i / (W * ROWS * CQ);
+        const int gy = y0 + r - PADL;
+        const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+        float v[4];
 #pragma unroll
-    for (int l = 0; l < NLX; ++l) {
-      const int i = tid + l * 256;
-      if (NIX % 256 != 0 && i >= NIX) break;
-      const int q = i % Q, r = (i / Q) % ROWS, cq = (i / (Q * ROWS)) % CQ, fi = i / (Q * ROWS * CQ);
-      f32x4 v[4];
+        for (int c = 0; c < 4; ++c) v[c] = (ok && cq * 4 + c < CIN) ? UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp) : 0.f;
+        put_x(i, v);
+      }
+    } else if constexpr (XPIPE) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] = sx[l][c].finish(y0 + r - PADL, q);
-      const int o0 = ((fi * ROWS + r) * TWPX + 4 * q + PADL) * PSX + cq * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s16x4 hv, lv;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          short h, lo;
-          split<PM>(v[c][e], h, lo);
-          hv[c] = h;
-          lv[c] = lo;
-        }
-        *reinterpret_cast<s16x4*>(Xh + o0 + e * PSX) = hv;
-        if (PM != 2) *reinterpret_cast<s16x4*>(Xl + o0 + e * PSX) = lv;
+      for (int l = 0; l < NLX; ++l) {
+        const int i = tid + l * 256;
+        if (NIX % 256 != 0 && i >= NIX) break;
+        put_x(i, sx[l]);
+      }
+    } else {
+#pragma unroll 1
+      for (int i = tid; i < NIX; i += 256) {
+        float v[4];
+        load_x(t, i, v);
+        put_x(i, v);
       }
     }
 #pragma unroll
@@ -449,15 +569,18 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
       const int i = tid + l * 256;
       if (NID % 256 != 0 && i >= NID) break;
       const int co = i / (C::TPX / 4), pt = 4 * (i % (C::TPX / 4));
+      f32x4 dv;
+      if constexpr (DPIPE) dv = sd[l];
+      else dv = load_d(t, l);
       s16x4 hv, lv;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         short h, lo;
-        split<PM>(sd[l][e], h, lo);
+        split<PM>(dv[e], h, lo);
         hv[e] = h;
         lv[e] = lo;
       }
-      bacc[l] += (sd[l][0] + sd[l][1]) + (sd[l][2] + sd[l][3]);
+      bacc[l] += (dv[0] + dv[1]) + (dv[2] + dv[3]);
       *reinterpret_cast<s16x4*>(Dh + co * DP + pt) = hv;
       if (PM != 2) *reinterpret_cast<s16x4*>(Dl + co * DP + pt) = lv;
     }
@@ -481,7 +604,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
         ah[m] = *reinterpret_cast<const s16x8*>(Dh + o);
         al[m] = PM != 2 ? *reinterpret_cast<const s16x8*>(Dl + o) : ah[m];
       }
-      const int r0 = (base + roff[0]) * PSX, r1 = (base + roff[1]) * PSX;
+      const int r0 = (base + roff[0]) * 4, r1 = (base + roff[1]) * 4;
 #pragma unroll
       for (int jn = 0; jn < NTW; ++jn) {
         if (wn + jn * WN < NT) {
@@ -539,16 +662,16 @@ template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
                        hipStream_t st) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, PM>;
+  constexpr int LDS = C::LDS + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   auto k = conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM>;
   static int resident = 0;
   if (!resident) {
-    if (C::LDS > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    resident = persistent_grid((const void*)k, C::LDS);
+    if (LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    resident = persistent_grid((const void*)k, LDS);
   }
   const int nb = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL(k, dim3(nb), dim3(256), C::LDS, st, in, out, aux, w, b, F, flags, ntiles);
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -556,17 +679,19 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
 static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st) {
   using C = SWgCfg<CIN, COUT, H, W, KS, PM>;
+  constexpr int STG = C::STG + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
+  constexpr int LDS = STG > C::RED ? STG : C::RED;
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   int nb = ntiles < nblk_max ? ntiles : nblk_max;
   if (nb < 1) nb = 1;
   *nblk_out = nb;
   auto k = conv_wgrad_split_k<CIN, COUT, H, W, KS, UPS, PM>;
   static bool attr = false;
-  if (!attr && C::LDS > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+  if (!attr && LDS > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(nb), dim3(256), C::LDS, st, x, dy, slab, F, ntiles);
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), LDS, st, x, dy, slab, F, ntiles);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
