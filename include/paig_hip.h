@@ -86,6 +86,14 @@ size_t paig_gemm_workspace(int M, int N, int K);
 int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
               long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
               const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, void* stream);
+/* paig_gemm on the 16-bit matrix cores with split-precision operands
+ * (gemm.hip): math 0 = f32-input MFMA (= paig_gemm), 1 = f16 hi+lo pieces
+ * (fp32-accurate; operands |v| < 65504), 2 = bf16 hi+lo pieces (fp32 range),
+ * 3 = bf16.  rowsum is fused only for ta = 1 (else math falls back to 0). */
+int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
+                 long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
+                 const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,
+                 void* stream);
 size_t paig_colsum_workspace(int M, int N);
 int paig_colsum(const float* X, int M, int N, long long ld, float* out, int accumulate, float* ws, void* stream);
 int paig_slab_reduce(const float* slab, int nblk, long long ld, int len, float* out, int accumulate, void* stream);

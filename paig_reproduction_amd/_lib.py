@@ -44,6 +44,7 @@ SIGNATURES = {
     "paig_pos_head_bwd": (I, [P, P, P, I, I, F32, P]),
     "paig_gemm_workspace": (SZ, [I, I, I]),
     "paig_gemm": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, P]),
+    "paig_gemm_ex": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, I, P]),
     "paig_colsum_workspace": (SZ, [I, I]),
     "paig_colsum": (I, [P, I, I, LL, P, I, P, P]),
     "paig_slab_reduce": (I, [P, I, LL, I, P, I, P]),

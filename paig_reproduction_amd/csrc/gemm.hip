@@ -182,6 +182,194 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
       }
 }
 
+// ============================================ split-precision 16-bit MFMA GEMM
+// The same contract on v_mfma_f32_16x16x32_{f16,bf16}: every fp32 operand is
+// split into hi + lo 16-bit parts while it is staged (v = hi + lo exactly up
+// to the lo rounding) and a product is hi*hi + hi*lo + lo*hi, fp32 accumulate.
+// Per K element the three MFMAs cost ~3/16 of the f32-input form, so these
+// GEMMs (K = 3072 / 2000 / 200) fall to the HBM roofline.  math: 1 = f16
+// pieces (22 significant bits; operands must satisfy |v| < 65504: forward
+// activations / weights), 2 = bf16 pieces (16 bits, fp32 range: gradients),
+// 3 = bf16 hi only (the bf16 configuration).
+// LDS images keep each operand's global orientation: k-contiguous operands
+// as [row][k] (pitch 40: the 16 rows of a b128 fragment read hit 16 distinct
+// bank groups), row-contiguous operands as [pi(k)][row] (pitch 80) read with
+// ds_read_b64_tr_b16; pi places the 8 k-rows one 32-lane half reads in 8
+// consecutive image rows, 5 x 32 B apart mod 256 B: conflict-free.
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int SPK = 40;          // [row][k] pitch (16-bit elements)
+constexpr int SPR = 80;          // [pi(k)][row] pitch
+constexpr int SIMG = 64 * SPK > BK * SPR ? 64 * SPK : BK * SPR;
+
+__device__ __forceinline__ int kperm(int k) {   // k = 8g + 4h + q
+  const int g = k >> 3, h = (k >> 2) & 1, q = k & 3;
+  return 16 * (g >> 1) + 8 * h + 4 * (g & 1) + q;
+}
+
+template <int PM>
+__device__ __forceinline__ void gsplit(float v, short& h, short& l) {
+  if constexpr (PM == 1) {
+    const _Float16 a = (_Float16)v;
+    h = __builtin_bit_cast(short, a);
+    l = __builtin_bit_cast(short, (_Float16)(v - (float)a));
+  } else {
+    const __bf16 a = (__bf16)v;
+    h = __builtin_bit_cast(short, a);
+    l = PM == 2 ? __builtin_bit_cast(short, (__bf16)(v - (float)a)) : (short)0;
+  }
+}
+
+template <int PM>
+__device__ __forceinline__ f32x4 gmma(s16x8 a, s16x8 b, f32x4 c) {
+  if constexpr (PM == 1)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+
+// 16-bit image of one 64 x BK operand tile (the fp32 Tile registers, split)
+template <bool KCONTIG, int PM>
+__device__ __forceinline__ void store16(const Tile<KCONTIG>& t, short* ih, short* il, int tid) {
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    s16x4 hv, lv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      short h, l;
+      gsplit<PM>(t.v[e][i], h, l);
+      hv[i] = h;
+      lv[i] = l;
+    }
+    int o;
+    if (KCONTIG) o = ((tid >> 3) + 32 * e) * SPK + (tid & 7) * 4;
+    else o = kperm((tid >> 4) + 16 * e) * SPR + (tid & 15) * 4;
+    *reinterpret_cast<s16x4*>(ih + o) = hv;
+    if (PM != 3) *reinterpret_cast<s16x4*>(il + o) = lv;
+  }
+}
+
+// fragment of 16 rows (r0 ..) x 32 k for this lane: row r0 + (lane & 15), k = 8(lane>>4) + j
+template <bool KCONTIG>
+__device__ __forceinline__ s16x8 frag16(const short* img, int r0, int lane) {
+  if (KCONTIG) return *reinterpret_cast<const s16x8*>(img + (r0 + (lane & 15)) * SPK + 8 * (lane >> 4));
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const short* b0 = img + kperm(8 * g + q) * SPR + r0 + 4 * p;
+  const short* b1 = img + kperm(8 * g + 4 + q) * SPR + r0 + 4 * p;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)b0);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)b1);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <bool TA, bool TB, int PM>
+__global__ void __launch_bounds__(256)
+gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
+             const float* __restrict__ B, long long ldb, int vecb, float* __restrict__ C, long long ldc, float beta,
+             const float* __restrict__ bias, int act, int auxm, const float* __restrict__ aux, long long ldaux,
+             float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart) {
+  constexpr int NI = PM == 3 ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) short S16[4 * SIMG];
+  short* Ah = S16;
+  short* Al = S16 + SIMG;
+  short* Bh = S16 + 2 * SIMG;
+  short* Bl = S16 + 3 * SIMG;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = blockIdx.z * kchunk;
+  int kend = kbeg + kchunk;
+  if (kend > K) kend = K;
+  // row sums of op(A) (= the bias gradient of a wgrad GEMM) in exact fp32
+  // from the staging registers; only the transposed-A form carries them
+  const bool do_rs = TA && rowsum != nullptr && blockIdx.x == 0;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 rs4 = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Tile<!TA> ta;
+  Tile<TB> tb;
+  if (kbeg < kend) {
+    ta.load(A, lda, m0, kbeg, M, kend, veca, tid);
+    tb.load(B, ldb, n0, kbeg, N, kend, vecb, tid);
+  }
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    store16<!TA, PM>(ta, Ah, Al, tid);
+    store16<TB, PM>(tb, Bh, Bl, tid);
+    if (do_rs) rs4 += ta.v[0] + ta.v[1];
+    __syncthreads();
+    if (k0 + BK < kend) {
+      ta.load(A, lda, m0, k0 + BK, M, kend, veca, tid);
+      tb.load(B, ldb, n0, k0 + BK, N, kend, vecb, tid);
+    }
+    s16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ah[i] = frag16<!TA>(Ah, wm * 32 + i * 16, lane);
+      al[i] = PM != 3 ? frag16<!TA>(Al, wm * 32 + i * 16, lane) : ah[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bh[j] = frag16<TB>(Bh, wn * 32 + j * 16, lane);
+      bl[j] = PM != 3 ? frag16<TB>(Bl, wn * 32 + j * 16, lane) : bh[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (PM != 3) {
+          acc[i][j] = gmma<PM>(al[i], bh[j], acc[i][j]);
+          acc[i][j] = gmma<PM>(ah[i], bl[j], acc[i][j]);
+        }
+        acc[i][j] = gmma<PM>(ah[i], bh[j], acc[i][j]);
+      }
+  }
+  if (do_rs) {
+    // thread (k = tid>>4 (+16), rows (tid&15)*4 .. +3): reduce over the 16 k-threads
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(S16);   // [16][64]
+    *reinterpret_cast<f32x4*>(red + (tid >> 4) * 64 + (tid & 15) * 4) = rs4;
+    __syncthreads();
+    if (tid < BM && m0 + tid < M) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v += red[k * 64 + tid];
+      if (rowpart) rowpart[(long long)blockIdx.z * M + m0 + tid] = alpha * v;
+      else rowsum[m0 + tid] = alpha * v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (m < M && n < N) {
+          float v = alpha * acc[i][j][r];
+          if (part) {
+            part[((long long)blockIdx.z * M + m) * N + n] = v;
+          } else {
+            if (beta != 0.f) v += beta * C[(long long)m * ldc + n];
+            if (bias) v += bias[n];
+            C[(long long)m * ldc + n] = epi(v, act, auxm, aux, (long long)m * ldaux + n);
+          }
+        }
+      }
+}
+
 // sum_{s<S} p[s*ld] in order s = 0..S-1 (deterministic), loads issued 8 at a
 // time so the partial slabs stream instead of one dependent load per split
 __device__ __forceinline__ float sum_strided(const float* __restrict__ p, long long ld, int S) {
@@ -233,9 +421,29 @@ static inline bool vec_ok(const float* p, long long ld) {
   return ((uintptr_t)p % 16 == 0) && (ld % 4 == 0);
 }
 
+template <bool TA, bool TB>
+static void launch_gemm(int math, dim3 grid, hipStream_t st, int M, int N, int K, int kchunk, float alpha,
+                        const float* A, long long lda, int va, const float* B, long long ldb, int vb, float* C,
+                        long long ldc, float beta, const float* bias, int act, int auxm, const float* aux,
+                        long long ldaux, float* part, float* rowsum, float* rowpart) {
+#define PAIG_L(KERN)                                                                                          \
+  hipLaunchKernelGGL(KERN, grid, dim3(256), 0, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, \
+                     bias, act, auxm, aux, ldaux, part, rowsum, rowpart)
+  if (math == 1) PAIG_L((gemm_split_k<TA, TB, 1>));
+  else if (math == 2) PAIG_L((gemm_split_k<TA, TB, 2>));
+  else if (math == 3) PAIG_L((gemm_split_k<TA, TB, 3>));
+  else PAIG_L((gemm_k<TA, TB>));
+#undef PAIG_L
+}
+
 }  // namespace
 
 extern "C" {
+
+int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
+                 long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
+                 const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,
+                 void* stream);
 
 size_t paig_gemm_workspace(int M, int N, int K) {
   int s = choose_split(M, N, K);
@@ -245,7 +453,20 @@ size_t paig_gemm_workspace(int M, int N, int K) {
 int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
               long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
               const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, void* stream) {
+  return paig_gemm_ex(ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, act, auxm, aux, ldaux, rowsum, ws,
+                      ws_floats, 0, stream);
+}
+
+int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
+                 long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
+                 const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,
+                 void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (math < 0 || math > 3) {
+    paig_set_error("paig_gemm_ex: math must be 0..3, got %d", math);
+    return PAIG_E_UNSUPPORTED;
+  }
+  if (rowsum && !ta) math = 0;   // fused row sums exist on the split path for op(A) = A^T only
   if (M <= 0 || N <= 0) return 0;
   int S = K > 0 ? choose_split(M, N, K) : 1;
   if (S > 1 && (ws == nullptr || ws_floats < (size_t)S * M * N + (size_t)S * M)) S = 1;
@@ -255,9 +476,9 @@ int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, 
   float* part = S > 1 ? ws : nullptr;
   float* rowpart = (S > 1 && rowsum) ? ws + (size_t)S * M * N : nullptr;
   const int va = vec_ok(A, lda), vb = vec_ok(B, ldb);
-#define PAIG_G(TA_, TB_)                                                                                          \
-  hipLaunchKernelGGL((gemm_k<TA_, TB_>), grid, dim3(256), 0, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, \
-                     ldc, beta, bias, act, auxm, aux, ldaux, part, rowsum, rowpart)
+#define PAIG_G(TA_, TB_)                                                                                       \
+  launch_gemm<TA_, TB_>(math, grid, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, bias, act, auxm, \
+                        aux, ldaux, part, rowsum, rowpart)
   if (ta && tb) PAIG_G(true, true);
   else if (ta) PAIG_G(true, false);
   else if (tb) PAIG_G(false, true);

@@ -237,6 +237,13 @@ class Engine:
     # (BASELINE config #2)
     CONV_MATH = {"split": 128, "fp32": 0, "bf16": 256}
 
+    # the same choice for the dense layers (paig_gemm_ex math): forward GEMMs
+    # take f16 pieces, gradient GEMMs bf16 pieces
+    GEMM_MATH = {"split": (1, 2), "fp32": (0, 0), "bf16": (3, 3)}
+
+    def gemm_math(self, backward):
+        return self.GEMM_MATH[getattr(self.model, "conv_math", "split")][1 if backward else 0]
+
     def conv_flags(self):
         m = getattr(self.model, "conv_math", "split")
         if m not in self.CONV_MATH:
@@ -259,8 +266,8 @@ class Engine:
         W, b = self.p(name + ".weight"), self.p(name + ".bias")
         O, I = W.shape
         with self._p("gemm_fwd:" + name, 2 * rows * O * I):
-            self.L.paig_gemm(0, 1, rows, O, I, 1.0, ptr(x), I, ptr(W), I, 0.0, ptr(out), O, ptr(b), act, 0, None, 0,
-                             None, ptr(ws), ws.numel() if ws is not None else 0, st)
+            self.L.paig_gemm_ex(0, 1, rows, O, I, 1.0, ptr(x), I, ptr(W), I, 0.0, ptr(out), O, ptr(b), act, 0, None,
+                                0, None, ptr(ws), ws.numel() if ws is not None else 0, self.gemm_math(False), st)
 
     def linear_bwd(self, x, dy, rows, name, dx, aux, auxm, st, ws, need_dx=True):
         """dW = dy^T x and db = colsum(dy) (one GEMM, fused row sums) ; dx = (dy W) * act'(aux)"""
@@ -269,12 +276,12 @@ class Engine:
         gW, gb = self.g(name + ".weight"), self.g(name + ".bias")
         n_ws = ws.numel()
         with self._p("gemm_wgrad:" + name, 2 * rows * O * I):
-            self.L.paig_gemm(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
-                             ptr(gb), ptr(ws), n_ws, st)
+            self.L.paig_gemm_ex(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
+                                ptr(gb), ptr(ws), n_ws, self.gemm_math(True), st)
         if need_dx:
             with self._p("gemm_dgrad:" + name, 2 * rows * O * I):
-                self.L.paig_gemm(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm,
-                                 ptr(aux), I, None, ptr(ws), n_ws, st)
+                self.L.paig_gemm_ex(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm,
+                                    ptr(aux), I, None, ptr(ws), n_ws, self.gemm_math(True), st)
 
     def workspace_floats(self, lay):
         K, F, B = lay.K, lay.F, lay.B

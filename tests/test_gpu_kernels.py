@@ -197,6 +197,33 @@ def test_gemm(ta, tb, M, N, K):
     assert rel_err(rs, (A.t() if ta else A).sum(1)) <= 2e-5
 
 
+# split-precision GEMM (paig_gemm_ex): math 1 f16 hi/lo, 2 bf16 hi/lo, 3 bf16
+GEMM_EX_TOL = {1: 2e-5, 2: 5e-5, 3: 3e-2}
+
+
+@pytest.mark.parametrize("math", [1, 2, 3])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(37, 50, 19), (130, 200, 3072), (200, 3072, 130), (6, 2, 200), (1, 513, 200),
+                                   (2000, 200, 3072)])
+def test_gemm_ex(ta, tb, M, N, K, math):
+    torch.manual_seed(M + N + K + math)
+    A = (torch.randn(K, M) if ta else torch.randn(M, K)) / K ** 0.5
+    Bm = torch.randn(N, K) if tb else torch.randn(K, N)
+    bias = torch.randn(N)
+    ref = torch.tanh((A.t() if ta else A) @ (Bm.t() if tb else Bm) + bias)
+    Ag, Bg, biasg = A.to(DEV), Bm.to(DEV), bias.to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    ws = torch.empty(max(1, L().paig_gemm_workspace(M, N, K)), device=DEV)
+    rs = torch.full((M,), 7.0, device=DEV)
+    rc = L().paig_gemm_ex(ta, tb, M, N, K, 1.0, p(Ag), A.shape[1], p(Bg), Bm.shape[1], 0.0, p(C), N, p(biasg), 2, 0,
+                          None, 0, p(rs) if ta else None, p(ws), ws.numel(), math, st())
+    torch.cuda.synchronize()
+    assert rc == 0
+    assert rel_err(C, ref) <= GEMM_EX_TOL[math]
+    if ta:   # fused row sums of op(A) in exact fp32
+        assert rel_err(rs, A.t().sum(1)) <= 2e-5
+
+
 def test_pool_upsample():
     x = torch.relu(torch.randn(5, 6, 16, 16))
     xg = x.to(DEV)
