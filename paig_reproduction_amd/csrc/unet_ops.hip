@@ -67,6 +67,65 @@ __global__ void maxpool_bwd_relu_k(FView x, FView dy, FViewW dx, int F, int C, i
   }
 }
 
+// Vector forms (W % 4 == 0, H even): one thread per 2 x 2-pooled outputs
+// (a 2-row x 4-column input block): float4 loads and stores, 32-bit
+// indexing, the argmax computed once per window in aten's scan order.
+__device__ __forceinline__ int argmax4(float a, float b, float c, float d, float& m) {
+  int am = 0;
+  m = a;
+  if (b > m || b != b) { m = b; am = 1; }
+  if (c > m || c != c) { m = c; am = 2; }
+  if (d > m || d != d) { m = d; am = 3; }
+  return am;
+}
+
+__global__ void maxpool_fwd_v_k(FView x, FViewW y, int F, int C, int H, int W) {
+  const int Ho = H / 2, Q = W / 4;
+  const int n = F * C * Ho * Q;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int q = i % Q, t = i / Q, pi = t % Ho, fc = t / Ho, c = fc % C, f = fc / C;
+    const float* xp = x.frame(f) + ((long long)c * H + 2 * pi) * W + 4 * q;
+    const float4 a = *reinterpret_cast<const float4*>(xp);
+    const float4 b = *reinterpret_cast<const float4*>(xp + W);
+    float m0, m1;
+    argmax4(a.x, a.y, b.x, b.y, m0);
+    argmax4(a.z, a.w, b.z, b.w, m1);
+    *reinterpret_cast<float2*>(y.frame(f) + ((long long)c * Ho + pi) * (W / 2) + 2 * q) = make_float2(m0, m1);
+  }
+}
+
+// dx = (dx + [argmax] * dy) * (x > 0)
+__global__ void maxpool_bwd_relu_v_k(FView x, FView dy, FViewW dx, int F, int C, int H, int W) {
+  const int Ho = H / 2, Q = W / 4;
+  const int n = F * C * Ho * Q;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int q = i % Q, t = i / Q, pi = t % Ho, fc = t / Ho, c = fc % C, f = fc / C;
+    const long long o = ((long long)c * H + 2 * pi) * W + 4 * q;
+    const float* xp = x.frame(f) + o;
+    float* dp = dx.frame(f) + o;
+    const float4 a = *reinterpret_cast<const float4*>(xp);
+    const float4 b = *reinterpret_cast<const float4*>(xp + W);
+    const float2 g = *reinterpret_cast<const float2*>(dy.frame(f) + ((long long)c * Ho + pi) * (W / 2) + 2 * q);
+    float4 d0 = *reinterpret_cast<const float4*>(dp);
+    float4 d1 = *reinterpret_cast<const float4*>(dp + W);
+    float m;
+    const int a0 = argmax4(a.x, a.y, b.x, b.y, m);
+    const int a1 = argmax4(a.z, a.w, b.z, b.w, m);
+    if (a0 == 0) d0.x += g.x; else if (a0 == 1) d0.y += g.x; else if (a0 == 2) d1.x += g.x; else d1.y += g.x;
+    if (a1 == 0) d0.z += g.y; else if (a1 == 1) d0.w += g.y; else if (a1 == 2) d1.z += g.y; else d1.w += g.y;
+    d0.x = a.x > 0.f ? d0.x : 0.f;
+    d0.y = a.y > 0.f ? d0.y : 0.f;
+    d0.z = a.z > 0.f ? d0.z : 0.f;
+    d0.w = a.w > 0.f ? d0.w : 0.f;
+    d1.x = b.x > 0.f ? d1.x : 0.f;
+    d1.y = b.y > 0.f ? d1.y : 0.f;
+    d1.z = b.z > 0.f ? d1.z : 0.f;
+    d1.w = b.w > 0.f ? d1.w : 0.f;
+    *reinterpret_cast<float4*>(dp) = d0;
+    *reinterpret_cast<float4*>(dp + W) = d1;
+  }
+}
+
 // ------------------------------------------------------- bilinear upsample ---
 // 1-D taps of aten's upsample_bilinear2d (align_corners=False, no scale given):
 //   src = max(0, (dst + 0.5) * in/out - 0.5); i0 = floor(src); i1 = min(i0+1, in-1)
@@ -142,6 +201,63 @@ __global__ void upsample_bwd_k(FView du, FView s, FViewW ds, int F, int C, int H
     }
     if (relu_mask) acc = s.frame(f)[((long long)c * Hs + sy) * Ws + sx] > 0.f ? acc : 0.f;
     ds.frame(f)[((long long)c * Hs + sy) * Ws + sx] = acc;
+  }
+}
+
+// Vector form (Ws even): one thread per 2 horizontally adjacent source
+// pixels; each reads its 4 du rows as float4 + 2 edge scalars.  The per-pixel
+// accumulation order (and the zero-weight taps, which add exact zeros) is the
+// scalar kernel's, so the two forms agree bit for bit on finite inputs.
+__global__ void upsample_bwd_v_k(FView du, FView s, FViewW ds, int F, int C, int Hs, int Ws, int relu_mask) {
+  const int Ho = 2 * Hs, Wo = 2 * Ws, P = Ws / 2;
+  const int n = F * C * Hs * P;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int m = i % P, t = i / P, sy = t % Hs, fc = t / Hs, c = fc % C, f = fc / C;
+    const float* dup = du.frame(f) + (long long)c * Ho * Wo;
+    float wy[4];
+    wy[0] = sy >= 1 ? 0.25f : 0.f;
+    wy[1] = sy == 0 ? 1.f : 0.75f;
+    wy[2] = sy == Hs - 1 ? 1.f : 0.75f;
+    wy[3] = sy <= Hs - 2 ? 0.25f : 0.f;
+    // source columns sx0 = 2m, sx1 = 2m + 1 read du columns 4m-1 .. 4m+4
+    const int s0 = 2 * m, s1 = 2 * m + 1;
+    float wx0[4], wx1[4];
+    wx0[0] = s0 >= 1 ? 0.25f : 0.f;
+    wx0[1] = s0 == 0 ? 1.f : 0.75f;
+    wx0[2] = s0 == Ws - 1 ? 1.f : 0.75f;
+    wx0[3] = s0 <= Ws - 2 ? 0.25f : 0.f;
+    wx1[0] = 0.25f;
+    wx1[1] = 0.75f;
+    wx1[2] = s1 == Ws - 1 ? 1.f : 0.75f;
+    wx1[3] = s1 <= Ws - 2 ? 0.25f : 0.f;
+    float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int y = 2 * sy - 1 + a;
+      if (wy[a] == 0.f) continue;
+      const float* rp = dup + y * Wo + 4 * m;
+      const float4 v = *reinterpret_cast<const float4*>(rp);
+      const float l = m > 0 ? rp[-1] : 0.f;
+      const float r = 4 * m + 4 < Wo ? rp[4] : 0.f;
+      float row0 = 0.f, row1 = 0.f;
+      if (wx0[0] != 0.f) row0 = fmaf(wx0[0], l, row0);
+      row0 = fmaf(wx0[1], v.x, row0);
+      row0 = fmaf(wx0[2], v.y, row0);
+      if (wx0[3] != 0.f) row0 = fmaf(wx0[3], v.z, row0);
+      row1 = fmaf(wx1[0], v.y, row1);
+      row1 = fmaf(wx1[1], v.z, row1);
+      row1 = fmaf(wx1[2], v.w, row1);
+      if (wx1[3] != 0.f) row1 = fmaf(wx1[3], r, row1);
+      acc0 = fmaf(wy[a], row0, acc0);
+      acc1 = fmaf(wy[a], row1, acc1);
+    }
+    const long long so = ((long long)c * Hs + sy) * Ws + 2 * m;
+    if (relu_mask) {
+      const float2 sv = *reinterpret_cast<const float2*>(s.frame(f) + so);
+      acc0 = sv.x > 0.f ? acc0 : 0.f;
+      acc1 = sv.y > 0.f ? acc1 : 0.f;
+    }
+    *reinterpret_cast<float2*>(ds.frame(f) + so) = make_float2(acc0, acc1);
   }
 }
 
@@ -432,6 +548,14 @@ extern "C" {
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,
                       void* stream) {
   if (F <= 0) return 0;
+  if (H % 2 == 0 && W % 4 == 0 && x_fs % 4 == 0 && y_fs % 2 == 0 && (long long)F * C * H * W < (1ll << 31) &&
+      (uintptr_t)x % 16 == 0 && (uintptr_t)y % 8 == 0) {
+    const long long nv = (long long)F * C * (H / 2) * (W / 4);
+    hipLaunchKernelGGL(maxpool_fwd_v_k, dim3(grid_for(nv)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
+                       FViewW{y, y_fs}, F, C, H, W);
+    PAIG_CHECK_LAUNCH();
+    return 0;
+  }
   long long n = (long long)F * C * (H / 2) * (W / 2);
   hipLaunchKernelGGL(maxpool_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
                      FViewW{y, y_fs}, F, C, H, W);
@@ -442,6 +566,15 @@ int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, 
 int paig_maxpool2_bwd_relu(const float* x, long long x_fs, const float* dy, long long dy_fs, float* dx, long long dx_fs,
                            int F, int C, int H, int W, void* stream) {
   if (F <= 0) return 0;
+  if (H % 2 == 0 && W % 4 == 0 && x_fs % 4 == 0 && dx_fs % 4 == 0 && dy_fs % 2 == 0 &&
+      (long long)F * C * H * W < (1ll << 31) && (uintptr_t)x % 16 == 0 && (uintptr_t)dx % 16 == 0 &&
+      (uintptr_t)dy % 8 == 0) {
+    const long long nv = (long long)F * C * (H / 2) * (W / 4);
+    hipLaunchKernelGGL(maxpool_bwd_relu_v_k, dim3(grid_for(nv)), dim3(256), 0, (hipStream_t)stream,
+                       FView{x, x_fs, 0, 0}, FView{dy, dy_fs, 0, 0}, FViewW{dx, dx_fs}, F, C, H, W);
+    PAIG_CHECK_LAUNCH();
+    return 0;
+  }
   long long n = (long long)F * C * H * W;
   hipLaunchKernelGGL(maxpool_bwd_relu_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
                      FView{dy, dy_fs, 0, 0}, FViewW{dx, dx_fs}, F, C, H, W);
@@ -463,6 +596,15 @@ int paig_upsample2_bwd(const float* du, long long du_fs, const float* s, long lo
                        int F, int C, int Hs, int Ws, int Ho, int Wo, int relu_mask, void* stream) {
   if (F <= 0) return 0;
   PAIG_REQUIRE(Ho == 2 * Hs && Wo == 2 * Ws, "upsample_bwd: exact 2x upscale only (Resize(H/2 -> H))");
+  if (Ws % 2 == 0 && Wo % 4 == 0 && du_fs % 4 == 0 && ds_fs % 2 == 0 && (!relu_mask || s_fs % 2 == 0) &&
+      (long long)F * C * Ho * Wo < (1ll << 31) && (uintptr_t)du % 16 == 0 && (uintptr_t)ds % 8 == 0 &&
+      (!relu_mask || (uintptr_t)s % 8 == 0)) {
+    const long long nv = (long long)F * C * Hs * (Ws / 2);
+    hipLaunchKernelGGL(upsample_bwd_v_k, dim3(grid_for(nv)), dim3(256), 0, (hipStream_t)stream,
+                       FView{du, du_fs, 0, 0}, FView{s, s_fs, 0, 0}, FViewW{ds, ds_fs}, F, C, Hs, Ws, relu_mask);
+    PAIG_CHECK_LAUNCH();
+    return 0;
+  }
   long long n = (long long)F * C * Hs * Ws;
   hipLaunchKernelGGL(upsample_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{du, du_fs, 0, 0},
                      FView{s, s_fs, 0, 0}, FViewW{ds, ds_fs}, F, C, Hs, Ws, Ho, Wo, relu_mask);
