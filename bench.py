@@ -64,6 +64,10 @@ def parse():
                     help="committed rocprofv3 FETCH_SIZE/WRITE_SIZE summary (tools/pmc_traffic.py)")
     ap.add_argument("--graph", type=int, default=1, help="capture fwd+loss+bwd in a HIP graph per resident batch")
     ap.add_argument("--probe_steps", type=int, default=5, help="eager steps timing the probed kernel")
+    ap.add_argument("--split_graph", type=int, default=-1,
+                    help="capture the step as two HIP graphs split where the early gradient bucket is final, and "
+                         "all-reduce that bucket between the replays, overlapping the U-Net backward "
+                         "(-1: on when N > 1)")
     ap.add_argument("--conv_math", default="split", choices=["split", "fp32", "bf16"],
                     help="U-Net conv arithmetic: split = f16/bf16 hi+lo operands on the 16-bit matrix cores, "
                          "fp32-accurate (meets the 1e-4 parity bar; default); fp32 = f32-input MFMA; "
@@ -109,9 +113,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PAIG_DIST_BACKEND=gloo / PAIG_BENCH_DEVICE=0 rehearse the N-rank code path
+    # with several ranks on ONE GPU (the production path is RCCL, one GPU per rank)
+    backend = os.environ.get("PAIG_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("PAIG_BENCH_DEVICE", local))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
 
     from paig_reproduction_amd.nn.datasets.synth import render_sequences, as_model_input
@@ -153,24 +164,53 @@ def main():
     for i in range(a.warmup):
         eager_step(i)
     graphs = None
+    split = a.split_graph if a.split_graph >= 0 else int(world > 1)
     if a.graph:
-        # one graph per resident batch, sharing one memory pool; the optimizer
-        # step (and the DP all-reduce inside it) stays eager
+        # one graph per resident batch (two when split), sharing one memory
+        # pool; the optimizer step and the DP all-reduce stay eager
         torch.cuda.synchronize()
         graphs, pool = [], None
         for x in data:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                lg = body(x)
-            pool = g.pool()
-            graphs.append((g, lg))
+            if not split:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    lg = body(x)
+                pool = g.pool()
+                graphs.append(((g,), lg))
+                continue
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            seen = []
+
+            def cut():   # engine.bucket_hook: the early bucket is final here
+                g1.capture_end()
+                g2.capture_begin(pool=g1.pool(), capture_error_mode="relaxed")
+                seen.append(1)
+
+            cap = torch.cuda.Stream()
+            cap.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cap):
+                # relaxed: the cut runs on the autograd engine's device thread
+                g1.capture_begin(pool=pool, capture_error_mode="relaxed")
+                eng.bucket_hook = cut
+                try:
+                    lg = body(x)
+                finally:
+                    eng.bucket_hook = m._flat.allreduce_early
+                g2.capture_end()
+            torch.cuda.current_stream().wait_stream(cap)
+            assert seen == [1], "backward did not reach the bucket split point"
+            pool = g1.pool()
+            graphs.append(((g1, g2), lg))
         torch.cuda.synchronize()
 
     def step(i):
         if graphs is None:
             return eager_step(i)
-        g, lg = graphs[i % len(graphs)]
-        g.replay()
+        gs, lg = graphs[i % len(graphs)]
+        gs[0].replay()
+        if len(gs) == 2:
+            m._flat.allreduce_early()   # overlaps the second graph (U-Net backward)
+            gs[1].replay()
         m.optimizer.step()
         return lg
 
@@ -223,7 +263,7 @@ def main():
                                    f"B={a.batch}/rank, {size}x{size}x3, seq_len {a.seq_len} "
                                    f"({ins} in / {pred} pred / {a.seq_len - ins - pred} extrap)",
                        "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}",
-                       "conv_math": a.conv_math},
+                       "conv_math": a.conv_math, "split_graph": bool(a.graph and split)},
             "roofline": roof, "cpu_baseline": cpu, "final_loss": round(lossv, 4),
             # whole-step memory-side traffic (committed PMC profile) at this run's step time
             "hbm_step": None if step_bytes is None else {

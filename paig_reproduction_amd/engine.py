@@ -230,6 +230,9 @@ class Engine:
         self.probe = None
         self.last_masked_objs = None
         self._side = None   # second stream (see _fork)
+        # called once per backward when the early gradient bucket is final
+        # (FlatParams.allreduce_early by default; bench.py splits its HIP graph here)
+        self.bucket_hook = model._flat.allreduce_early
 
     # conv arithmetic (include/paig_hip.h flags): "split" = f16 hi/lo forward and
     # bf16 hi/lo dgrad/wgrad on the 16-bit matrix cores (fp32-accurate: the
@@ -588,6 +591,10 @@ class Engine:
         dobjs = _empty(K * F * lay.l1_in, dev)
         self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws)
         self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
+        # every gradient of the flat buffer's early bucket is final (queued on
+        # this stream): the data-parallel all-reduce of that bucket may start
+        if self.bucket_hook is not None:
+            self.bucket_hook()
 
         # ---- mask softmax backward (incl. ReLU' of ShallowUNet's c13, Q13, and
         # the AvgPool2d backward of the UNet path)

@@ -17,13 +17,16 @@ from ._lib import lib, ptr, stream_handle
 
 
 class FlatParams:
-    def __init__(self, model, names):
+    def __init__(self, model, names, early=()):
         self.model = model
         self.names = list(names)
+        self.early = tuple(early)   # name prefixes of the early-final gradient bucket (a prefix of names)
         self.index = {}
         self.p32 = self.p64 = self.g32 = self.g64 = None
         self.device = None
         self._redirect = None
+        self._early_work = None
+        self.n32_early = 0
 
     def _params(self):
         pd = dict(self.model.named_parameters())
@@ -71,7 +74,14 @@ class FlatParams:
                 else:
                     raise TypeError(f"{n}: unsupported dtype {p.dtype}")
         self.n32, self.n64 = n32, n64
+        # the early bucket = the leading fp32 parameters named by self.early
+        self.n32_early = 0
+        for n, p in params:
+            if p.dtype != torch.float32 or not n.startswith(self.early):
+                break
+            self.n32_early += p.numel()
         self.device = dev
+        self._early_work = None
         return True
 
     def grad_view(self, name):
@@ -104,23 +114,49 @@ class FlatParams:
         for n, p in self._params():
             p.grad = self.grad_view(n)
 
-    def allreduce_grads(self, group=None):
-        """Mean of the gradients over the data-parallel group (RCCL over xGMI)."""
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-            return
-        ws = dist.get_world_size(group)
+    @staticmethod
+    def _dp(group):
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+    @staticmethod
+    def _mean(t, group, async_op=False):
+        """In-place mean over the group: RCCL AVG over xGMI; gloo (the CPU
+        harness of the DP path) has no AVG, so SUM then scale."""
         if dist.get_backend(group) == "nccl":
-            # RCCL over xGMI: one in-place AVG all-reduce per dtype buffer
-            dist.all_reduce(self.g32, op=dist.ReduceOp.AVG, group=group)
-            if self.n64:
-                dist.all_reduce(self.g64, op=dist.ReduceOp.AVG, group=group)
-        else:
-            # gloo (the CPU test harness of the DP path): no AVG op
-            dist.all_reduce(self.g32, op=dist.ReduceOp.SUM, group=group)
-            self.g32.div_(ws)
-            if self.n64:
-                dist.all_reduce(self.g64, op=dist.ReduceOp.SUM, group=group)
-                self.g64.div_(ws)
+            return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group, async_op=async_op)
+        w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.div_(dist.get_world_size(group))
+        return None
+
+    def allreduce_early(self, group=None):
+        """Start the mean all-reduce of the early-final bucket (asynchronous
+        on RCCL: it runs on the process group's stream, ordered after the
+        gradient kernels already queued, while the U-Net backward proceeds).
+        A no-op while gradients accumulate into a redirect buffer."""
+        if not self._dp(group) or self._redirect is not None or self.n32_early == 0 or self._early_work is not None:
+            return
+        self._early_work = (self._mean(self.g32[:self.n32_early], group, async_op=True), group)
+        if self._early_work[0] is None:   # gloo: completed synchronously
+            self._early_work = (True, group)
+
+    def allreduce_grads(self, group=None):
+        """Mean of the gradients over the data-parallel group (RCCL over xGMI):
+        the late bucket (+ the fp64 scalars) now, the early bucket unless
+        allreduce_early already started it, whose completion is then awaited."""
+        if not self._dp(group):
+            self._early_work = None
+            return
+        started = self._early_work is not None
+        lo = self.n32_early if started else 0
+        if lo < self.n32:
+            self._mean(self.g32[lo:], group)
+        if self.n64:
+            self._mean(self.g64, group)
+        if started:
+            w = self._early_work[0]
+            if w is not True:
+                w.wait()
+            self._early_work = None
 
 
 class FlatOptimizer:

@@ -3,7 +3,8 @@
 Checks, per rank, the pieces the N-GPU bench relies on:
   * DataIterator(rank, world) hands each rank a disjoint shard of every epoch
     of a shared permutation (drop-last per global batch);
-  * FlatParams.allreduce_grads averages the ONE flat gradient buffer;
+  * FlatParams.allreduce_grads averages the ONE flat gradient buffer, also
+    when its early-final bucket was started ahead (allreduce_early);
   * the averaged per-rank gradients of the oracle step equal the gradient of
     the concatenated batch (the reference's losses are batch means, so equal
     per-rank batches make DP exact) -- the contract weak scaling depends on.
@@ -65,6 +66,24 @@ def _worker(rank, world, port, q):
         flat.allreduce_grads()
         assert torch.allclose(flat.g32, torch.full_like(flat.g32, 1.5))
         assert torch.allclose(flat.g64, torch.full_like(flat.g64, 15.0))
+
+        # 2b) bucketed exchange: the early-final bucket (VariableFromNetwork +
+        # localiser l1/l2, leading the flat buffer) is reduced first, the rest
+        # after the U-Net backward; the result is the same mean
+        assert 0 < flat.n32_early < flat.n32
+        for n in flat.names:
+            kind, off, num, _ = flat.index[n]
+            early = n.startswith(m.EARLY_GRADS)
+            assert kind != 32 or early == (off + num <= flat.n32_early), n
+        assert flat.n32_early / flat.n32 > 0.9   # most gradient bytes overlap the U-Net backward
+        flat.g32.copy_(torch.arange(flat.n32, dtype=torch.float32) * (rank + 1))
+        flat.g64.fill_(float(rank))
+        flat.allreduce_early()
+        flat.g32[flat.n32_early:].mul_(1.0)   # the late bucket is still being written here
+        flat.allreduce_grads()
+        assert torch.allclose(flat.g32, torch.arange(flat.n32, dtype=torch.float32) * 1.5)
+        assert torch.allclose(flat.g64, torch.full_like(flat.g64, 0.5))
+        assert flat._early_work is None
 
         # 3) DP equivalence on the oracle step (golden weights, B = 3 -> shards)
         z = load_golden("spring_s12")
