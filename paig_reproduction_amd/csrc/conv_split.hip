@@ -108,8 +108,9 @@ struct UpStage {
       const int q = i % QS, sr = (i / QS) % SRN, c = (i / (QS * SRN)) % CIN, fi = i / (QS * SRN * CIN);
       const int srow = y0 / 2 - 1 + sr;
       const bool ok = i < NSU && f0 + fi < F && srow >= 0 && srow < HS;
-      v[l] = ok ? *reinterpret_cast<const f32x4*>(x.frame(f0 + fi) + (long long)c * HS * WS + srow * WS + 4 * q)
-                : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int off = ok ? fi * (int)x.fs + c * HS * WS + srow * WS + 4 * q : 0;
+      const f32x4 u = *reinterpret_cast<const f32x4*>(x.frame(f0) + off);
+      v[l] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   __device__ __forceinline__ void commit(float* Sl, int tid) const {
@@ -178,7 +179,8 @@ struct SFwdCfg {
   static constexpr int LDS = (IMG + WIMG) * 2 * NIMG;
   // staging unit = one pixel x 8 channels: consecutive lanes take consecutive
   // pixels (coalesced loads, b128 LDS writes PS slots apart: conflict-free)
-  static constexpr int NI = FPT * ROWS * W * CC;
+  static constexpr int W2 = W / 2;
+  static constexpr int NI = FPT * ROWS * W2 * CC;            // units: 2 pixels x 8 channels
   static constexpr int NL = (NI + 255) / 256;
   static_assert(W % 8 == 0 && (W >= 16 || 16 % W == 0), "M-tile rows");
   static_assert(RT * W * FPT == TPX || RT == H, "tile");
@@ -192,7 +194,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   using C = SFwdCfg<CIN, COUT, H, W, KS, PM>;
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
   constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP;
-  constexpr int NI = C::NI, NL = C::NL, PADL = C::PADL;
+  constexpr int NI = C::NI, NL = C::NL, PADL = C::PADL, W2 = C::W2;
   constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   constexpr long long HW = (long long)H * W;
   extern __shared__ __attribute__((aligned(16))) short lds16[];
@@ -254,38 +256,49 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   // the next tile's loads are in flight during this tile's MFMAs
   using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
   float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::IMG + C::WIMG));
-  auto put_px = [&](int i, const float* v) {
-    const int xp = i % W, r = (i / W) % ROWS, cc = (i / (W * ROWS)) % CC, fi = i / (W * ROWS * CC);
+  auto put_px = [&](int i, const float2* v) {
+    const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
     const int o = ((fi * ROWS + r) * RP + (xp + PADL) * PS + cc) * 8;
-    s16x8 hv, lv;
+    s16x8 h0, l0, h1, l1;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       short h, lo;
-      split<PM>(v[c], h, lo);
-      hv[c] = h;
-      lv[c] = lo;
+      split<PM>(v[c].x, h, lo);
+      h0[c] = h;
+      l0[c] = lo;
+      split<PM>(v[c].y, h, lo);
+      h1[c] = h;
+      l1[c] = lo;
     }
-    *reinterpret_cast<s16x8*>(Xh + o) = hv;
-    if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = lv;
+    *reinterpret_cast<s16x8*>(Xh + o) = h0;
+    *reinterpret_cast<s16x8*>(Xh + o + PS * 8) = h1;
+    if (PM != 2) {
+      *reinterpret_cast<s16x8*>(Xl + o) = l0;
+      *reinterpret_cast<s16x8*>(Xl + o + PS * 8) = l1;
+    }
   };
-  float pre[UPS ? 1 : NL][8];
+  float2 pre[UPS ? 1 : NL][8];
   UP up;
   auto issue = [&](int t) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
     if constexpr (UPS) {
       up.issue(in, F, f0, y0, tid);
     } else {
+      // branch-free: every lane loads (out-of-tile lanes re-read the tile's
+      // first pixels) and zeroes afterwards; 32-bit offsets from the tile's
+      // frame (frames of one tile are fs apart: FPT > 1 only for plain views)
+      const float* fb = in.frame(f0);
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         const int i = tid + l * 256;
-        const int xp = i % W, r = (i / W) % ROWS, cc = (i / (W * ROWS)) % CC, fi = i / (W * ROWS * CC);
-        const int f = f0 + fi, gy = y0 + r - PADL;
-        const bool ok = i < NI && f < F && gy >= 0 && gy < H;
-        const float* src = in.frame(ok ? f : 0) + (long long)(ok ? gy : 0) * W + xp;
+        const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
+        const int gy = y0 + r - PADL;
+        const bool ok = i < NI && f0 + fi < F && gy >= 0 && gy < H;
+        const int off = ok ? fi * (int)in.fs + cc * 8 * (int)PLANE + gy * W + xp : 0;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          const int ci = cc * 8 + c;
-          pre[l][c] = (ok && ci < CIN) ? src[ci * PLANE] : 0.f;
+          const float2 v = *reinterpret_cast<const float2*>(fb + off + (cc * 8 + c < CIN ? c : 0) * (int)PLANE);
+          pre[l][c] = (ok && cc * 8 + c < CIN) ? v : make_float2(0.f, 0.f);
         }
       }
     }
@@ -297,12 +310,15 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       __syncthreads();
 #pragma unroll 1
       for (int i = tid; i < NI; i += 256) {
-        const int xp = i % W, r = (i / W) % ROWS, cc = (i / (W * ROWS)) % CC, fi = i / (W * ROWS * CC);
+        const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
         const int gy = y0 + r - PADL;
         const bool ok = f0 + fi < F && gy >= 0 && gy < H;
-        float v[8];
+        float2 v[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = (ok && cc * 8 + c < CIN) ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp) : 0.f;
+        for (int c = 0; c < 8; ++c)
+          v[c] = (ok && cc * 8 + c < CIN)
+                     ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp), UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1))
+                     : make_float2(0.f, 0.f);
         put_px(i, v);
       }
     } else {
@@ -394,7 +410,10 @@ struct SWgCfg {
   static constexpr int FPT = H * W >= TPX ? 1 : TPX / (H * W);
   static constexpr int RT = H * W >= TPX ? TPX / W : H;
   static constexpr int ROWS = RT + KS - 1;
-  static constexpr int TWPX = W + 2 * PADL;
+  // input column x sits at image column x + OFFX: even, so a 2-pixel staging
+  // unit is one aligned 16-B write per plane
+  static constexpr int OFFX = PADL > 0 ? 2 : 0;
+  static constexpr int TWPX = W + 2 * OFFX;
   // X image: one plane per 4-channel quad, [pixel position][4] (8 B per pixel)
   // so the staging writes of consecutive pixels are consecutive; plane bases
   // are 256-B aligned plus {0, 32, 128, 160} B so the transposed reads of an
@@ -408,7 +427,8 @@ struct SWgCfg {
   static constexpr int RED = 4 * MT * NTW * 4 * 64 * 4;
   static constexpr int LDS = STG > RED ? STG : RED;
   static constexpr int Q = W / 4;
-  static constexpr int NIX = FPT * ROWS * W * CQ, NLX = (NIX + 255) / 256;   // X units: 1 px x 4 ch
+  static constexpr int W2 = W / 2;
+  static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = (NIX + 255) / 256;  // X units: 2 px x 4 ch
   static constexpr int NID = COUT * TPX / 4, NLD = (NID + 255) / 256;         // dY units: 4 px x 1 ch
   static constexpr int SLAB = COUT * NCOL + COUT;
   static constexpr int MINW = 2;                              // waves per SIMD the registers must allow
@@ -423,7 +443,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   using C = SWgCfg<CIN, COUT, H, W, KS, PM>;
   constexpr int KK = C::KK, CQ = C::CQ, NQ = C::NQ, NT = C::NT, NCOL = C::NCOL, MT = C::MT, COP = C::COP;
   constexpr int WN = C::WN, WP = C::WP, NTW = C::NTW, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS;
-  constexpr int TWPX = C::TWPX, XPL = C::XPL, DP = C::DP, KB = C::KB, PADL = C::PADL;
+  constexpr int TWPX = C::TWPX, XPL = C::XPL, DP = C::DP, KB = C::KB, PADL = C::PADL, OFFX = C::OFFX, W2 = C::W2;
   constexpr int NIX = C::NIX, NLX = C::NLX, NID = C::NID, NLD = C::NLD;
   constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   constexpr long long HW = (long long)H * W;
@@ -438,10 +458,10 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
 
   auto xplane = [](int cq) { return cq * XPL + ((cq & 1) ? 16 : 0) + ((cq & 2) ? 64 : 0); };
   // ---- zero the halo columns of X and the padded co rows of dY (never staged)
-  if (PADL > 0) {
-    for (int i = tid; i < FPT * ROWS * 2 * PADL; i += 256) {
-      const int hc = i % (2 * PADL), r = i / (2 * PADL);
-      const int xc = hc < PADL ? hc : W + hc;
+  if (OFFX > 0) {
+    for (int i = tid; i < FPT * ROWS * 2 * OFFX; i += 256) {
+      const int hc = i % (2 * OFFX), r = i / (2 * OFFX);
+      const int xc = hc < OFFX ? hc : W + hc;
       for (int cq = 0; cq < CQ; ++cq) {
         *reinterpret_cast<s16x4*>(Xh + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
         if (PM != 2) *reinterpret_cast<s16x4*>(Xl + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
@@ -461,7 +481,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int j = 8 * g + 4 * h + qq;
-    roff[h] = (j / W) * TWPX + j % W;
+    roff[h] = (j / W) * TWPX + j % W + (OFFX - PADL);
   }
   int colt[NTW];
 #pragma unroll
@@ -485,40 +505,48 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   // upsample inputs go through UpStage (half-resolution window, prefetched).
   using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
   float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::XIMG + C::DIMG));
-  constexpr bool XPIPE = !UPS && NLX * 4 + NLD * 4 <= 48;
-  auto load_x = [&](int t, int i, float* v) {
+  constexpr bool XPIPE = !UPS && NLX * 8 + NLD * 4 <= 48;
+  auto load_x = [&](int t, int i, float2* v) {   // branch-free, 32-bit offsets (see the forward kernel)
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
-    const int xp = i % W, r = (i / W) % ROWS, cq = (i / (W * ROWS)) % CQ, fi = i / (W * ROWS * CQ);
-    const int f = f0 + fi, gy = y0 + r - PADL;
-    const bool ok = i < NIX && f < F && gy >= 0 && gy < H;
-    const float* src = x.frame(ok ? f : 0) + (long long)(ok ? gy : 0) * W + xp;
+    const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+    const int gy = y0 + r - PADL;
+    const bool ok = i < NIX && f0 + fi < F && gy >= 0 && gy < H;
+    const float* fb = x.frame(f0);
+    const int off = ok ? fi * (int)x.fs + cq * 4 * (int)PLANE + gy * W + xp : 0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = (ok && cq * 4 + c < CIN) ? src[(cq * 4 + c) * PLANE] : 0.f;
+    for (int c = 0; c < 4; ++c) {
+      const float2 u = *reinterpret_cast<const float2*>(fb + off + (cq * 4 + c < CIN ? c : 0) * (int)PLANE);
+      v[c] = (ok && cq * 4 + c < CIN) ? u : make_float2(0.f, 0.f);
+    }
   };
-  auto put_x = [&](int i, const float* v) {
-    const int xp = i % W, r = (i / W) % ROWS, cq = (i / (W * ROWS)) % CQ, fi = i / (W * ROWS * CQ);
-    const int o = xplane(cq) + ((fi * ROWS + r) * TWPX + xp + PADL) * 4;
-    s16x4 hv, lv;
+  auto put_x = [&](int i, const float2* v) {
+    const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+    const int o = xplane(cq) + ((fi * ROWS + r) * TWPX + xp + OFFX) * 4;
+    s16x8 hv, lv;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       short h, lo;
-      split<PM>(v[c], h, lo);
+      split<PM>(v[c].x, h, lo);
       hv[c] = h;
       lv[c] = lo;
+      split<PM>(v[c].y, h, lo);
+      hv[4 + c] = h;
+      lv[4 + c] = lo;
     }
-    *reinterpret_cast<s16x4*>(Xh + o) = hv;
-    if (PM != 2) *reinterpret_cast<s16x4*>(Xl + o) = lv;
+    *reinterpret_cast<s16x8*>(Xh + o) = hv;
+    if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = lv;
   };
   UP up;
-  float sx[XPIPE ? NLX : 1][4];
+  float2 sx[XPIPE ? NLX : 1][4];
   auto load_d = [&](int t, int l) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
     const int i = tid + l * 256;
     const int co = i / (C::TPX / 4), pt = 4 * (i % (C::TPX / 4));
     const int fi = pt / (RT * W), y = (pt / W) % RT, xx = pt % W;
-    const int f = f0 + fi;
-    return (i < NID && f < F) ? *reinterpret_cast<const f32x4*>(dy.frame(f) + co * HW + (long long)(y0 + y) * W + xx)
-                              : f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool ok = i < NID && f0 + fi < F;
+    const int off = ok ? fi * (int)dy.fs + co * (int)HW + (y0 + y) * W + xx : 0;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(dy.frame(f0) + off);
+    return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   constexpr bool DPIPE = XPIPE || UPS;
   f32x4 sd[DPIPE ? NLD : 1];
@@ -541,12 +569,15 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
       __syncthreads();
 #pragma unroll 1
       for (int i = tid; i < NIX; i += 256) {
-        const int xp = i % W, r = (i / W) % ROWS, cq = (i / (W * ROWS)) % CQ, fi = i / (W * ROWS * CQ);
+        const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
         const int gy = y0 + r - PADL;
         const bool ok = f0 + fi < F && gy >= 0 && gy < H;
-        float v[4];
+        float2 v[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = (ok && cq * 4 + c < CIN) ? UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp) : 0.f;
+        for (int c = 0; c < 4; ++c)
+          v[c] = (ok && cq * 4 + c < CIN)
+                     ? make_float2(UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp), UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp + 1))
+                     : make_float2(0.f, 0.f);
         put_x(i, v);
       }
     } else if constexpr (XPIPE) {
@@ -559,7 +590,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
     } else {
 #pragma unroll 1
       for (int i = tid; i < NIX; i += 256) {
-        float v[4];
+        float2 v[4];
         load_x(t, i, v);
         put_x(i, v);
       }
@@ -717,6 +748,7 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
   const bool dg = (flags & 8) != 0, up = (flags & 32) != 0, b16 = (flags & 256) != 0;
   const int fl = flags & 7;
   if (H != W || !(flags & (128 | 256))) return 0;
+  if (in.grp > 0 && H * W < 256) return 0;   // multi-frame tiles step frames by a plain stride
   if (up) {
     if (dg) return 0;
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
@@ -748,6 +780,7 @@ int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nbl
                           int H, int W, int ks, int flags, hipStream_t st, int* rc) {
   const bool up = (flags & 32) != 0, b16 = (flags & 256) != 0;
   if (H != W || !(flags & (128 | 256))) return 0;
+  if (x.grp > 0 && H * W < 256) return 0;   // multi-frame tiles step frames by a plain stride
   if (up) {
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
     if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \

@@ -177,8 +177,9 @@ class KernelProbe:
         self.tag = tag
         self.events = []
         self.flops = 0
+        self.nbytes = 0
 
-    def wrap(self, tag, flops):
+    def wrap(self, tag, flops, nbytes=0):
         probe = self
 
         class _Ctx:
@@ -194,6 +195,7 @@ class KernelProbe:
                     self.e1.record()
                     probe.events.append((self.e0, self.e1))
                     probe.flops = flops
+                    probe.nbytes = nbytes
                 return False
 
         return _Ctx()
@@ -203,7 +205,8 @@ class KernelProbe:
             return None
         torch.cuda.synchronize()
         ms = [a.elapsed_time(b) for a, b in self.events]
-        return {"tag": self.tag, "n": len(ms), "avg_ms": sum(ms) / len(ms), "flops": self.flops}
+        return {"tag": self.tag, "n": len(ms), "avg_ms": sum(ms) / len(ms), "flops": self.flops,
+                "bytes": self.nbytes}
 
 
 class _NoProbe:
@@ -253,8 +256,10 @@ class Engine:
             raise ValueError(f"conv_math must be one of {sorted(self.CONV_MATH)}, got {m!r}")
         return self.CONV_MATH[m]
 
-    def _p(self, tag, flops=0):
-        return self.probe.wrap(tag, flops) if self.probe is not None else _NOPROBE
+    def _p(self, tag, flops=0, nbytes=0):
+        """Probe context of one launch: algorithmic FLOPs and HBM bytes (the
+        compulsory operand reads + result writes) for bench.py's roofline."""
+        return self.probe.wrap(tag, flops, nbytes) if self.probe is not None else _NOPROBE
 
     # -- parameter access ------------------------------------------------
     def p(self, name):
@@ -364,7 +369,8 @@ class Engine:
                 W_ = self.p(lay.prefix + op["name"] + ".weight")
                 b_ = self.p(lay.prefix + op["name"] + ".bias")
                 fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
-                with self._p("conv_fwd:" + op["name"], fl):
+                nbytes = 4 * F * (op["src"][2] * (Hl // (2 if xfl else 1)) ** 2 + op["dst"][2] * Hl * Hl)
+                with self._p("conv_fwd:" + op["name"], fl, nbytes):
                     L.paig_conv2d_fwd(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
                                       op["src"][2], op["dst"][2], Hl, Hl, op["ks"], (1 if op["relu"] else 0) | xfl | cm,
                                       st)
@@ -655,7 +661,8 @@ class Engine:
                 slab = _empty(nblk_max * (cout * cin * ks * ks + cout), dev)
                 nb = ctypes.c_int(0)
                 fl = 2 * F * cin * cout * ks * ks * Hl * Hl
-                with self._p("conv_wgrad:" + op["name"], fl):
+                nbytes = 4 * F * (cin * (Hl // (2 if xfl else 1)) ** 2 + cout * Hl * Hl)
+                with self._p("conv_wgrad:" + op["name"], fl, nbytes):
                     L.paig_conv2d_wgrad(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], ptr(slab), nblk_max,
                                         ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, xfl | cm, st)
                 gw = self.g(lay.prefix + op["name"] + ".weight")
@@ -675,7 +682,8 @@ class Engine:
                     aux = (a[0], a[1])
                     flags |= 2
                 W_ = self.p(lay.prefix + op["name"] + ".weight")
-                with self._p("conv_dgrad:" + op["name"], fl):
+                nbytes = 4 * F * Hl * Hl * (cout + cin * (1 + (1 if flags & 2 else 0) + (1 if flags & 4 else 0)))
+                with self._p("conv_dgrad:" + op["name"], fl, nbytes):
                     L.paig_conv2d_fwd(dyv[0], dyv[1], 0, 0, dxv[0], dxv[1], aux[0] or None, aux[1], ptr(W_), None, F,
                                       cout, cin, Hl, Hl, ks, flags | cm, st)
                 mark(src)
