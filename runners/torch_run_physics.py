@@ -88,6 +88,11 @@ def build_parser():
     p.add_argument("--data_dir", type=str, default=os.path.join(REPO, "data", "datasets"))
     p.add_argument("--synthetic", type=int, default=0)
     p.add_argument("--seed", type=int, default=None)
+    p.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                   help="fp32: fp32-accurate results (convs/GEMMs on the 16-bit matrix cores with split "
+                        "hi+lo operands); bf16: bf16 operands, fp32 accumulation (BASELINE config #2)")
+    p.add_argument("--conv_math", choices=("split", "fp32", "bf16"), default=None,
+                   help="override the conv/GEMM arithmetic directly (fp32 = f32-input MFMA)")
     p.add_argument("--device_data", type=int, default=1,
                    help="1: dataset resident in HBM as uint8, batches gathered on the GPU (F2); 0: host iterators")
     return p
@@ -143,6 +148,7 @@ def main(argv=None):
                     args.autoencoder_loss, args.alt_vel, args.color, input_size, args.encoder_type,
                     args.decoder_type, device=device)
         net.loss_mode = args.loss_mode
+        net.conv_math = args.conv_math or ("bf16" if args.dtype == "bf16" else "split")
         net.to(net.device)
         if world > 1:
             for t in net.state_dict().values():
