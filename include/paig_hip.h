@@ -40,7 +40,11 @@ int paig_abi_version(void);
  *        16 force the VALU path (tests), 64 skip the Cout=8 pixel-pair
  *        MFMA kernel (tests), 32 the input is the 2x bilinear
  *        upsample of the given (H/2 x W/2) planes, formed while staging
- *        (torchvision Resize of blocks.py:260,269 fused, never materialised). */
+ *        (torchvision Resize of blocks.py:260,269 fused, never materialised),
+ *        128 split-precision 16-bit MFMA (f16 hi+lo pieces for the forward,
+ *        bf16 hi+lo for dgrad: fp32-accurate), 256 bf16 operands (config #2).
+ *        Shapes without a split instantiation fall back to the f32 MFMA /
+ *        VALU kernels (same results within fp32 accuracy). */
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                     const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin, int Cout,
                     int H, int W, int ks, int flags, void* stream);
