@@ -112,6 +112,14 @@ int paig_vfn_fwd(const float* W1, const float* b1, const float* W2, const float*
 int paig_vfn_bwd_blocks(int P);
 int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,
                  float* dW2, float* db2, float* part, int P, void* stream);
+/* the same for n <= 4 instances in ONE launch per phase (host arrays of n entries;
+ * ypost may be NULL or hold NULL entries) */
+int paig_vfn_fwd_multi(int n, const float* const* W1, const float* const* b1, const float* const* W2,
+                       const float* const* b2, float* const* hout, float* const* y, float* const* ypost, const int* P,
+                       void* stream);
+int paig_vfn_bwd_multi(int n, const float* const* d, const float* const* y, const int* sig, const float* const* h,
+                       const float* const* W2, float* const* dW1, float* const* db1, float* const* dW2,
+                       float* const* db2, float* const* part, const int* P, void* stream);
 
 /* ---- velocity encoder MLP fused (blocks.py:22-29, forward :43-48): rows
  * K*B of [2S] packed from pos [B][Te][2K] -> 100 tanh -> 100 tanh -> 2.

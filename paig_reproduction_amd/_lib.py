@@ -53,6 +53,8 @@ SIGNATURES = {
     "paig_vfn_fwd": (I, [P, P, P, P, P, P, P, I, P]),
     "paig_vfn_bwd_blocks": (I, [I]),
     "paig_vfn_bwd": (I, [P, P, I, P, P, P, P, P, P, P, I, P]),
+    "paig_vfn_fwd_multi": (I, [I, P, P, P, P, P, P, P, P, P]),
+    "paig_vfn_bwd_multi": (I, [I, P, P, P, P, P, P, P, P, P, P, P, P]),
     "paig_vel_pack": (I, [P, P, I, I, I, I, I, P]),
     "paig_vel_unpack_add": (I, [P, P, P, I, I, I, I, I, P]),
     "paig_rollout_fwd": (I, [I, P, LL, P, P, P, P, P, I, I, I, P]),

@@ -27,74 +27,119 @@ namespace {
 constexpr int VH = 200;  // VariableFromNetwork hidden width (blocks.py:314)
 constexpr int VIN = 10;  // ones[1, 10]
 
+// The three VariableFromNetwork instances (template, content, background) of a
+// step run as ONE launch per phase: a block finds its instance in a small
+// task table (block ranges), so the three latency-bound GEMVs overlap.
+constexpr int VMAX = 4;
+struct VfnFwdTasks {
+  const float* W1[VMAX];
+  const float* b1[VMAX];
+  const float* W2[VMAX];
+  const float* b2[VMAX];
+  float* hout[VMAX];
+  float* y[VMAX];
+  float* ypost[VMAX];
+  int P[VMAX];
+  int blk0[VMAX + 1];
+  int n;
+};
+struct VfnBwdTasks {
+  const float* d[VMAX];
+  const float* y[VMAX];
+  const float* h[VMAX];
+  const float* W2[VMAX];
+  float* dW1[VMAX];
+  float* db1[VMAX];
+  float* dW2[VMAX];
+  float* db2[VMAX];
+  float* part[VMAX];
+  int sig[VMAX];
+  int P[VMAX];
+  int blk0[VMAX + 1];   // bwd1 block ranges (rows per block = VROWS)
+  int n;
+};
+constexpr int VROWS = 8;
+
+__device__ __forceinline__ int task_of(const int* blk0, int n, int b) {
+  int k = 0;
+  while (k + 1 < n && b >= blk0[k + 1]) ++k;
+  return k;
+}
+
 // h = tanh(W1 @ ones + b1) in LDS; one wave per output row afterwards.
-__global__ void __launch_bounds__(256)
-vfn_fwd_k(const float* __restrict__ W1, const float* __restrict__ b1, const float* __restrict__ W2,
-          const float* __restrict__ b2, float* __restrict__ hout, float* __restrict__ y, float* __restrict__ ypost,
-          int P) {
+__global__ void __launch_bounds__(256) vfn_fwd_k(VfnFwdTasks T) {
+  const int k = task_of(T.blk0, T.n, blockIdx.x);
+  const int bid = blockIdx.x - T.blk0[k], nb = T.blk0[k + 1] - T.blk0[k];
+  const float* __restrict__ W1 = T.W1[k];
+  const float* __restrict__ W2 = T.W2[k];
+  const int P = T.P[k];
   __shared__ float h[VH];
   for (int j = threadIdx.x; j < VH; j += blockDim.x) {
     float s = 0.f;
     for (int i = 0; i < VIN; ++i) s += W1[j * VIN + i];  // x = ones
-    const float v = tanhf(s + b1[j]);
+    const float v = tanhf(s + T.b1[k][j]);
     h[j] = v;
-    if (blockIdx.x == 0) hout[j] = v;
+    if (bid == 0) T.hout[k][j] = v;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nw = (gridDim.x * blockDim.x) >> 6;
+  const int wg = (bid * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (nb * blockDim.x) >> 6;
   for (int p = wg; p < P; p += nw) {
     float s = 0.f;
     for (int j = lane; j < VH; j += 64) s = fmaf(W2[(long long)p * VH + j], h[j], s);
     s = wave_sum(s);
     if (lane == 0) {
-      const float v = s + b2[p];
-      y[p] = v;
-      if (ypost) ypost[p] = 1.f / (1.f + expf(-v));
+      const float v = s + T.b2[k][p];
+      T.y[k][p] = v;
+      if (T.ypost[k]) T.ypost[k][p] = 1.f / (1.f + expf(-v));
     }
   }
 }
 
 // dy = d (raw) or d * s (1 - s), s = sigmoid(y) ; dW2 = dy h^T ; db2 = dy ;
 // part[blk][j] = sum_{p in blk} W2[p][j] dy[p]
-__global__ void __launch_bounds__(256)
-vfn_bwd1_k(const float* __restrict__ d, const float* __restrict__ y, int sig, const float* __restrict__ h,
-           const float* __restrict__ W2, float* __restrict__ dW2, float* __restrict__ db2, float* __restrict__ part,
-           int P, int rows) {
+__global__ void __launch_bounds__(256) vfn_bwd1_k(VfnBwdTasks T) {
+  const int k = task_of(T.blk0, T.n, blockIdx.x);
+  const int bid = blockIdx.x - T.blk0[k];
+  const float* __restrict__ d = T.d[k];
+  const float* __restrict__ W2 = T.W2[k];
+  float* __restrict__ dW2 = T.dW2[k];
+  const int P = T.P[k], sig = T.sig[k];
   const int j = threadIdx.x;
-  const int p0 = blockIdx.x * rows;
-  int p1 = p0 + rows;
+  const int p0 = bid * VROWS;
+  int p1 = p0 + VROWS;
   if (p1 > P) p1 = P;
-  const float hj = j < VH ? h[j] : 0.f;
+  const float hj = j < VH ? T.h[k][j] : 0.f;
   float acc = 0.f;
   for (int p = p0; p < p1; ++p) {
     float g = d[p];
     if (sig) {
-      const float s = 1.f / (1.f + expf(-y[p]));
+      const float s = 1.f / (1.f + expf(-T.y[k][p]));
       g = g * (s * (1.f - s));
     }
     if (j < VH) {
       dW2[(long long)p * VH + j] = g * hj;
       acc = fmaf(W2[(long long)p * VH + j], g, acc);
     }
-    if (j == 0) db2[p] = g;
+    if (j == 0) T.db2[k][p] = g;
   }
-  if (j < VH) part[blockIdx.x * VH + j] = acc;
+  if (j < VH) T.part[k][bid * VH + j] = acc;
 }
 
-// one 64-lane block per hidden unit j: dh[j] = sum of the partials, then the
-// tanh' and the first layer's grads (input = ones)
-__global__ void vfn_bwd2_k(const float* __restrict__ part, int nblk, const float* __restrict__ h,
-                           float* __restrict__ dW1, float* __restrict__ db1) {
-  const int j = blockIdx.x;
+// one 64-lane block per (instance, hidden unit j): dh[j] = sum of the
+// partials, then the tanh' and the first layer's grads (input = ones)
+__global__ void vfn_bwd2_k(VfnBwdTasks T) {
+  const int k = blockIdx.x / VH, j = blockIdx.x % VH;
+  const int nblk = T.blk0[k + 1] - T.blk0[k];
+  const float* __restrict__ part = T.part[k];
   float s = 0.f;
   for (int b = threadIdx.x; b < nblk; b += 64) s += part[b * VH + j];
   s = wave_sum(s);
-  const float hj = h[j];
+  const float hj = T.h[k][j];
   const float g = s * (1.f - hj * hj);
-  if (threadIdx.x < VIN) dW1[j * VIN + threadIdx.x] = g;
-  if (threadIdx.x == 0) db1[j] = g;
+  if (threadIdx.x < VIN) T.dW1[k][j * VIN + threadIdx.x] = g;
+  if (threadIdx.x == 0) T.db1[k][j] = g;
 }
 
 // losses: pred, extrap, recons (means of per-frame SSE)
@@ -233,29 +278,71 @@ const char* paig_last_error(void) { return g_err; }
 int paig_abi_version(void) { return 1; }
 
 // y[P] = W2 tanh(W1 1 + b1) + b2 ; hout[200] ; ypost = sigmoid(y) if non-null
-int paig_vfn_fwd(const float* W1, const float* b1, const float* W2, const float* b2, float* hout, float* y,
-                 float* ypost, int P, void* stream) {
-  int g = (P + 3) / 4;
-  if (g > 1024) g = 1024;
-  if (g < 1) g = 1;
-  hipLaunchKernelGGL(vfn_fwd_k, dim3(g), dim3(256), 0, (hipStream_t)stream, W1, b1, W2, b2, hout, y, ypost, P);
+int paig_vfn_fwd_multi(int n, const float* const* W1, const float* const* b1, const float* const* W2,
+                       const float* const* b2, float* const* hout, float* const* y, float* const* ypost, const int* P,
+                       void* stream) {
+  PAIG_REQUIRE(n >= 1 && n <= VMAX, "paig_vfn_fwd_multi: n=%d (1..%d)", n, VMAX);
+  VfnFwdTasks T{};
+  T.n = n;
+  T.blk0[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    T.W1[k] = W1[k];
+    T.b1[k] = b1[k];
+    T.W2[k] = W2[k];
+    T.b2[k] = b2[k];
+    T.hout[k] = hout[k];
+    T.y[k] = y[k];
+    T.ypost[k] = ypost ? ypost[k] : nullptr;
+    T.P[k] = P[k];
+    int g = (P[k] + 3) / 4;
+    if (g > 1024) g = 1024;
+    if (g < 1) g = 1;
+    T.blk0[k + 1] = T.blk0[k] + g;
+  }
+  hipLaunchKernelGGL(vfn_fwd_k, dim3(T.blk0[n]), dim3(256), 0, (hipStream_t)stream, T);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
 
-int paig_vfn_bwd_blocks(int P) { return cdiv(P, 8); }
+int paig_vfn_fwd(const float* W1, const float* b1, const float* W2, const float* b2, float* hout, float* y,
+                 float* ypost, int P, void* stream) {
+  return paig_vfn_fwd_multi(1, &W1, &b1, &W2, &b2, &hout, &y, &ypost, &P, stream);
+}
 
-// d: adjoint of y (sig = 0) or of sigmoid(y) (sig = 1). part: >= blocks*200 floats.
-int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,
-                 float* dW2, float* db2, float* part, int P, void* stream) {
-  const int rows = 8;
-  const int nblk = cdiv(P, rows);
-  hipLaunchKernelGGL(vfn_bwd1_k, dim3(nblk), dim3(256), 0, (hipStream_t)stream, d, y, sig, h, W2, dW2, db2, part, P,
-                     rows);
+int paig_vfn_bwd_blocks(int P) { return cdiv(P, VROWS); }
+
+// d: adjoint of y (sig = 0) or of sigmoid(y) (sig = 1). part[k]: >= blocks(P[k])*200 floats.
+int paig_vfn_bwd_multi(int n, const float* const* d, const float* const* y, const int* sig, const float* const* h,
+                       const float* const* W2, float* const* dW1, float* const* db1, float* const* dW2,
+                       float* const* db2, float* const* part, const int* P, void* stream) {
+  PAIG_REQUIRE(n >= 1 && n <= VMAX, "paig_vfn_bwd_multi: n=%d (1..%d)", n, VMAX);
+  VfnBwdTasks T{};
+  T.n = n;
+  T.blk0[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    T.d[k] = d[k];
+    T.y[k] = y[k];
+    T.sig[k] = sig[k];
+    T.h[k] = h[k];
+    T.W2[k] = W2[k];
+    T.dW1[k] = dW1[k];
+    T.db1[k] = db1[k];
+    T.dW2[k] = dW2[k];
+    T.db2[k] = db2[k];
+    T.part[k] = part[k];
+    T.P[k] = P[k];
+    T.blk0[k + 1] = T.blk0[k] + cdiv(P[k], VROWS);
+  }
+  hipLaunchKernelGGL(vfn_bwd1_k, dim3(T.blk0[n]), dim3(256), 0, (hipStream_t)stream, T);
   PAIG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(vfn_bwd2_k, dim3(VH), dim3(64), 0, (hipStream_t)stream, part, nblk, h, dW1, db1);
+  hipLaunchKernelGGL(vfn_bwd2_k, dim3(VH * n), dim3(64), 0, (hipStream_t)stream, T);
   PAIG_CHECK_LAUNCH();
   return 0;
+}
+
+int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,
+                 float* dW2, float* db2, float* part, int P, void* stream) {
+  return paig_vfn_bwd_multi(1, &d, &y, &sig, &h, &W2, &dW1, &db1, &dW2, &db2, &part, &P, stream);
 }
 
 int paig_loss_reduce(const float* sse_rec, const float* sse_roll, int B, int Te, int R, int pred, float ae, float* pred_out,

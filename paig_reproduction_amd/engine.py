@@ -220,6 +220,14 @@ class _NoProbe:
 _NOPROBE = _NoProbe()
 
 
+def _parr(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+def _iarr(vals):
+    return (ctypes.c_int * len(vals))(*vals)
+
+
 def _empty(n, device, dtype=torch.float32):
     return torch.empty(n, device=device, dtype=dtype)
 
@@ -319,14 +327,14 @@ class Engine:
 
         # ---- VariableFromNetwork sources (once per step, Q12)
         src = {}
-        for nm, P, post in (("var_net_template", K * h * h, False), ("var_net_content", K * 3 * h * h, False),
-                            ("var_net_background", 3 * HW, True)):
-            hv = _empty(200, dev)
-            y = _empty(P, dev)
-            yp = _empty(P, dev) if post else None
-            L.paig_vfn_fwd(ptr(self.p(nm + ".l1.weight")), ptr(self.p(nm + ".l1.bias")), ptr(self.p(nm + ".l2.weight")),
-                           ptr(self.p(nm + ".l2.bias")), ptr(hv), ptr(y), ptr(yp), P, st)
-            src[nm] = (hv, y, yp)
+        vf = (("var_net_template", K * h * h, False), ("var_net_content", K * 3 * h * h, False),
+              ("var_net_background", 3 * HW, True))
+        for nm, P, post in vf:
+            src[nm] = (_empty(200, dev), _empty(P, dev), _empty(P, dev) if post else None)
+        L.paig_vfn_fwd_multi(3, *[_parr([ptr(self.p(nm + suf)) for nm, _, _ in vf])
+                                  for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                             _parr([ptr(src[nm][0]) for nm, _, _ in vf]), _parr([ptr(src[nm][1]) for nm, _, _ in vf]),
+                             _parr([ptr(src[nm][2]) for nm, _, _ in vf]), _iarr([P for _, P, _ in vf]), st)
         S["src"] = src
         tmpl, cont, bgp = src["var_net_template"][1], src["var_net_content"][1], src["var_net_background"][2]
 
@@ -573,13 +581,13 @@ class Engine:
                                  (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, st)
         if d_enc_pos is not None:
             L.paig_axpby(ptr(d_enc_pos.contiguous()), ptr(denc), F * D, 1.0, 1.0, st)
-        off = 0
-        for (nm, P, sig, raw), part in zip(vfn, vparts):
-            hv = S["src"][nm][0]
-            L.paig_vfn_bwd(ptr(dsrc) + off * 4, ptr(raw), sig, ptr(hv), ptr(self.p(nm + ".l2.weight")),
-                           ptr(self.g(nm + ".l1.weight")), ptr(self.g(nm + ".l1.bias")), ptr(self.g(nm + ".l2.weight")),
-                           ptr(self.g(nm + ".l2.bias")), ptr(part), P, st)
-            off += P
+        offs = [0, vfn[0][1], vfn[0][1] + vfn[1][1]]
+        L.paig_vfn_bwd_multi(3, _parr([ptr(dsrc) + o * 4 for o in offs]), _parr([ptr(r) for _, _, _, r in vfn]),
+                             _iarr([sg for _, _, sg, _ in vfn]), _parr([ptr(S["src"][nm][0]) for nm, _, _, _ in vfn]),
+                             _parr([ptr(self.p(nm + ".l2.weight")) for nm, _, _, _ in vfn]),
+                             *[_parr([ptr(self.g(nm + suf)) for nm, _, _, _ in vfn])
+                               for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                             _parr([ptr(pt) for pt in vparts]), _iarr([P for _, P, _, _ in vfn]), st)
         self._join(dev)
 
         L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
