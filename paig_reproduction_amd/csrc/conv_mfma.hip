@@ -648,15 +648,17 @@ template <int CIN, int COUT, int H, int W, int KS, bool UPS>
 static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st) {
   using C = WgCfg<CIN, COUT, H, W, KS>;
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
-  int nb = ntiles < nblk_max ? ntiles : nblk_max;
+  auto k = conv_wgrad_mfma_k<CIN, COUT, H, W, KS, UPS>;
+  static int resident = 0;
+  if (!resident) {
+    if (C::LDS > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    resident = persistent_grid((const void*)k, C::LDS);
+  }
+  int nb = ntiles < nblk_max ? ntiles : nblk_max;   // one wave of co-resident blocks
+  if (nb > resident) nb = resident;
   if (nb < 1) nb = 1;
   *nblk_out = nb;
-  auto k = conv_wgrad_mfma_k<CIN, COUT, H, W, KS, UPS>;
-  static bool attr = false;
-  if (!attr && C::LDS > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr = true;
-  }
   hipLaunchKernelGGL(k, dim3(nb), dim3(256), C::LDS, st, x, dy, slab, F, ntiles);
   PAIG_CHECK_LAUNCH();
   return 0;

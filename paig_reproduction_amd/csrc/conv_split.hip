@@ -713,15 +713,18 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
   constexpr int STG = C::STG + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
   constexpr int LDS = STG > C::RED ? STG : C::RED;
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
+  auto k = conv_wgrad_split_k<CIN, COUT, H, W, KS, UPS, PM>;
+  static int resident = 0;
+  if (!resident) {
+    if (LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    resident = persistent_grid((const void*)k, LDS);
+  }
+  // one wave of co-resident persistent blocks: more would leave a partial
+  // second wave running at a fraction of the chip (and add slab rows)
   int nb = ntiles < nblk_max ? ntiles : nblk_max;
+  if (nb > resident) nb = resident;
   if (nb < 1) nb = 1;
   *nblk_out = nb;
-  auto k = conv_wgrad_split_k<CIN, COUT, H, W, KS, UPS, PM>;
-  static bool attr = false;
-  if (!attr && LDS > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
   hipLaunchKernelGGL(k, dim3(nb), dim3(256), LDS, st, x, dy, slab, F, ntiles);
   PAIG_CHECK_LAUNCH();
   return 0;
