@@ -421,7 +421,7 @@ struct SWgCfg {
   static constexpr int XPL = rup(FPT * ROWS * TWPX * 4 + 80, 128);   // room for the <= 80-element offset
   static constexpr int XIMG = CQ * XPL;
   static constexpr int DP = TPX + 8;                          // dY row pitch: 16 rows -> 16 bank groups
-  static constexpr int DIMG = COP * DP;
+  static constexpr int DIMG = COUT * DP;   // rows co >= COUT of an A fragment re-read rows co % COUT
   static constexpr int KB = TPX / 32;                         // k-blocks of 32 pixels per tile
   static constexpr int STG = (XIMG + DIMG) * 2 * NIMG;
   static constexpr int RED = 4 * MT * NTW * 4 * 64 * 4;
@@ -431,7 +431,8 @@ struct SWgCfg {
   static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = (NIX + 255) / 256;  // X units: 2 px x 4 ch
   static constexpr int NID = COUT * TPX / 4, NLD = (NID + 255) / 256;         // dY units: 4 px x 1 ch
   static constexpr int SLAB = COUT * NCOL + COUT;
-  static constexpr int MINW = 2;                              // waves per SIMD the registers must allow
+  // waves per SIMD the registers must allow: 3 where three blocks fit the LDS
+  static constexpr int MINW = 3 * LDS <= 160 * 1024 ? 3 : 2;
   static_assert(FPT * RT * W == TPX, "tile = 256 pixels");
   static_assert((RT * W) % 32 == 0 && (W % 32 == 0 || 32 % W == 0), "k-blocks stay in one frame");
   static_assert(H % RT == 0, "RT divides H");
@@ -457,7 +458,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   constexpr int NRB = H / RT;
 
   auto xplane = [](int cq) { return cq * XPL + ((cq & 1) ? 16 : 0) + ((cq & 2) ? 64 : 0); };
-  // ---- zero the halo columns of X and the padded co rows of dY (never staged)
+  // ---- zero the halo columns of X (never staged)
   if (OFFX > 0) {
     for (int i = tid; i < FPT * ROWS * 2 * OFFX; i += 256) {
       const int hc = i % (2 * OFFX), r = i / (2 * OFFX);
@@ -466,12 +467,6 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
         *reinterpret_cast<s16x4*>(Xh + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
         if (PM != 2) *reinterpret_cast<s16x4*>(Xl + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
       }
-    }
-  }
-  if (COP > COUT) {
-    for (int i = tid; i < (COP - COUT) * DP / 4; i += 256) {
-      *reinterpret_cast<s16x4*>(Dh + COUT * DP + 4 * i) = s16x4{0, 0, 0, 0};
-      if (PM != 2) *reinterpret_cast<s16x4*>(Dl + COUT * DP + 4 * i) = s16x4{0, 0, 0, 0};
     }
   }
   // ---- per-lane transposed-read addressing. Lane 4q+p of its 16-lane group
@@ -505,7 +500,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   // upsample inputs go through UpStage (half-resolution window, prefetched).
   using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
   float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::XIMG + C::DIMG));
-  constexpr bool XPIPE = !UPS && NLX * 8 + NLD * 4 <= 48;
+  constexpr bool XPIPE = !UPS && NLX * 8 + NLD * 4 <= (C::MINW == 3 ? 24 : 48);
   auto load_x = [&](int t, int i, float2* v) {   // branch-free, 32-bit offsets (see the forward kernel)
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
     const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
@@ -548,7 +543,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
     const f32x4 v = *reinterpret_cast<const f32x4*>(dy.frame(f0) + off);
     return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   };
-  constexpr bool DPIPE = XPIPE || UPS;
+  constexpr bool DPIPE = XPIPE || UPS || NLD * 4 <= 16;
   f32x4 sd[DPIPE ? NLD : 1];
   auto issue = [&](int t) {
     if constexpr (UPS) {
@@ -631,22 +626,31 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
       s16x8 ah[MT], al[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const int o = (m * 16 + (lane & 15)) * DP + p0 + 8 * g;
+        const int co = m * 16 + (lane & 15);
+        const int o = (co < COUT ? co : co % COUT) * DP + p0 + 8 * g;   // padded rows: finite, discarded
         ah[m] = *reinterpret_cast<const s16x8*>(Dh + o);
         al[m] = PM != 2 ? *reinterpret_cast<const s16x8*>(Dl + o) : ah[m];
       }
       const int r0 = (base + roff[0]) * 4, r1 = (base + roff[1]) * 4;
+      // B fragments one N-tile ahead: the transposed reads of tile jn+1 are
+      // in flight during tile jn's MFMAs
+      auto ldb = [&](int jn, s16x8& bh, s16x8& bl) {
+        if (wn + jn * WN < NT) {   // wave-uniform: EXEC stays full for the tr reads
+          bh = __builtin_shufflevector(tr_read(Xh + r0 + colt[jn]), tr_read(Xh + r1 + colt[jn]), 0, 1, 2, 3, 4, 5, 6,
+                                       7);
+          bl = PM != 2 ? __builtin_shufflevector(tr_read(Xl + r0 + colt[jn]), tr_read(Xl + r1 + colt[jn]), 0, 1, 2,
+                                                 3, 4, 5, 6, 7)
+                       : bh;
+        }
+      };
+      s16x8 bh[2], bl[2];
+      ldb(0, bh[0], bl[0]);
 #pragma unroll
       for (int jn = 0; jn < NTW; ++jn) {
+        if (jn + 1 < NTW) ldb(jn + 1, bh[(jn + 1) & 1], bl[(jn + 1) & 1]);
         if (wn + jn * WN < NT) {
-          const s16x8 bh = __builtin_shufflevector(tr_read(Xh + r0 + colt[jn]), tr_read(Xh + r1 + colt[jn]), 0, 1,
-                                                   2, 3, 4, 5, 6, 7);
-          s16x8 bl = bh;
-          if (PM != 2)
-            bl = __builtin_shufflevector(tr_read(Xl + r0 + colt[jn]), tr_read(Xl + r1 + colt[jn]), 0, 1, 2, 3, 4, 5,
-                                         6, 7);
 #pragma unroll
-          for (int m = 0; m < MT; ++m) acc[m][jn] = mma3<PM>(ah[m], al[m], bh, bl, acc[m][jn]);
+          for (int m = 0; m < MT; ++m) acc[m][jn] = mma3<PM>(ah[m], al[m], bh[jn & 1], bl[jn & 1], acc[m][jn]);
         }
       }
     }
