@@ -297,43 +297,54 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 rs4 = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Tile<!TA> ta;
-  Tile<TB> tb;
-  if (kbeg < kend) {
-    ta.load(A, lda, m0, kbeg, M, kend, veca, tid);
-    tb.load(B, ldb, n0, kbeg, N, kend, vecb, tid);
-  }
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    store16<!TA, PM>(ta, Ah, Al, tid);
-    store16<TB, PM>(tb, Bh, Bl, tid);
-    if (do_rs) rs4 += ta.v[0] + ta.v[1];
-    __syncthreads();
-    if (k0 + BK < kend) {
-      ta.load(A, lda, m0, k0 + BK, M, kend, veca, tid);
-      tb.load(B, ldb, n0, k0 + BK, N, kend, vecb, tid);
-    }
-    s16x8 ah[2], al[2], bh[2], bl[2];
+  // register ring of NS K-tiles: the loads of tile k + NS are issued right
+  // after tile k is parked in LDS, so NS-1 tiles stay in flight behind the
+  // MFMAs (these GEMMs are short per block: latency, not bandwidth, bound)
+  constexpr int NS = 3;
+  Tile<!TA> ta[NS];
+  Tile<TB> tb[NS];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      ah[i] = frag16<!TA>(Ah, wm * 32 + i * 16, lane);
-      al[i] = PM != 3 ? frag16<!TA>(Al, wm * 32 + i * 16, lane) : ah[i];
+  for (int st = 0; st < NS; ++st)
+    if (kbeg + st * BK < kend) {
+      ta[st].load(A, lda, m0, kbeg + st * BK, M, kend, veca, tid);
+      tb[st].load(B, ldb, n0, kbeg + st * BK, N, kend, vecb, tid);
     }
+  for (int k0 = kbeg; k0 < kend; k0 += NS * BK) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bh[j] = frag16<TB>(Bh, wn * 32 + j * 16, lane);
-      bl[j] = PM != 3 ? frag16<TB>(Bl, wn * 32 + j * 16, lane) : bh[j];
-    }
+    for (int st = 0; st < NS; ++st) {
+      const int kk = k0 + st * BK;
+      if (kk >= kend) break;
+      __syncthreads();
+      store16<!TA, PM>(ta[st], Ah, Al, tid);
+      store16<TB, PM>(tb[st], Bh, Bl, tid);
+      if (do_rs) rs4 += ta[st].v[0] + ta[st].v[1];
+      __syncthreads();
+      if (kk + NS * BK < kend) {
+        ta[st].load(A, lda, m0, kk + NS * BK, M, kend, veca, tid);
+        tb[st].load(B, ldb, n0, kk + NS * BK, N, kend, vecb, tid);
+      }
+      s16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = frag16<!TA>(Ah, wm * 32 + i * 16, lane);
+        al[i] = PM != 3 ? frag16<!TA>(Al, wm * 32 + i * 16, lane) : ah[i];
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        if constexpr (PM != 3) {
-          acc[i][j] = gmma<PM>(al[i], bh[j], acc[i][j]);
-          acc[i][j] = gmma<PM>(ah[i], bl[j], acc[i][j]);
-        }
-        acc[i][j] = gmma<PM>(ah[i], bh[j], acc[i][j]);
+        bh[j] = frag16<TB>(Bh, wn * 32 + j * 16, lane);
+        bl[j] = PM != 3 ? frag16<TB>(Bl, wn * 32 + j * 16, lane) : bh[j];
       }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (PM != 3) {
+            acc[i][j] = gmma<PM>(al[i], bh[j], acc[i][j]);
+            acc[i][j] = gmma<PM>(ah[i], bl[j], acc[i][j]);
+          }
+          acc[i][j] = gmma<PM>(ah[i], bh[j], acc[i][j]);
+        }
+    }
   }
   if (do_rs) {
     // thread (k = tid>>4 (+16), rows (tid&15)*4 .. +3): reduce over the 16 k-threads
