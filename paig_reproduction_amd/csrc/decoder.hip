@@ -46,9 +46,10 @@ __device__ __forceinline__ double base_coord(int j, int n) {
   return v * (double)(n - 1) / (double)n;
 }
 
-// grid_sample unnormalized source coordinate for output index j
-__device__ __forceinline__ float src_coord(int j, int n, double t, int h) {
-  const float g = (float)(base_coord(j, n) + t);
+// grid_sample unnormalized source coordinate for output index j, from the
+// block's table of base coordinates bc[j] = base_coord(j, n)
+__device__ __forceinline__ float src_coord(double bcj, double t, int h) {
+  const float g = (float)(bcj + t);
   return ((g + 1.f) * (float)h - 1.f) / 2.f;
 }
 
@@ -86,14 +87,21 @@ __device__ __forceinline__ void sample(const float* s, int h, const Bil& b, floa
 // per (frame, object, row/col) instead of per pixel.  Caller syncs.
 constexpr int MAXH = 64;
 template <int K>
-__device__ __forceinline__ void coord_tables(const float* pf, int H, int h, float (*cx)[MAXH], float (*cy)[MAXH]) {
+__device__ __forceinline__ void coord_tables(const float* pf, int H, int h, float (*cx)[MAXH], float (*cy)[MAXH],
+                                             const double* bc) {
   for (int t = threadIdx.x; t < K * 2 * H; t += blockDim.x) {
     const int k = t / (2 * H), r = t % (2 * H);
     const float l = r < H ? pf[2 * k] : pf[2 * k + 1];
     const double tt = (double)(((float)H / 2.f - l) / (float)h);
-    if (r < H) cx[k][r] = src_coord(r, H, tt, h);
-    else cy[k][r - H] = src_coord(r - H, H, tt, h);
+    if (r < H) cx[k][r] = src_coord(bc[r], tt, h);
+    else cy[k][r - H] = src_coord(bc[r - H], tt, h);
   }
+}
+
+// the fp64 affine_grid base coordinates (frame-invariant): computed once per
+// block; the kernels' first in-loop barrier orders them before use
+__device__ __forceinline__ void init_base(double* bc, int H) {
+  for (int j = threadIdx.x; j < H; j += blockDim.x) bc[j] = base_coord(j, H);
 }
 
 template <int K>
@@ -149,11 +157,13 @@ dec_fwd_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse, in
   float* Cn = T + K * hh;
   __shared__ float red[4];
   __shared__ float cx[K][MAXH], cy[K][MAXH];
+  __shared__ double bc[MAXH];
+  init_base(bc, H);
   stage_sources<K>(S, h, T, Cn);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int f = blockIdx.x; f < F; f += gridDim.x) {
     __syncthreads();   // previous frame done with the tables
-    coord_tables<K>(pos.at(f), H, h, cx, cy);
+    coord_tables<K>(pos.at(f), H, h, cx, cy, bc);
     __syncthreads();
     float* of = out.frame(f);
     const float* tf = sse ? tgt.frame(f) : nullptr;
@@ -201,6 +211,8 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
   __shared__ double redd[4][2 * K];
   __shared__ int skip_s;
   __shared__ float cx[K][MAXH], cy[K][MAXH];
+  __shared__ double bc[MAXH];
+  init_base(bc, H);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nw = blockDim.x >> 6;
   const long long slab_len = (long long)K * hh + (long long)K * 3 * hh + 3LL * HW;
@@ -230,7 +242,7 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
       __syncthreads();
       continue;
     }
-    coord_tables<K>(pos.at(f), H, h, cx, cy);
+    coord_tables<K>(pos.at(f), H, h, cx, cy, bc);
     __syncthreads();
     const float* tf = tgt.frame(f);
     double sx[K], sy[K];
@@ -440,6 +452,8 @@ dec_fwd_reg_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse
   float* Cn = T + K * hh;
   __shared__ float red[4];
   __shared__ float cx[K][MAXH], cy[K][MAXH];
+  __shared__ double bc[MAXH];
+  init_base(bc, H);
   stage_sources<K>(S, h, T, Cn);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   float bgv[PPT][3], tn[PPT][3];
@@ -461,7 +475,7 @@ dec_fwd_reg_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse
   if (sse && (int)blockIdx.x < F) fetch(blockIdx.x);
   for (int f = blockIdx.x; f < F; f += gridDim.x) {
     __syncthreads();   // previous frame done with the tables
-    coord_tables<K>(pos.at(f), H, h, cx, cy);
+    coord_tables<K>(pos.at(f), H, h, cx, cy, bc);
     __syncthreads();
     float tc[PPT][3];
 #pragma unroll
@@ -542,6 +556,8 @@ dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVi
   float* G = Cn + K * 3 * hh;   // [K][4][HW] per-frame pixel-gradient image
   __shared__ double redd[4][2 * K];
   __shared__ float cx[K][MAXH], cy[K][MAXH];
+  __shared__ double bc[MAXH];
+  init_base(bc, H);
   __shared__ int j0[K][2][h];
   __shared__ float wt[K][2][h][GW];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -587,7 +603,7 @@ dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVi
     }
     const float* dof = dout.p ? dout.frame(f) : nullptr;
     __syncthreads();   // previous frame's pass 2 done with G and the tables
-    coord_tables<K>(pos.at(f), H, h, cx, cy);
+    coord_tables<K>(pos.at(f), H, h, cx, cy, bc);
     __syncthreads();
     gather_tables<K, H>(cx, cy, j0, wt);   // read only after the barrier below
     double sx[K], sy[K];
