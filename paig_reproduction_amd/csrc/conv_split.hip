@@ -43,6 +43,13 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int rup(int a, int b) { return ceil_div(a, b) * b; }
+// largest divisor d of n with d * w <= cap (at least 1): rows per tile
+constexpr int rows_fit(int n, int w, int cap) {
+  int best = 1;
+  for (int d = 1; d <= n; ++d)
+    if (n % d == 0 && d * w <= cap) best = d;
+  return best;
+}
 // smallest y >= x with y % 16 == r
 constexpr int to_mod16(int x, int r) { return x + ((r - x % 16) + 16) % 16; }
 
@@ -96,11 +103,15 @@ __device__ __forceinline__ s16x4 tr_read(const short* p) {
 // from LDS while building the 16-bit operand image.
 template <int CIN, int H, int W, int FPT, int RT>
 struct UpStage {
-  static constexpr int HS = H / 2, WS = W / 2, SRN = RT / 2 + 2, QS = WS / 4;
+  // window rows y0/2 - 1 .. : RT/2 + 2 rows for an even tile height, one more
+  // for an odd one (3bp's 18-row frames tile as 2 x 9 rows)
+  static constexpr int HS = H / 2, WS = W / 2, SRN = RT / 2 + 2 + (RT & 1);
+  static constexpr int VS = WS % 4 == 0 ? 4 : 1;               // floats per load unit
+  static constexpr int QS = WS / VS;
   static constexpr int NSU = FPT * CIN * SRN * QS, NLS = (NSU + 255) / 256;
   static constexpr int SL = FPT * CIN * SRN * WS;   // floats of LDS
-  static_assert(WS % 4 == 0 && RT % 2 == 0, "upsample window");
-  f32x4 v[NLS];
+  f32x4 v[VS == 4 ? NLS : 1];
+  float v1[VS == 1 ? NLS : 1];
   __device__ __forceinline__ void issue(const FView& x, int F, int f0, int y0, int tid) {
 #pragma unroll
     for (int l = 0; l < NLS; ++l) {
@@ -108,17 +119,23 @@ struct UpStage {
       const int q = i % QS, sr = (i / QS) % SRN, c = (i / (QS * SRN)) % CIN, fi = i / (QS * SRN * CIN);
       const int srow = y0 / 2 - 1 + sr;
       const bool ok = i < NSU && f0 + fi < F && srow >= 0 && srow < HS;
-      const int off = ok ? fi * (int)x.fs + c * HS * WS + srow * WS + 4 * q : 0;
-      const f32x4 u = *reinterpret_cast<const f32x4*>(x.frame(f0) + off);
-      v[l] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int off = ok ? fi * (int)x.fs + c * HS * WS + srow * WS + VS * q : 0;
+      if constexpr (VS == 4) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(x.frame(f0) + off);
+        v[l] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        const float u = x.frame(f0)[off];
+        v1[l] = ok ? u : 0.f;
+      }
     }
   }
   __device__ __forceinline__ void commit(float* Sl, int tid) const {
 #pragma unroll
     for (int l = 0; l < NLS; ++l) {
-      const int i = tid + l * 256;   // Sl is [fi][c][sr][WS]: unit i sits at 4*i
+      const int i = tid + l * 256;   // Sl is [fi][c][sr][WS]: unit i sits at VS*i
       if (NSU % 256 != 0 && i >= NSU) break;
-      *reinterpret_cast<f32x4*>(Sl + 4 * i) = v[l];
+      if constexpr (VS == 4) *reinterpret_cast<f32x4*>(Sl + 4 * i) = v[l];
+      else Sl[i] = v1[l];
     }
   }
   // output pixel (row gy, column x) of channel c of frame fi (0 <= gy < H), in
@@ -163,27 +180,31 @@ struct SFwdCfg {
   static constexpr int CINP = rup(CIN, 8), CC = CINP / 8;    // 8-channel chunks per pixel
   static constexpr int KC = KK * CC, NS = ceil_div(KC, 4);   // k-chunks, MFMA k-steps (4 chunks each)
   static constexpr int NT = ceil_div(COUT, 16);
-  static constexpr int MW = W >= 16 ? 4 : 2;                 // M-tiles per wave
-  static constexpr int TPX = 4 * MW * 16;
-  static constexpr int FPT = TPX >= H * W ? TPX / (H * W) : 1;
-  static constexpr int RT = TPX >= H * W ? H : TPX / W;
+  // tile: whole rows (RT divides H) of one frame, or FPT whole frames; at
+  // most TPXM pixels (256; 128 at W = 8, whose tuned tile is 2 frames)
+  static constexpr int TPXM = W == 8 ? 128 : 256;
+  static constexpr int FPT = H * W <= TPXM ? TPXM / (H * W) : 1;
+  static constexpr int RT = H * W <= TPXM ? H : rows_fit(H, W, TPXM);
+  static constexpr int TPXV = FPT * RT * W;                  // valid pixels per tile
+  static constexpr int NMT = ceil_div(TPXV, 16);             // M-tiles of 16 pixels
+  static constexpr int MW = ceil_div(NMT, 4);                // M-tiles per wave
   static constexpr int ROWS = RT + KS - 1;
   static constexpr int TWPX = W + 2 * PADL;                  // pixel columns incl. halo
   // 16-B slots per pixel: odd, so 16 consecutive pixels hit 16 distinct
   // bank groups; an M-tile spanning two rows (W = 8) needs the row pitch
   // = 8 (mod 16) slots so the second row lands on the other 8 groups
   static constexpr int PS = CC % 2 == 0 ? CC + 1 : CC;
-  static constexpr int RP = W >= 16 ? TWPX * PS : to_mod16(TWPX * PS, 8);
+  static constexpr int RP = W == 8 ? to_mod16(TWPX * PS, 8) : TWPX * PS;
   static constexpr int IMG = FPT * ROWS * RP * 8;            // 16-bit elements per image
   static constexpr int WIMG = NS * NT * 64 * 8;
   static constexpr int LDS = (IMG + WIMG) * 2 * NIMG;
-  // staging unit = one pixel x 8 channels: consecutive lanes take consecutive
+  // staging unit = UPX pixels x 8 channels, consecutive lanes on consecutive
   // pixels (coalesced loads, b128 LDS writes PS slots apart: conflict-free)
-  static constexpr int W2 = W / 2;
-  static constexpr int NI = FPT * ROWS * W2 * CC;            // units: 2 pixels x 8 channels
+  static constexpr int UPX = W % 2 == 0 ? 2 : 1;
+  static constexpr int W2 = W / UPX;
+  static constexpr int NI = FPT * ROWS * W2 * CC;
   static constexpr int NL = (NI + 255) / 256;
-  static_assert(W % 8 == 0 && (W >= 16 || 16 % W == 0), "M-tile rows");
-  static_assert(RT * W * FPT == TPX || RT == H, "tile");
+  static constexpr bool VEC4 = W % 4 == 0;                   // 4-pixel epilogue stores stay in one row
   static_assert(H % RT == 0, "RT divides H");
 };
 
@@ -239,7 +260,8 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   int pbase[MW];
 #pragma unroll
   for (int mt = 0; mt < MW; ++mt) {
-    const int pix = (wv * MW + mt) * 16 + (lane & 15);
+    int pix = (wv * MW + mt) * 16 + (lane & 15);
+    if (pix >= C::TPXV) pix = 0;   // padding rows of the last M-tile: finite data, never stored
     const int fi = pix / (RT * W), rem = pix % (RT * W);
     pbase[mt] = (fi * ROWS + rem / W) * RP + (rem % W) * PS;
   }
@@ -256,8 +278,9 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   // the next tile's loads are in flight during this tile's MFMAs
   using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
   float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::IMG + C::WIMG));
+  constexpr int UPX = C::UPX;
   auto put_px = [&](int i, const float2* v) {
-    const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
+    const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
     const int o = ((fi * ROWS + r) * RP + (xp + PADL) * PS + cc) * 8;
     s16x8 h0, l0, h1, l1;
 #pragma unroll
@@ -271,10 +294,10 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       l1[c] = lo;
     }
     *reinterpret_cast<s16x8*>(Xh + o) = h0;
-    *reinterpret_cast<s16x8*>(Xh + o + PS * 8) = h1;
-    if (PM != 2) {
-      *reinterpret_cast<s16x8*>(Xl + o) = l0;
-      *reinterpret_cast<s16x8*>(Xl + o + PS * 8) = l1;
+    if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = l0;
+    if constexpr (UPX == 2) {
+      *reinterpret_cast<s16x8*>(Xh + o + PS * 8) = h1;
+      if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o + PS * 8) = l1;
     }
   };
   float2 pre[UPS ? 1 : NL][8];
@@ -291,13 +314,14 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         const int i = tid + l * 256;
-        const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
+        const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
         const int gy = y0 + r - PADL;
         const bool ok = i < NI && f0 + fi < F && gy >= 0 && gy < H;
         const int off = ok ? fi * (int)in.fs + cc * 8 * (int)PLANE + gy * W + xp : 0;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          const float2 v = *reinterpret_cast<const float2*>(fb + off + (cc * 8 + c < CIN ? c : 0) * (int)PLANE);
+          const float* q = fb + off + (cc * 8 + c < CIN ? c : 0) * (int)PLANE;
+          const float2 v = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
           pre[l][c] = (ok && cc * 8 + c < CIN) ? v : make_float2(0.f, 0.f);
         }
       }
@@ -310,14 +334,15 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       __syncthreads();
 #pragma unroll 1
       for (int i = tid; i < NI; i += 256) {
-        const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
+        const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
         const int gy = y0 + r - PADL;
         const bool ok = f0 + fi < F && gy >= 0 && gy < H;
         float2 v[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c)
           v[c] = (ok && cc * 8 + c < CIN)
-                     ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp), UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1))
+                     ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp),
+                                   UPX == 2 ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1) : 0.f)
                      : make_float2(0.f, 0.f);
         put_px(i, v);
       }
@@ -371,24 +396,43 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
       for (int mt = 0; mt < MW; ++mt) {
         const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
-        const int fi = pix / (RT * W), rem = pix % (RT * W);
-        const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
-        if (f >= F) continue;
-        float* op = out.frame(f) + co * HW + (long long)y * W + x;
-        f32x4 v = acc[mt][nt];
+        if constexpr (C::VEC4) {
+          // 4 pixels of one row (rows hold a multiple of 4 pixels)
+          if (pix >= C::TPXV) continue;
+          const int fi = pix / (RT * W), rem = pix % (RT * W);
+          const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
+          if (f >= F) continue;
+          float* op = out.frame(f) + co * HW + (long long)y * W + x;
+          f32x4 v = acc[mt][nt];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += bv;
-        if (flags & 1) {
+          for (int r = 0; r < 4; ++r) v[r] += bv;
+          if (flags & 1) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] < 0.f ? 0.f : v[r];
+            for (int r = 0; r < 4; ++r) v[r] = v[r] < 0.f ? 0.f : v[r];
+          }
+          if (flags & 4) v += *reinterpret_cast<const f32x4*>(op);
+          if (flags & 2) {
+            const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
+          }
+          *reinterpret_cast<f32x4*>(op) = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int pr = pix + r;
+            if (pr >= C::TPXV) break;
+            const int fi = pr / (RT * W), rem = pr % (RT * W);
+            const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
+            if (f >= F) continue;
+            float* op = out.frame(f) + co * HW + (long long)y * W + x;
+            float v = acc[mt][nt][r] + bv;
+            if (flags & 1) v = v < 0.f ? 0.f : v;
+            if (flags & 4) v += *op;
+            if (flags & 2) v = aux.frame(f)[co * HW + (long long)y * W + x] > 0.f ? v : 0.f;
+            *op = v;
+          }
         }
-        if (flags & 4) v += *reinterpret_cast<const f32x4*>(op);
-        if (flags & 2) {
-          const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
-        }
-        *reinterpret_cast<f32x4*>(op) = v;
       }
     }
   }
@@ -406,9 +450,16 @@ struct SWgCfg {
   static constexpr int MT = ceil_div(COUT, 16), COP = MT * 16;
   static constexpr int WN = (MT * NT * 4 <= 40) ? 1 : ((MT * ceil_div(NT, 2) * 4 <= 40) ? 2 : 4);
   static constexpr int WP = 4 / WN, NTW = ceil_div(NT, WN);
-  static constexpr int TPX = 256;                             // pixels per tile
-  static constexpr int FPT = H * W >= TPX ? 1 : TPX / (H * W);
-  static constexpr int RT = H * W >= TPX ? TPX / W : H;
+  // tile: whole rows (RT divides H) of one frame or FPT whole frames, <= 256
+  // pixels; k-blocks of 32 tile pixels (the last one zero-padded in dY)
+  static constexpr int TPX = 256;
+  static constexpr int FPT = H * W <= TPX ? TPX / (H * W) : 1;
+  static constexpr int RT = H * W <= TPX ? H : rows_fit(H, W, TPX);
+  static constexpr int TPXV = FPT * RT * W;                   // valid pixels per tile
+  static constexpr int KB = ceil_div(TPXV, 32);               // k-blocks of 32 pixels per tile
+  // FAST: every k-block is 32 pixels of whole rows of one frame, so a lane's
+  // transposed-read rows are a fixed offset from the k-block base
+  static constexpr bool FAST = TPXV == 256 && (RT * W) % 32 == 0 && (W % 32 == 0 || 32 % W == 0);
   static constexpr int ROWS = RT + KS - 1;
   // input column x sits at image column x + OFFX: even, so a 2-pixel staging
   // unit is one aligned 16-B write per plane
@@ -422,20 +473,20 @@ struct SWgCfg {
   static constexpr int XIMG = CQ * XPL;
   static constexpr int DP = TPX + 8;                          // dY row pitch: 16 rows -> 16 bank groups
   static constexpr int DIMG = COUT * DP;   // rows co >= COUT of an A fragment re-read rows co % COUT
-  static constexpr int KB = TPX / 32;                         // k-blocks of 32 pixels per tile
   static constexpr int STG = (XIMG + DIMG) * 2 * NIMG;
   static constexpr int RED = 4 * MT * NTW * 4 * 64 * 4;
   static constexpr int LDS = STG > RED ? STG : RED;
-  static constexpr int Q = W / 4;
-  static constexpr int W2 = W / 2;
-  static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = (NIX + 255) / 256;  // X units: 2 px x 4 ch
-  static constexpr int NID = COUT * TPX / 4, NLD = (NID + 255) / 256;         // dY units: 4 px x 1 ch
+  static constexpr int UPX = W % 2 == 0 ? 2 : 1;              // X units: UPX pixels x 4 channels
+  static constexpr int W2 = W / UPX;
+  static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = (NIX + 255) / 256;
+  static constexpr int DU = W % 4 == 0 ? 4 : (W % 2 == 0 ? 2 : 1);   // dY units: DU pixels x 1 channel
+  static constexpr int NPU = TPXV / DU;                       // dY units per channel
+  static constexpr int NID = COUT * NPU, NLD = (NID + 255) / 256;
   static constexpr int SLAB = COUT * NCOL + COUT;
   // waves per SIMD the registers must allow: 3 where three blocks fit the LDS
   static constexpr int MINW = 3 * LDS <= 160 * 1024 ? 3 : 2;
-  static_assert(FPT * RT * W == TPX, "tile = 256 pixels");
-  static_assert((RT * W) % 32 == 0 && (W % 32 == 0 || 32 % W == 0), "k-blocks stay in one frame");
   static_assert(H % RT == 0, "RT divides H");
+  static_assert(TPXV % DU == 0, "dY units");
 };
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
@@ -445,6 +496,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   constexpr int KK = C::KK, CQ = C::CQ, NQ = C::NQ, NT = C::NT, NCOL = C::NCOL, MT = C::MT, COP = C::COP;
   constexpr int WN = C::WN, WP = C::WP, NTW = C::NTW, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS;
   constexpr int TWPX = C::TWPX, XPL = C::XPL, DP = C::DP, KB = C::KB, PADL = C::PADL, OFFX = C::OFFX, W2 = C::W2;
+  constexpr int UPX = C::UPX, DU = C::DU, NPU = C::NPU, TPXV = C::TPXV;
   constexpr int NIX = C::NIX, NLX = C::NLX, NID = C::NID, NLD = C::NLD;
   constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   constexpr long long HW = (long long)H * W;
@@ -467,6 +519,14 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
         *reinterpret_cast<s16x4*>(Xh + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
         if (PM != 2) *reinterpret_cast<s16x4*>(Xl + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
       }
+    }
+  }
+  // padded pixels of the last k-block: dY = 0 (never staged)
+  if (KB * 32 > TPXV) {
+    for (int i = tid; i < COUT * (KB * 32 - TPXV); i += 256) {
+      const int co = i / (KB * 32 - TPXV), pt = TPXV + i % (KB * 32 - TPXV);
+      Dh[co * DP + pt] = 0;
+      if (PM != 2) Dl[co * DP + pt] = 0;
     }
   }
   // ---- per-lane transposed-read addressing. Lane 4q+p of its 16-lane group
@@ -503,19 +563,20 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   constexpr bool XPIPE = !UPS && NLX * 8 + NLD * 4 <= (C::MINW == 3 ? 24 : 48);
   auto load_x = [&](int t, int i, float2* v) {   // branch-free, 32-bit offsets (see the forward kernel)
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
-    const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+    const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
     const int gy = y0 + r - PADL;
     const bool ok = i < NIX && f0 + fi < F && gy >= 0 && gy < H;
     const float* fb = x.frame(f0);
     const int off = ok ? fi * (int)x.fs + cq * 4 * (int)PLANE + gy * W + xp : 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float2 u = *reinterpret_cast<const float2*>(fb + off + (cq * 4 + c < CIN ? c : 0) * (int)PLANE);
+      const float* q = fb + off + (cq * 4 + c < CIN ? c : 0) * (int)PLANE;
+      const float2 u = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
       v[c] = (ok && cq * 4 + c < CIN) ? u : make_float2(0.f, 0.f);
     }
   };
   auto put_x = [&](int i, const float2* v) {
-    const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+    const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
     const int o = xplane(cq) + ((fi * ROWS + r) * TWPX + xp + OFFX) * 4;
     s16x8 hv, lv;
 #pragma unroll
@@ -528,19 +589,32 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
       hv[4 + c] = h;
       lv[4 + c] = lo;
     }
-    *reinterpret_cast<s16x8*>(Xh + o) = hv;
-    if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = lv;
+    if constexpr (UPX == 2) {
+      *reinterpret_cast<s16x8*>(Xh + o) = hv;
+      if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = lv;
+    } else {
+      *reinterpret_cast<s16x4*>(Xh + o) = s16x4{hv[0], hv[1], hv[2], hv[3]};
+      if (PM != 2) *reinterpret_cast<s16x4*>(Xl + o) = s16x4{lv[0], lv[1], lv[2], lv[3]};
+    }
   };
   UP up;
   float2 sx[XPIPE ? NLX : 1][4];
   auto load_d = [&](int t, int l) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
     const int i = tid + l * 256;
-    const int co = i / (C::TPX / 4), pt = 4 * (i % (C::TPX / 4));
+    const int co = i / NPU, pt = DU * (i % NPU);
     const int fi = pt / (RT * W), y = (pt / W) % RT, xx = pt % W;
     const bool ok = i < NID && f0 + fi < F;
     const int off = ok ? fi * (int)dy.fs + co * (int)HW + (y0 + y) * W + xx : 0;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(dy.frame(f0) + off);
+    const float* q = dy.frame(f0) + off;
+    f32x4 v;
+    if constexpr (DU == 4) v = *reinterpret_cast<const f32x4*>(q);
+    else if constexpr (DU == 2) {
+      const float2 u = *reinterpret_cast<const float2*>(q);
+      v = f32x4{u.x, u.y, 0.f, 0.f};
+    } else {
+      v = f32x4{*q, 0.f, 0.f, 0.f};
+    }
     return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   constexpr bool DPIPE = XPIPE || UPS || NLD * 4 <= 16;
@@ -564,14 +638,15 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
       __syncthreads();
 #pragma unroll 1
       for (int i = tid; i < NIX; i += 256) {
-        const int xp = 2 * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+        const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
         const int gy = y0 + r - PADL;
         const bool ok = f0 + fi < F && gy >= 0 && gy < H;
         float2 v[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           v[c] = (ok && cq * 4 + c < CIN)
-                     ? make_float2(UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp), UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp + 1))
+                     ? make_float2(UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp),
+                                   UPX == 2 ? UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp + 1) : 0.f)
                      : make_float2(0.f, 0.f);
         put_x(i, v);
       }
@@ -594,7 +669,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
     for (int l = 0; l < NLD; ++l) {
       const int i = tid + l * 256;
       if (NID % 256 != 0 && i >= NID) break;
-      const int co = i / (C::TPX / 4), pt = 4 * (i % (C::TPX / 4));
+      const int co = i / NPU, pt = DU * (i % NPU);
       f32x4 dv;
       if constexpr (DPIPE) dv = sd[l];
       else dv = load_d(t, l);
@@ -606,9 +681,17 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
         hv[e] = h;
         lv[e] = lo;
       }
-      bacc[l] += (dv[0] + dv[1]) + (dv[2] + dv[3]);
-      *reinterpret_cast<s16x4*>(Dh + co * DP + pt) = hv;
-      if (PM != 2) *reinterpret_cast<s16x4*>(Dl + co * DP + pt) = lv;
+      bacc[l] += (dv[0] + dv[1]) + (dv[2] + dv[3]);   // zeros past DU
+      if constexpr (DU == 4) {
+        *reinterpret_cast<s16x4*>(Dh + co * DP + pt) = hv;
+        if (PM != 2) *reinterpret_cast<s16x4*>(Dl + co * DP + pt) = lv;
+      } else {
+#pragma unroll
+        for (int e = 0; e < DU; ++e) {
+          Dh[co * DP + pt + e] = hv[e];
+          if (PM != 2) Dl[co * DP + pt + e] = lv[e];
+        }
+      }
     }
   };
 
@@ -631,7 +714,22 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
         ah[m] = *reinterpret_cast<const s16x8*>(Dh + o);
         al[m] = PM != 2 ? *reinterpret_cast<const s16x8*>(Dl + o) : ah[m];
       }
-      const int r0 = (base + roff[0]) * 4, r1 = (base + roff[1]) * 4;
+      int r0, r1;
+      if constexpr (C::FAST) {
+        r0 = (base + roff[0]) * 4;
+        r1 = (base + roff[1]) * 4;
+      } else {
+        // pixel p of the k-block -> its image position (padded pixels: any
+        // valid position; their dY is zero)
+        auto posof = [&](int j) {
+          int pp = p0 + j;
+          if (pp >= TPXV) pp = 0;
+          const int pf = pp / (RT * W), prr = pp % (RT * W);
+          return ((pf * ROWS + prr / W) * TWPX + prr % W + (OFFX - PADL)) * 4;
+        };
+        r0 = posof(8 * g + qq);
+        r1 = posof(8 * g + 4 + qq);
+      }
       // B fragments one N-tile ahead: the transposed reads of tile jn+1 are
       // in flight during tile jn's MFMAs
       auto ldb = [&](int jn, s16x8& bh, s16x8& bl) {
@@ -684,12 +782,18 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
         }
       }
   }
-  // bias: dY unit i covers channel i / 64, i.e. one channel per (wave, l)
+  // bias: every dY unit i (channel i / NPU) kept its fp32 partial in thread
+  // i % 256, slot i / 256; one thread per channel sums them in unit order
+  // (deterministic)
+  __syncthreads();
+  float* Rb = reinterpret_cast<float*>(lds16);   // [NLD][256]
 #pragma unroll
-  for (int l = 0; l < NLD; ++l) {
-    const float v = wave_sum(bacc[l]);
-    const int i = tid + l * 256;
-    if (lane == 0 && i < NID) s[COUT * NCOL + i / (C::TPX / 4)] = v;
+  for (int l = 0; l < NLD; ++l) Rb[l * 256 + tid] = bacc[l];
+  __syncthreads();
+  if (tid < COUT) {
+    float v = 0.f;
+    for (int i = tid * NPU; i < (tid + 1) * NPU; ++i) v += Rb[(i / 256) * 256 + i % 256];
+    s[COUT * NCOL + tid] = v;
   }
 }
 
@@ -740,11 +844,22 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
 #define PAIG_SPLIT_FWD(X)                                                                                 \
   X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1) X(16, 8, 16, 3) X(8, 24, 32, 3)       \
-  X(2, 8, 32, 1) X(32, 16, 8, 3) X(16, 32, 16, 3)
+  X(2, 8, 32, 1) X(32, 16, 8, 3) X(16, 32, 16, 3)                                                         \
+  PAIG_SPLIT_FWD_3BP(X)
 #define PAIG_SPLIT_WG(X)                                                                                  \
   X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
-  X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1)
-#define PAIG_SPLIT_UP(X) X(32, 16, 16, 3) X(16, 16, 32, 3)
+  X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1)                                        \
+  PAIG_SPLIT_WG_3BP(X)
+#define PAIG_SPLIT_UP(X) X(32, 16, 16, 3) X(16, 16, 32, 3) X(32, 16, 18, 3) X(16, 16, 36, 3)
+// 3bp_color (ShallowUNet hidden 8 on 36 x 36 frames, K = 3 objects): levels
+// 36 / 18 / 9; tiles of 6 rows (36), 9 rows (18) or 3 frames (9 x 9)
+#define PAIG_SPLIT_FWD_3BP(X)                                                                             \
+  X(3, 8, 36, 3) X(8, 8, 36, 3) X(8, 16, 18, 3) X(16, 16, 18, 3) X(16, 32, 9, 3) X(32, 32, 9, 3)         \
+  X(32, 16, 18, 3) X(16, 16, 36, 3) X(24, 8, 36, 3) X(8, 3, 36, 1) X(16, 8, 18, 3) X(32, 16, 9, 3)       \
+  X(16, 32, 18, 3) X(8, 24, 36, 3) X(3, 8, 36, 1)
+#define PAIG_SPLIT_WG_3BP(X)                                                                              \
+  X(3, 8, 36, 3) X(8, 8, 36, 3) X(8, 16, 18, 3) X(16, 16, 18, 3) X(16, 32, 9, 3) X(32, 32, 9, 3)         \
+  X(32, 16, 18, 3) X(16, 16, 36, 3) X(24, 8, 36, 3) X(8, 3, 36, 1)
 
 }  // namespace
 

@@ -162,7 +162,8 @@ class Layout:
                 continue
             c = self.ops[consumers[0]]
             Hc = self.H // self.bufs[op["dst"][0]][1]
-            if all(L.paig_conv2d_mfma_supported(w, c["src"][2], c["dst"][2], Hc, Hc, c["ks"], 32) for w in (0, 1)):
+            cm = Engine.CONV_MATH.get(getattr(model, "conv_math", "split"), 0)
+            if all(L.paig_conv2d_mfma_supported(w, c["src"][2], c["dst"][2], Hc, Hc, c["ks"], 32 | cm) for w in (0, 1)):
                 self.fused_up[consumers[0]] = op
                 self.fused_bufs.add(op["dst"][0])
         self.HW = self.H * self.H

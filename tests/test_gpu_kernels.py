@@ -80,7 +80,11 @@ def test_conv_fwd_dgrad_wgrad(cin, cout, hw, ks, F_):
 
 SPLIT_CASES = [(3, 8, 32, 3, 5), (8, 8, 32, 3, 3), (8, 16, 16, 3, 7), (16, 16, 16, 3, 4), (16, 32, 8, 3, 9),
                (32, 32, 8, 3, 3), (32, 16, 16, 3, 2), (24, 8, 32, 3, 2), (8, 2, 32, 1, 3), (16, 16, 32, 3, 2),
-               (16, 8, 16, 3, 3), (8, 24, 32, 3, 2), (2, 8, 32, 1, 3), (32, 16, 8, 3, 3), (16, 32, 16, 3, 2)]
+               (16, 8, 16, 3, 3), (8, 24, 32, 3, 2), (2, 8, 32, 1, 3), (32, 16, 8, 3, 3), (16, 32, 16, 3, 2),
+               # 3bp (36 x 36 frames): ragged widths 36 / 18 / 9, multi-frame tiles, odd frame counts
+               (3, 8, 36, 3, 3), (8, 8, 36, 3, 2), (8, 16, 18, 3, 5), (16, 16, 18, 3, 3), (16, 32, 9, 3, 7),
+               (32, 32, 9, 3, 4), (32, 16, 18, 3, 3), (16, 16, 36, 3, 2), (24, 8, 36, 3, 2), (8, 3, 36, 1, 3),
+               (16, 8, 18, 3, 3), (32, 16, 9, 3, 5), (16, 32, 18, 3, 2), (8, 24, 36, 3, 2), (3, 8, 36, 1, 2)]
 # normwise bars: f16 hi/lo forward ~2^-22 per product (fp32-level); bf16 hi/lo
 # dgrad/wgrad ~2^-17; bf16 (hi only) ~2^-9
 SPLIT_TOL = {128: (1e-5, 3e-5), 256: (8e-3, 8e-3)}
@@ -131,7 +135,7 @@ def test_conv_split(cin, cout, hw, ks, F_, mode):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32)])
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (32, 16, 18), (16, 16, 36)])
 def test_conv_split_fused_upsample(cin, cout, hw, mode):
     """c7/c10: the conv input is the 2x bilinear upsample, formed while staging."""
     tf, tb = SPLIT_TOL[mode]
