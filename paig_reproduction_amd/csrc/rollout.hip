@@ -30,9 +30,15 @@ struct Phys {
 };
 
 // ---------------------------------------------------------------- spring ----
+// sqrt(|d*d|) of the reference: in binary IEEE arithmetic with round to
+// nearest, sqrt(fl(d*d)) == |d| exactly unless d*d underflows (then 0) or
+// overflows (impossible for pixel coordinates) -- one op instead of the IEEE
+// sqrt sequence on the rollout's serial chain
+__device__ __forceinline__ float abs_via_sq(float d) { return d * d == 0.f ? 0.f : fabsf(d); }
+
 __device__ __forceinline__ void spring_sub(const Phys& P, float* p, float* v) {
   const float d = p[0] - p[1];
-  const float n = sqrtf(fabsf(d * d));
+  const float n = abs_via_sq(d);
   const float dir = d / (n + 1e-4f);
   const float F = P.ek * (n - P.tee) * dir;
   v[0] = v[0] - P.h * F;
@@ -43,13 +49,19 @@ __device__ __forceinline__ void spring_sub(const Phys& P, float* p, float* v) {
 
 // adjoint of one spring substep, given the substep's INPUT state (p, v).
 // gp/gv: adjoints of outputs -> overwritten with adjoints of inputs.
+// The adjoint is a long serial chain (46 steps x 5 substeps per thread): its
+// divisions use one v_rcp_f32 (1 ulp) instead of the IEEE division sequence,
+// and the parameter adjoints accumulate in fp32 within a step (flushed to
+// fp64 per step by the caller) -- gradient-side only; the forward keeps the
+// reference's exact operations.
 __device__ __forceinline__ void spring_sub_bwd(const Phys& P, const float* p, const float* v, float* gp, float* gv,
-                                               double& gek, double& gtee) {
+                                               float& gek, float& gtee) {
   const float d = p[0] - p[1];
   const float dd = d * d;
-  const float n = sqrtf(fabsf(dd));
+  const float n = abs_via_sq(d);
   const float den = n + 1e-4f;
-  const float dir = d / den;
+  const float rden = __builtin_amdgcn_rcpf(den);
+  const float dir = d * rden;
   const float nm = n - P.tee;
   // p' = p + h v'
   gv[0] += P.h * gp[0];
@@ -57,15 +69,15 @@ __device__ __forceinline__ void spring_sub_bwd(const Phys& P, const float* p, co
   // v0' = v0 - h F ; v1' = v1 + h F
   const float gF = P.h * gv[1] - P.h * gv[0];
   // F = ek * (n - tee) * dir
-  gek += (double)(gF * nm * dir);
+  gek += gF * nm * dir;
   const float gnm = gF * P.ek * dir;
-  gtee -= (double)gnm;
+  gtee -= gnm;
   const float gdir = gF * P.ek * nm;
   // dir = d / (n + 1e-4)
-  float gd = gdir / den;
-  float gn = gnm - gdir * d / (den * den);
+  float gd = gdir * rden;
+  float gn = gnm - gdir * d * (rden * rden);
   // n = sqrt(|d*d|)  (aten: sqrt' = g/(2 sqrt), abs' = sgn, pow' = 2d)
-  const float gsq = gn / (2.f * n);
+  const float gsq = gn * __builtin_amdgcn_rcpf(2.f * n);
   const float sg = dd > 0.f ? 1.f : (dd < 0.f ? -1.f : 0.f);
   gd += gsq * sg * 2.f * d;
   gp[0] += gd;
@@ -134,7 +146,7 @@ __device__ __forceinline__ void grav_sub(const Phys& P, float* p, float* v) {
   for (int i = 0; i < 6; ++i) p[i] = p[i] + P.h * v[i];
 }
 
-__device__ __forceinline__ void grav_sub_bwd(const Phys& P, const float* p, float* gp, float* gv, double& gnegA) {
+__device__ __forceinline__ void grav_sub_bwd(const Phys& P, const float* p, float* gp, float* gv, float& gnegA) {
   for (int i = 0; i < 6; ++i) gv[i] += P.h * gp[i];
   float gF[6];
   for (int i = 0; i < 6; ++i) gF[i] = P.h * gv[i];
@@ -156,7 +168,7 @@ __device__ __forceinline__ void grav_sub_bwd(const Phys& P, const float* p, floa
   // F0 = negA (Fi0 - Fi2), F1 = negA (Fi1 - Fi0), F2 = negA (Fi2 - Fi1)
   float gFi[3][2];
   for (int c = 0; c < 2; ++c) {
-    gnegA += (double)(gF[0 + c] * (Fi[0][c] - Fi[2][c]) + gF[2 + c] * (Fi[1][c] - Fi[0][c]) +
+    gnegA += (gF[0 + c] * (Fi[0][c] - Fi[2][c]) + gF[2 + c] * (Fi[1][c] - Fi[0][c]) +
                       gF[4 + c] * (Fi[2][c] - Fi[1][c]));
     const float a = P.negA * gF[0 + c], b = P.negA * gF[2 + c], d = P.negA * gF[4 + c];
     gFi[0][c] = a - b;
@@ -297,12 +309,15 @@ rollout_bwd_k(const float* __restrict__ pvs, const float* __restrict__ dpos_roll
         else if (CELL == CELL_BOUNCE) bounce_sub(P, p, v, &fl[s]);
         else grav_sub(P, p, v);
       }
+      float s0 = 0.f, s1 = 0.f;   // this step's parameter adjoints
 #pragma unroll
       for (int s = 4; s >= 0; --s) {
-        if (CELL == CELL_SPRING) spring_sub_bwd(P, ps[s], vs[s], gp, gv, g0, g1);
+        if (CELL == CELL_SPRING) spring_sub_bwd(P, ps[s], vs[s], gp, gv, s0, s1);
         else if (CELL == CELL_BOUNCE) bounce_sub_bwd(P, fl[s], gp, gv);
-        else grav_sub_bwd(P, ps[s], gp, gv, g0);
+        else grav_sub_bwd(P, ps[s], gp, gv, s0);
       }
+      g0 += (double)s0;
+      g1 += (double)s1;
     }
     if (dpvs)
       for (int d = 0; d < D; ++d) {

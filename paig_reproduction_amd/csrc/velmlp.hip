@@ -13,6 +13,7 @@
 namespace {
 
 constexpr int HID = 100, OUT = 2, RB = 8, MAXIN = 16;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 // X[r][2t+j] = pos[b][t][2k+j], r = k*B + b (the chunk/cat of blocks.py:43-45)
 __device__ __forceinline__ float packed_in(const float* pos, int B, int Te, int K, int r, int col) {
@@ -27,8 +28,13 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
              float* __restrict__ h1, float* __restrict__ h2, float* __restrict__ vel) {
   __shared__ float Xs[RB][MAXIN];
   __shared__ float H1[RB][HID + 1], H2[RB][HID + 1];
+  __shared__ __attribute__((aligned(16))) float W2s[HID * HID];   // staged once, coalesced
   const int rows = K * B, r0 = blockIdx.x * RB, tid = threadIdx.x;
   const int nr = rows - r0 < RB ? rows - r0 : RB;
+  // all of W2 in flight at once (20 float4 per thread) instead of one dependent
+  // row walk per thread
+  for (int e = tid; e < HID * HID / 4; e += blockDim.x)
+    reinterpret_cast<f32x4v*>(W2s)[e] = reinterpret_cast<const f32x4v*>(W2)[e];
   for (int e = tid; e < nr * IN; e += blockDim.x) {
     const int r = e / IN, c = e % IN;
     const float v = packed_in(pos, B, Te, K, r0 + r, c);
@@ -52,7 +58,7 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
   if (tid < HID) {
     float a[RB];
     for (int r = 0; r < RB; ++r) a[r] = b2[tid];
-    const float* wr = W2 + tid * HID;
+    const float* wr = W2s + tid * HID;
     for (int u = 0; u < HID; ++u) {
       const float w = wr[u];
 #pragma unroll
