@@ -9,16 +9,17 @@
 // residual of lo are below fp32 accumulation noise for f16 pieces).  Per K
 // element a 16x16x32 MFMA costs 1/16 of the f32-input v_mfma_f32_16x16x4_f32,
 // so the three-term product does fp32-accurate convolutions at ~5x the f32
-// matrix rate; these layers (3..32 channels) then run at the HBM/LDS
+// matrix rate; these layers (3..128 channels) then run at the HBM/LDS
 // roofline instead of the MFMA one.  Precision modes (PM):
 //   0  f16 hi/lo   (22 significant bits: forward activations and weights,
-//                  whose range |v| < 65504 this mode requires)
-//   1  bf16 hi/lo  (16 significant bits, fp32 range: dgrad and wgrad, whose
-//                  gradients have no useful range bound)
+//                  whose range |v| < 65504 this mode requires; dgrad too,
+//                  each tile's gradients scaled by a power of two into that
+//                  range and the result scaled back exactly)
+//   1  bf16 hi/lo  (16 significant bits, fp32 range: wgrad, whose pixel sums
+//                  span many tiles, so no per-tile scale applies)
 //   2  bf16 hi only (one MFMA: the bf16 configuration, BASELINE config #2)
 // Measured against the reference's golden vectors (tests/golden): outputs
-// within 1e-6 and gradients within fp32 noise with PM 0 forward + PM 1
-// backward.
+// within 1e-6 and gradients within fp32 noise.
 //
 // forward / dgrad  D[pixel][co] = im2col(X)[pixel][k] * Wt[k][co], with
 //   k = (tap, ci) in 8-channel chunks: the block stages its input tile as an
@@ -173,16 +174,66 @@ struct UpStage {
 };
 
 // ============================================================ forward / dgrad
-template <int CIN, int COUT, int H, int W, int KS, int PM>
+// LDS available to one block (gfx950: 160 KB per CU)
+constexpr int LDS_MAX = 160 * 1024;
+
+// bytes of LDS a forward block needs for a tile of <= tpxm pixels and ntb
+// 16-channel output tiles (weights of that COUT slice + the operand images +
+// the fused-upsample window)
+constexpr int sfwd_lds(int CIN, int H, int W, int KS, bool UPS, int PM, int tpxm, int ntb) {
+  const int CC = rup(CIN, 8) / 8, PS = CC % 2 == 0 ? CC + 1 : CC;
+  const int NS = ceil_div(KS * KS * CC, 4);
+  const int FPT = H * W <= tpxm ? tpxm / (H * W) : 1;
+  const int RT = H * W <= tpxm ? H : rows_fit(H, W, tpxm);
+  const int TWPX = W + 2 * (KS / 2);
+  const int RP = W == 8 ? to_mod16(TWPX * PS, 8) : TWPX * PS;
+  const int img = FPT * (RT + KS - 1) * RP * 8, wimg = NS * ntb * 64 * 8;
+  const int ups = UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0;
+  return (img + wimg) * 2 * (PM == 2 ? 1 : 2) + ups;
+}
+// VGPRs per lane of a forward block (fitted to the compiler's allocation):
+// accumulators, A fragments, B fragments, k-step offsets, and the staging
+// registers of the next tile (prefetched); must stay within the 256 of
+// 2 waves per SIMD
+constexpr int sfwd_vgprs(int CIN, int H, int W, int KS, bool UPS, int tpxm, int ntb) {
+  const int CC = rup(CIN, 8) / 8, NS = ceil_div(KS * KS * CC, 4);
+  const int FPT = H * W <= tpxm ? tpxm / (H * W) : 1;
+  const int RT = H * W <= tpxm ? H : rows_fit(H, W, tpxm);
+  const int MW = ceil_div(ceil_div(FPT * RT * W, 16), 4);
+  const int NL = UPS ? 1 : ceil_div(FPT * (RT + KS - 1) * (W % 2 == 0 ? W / 2 : W) * CC, 256);
+  return MW * ntb * 4 + NL * 30 + ntb * 8 + NS + MW * 8 + 40;
+}
+// forward tile geometry, (pixels per tile) * 256 + (COUT slices): the whole
+// COUT in one block on the tuned tile (256 pixels; 128 at W = 8) where that
+// fits the LDS and the registers; wide layers (UNet, 48..128 channels) split
+// COUT over blocks (grid.y; each slice's weights resident) and/or take
+// smaller pixel tiles.  At most 4 output tiles per block.
+constexpr int sfwd_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM) {
+  const int base = W == 8 ? 128 : 256, NT = ceil_div(COUT, 16);
+  for (int pass = 0; pass < 2; ++pass)
+    for (int nb = 1; nb <= NT; ++nb) {
+      if (NT % nb != 0 || NT / nb > 4) continue;
+      for (int tp = base; tp >= (pass == 0 ? base / 2 : 64); tp /= 2)
+        if (sfwd_lds(CIN, H, W, KS, UPS, PM, tp, NT / nb) <= LDS_MAX &&
+            sfwd_vgprs(CIN, H, W, KS, UPS, tp, NT / nb) <= 264)
+          return tp * 256 + nb;
+    }
+  return 0;
+}
+
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
 struct SFwdCfg {
   static constexpr int KK = KS * KS, PADL = KS / 2;
   static constexpr int NIMG = PM == 2 ? 1 : 2;               // hi (+ lo) images
   static constexpr int CINP = rup(CIN, 8), CC = CINP / 8;    // 8-channel chunks per pixel
   static constexpr int KC = KK * CC, NS = ceil_div(KC, 4);   // k-chunks, MFMA k-steps (4 chunks each)
-  static constexpr int NT = ceil_div(COUT, 16);
+  static constexpr int GEO = sfwd_pick(CIN, COUT, H, W, KS, UPS, PM);
+  static_assert(GEO > 0, "no forward tile geometry fits the LDS");
+  static constexpr int NB = GEO % 256;                       // COUT slices (grid.y)
+  static constexpr int NT = ceil_div(COUT, 16) / NB;         // 16-channel output tiles per block
   // tile: whole rows (RT divides H) of one frame, or FPT whole frames; at
-  // most TPXM pixels (256; 128 at W = 8, whose tuned tile is 2 frames)
-  static constexpr int TPXM = W == 8 ? 128 : 256;
+  // most TPXM pixels
+  static constexpr int TPXM = GEO / 256;
   static constexpr int FPT = H * W <= TPXM ? TPXM / (H * W) : 1;
   static constexpr int RT = H * W <= TPXM ? H : rows_fit(H, W, TPXM);
   static constexpr int TPXV = FPT * RT * W;                  // valid pixels per tile
@@ -212,7 +263,7 @@ template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 __global__ void __launch_bounds__(256, 2)
 conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
                  int flags, int ntiles) {
-  using C = SFwdCfg<CIN, COUT, H, W, KS, PM>;
+  using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
   constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP;
   constexpr int NI = C::NI, NL = C::NL, PADL = C::PADL, W2 = C::W2;
@@ -225,11 +276,12 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   short* Wl = Wh + (C::NIMG == 2 ? C::WIMG : 0);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
   constexpr int NRB = H / RT;
+  const int co0 = blockIdx.y * NT * 16;   // this block's COUT slice
 
   // ---- weights in fragment order: [s][nt][lane][8]; dgrad: transposed + flipped
   for (int idx = tid; idx < NS * NT * 64; idx += 256) {
     const int ln = idx & 63, snt = idx >> 6, nt = snt % NT, s = snt / NT;
-    const int kc = 4 * s + (ln >> 4), co = nt * 16 + (ln & 15);
+    const int kc = 4 * s + (ln >> 4), co = co0 + nt * 16 + (ln & 15);
     s16x8 vh, vl;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -302,6 +354,10 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   };
   float2 pre[UPS ? 1 : NL][8];
   UP up;
+  // dgrad with f16 pieces (PM 0): per-tile scale (see commit)
+  constexpr bool SC = DG && PM == 0;
+  __shared__ float smax[4];
+  float tsc = 1.f, tinv = 1.f;
   auto issue = [&](int t) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
     if constexpr (UPS) {
@@ -347,6 +403,31 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
         put_px(i, v);
       }
     } else {
+      if constexpr (SC) {
+        // dgrad in f16 pieces: the tile's gradients scaled by one power of
+        // two (max -> [2^14, 2^15)) so they sit in f16's range; the epilogue
+        // undoes it exactly
+        float m = 0.f;
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) m = fmaxf(m, fmaxf(fabsf(pre[l][c].x), fabsf(pre[l][c].y)));
+        m = wave_max(m);
+        if (lane == 0) smax[wv] = m;
+        __syncthreads();
+        m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+        int e = 15 - (m > 0.f ? (int)((__builtin_bit_cast(unsigned, m) >> 23) & 255) - 126 : 0);
+        e = e < -100 ? -100 : (e > 100 ? 100 : e);
+        tsc = __builtin_amdgcn_ldexpf(1.f, e);
+        tinv = __builtin_amdgcn_ldexpf(1.f, -e);
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            pre[l][c].x *= tsc;
+            pre[l][c].y *= tsc;
+          }
+      }
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         const int i = tid + l * 256;
@@ -390,7 +471,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     // ---- epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for co = nt*16 + (lane&15)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int co = nt * 16 + (lane & 15);
+      const int co = co0 + nt * 16 + (lane & 15);
       if (co >= COUT) continue;
       const float bv = bias ? bias[co] : 0.f;
 #pragma unroll
@@ -404,6 +485,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
           if (f >= F) continue;
           float* op = out.frame(f) + co * HW + (long long)y * W + x;
           f32x4 v = acc[mt][nt];
+          if constexpr (SC) v *= tinv;
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += bv;
           if (flags & 1) {
@@ -426,7 +508,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
             const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
             if (f >= F) continue;
             float* op = out.frame(f) + co * HW + (long long)y * W + x;
-            float v = acc[mt][nt][r] + bv;
+            float v = (SC ? acc[mt][nt][r] * tinv : acc[mt][nt][r]) + bv;
             if (flags & 1) v = v < 0.f ? 0.f : v;
             if (flags & 4) v += *op;
             if (flags & 2) v = aux.frame(f)[co * HW + (long long)y * W + x] > 0.f ? v : 0.f;
@@ -439,16 +521,60 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 }
 
 // ===================================================================== wgrad
-template <int CIN, int COUT, int H, int W, int KS, int PM>
+// waves splitting the N-tiles: as few as keep <= 40 accumulators per lane
+constexpr int swg_wn(int MT, int NT) { return MT * NT * 4 <= 40 ? 1 : (MT * ceil_div(NT, 2) * 4 <= 40 ? 2 : 4); }
+// LDS of a wgrad block staging CINB input and COUTB output-gradient channels
+constexpr int swg_lds(int CINB, int COUTB, int H, int W, int KS, bool UPS, int PM) {
+  const int CQ = rup(CINB, 4) / 4, FPT = H * W <= 256 ? 256 / (H * W) : 1;
+  const int RT = H * W <= 256 ? H : rows_fit(H, W, 256);
+  const int TWPX = W + 2 * (KS / 2 > 0 ? 2 : 0);
+  const int XPL = rup(FPT * (RT + KS - 1) * TWPX * 4 + 80, 128);
+  const int stg = (CQ * XPL + COUTB * 264) * 2 * (PM == 2 ? 1 : 2) +
+                  (UPS ? FPT * CINB * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0);
+  const int MT = ceil_div(COUTB, 16), NT = ceil_div(KS * KS * CQ, 4);
+  const int red = 4 * MT * ceil_div(NT, swg_wn(MT, NT)) * 4 * 64 * 4;
+  return stg > red ? stg : red;
+}
+// channel slices of a wgrad block, CINB * 4096 + COUTB: the block reduces the
+// gradient of CINB input x COUTB output channels (grid.y, grid.z) over its
+// pixel tiles.  The whole layer where its accumulators (4 waves splitting N)
+// and staging fit; wide layers take the slice with the most work per block.
+constexpr int swg_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM) {
+  const int ci[] = {CIN, 128, 64, 32, 16, 8}, oc[] = {COUT, 128, 64, 32, 16};
+  int best = 0, bw = 0, bs = 0;
+  for (int cb : ci) {
+    if (cb > CIN || CIN % cb != 0 || (cb != CIN && cb % 4 != 0)) continue;
+    for (int ob : oc) {
+      if (ob > COUT || COUT % ob != 0) continue;
+      const int MT = ceil_div(ob, 16), NT = ceil_div(KS * KS * ceil_div(cb, 4), 4);
+      if (MT * ceil_div(NT, 4) * 4 > 40 || swg_lds(cb, ob, H, W, KS, UPS, PM) > LDS_MAX) continue;
+      // ties: the fewest staged channels; fused-upsample inputs: the fewest
+      // output channels (the dY staging registers are what spills there)
+      const int sc = UPS ? ob : cb + ob;
+      if (cb * ob > bw || (cb * ob == bw && sc < bs)) {
+        bw = cb * ob;
+        bs = sc;
+        best = cb * 4096 + ob;
+      }
+    }
+  }
+  return best;
+}
+
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
 struct SWgCfg {
   static constexpr int KK = KS * KS, PADL = KS / 2;
   static constexpr int NIMG = PM == 2 ? 1 : 2;
-  static constexpr int CINQ = rup(CIN, 4), CQ = CINQ / 4;     // 4-channel quads per pixel
+  static constexpr int SLC = swg_pick(CIN, COUT, H, W, KS, UPS, PM);
+  static_assert(SLC > 0, "no wgrad channel slice fits");
+  static constexpr int CINB = SLC / 4096, COUTB = SLC % 4096;  // channels per block
+  static constexpr int NSI = CIN / CINB, NSO = COUT / COUTB;   // slices (grid.y, grid.z)
+  static constexpr int CINQ = rup(CINB, 4), CQ = CINQ / 4;    // 4-channel quads per pixel
   static constexpr int NQ = KK * CQ;                          // (tap, quad) column quads
   static constexpr int NT = ceil_div(NQ, 4);                  // N-tiles of 16 columns
-  static constexpr int NCOL = CIN * KK;
-  static constexpr int MT = ceil_div(COUT, 16), COP = MT * 16;
-  static constexpr int WN = (MT * NT * 4 <= 40) ? 1 : ((MT * ceil_div(NT, 2) * 4 <= 40) ? 2 : 4);
+  static constexpr int NCOL = CIN * KK;                       // slab row: the whole layer
+  static constexpr int MT = ceil_div(COUTB, 16), COP = MT * 16;
+  static constexpr int WN = swg_wn(MT, NT);
   static constexpr int WP = 4 / WN, NTW = ceil_div(NT, WN);
   // tile: whole rows (RT divides H) of one frame or FPT whole frames, <= 256
   // pixels; k-blocks of 32 tile pixels (the last one zero-padded in dY)
@@ -472,7 +598,7 @@ struct SWgCfg {
   static constexpr int XPL = rup(FPT * ROWS * TWPX * 4 + 80, 128);   // room for the <= 80-element offset
   static constexpr int XIMG = CQ * XPL;
   static constexpr int DP = TPX + 8;                          // dY row pitch: 16 rows -> 16 bank groups
-  static constexpr int DIMG = COUT * DP;   // rows co >= COUT of an A fragment re-read rows co % COUT
+  static constexpr int DIMG = COUTB * DP;   // rows co >= COUTB of an A fragment re-read rows co % COUTB
   static constexpr int STG = (XIMG + DIMG) * 2 * NIMG;
   static constexpr int RED = 4 * MT * NTW * 4 * 64 * 4;
   static constexpr int LDS = STG > RED ? STG : RED;
@@ -481,18 +607,22 @@ struct SWgCfg {
   static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = (NIX + 255) / 256;
   static constexpr int DU = W % 4 == 0 ? 4 : (W % 2 == 0 ? 2 : 1);   // dY units: DU pixels x 1 channel
   static constexpr int NPU = TPXV / DU;                       // dY units per channel
-  static constexpr int NID = COUT * NPU, NLD = (NID + 255) / 256;
+  static constexpr int NID = COUTB * NPU, NLD = (NID + 255) / 256;
   static constexpr int SLAB = COUT * NCOL + COUT;
   // waves per SIMD the registers must allow: 3 where three blocks fit the LDS
-  static constexpr int MINW = 3 * LDS <= 160 * 1024 ? 3 : 2;
+  // (narrow whole-layer blocks only: the 32-wide / channel-sliced ones need
+  // more than the 168 registers of 3 waves)
+  static constexpr int MINW =
+      3 * LDS <= 160 * 1024 && NSI * NSO == 1 && (CIN <= 24 || (UPS && COUT <= 16)) && !(MT == 2 && FPT > 1) ? 3 : 2;
   static_assert(H % RT == 0, "RT divides H");
   static_assert(TPXV % DU == 0, "dY units");
 };
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
-__global__ void __launch_bounds__(256, (SWgCfg<CIN, COUT, H, W, KS, PM>::MINW))
-conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntiles) {
-  using C = SWgCfg<CIN, COUT, H, W, KS, PM>;
+__global__ void __launch_bounds__(256, (SWgCfg<CIN, COUT, H, W, KS, UPS, PM>::MINW))
+conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int ntiles) {
+  using C = SWgCfg<CIN, COUT, H, W, KS, UPS, PM>;
+  constexpr int CINB = C::CINB, COUTB = C::COUTB;
   constexpr int KK = C::KK, CQ = C::CQ, NQ = C::NQ, NT = C::NT, NCOL = C::NCOL, MT = C::MT, COP = C::COP;
   constexpr int WN = C::WN, WP = C::WP, NTW = C::NTW, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS;
   constexpr int TWPX = C::TWPX, XPL = C::XPL, DP = C::DP, KB = C::KB, PADL = C::PADL, OFFX = C::OFFX, W2 = C::W2;
@@ -500,6 +630,11 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   constexpr int NIX = C::NIX, NLX = C::NLX, NID = C::NID, NLD = C::NLD;
   constexpr long long PLANE = UPS ? (long long)(H / 2) * (W / 2) : (long long)H * W;
   constexpr long long HW = (long long)H * W;
+  // this block's channel slice: input channels ci0.., output channels co0..
+  const int ci0 = blockIdx.y * CINB, co0 = blockIdx.z * COUTB;
+  FView x = x_, dy = dy_;
+  x.p += ci0 * PLANE;
+  dy.p += co0 * HW;
   extern __shared__ __attribute__((aligned(16))) short lds16[];
   short* Xh = lds16;
   short* Xl = Xh + (C::NIMG == 2 ? C::XIMG : 0);
@@ -523,7 +658,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   }
   // padded pixels of the last k-block: dY = 0 (never staged)
   if (KB * 32 > TPXV) {
-    for (int i = tid; i < COUT * (KB * 32 - TPXV); i += 256) {
+    for (int i = tid; i < COUTB * (KB * 32 - TPXV); i += 256) {
       const int co = i / (KB * 32 - TPXV), pt = TPXV + i % (KB * 32 - TPXV);
       Dh[co * DP + pt] = 0;
       if (PM != 2) Dl[co * DP + pt] = 0;
@@ -558,7 +693,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
   // X units (1 pixel x 4 channels, pixel fastest) are prefetched a tile
   // ahead where their registers are cheap, else loaded synchronously; fused-
   // upsample inputs go through UpStage (half-resolution window, prefetched).
-  using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
+  using UP = UpStage<UPS ? CINB : 1, H, W, FPT, RT>;
   float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::XIMG + C::DIMG));
   constexpr bool XPIPE = !UPS && NLX * 8 + NLD * 4 <= (C::MINW == 3 ? 24 : 48);
   auto load_x = [&](int t, int i, float2* v) {   // branch-free, 32-bit offsets (see the forward kernel)
@@ -570,9 +705,9 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
     const int off = ok ? fi * (int)x.fs + cq * 4 * (int)PLANE + gy * W + xp : 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float* q = fb + off + (cq * 4 + c < CIN ? c : 0) * (int)PLANE;
+      const float* q = fb + off + (cq * 4 + c < CINB ? c : 0) * (int)PLANE;
       const float2 u = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
-      v[c] = (ok && cq * 4 + c < CIN) ? u : make_float2(0.f, 0.f);
+      v[c] = (ok && cq * 4 + c < CINB) ? u : make_float2(0.f, 0.f);
     }
   };
   auto put_x = [&](int i, const float2* v) {
@@ -644,7 +779,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
         float2 v[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          v[c] = (ok && cq * 4 + c < CIN)
+          v[c] = (ok && cq * 4 + c < CINB)
                      ? make_float2(UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp),
                                    UPX == 2 ? UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp + 1) : 0.f)
                      : make_float2(0.f, 0.f);
@@ -710,7 +845,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int co = m * 16 + (lane & 15);
-        const int o = (co < COUT ? co : co % COUT) * DP + p0 + 8 * g;   // padded rows: finite, discarded
+        const int o = (co < COUTB ? co : co % COUTB) * DP + p0 + 8 * g;   // padded rows: finite, discarded
         ah[m] = *reinterpret_cast<const s16x8*>(Dh + o);
         al[m] = PM != 2 ? *reinterpret_cast<const s16x8*>(Dl + o) : ah[m];
       }
@@ -778,7 +913,7 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
           float v = 0.f;
           for (int p = 0; p < WP; ++p) v += R[((((p * WN + wn) * MT + m) * NTW + j) * 4 + r) * 64 + lane];
           const int co = m * 16 + (lane >> 4) * 4 + r;
-          if (co < COUT && cq < NQ && ci < CIN) s[co * NCOL + ci * KK + tap] = v;
+          if (co < COUTB && cq < NQ && ci < CINB) s[(co0 + co) * NCOL + (ci0 + ci) * KK + tap] = v;
         }
       }
   }
@@ -790,17 +925,17 @@ conv_wgrad_split_k(FView x, FView dy, float* __restrict__ slab, int F, int ntile
 #pragma unroll
   for (int l = 0; l < NLD; ++l) Rb[l * 256 + tid] = bacc[l];
   __syncthreads();
-  if (tid < COUT) {
+  if (tid < COUTB && blockIdx.y == 0) {   // bias: by the first input-channel slice
     float v = 0.f;
     for (int i = tid * NPU; i < (tid + 1) * NPU; ++i) v += Rb[(i / 256) * 256 + i % 256];
-    s[COUT * NCOL + tid] = v;
+    s[COUT * NCOL + co0 + tid] = v;
   }
 }
 
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
                        hipStream_t st) {
-  using C = SFwdCfg<CIN, COUT, H, W, KS, PM>;
+  using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int LDS = C::LDS + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   auto k = conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM>;
@@ -809,16 +944,18 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
     if (LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     resident = persistent_grid((const void*)k, LDS);
   }
-  const int nb = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL(k, dim3(nb), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles);
+  int nb = resident / C::NB;   // persistent blocks per COUT slice
+  if (nb > ntiles) nb = ntiles;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
 static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st) {
-  using C = SWgCfg<CIN, COUT, H, W, KS, PM>;
-  constexpr int STG = C::STG + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
+  using C = SWgCfg<CIN, COUT, H, W, KS, UPS, PM>;
+  constexpr int STG = C::STG + (UPS ? UpStage<C::CINB, H, W, C::FPT, C::RT>::SL * 4 : 0);
   constexpr int LDS = STG > C::RED ? STG : C::RED;
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   auto k = conv_wgrad_split_k<CIN, COUT, H, W, KS, UPS, PM>;
@@ -830,10 +967,10 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
   // one wave of co-resident persistent blocks: more would leave a partial
   // second wave running at a fraction of the chip (and add slab rows)
   int nb = ntiles < nblk_max ? ntiles : nblk_max;
-  if (nb > resident) nb = resident;
+  if (nb > resident / (C::NSI * C::NSO)) nb = resident / (C::NSI * C::NSO);
   if (nb < 1) nb = 1;
   *nblk_out = nb;
-  hipLaunchKernelGGL(k, dim3(nb), dim3(256), LDS, st, x, dy, slab, F, ntiles);
+  hipLaunchKernelGGL(k, dim3(nb, C::NSI, C::NSO), dim3(256), LDS, st, x, dy, slab, F, ntiles);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -845,25 +982,37 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
   X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1) X(16, 8, 16, 3) X(8, 24, 32, 3)       \
   X(2, 8, 32, 1) X(32, 16, 8, 3) X(16, 32, 16, 3)                                                         \
-  PAIG_SPLIT_FWD_3BP(X)
+  PAIG_SPLIT_FWD_3BP(X) PAIG_SPLIT_FWD_UNET(X)
 #define PAIG_SPLIT_WG(X)                                                                                  \
   X(3, 8, 32, 3) X(8, 8, 32, 3) X(8, 16, 16, 3) X(16, 16, 16, 3) X(16, 32, 8, 3) X(32, 32, 8, 3)         \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(24, 8, 32, 3) X(8, 2, 32, 1)                                        \
-  PAIG_SPLIT_WG_3BP(X)
-#define PAIG_SPLIT_UP(X) X(32, 16, 16, 3) X(16, 16, 32, 3) X(32, 16, 18, 3) X(16, 16, 36, 3)
+  PAIG_SPLIT_WG_3BP(X) PAIG_SPLIT_WG_UNET(X)
+#define PAIG_SPLIT_UP(X)                                                                                  \
+  X(32, 16, 16, 3) X(16, 16, 32, 3) X(32, 16, 18, 3) X(16, 16, 36, 3) X(128, 32, 16, 3) X(64, 32, 32, 3) \
+  X(32, 16, 64, 3)
 // 3bp_color (ShallowUNet hidden 8 on 36 x 36 frames, K = 3 objects): levels
 // 36 / 18 / 9; tiles of 6 rows (36), 9 rows (18) or 3 frames (9 x 9)
 #define PAIG_SPLIT_FWD_3BP(X)                                                                             \
   X(3, 8, 36, 3) X(8, 8, 36, 3) X(8, 16, 18, 3) X(16, 16, 18, 3) X(16, 32, 9, 3) X(32, 32, 9, 3)         \
   X(32, 16, 18, 3) X(16, 16, 36, 3) X(24, 8, 36, 3) X(8, 3, 36, 1) X(16, 8, 18, 3) X(32, 16, 9, 3)       \
   X(16, 32, 18, 3) X(8, 24, 36, 3) X(3, 8, 36, 1)
+// mnist_spring_color (UNet hidden 16 on 64 x 64 frames): levels 64 / 32 /
+// 16 / 8, 3..128 channels; forward then dgrad-only shapes
+#define PAIG_SPLIT_FWD_UNET(X)                                                                            \
+  X(3, 16, 64, 3) X(16, 16, 64, 3) X(16, 32, 32, 3) X(32, 32, 32, 3) X(32, 64, 16, 3) X(64, 64, 16, 3)   \
+  X(64, 128, 8, 3) X(128, 128, 8, 3) X(96, 64, 16, 3) X(64, 32, 32, 3) X(48, 16, 64, 3) X(16, 2, 64, 1)   \
+  X(32, 16, 32, 3) X(64, 32, 16, 3) X(128, 64, 8, 3) X(32, 128, 16, 3) X(64, 96, 16, 3) X(32, 64, 32, 3)  \
+  X(16, 32, 64, 3) X(16, 48, 64, 3) X(2, 16, 64, 1)
+#define PAIG_SPLIT_WG_UNET(X)                                                                             \
+  X(3, 16, 64, 3) X(16, 16, 64, 3) X(16, 32, 32, 3) X(32, 32, 32, 3) X(32, 64, 16, 3) X(64, 64, 16, 3)   \
+  X(64, 128, 8, 3) X(128, 128, 8, 3) X(96, 64, 16, 3) X(64, 32, 32, 3) X(48, 16, 64, 3) X(16, 2, 64, 1)
 #define PAIG_SPLIT_WG_3BP(X)                                                                              \
   X(3, 8, 36, 3) X(8, 8, 36, 3) X(8, 16, 18, 3) X(16, 16, 18, 3) X(16, 32, 9, 3) X(32, 32, 9, 3)         \
   X(32, 16, 18, 3) X(16, 16, 36, 3) X(24, 8, 36, 3) X(8, 3, 36, 1)
 
 }  // namespace
 
-// flags & 128: split precision (f16 x3 forward, bf16 x3 dgrad), flags & 256:
+// flags & 128: split precision (f16 x3 forward and scaled dgrad), flags & 256:
 // bf16 hi only.  Returns 1 if the shape is instantiated here (rc in *rc).
 int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
                         int H, int W, int ks, int flags, hipStream_t st, int* rc) {
@@ -889,7 +1038,7 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
       *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 2>(in, out, aux, w, b, F, fl, st)              \
                : sfwd_launch<CI, CO, HH, HH, K, false, false, 2>(in, out, aux, w, b, F, fl, st);            \
     else                                                                                                    \
-      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 1>(in, out, aux, w, b, F, fl, st)              \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 0>(in, out, aux, w, b, F, fl, st)              \
                : sfwd_launch<CI, CO, HH, HH, K, false, false, 0>(in, out, aux, w, b, F, fl, st);            \
     return 1;                                                                                               \
   }

