@@ -545,12 +545,11 @@ constexpr int swg_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM
   for (int cb : ci) {
     if (cb > CIN || CIN % cb != 0 || (cb != CIN && cb % 4 != 0)) continue;
     for (int ob : oc) {
-      if (ob > COUT || COUT % ob != 0) continue;
+      if (ob > COUT || COUT % ob != 0 || (UPS && ob > 16)) continue;   // UPS: dY staging registers
       const int MT = ceil_div(ob, 16), NT = ceil_div(KS * KS * ceil_div(cb, 4), 4);
       if (MT * ceil_div(NT, 4) * 4 > 40 || swg_lds(cb, ob, H, W, KS, UPS, PM) > LDS_MAX) continue;
-      // ties: the fewest staged channels; fused-upsample inputs: the fewest
-      // output channels (the dY staging registers are what spills there)
-      const int sc = UPS ? ob : cb + ob;
+      // ties: the fewest staged channels
+      const int sc = cb + ob;
       if (cb * ob > bw || (cb * ob == bw && sc < bs)) {
         bw = cb * ob;
         bs = sc;
@@ -989,7 +988,7 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
   PAIG_SPLIT_WG_3BP(X) PAIG_SPLIT_WG_UNET(X)
 #define PAIG_SPLIT_UP(X)                                                                                  \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(32, 16, 18, 3) X(16, 16, 36, 3) X(128, 32, 16, 3) X(64, 32, 32, 3) \
-  X(32, 16, 64, 3)
+  X(32, 32, 64, 3)
 // 3bp_color (ShallowUNet hidden 8 on 36 x 36 frames, K = 3 objects): levels
 // 36 / 18 / 9; tiles of 6 rows (36), 9 rows (18) or 3 frames (9 x 9)
 #define PAIG_SPLIT_FWD_3BP(X)                                                                             \
@@ -1002,7 +1001,7 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
   X(3, 16, 64, 3) X(16, 16, 64, 3) X(16, 32, 32, 3) X(32, 32, 32, 3) X(32, 64, 16, 3) X(64, 64, 16, 3)   \
   X(64, 128, 8, 3) X(128, 128, 8, 3) X(96, 64, 16, 3) X(64, 32, 32, 3) X(48, 16, 64, 3) X(16, 2, 64, 1)   \
   X(32, 16, 32, 3) X(64, 32, 16, 3) X(128, 64, 8, 3) X(32, 128, 16, 3) X(64, 96, 16, 3) X(32, 64, 32, 3)  \
-  X(16, 32, 64, 3) X(16, 48, 64, 3) X(2, 16, 64, 1)
+  X(32, 32, 64, 3) X(16, 48, 64, 3) X(2, 16, 64, 1)
 #define PAIG_SPLIT_WG_UNET(X)                                                                             \
   X(3, 16, 64, 3) X(16, 16, 64, 3) X(16, 32, 32, 3) X(32, 32, 32, 3) X(32, 64, 16, 3) X(64, 64, 16, 3)   \
   X(64, 128, 8, 3) X(128, 128, 8, 3) X(96, 64, 16, 3) X(64, 32, 32, 3) X(48, 16, 64, 3) X(16, 2, 64, 1)
