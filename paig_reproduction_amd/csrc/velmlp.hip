@@ -21,20 +21,36 @@ __device__ __forceinline__ float packed_in(const float* pos, int B, int Te, int 
   return pos[((long long)b * Te + t) * 2 * K + 2 * k + j];
 }
 
+// forward rows per block: 2 (100 blocks for the 200 rows of spring B=100),
+// so the per-thread hidden-layer loop is short; W2 is staged per block into
+// LDS with an odd row pitch (lanes walk different rows: conflict-free)
+constexpr int FRB = 2, W2P = HID + 1;
+static_assert(FRB == 2, "the hidden-layer loop below is written for 2 rows");
+
 __global__ void __launch_bounds__(128)
 velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const float* __restrict__ W0,
              const float* __restrict__ b0, const float* __restrict__ W2, const float* __restrict__ b2,
              const float* __restrict__ W4, const float* __restrict__ b4, float* __restrict__ X,
              float* __restrict__ h1, float* __restrict__ h2, float* __restrict__ vel) {
-  __shared__ float Xs[RB][MAXIN];
-  __shared__ float H1[RB][HID + 1], H2[RB][HID + 1];
-  __shared__ __attribute__((aligned(16))) float W2s[HID * HID];   // staged once, coalesced
-  const int rows = K * B, r0 = blockIdx.x * RB, tid = threadIdx.x;
-  const int nr = rows - r0 < RB ? rows - r0 : RB;
-  // all of W2 in flight at once (20 float4 per thread) instead of one dependent
-  // row walk per thread
-  for (int e = tid; e < HID * HID / 4; e += blockDim.x)
-    reinterpret_cast<f32x4v*>(W2s)[e] = reinterpret_cast<const f32x4v*>(W2)[e];
+  __shared__ float Xs[FRB][MAXIN];
+  __shared__ float H1[HID][FRB], H2[FRB][HID + 1];   // H1 [u][r]: one broadcast read per u
+  __shared__ float W2s[HID * W2P];
+  const int rows = K * B, r0 = blockIdx.x * FRB, tid = threadIdx.x;
+  const int nr = rows - r0 < FRB ? rows - r0 : FRB;
+  if (((uintptr_t)W2 & 15) == 0) {   // all of W2 in flight at once: 20 float4 per thread
+#pragma unroll 5
+    for (int e = tid; e < HID * HID / 4; e += 128) {
+      const f32x4v v = reinterpret_cast<const f32x4v*>(W2)[e];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = 4 * e + j;
+        W2s[(q / HID) * W2P + q % HID] = v[j];
+      }
+    }
+  } else {
+#pragma unroll 8
+    for (int q = tid; q < HID * HID; q += 128) W2s[(q / HID) * W2P + q % HID] = W2[q];
+  }
   for (int e = tid; e < nr * IN; e += blockDim.x) {
     const int r = e / IN, c = e % IN;
     const float v = packed_in(pos, B, Te, K, r0 + r, c);
@@ -45,24 +61,30 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
   if (tid < HID) {
     float w[MAXIN];
     for (int i = 0; i < IN; ++i) w[i] = W0[tid * IN + i];
-    for (int r = 0; r < nr; ++r) {
-      float a = b0[tid];
-      for (int i = 0; i < IN; ++i) a = fmaf(Xs[r][i], w[i], a);
-      a = tanhf(a);
-      H1[r][tid] = a;
-      h1[(long long)(r0 + r) * HID + tid] = a;
+#pragma unroll
+    for (int r = 0; r < FRB; ++r) {
+      float a = 0.f;
+      if (r < nr) {
+        a = b0[tid];
+        for (int i = 0; i < IN; ++i) a = fmaf(Xs[r][i], w[i], a);
+        a = tanhf(a);
+        h1[(long long)(r0 + r) * HID + tid] = a;
+      }
+      H1[tid][r] = a;   // ragged last block: zeros
     }
-    for (int r = nr; r < RB; ++r) H1[r][tid] = 0.f;   // ragged last block
   }
   __syncthreads();
   if (tid < HID) {
-    float a[RB];
-    for (int r = 0; r < RB; ++r) a[r] = b2[tid];
-    const float* wr = W2s + tid * HID;
+    float a[FRB];
+#pragma unroll
+    for (int r = 0; r < FRB; ++r) a[r] = b2[tid];
+    const float* wr = W2s + tid * W2P;
+#pragma unroll 10
     for (int u = 0; u < HID; ++u) {
       const float w = wr[u];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) a[r] = fmaf(H1[r][u], w, a[r]);
+      const float2 hv = *reinterpret_cast<const float2*>(&H1[u][0]);
+      a[0] = fmaf(hv.x, w, a[0]);
+      a[1] = fmaf(hv.y, w, a[1]);
     }
     for (int r = 0; r < nr; ++r) {
       const float v = tanhf(a[r]);
@@ -185,7 +207,7 @@ int paig_velmlp_fwd(const float* pos, int B, int Te, int K, int S, const float* 
   const int IN = 2 * S, rows = K * B;
   if (rows <= 0) return 0;
   PAIG_REQUIRE(IN <= MAXIN && S <= Te, "velmlp: input_steps %d unsupported (max %d)", S, MAXIN / 2);
-  hipLaunchKernelGGL(velmlp_fwd_k, dim3(cdiv(rows, RB)), dim3(128), 0, (hipStream_t)stream, pos, B, Te, K, IN, W0, b0,
+  hipLaunchKernelGGL(velmlp_fwd_k, dim3(cdiv(rows, FRB)), dim3(128), 0, (hipStream_t)stream, pos, B, Te, K, IN, W0, b0,
                      W2, b2, W4, b4, X, h1, h2, vel);
   PAIG_CHECK_LAUNCH();
   return 0;
