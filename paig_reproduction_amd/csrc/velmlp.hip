@@ -111,6 +111,8 @@ velmlp_bwd_k(const float* __restrict__ dvel, const float* __restrict__ X, const 
              const float* __restrict__ W4, float* __restrict__ dX, float* __restrict__ slab, int rows, int IN) {
   __shared__ float Xs[RB][MAXIN], DV[RB][OUT];
   __shared__ float H1[RB][HID + 1], DZ2[RB][HID + 1], DZ1[RB][HID + 1];
+  __shared__ __attribute__((aligned(16))) float W2s[HID * HID];   // read in the dz1 loop
+  __shared__ float W0s[HID * MAXIN];                               // read in the dX loop
   const int r0 = blockIdx.x * RB, tid = threadIdx.x;
   const int nr = rows - r0 < RB ? rows - r0 : RB;
   const long long len = (long long)HID * IN + HID + HID * HID + HID + OUT * HID + OUT;
@@ -121,10 +123,23 @@ velmlp_bwd_k(const float* __restrict__ dvel, const float* __restrict__ X, const 
   float* sb2 = sW2 + HID * HID;
   float* sW4 = sb2 + HID;
   float* sb4 = sW4 + OUT * HID;
+  // weights staged with all loads in flight (a dependent global load per loop
+  // iteration is what a 100-long dot product would otherwise wait on)
+  if (((uintptr_t)W2 & 15) == 0) {
+#pragma unroll 10
+    for (int e = tid; e < HID * HID / 4; e += 256)
+      reinterpret_cast<f32x4v*>(W2s)[e] = reinterpret_cast<const f32x4v*>(W2)[e];
+  } else {
+#pragma unroll 8
+    for (int q = tid; q < HID * HID; q += 256) W2s[q] = W2[q];
+  }
+#pragma unroll 4
+  for (int q = tid; q < HID * IN; q += 256) W0s[q] = W0[q];
   for (int e = tid; e < RB * IN; e += blockDim.x) {
     const int r = e / IN, c = e % IN;
     Xs[r][c] = r < nr ? X[(long long)(r0 + r) * IN + c] : 0.f;
   }
+#pragma unroll 4
   for (int e = tid; e < RB * HID; e += blockDim.x) {
     const int r = e / HID, u = e % HID;
     H1[r][u] = r < nr ? h1[(long long)(r0 + r) * HID + u] : 0.f;
@@ -168,8 +183,9 @@ velmlp_bwd_k(const float* __restrict__ dvel, const float* __restrict__ X, const 
     // dz1[r][u = tid] = (sum_t dz2[r][t] W2[t][u]) * tanh'(h1)
     float d[RB];
     for (int r = 0; r < RB; ++r) d[r] = 0.f;
+#pragma unroll 4
     for (int t = 0; t < HID; ++t) {
-      const float w = W2[t * HID + tid];
+      const float w = W2s[t * HID + tid];
 #pragma unroll
       for (int r = 0; r < RB; ++r) d[r] = fmaf(DZ2[r][t], w, d[r]);
     }
@@ -192,7 +208,8 @@ velmlp_bwd_k(const float* __restrict__ dvel, const float* __restrict__ X, const 
   for (int e = tid; e < nr * IN; e += blockDim.x) {
     const int r = e / IN, i = e % IN;
     float a = 0.f;
-    for (int u = 0; u < HID; ++u) a = fmaf(DZ1[r][u], W0[u * IN + i], a);
+#pragma unroll 4
+    for (int u = 0; u < HID; ++u) a = fmaf(DZ1[r][u], W0s[u * IN + i], a);
     dX[(long long)(r0 + r) * IN + i] = a;
   }
 }
