@@ -145,7 +145,9 @@ class BaseNetTorch(torch.nn.Module):
                 self.eval_metrics["eval_recons_loss"] = self.eval_losses[2]
                 self.loss = self.train_loss
                 self.optimizer.zero_grad(set_to_none=True)
-                self.loss.backward()
+                if getattr(self, "_seed_grad", None) is None or self._seed_grad.shape != self.loss.shape:
+                    self._seed_grad = torch.ones_like(self.loss)   # reused: no fill kernel per step
+                self.loss.backward(self._seed_grad)
                 self.optimizer.step()
                 self.run_extra_fns("train")
                 if step % print_interval == 0:
