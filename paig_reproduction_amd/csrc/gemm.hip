@@ -98,6 +98,32 @@ struct Tile {
   }
 };
 
+// XCD-aware tile order.  Workgroups are dispatched round-robin over the 8
+// XCDs (linear id mod 8), each with its own L2.  Logical tiles are renumbered
+// so each XCD gets a contiguous run, ordered along the smaller grid dimension
+// first: the blocks that re-read one operand tile (the N-tiles of an M-row
+// block, or the M-tiles of an N-column block) then share that XCD's L2
+// instead of fetching the operand once per XCD.
+struct TileId {
+  int x, y, z;
+};
+__device__ __forceinline__ TileId xcd_tile() {
+  const int nx = gridDim.x, ny = gridDim.y, total = nx * ny * gridDim.z;
+  int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
+  TileId t;
+  if (nx <= ny) {
+    t.x = lin % nx;
+    t.y = (lin / nx) % ny;
+    t.z = lin / (nx * ny);
+  } else {
+    t.y = lin % ny;
+    t.x = (lin / ny) % nx;
+    t.z = lin / (nx * ny);
+  }
+  return t;
+}
+
 template <bool TA, bool TB>
 __global__ void __launch_bounds__(256)
 gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
@@ -109,11 +135,12 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = blockIdx.z * kchunk;
+  const TileId bt = xcd_tile();
+  const int m0 = bt.y * BM, n0 = bt.x * BN;
+  const int kbeg = bt.z * kchunk;
   int kend = kbeg + kchunk;
   if (kend > K) kend = K;
-  const bool do_rs = rowsum != nullptr && blockIdx.x == 0;
+  const bool do_rs = rowsum != nullptr && bt.x == 0;
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -156,7 +183,7 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
     }
   }
   if (do_rs && tid < BM && m0 + tid < M) {
-    if (rowpart) rowpart[(long long)blockIdx.z * M + m0 + tid] = alpha * rs;
+    if (rowpart) rowpart[(long long)bt.z * M + m0 + tid] = alpha * rs;
     else rowsum[m0 + tid] = alpha * rs;
   }
 
@@ -172,7 +199,7 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
         if (m < M && n < N) {
           float v = alpha * acc[i][j][r];
           if (part) {
-            part[((long long)blockIdx.z * M + m) * N + n] = v;
+            part[((long long)bt.z * M + m) * N + n] = v;
           } else {
             if (beta != 0.f) v += beta * C[(long long)m * ldc + n];
             if (bias) v += bias[n];
@@ -192,8 +219,7 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
 // activations / weights), 2 = bf16 pieces (16 bits, fp32 range: gradients),
 // 3 = bf16 hi only (the bf16 configuration).
 // LDS images keep each operand's global orientation: k-contiguous operands
-// as [row][k] (pitch 40: the 16 rows of a b128 fragment read hit 16 distinct
-// bank groups), row-contiguous operands as [pi(k)][row] (pitch 80) read with
+// as [row][k] (pitch 48, see SPK), row-contiguous operands as [pi(k)][row] (pitch 80) read with
 // ds_read_b64_tr_b16; pi places the 8 k-rows one 32-lane half reads in 8
 // consecutive image rows, 5 x 32 B apart mod 256 B: conflict-free.
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -202,7 +228,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-constexpr int SPK = 40;          // [row][k] pitch (16-bit elements)
+// [row][k] pitch (16-bit elements): 6 16-B slots.  ds_read_b128 serves a
+// wave in lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): 8 rows at
+// k-offset g and 8 rows at g+1 slot.  A pitch of 2 (mod 4) slots puts the 8
+// rows of one on the 8 even slots of a 256-B bank row and the other 8 on the
+// odd ones (the former 5-slot pitch collided 2-way)
+constexpr int SPK = 48;
 constexpr int SPR = 80;          // [pi(k)][row] pitch
 constexpr int SIMG = 64 * SPK > BK * SPR ? 64 * SPK : BK * SPR;
 
@@ -282,13 +313,14 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = blockIdx.z * kchunk;
+  const TileId bt = xcd_tile();
+  const int m0 = bt.y * BM, n0 = bt.x * BN;
+  const int kbeg = bt.z * kchunk;
   int kend = kbeg + kchunk;
   if (kend > K) kend = K;
   // row sums of op(A) (= the bias gradient of a wgrad GEMM) in exact fp32
   // from the staging registers; only the transposed-A form carries them
-  const bool do_rs = TA && rowsum != nullptr && blockIdx.x == 0;
+  const bool do_rs = TA && rowsum != nullptr && bt.x == 0;
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -356,7 +388,7 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
       float v = 0.f;
 #pragma unroll
       for (int k = 0; k < 16; ++k) v += red[k * 64 + tid];
-      if (rowpart) rowpart[(long long)blockIdx.z * M + m0 + tid] = alpha * v;
+      if (rowpart) rowpart[(long long)bt.z * M + m0 + tid] = alpha * v;
       else rowsum[m0 + tid] = alpha * v;
     }
   }
@@ -371,7 +403,7 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
         if (m < M && n < N) {
           float v = alpha * acc[i][j][r];
           if (part) {
-            part[((long long)blockIdx.z * M + m) * N + n] = v;
+            part[((long long)bt.z * M + m) * N + n] = v;
           } else {
             if (beta != 0.f) v += beta * C[(long long)m * ldc + n];
             if (bias) v += bias[n];
