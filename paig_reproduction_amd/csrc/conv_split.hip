@@ -44,6 +44,15 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int rup(int a, int b) { return ceil_div(a, b) * b; }
+
+// Physical tile of persistent-loop tile L.  Workgroups sit on XCD
+// (id mod 8), each XCD with its own L2; with the grid a multiple of 8, the
+// tiles of one XCD are L = x, x + 8, ...  Renumbering them into one
+// contiguous run keeps neighbouring row blocks of a frame (which re-read
+// each other's halo rows) on one XCD, processed at the same time.
+__device__ __forceinline__ int xcd_tile(int L, int ntiles) {
+  return (ntiles % 8 == 0 && gridDim.x % 8 == 0) ? (L % 8) * (ntiles / 8) + L / 8 : L;
+}
 // largest divisor d of n with d * w <= cap (at least 1): rows per tile
 constexpr int rows_fit(int n, int w, int cap) {
   int best = 1;
@@ -437,14 +446,15 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     }
   };
 
-  int tile = blockIdx.x;
-  if (tile < ntiles) issue(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+  int lt = blockIdx.x;   // logical tile; xcd_tile() gives the physical one
+  if (lt < ntiles) issue(xcd_tile(lt, ntiles));
+  for (; lt < ntiles; lt += gridDim.x) {
+    const int tile = xcd_tile(lt, ntiles);
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
     __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
+    if (lt + (int)gridDim.x < ntiles) issue(xcd_tile(lt + gridDim.x, ntiles));
     f32x4 acc[MW][NT];
 #pragma unroll
     for (int mt = 0; mt < MW; ++mt)
@@ -829,12 +839,13 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     }
   };
 
-  if ((int)blockIdx.x < ntiles) issue(blockIdx.x);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  if ((int)blockIdx.x < ntiles) issue(xcd_tile(blockIdx.x, ntiles));
+  for (int lt = blockIdx.x; lt < ntiles; lt += gridDim.x) {
+    const int tile = xcd_tile(lt, ntiles);
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
     __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
+    if (lt + (int)gridDim.x < ntiles) issue(xcd_tile(lt + gridDim.x, ntiles));
 #pragma unroll
     for (int kb = wp; kb < KB; kb += WP) {
       // k-block kb: 32 consecutive tile pixels, all in one frame
