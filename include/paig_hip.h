@@ -194,6 +194,10 @@ int paig_gather_u8_f32(const unsigned char* src, const long long* idx, float* ou
 
 /* ---- optimizers over the flat parameter buffer (base.py:12-17, torch defaults) */
 int paig_rmsprop_f32(float* p, const float* g, float* sa, long long n, float lr, float alpha, float eps, void* stream);
+/* both flat buffers in one launch (the fp32 hyper-parameters are the
+ * doubles rounded to float, as the separate entry points receive them) */
+int paig_rmsprop_mixed(float* p32, const float* g32, float* s32, long long n32, double* p64, const double* g64,
+                       double* s64, long long n64, double lr, double alpha, double eps, void* stream);
 int paig_rmsprop_f64(double* p, const double* g, double* sa, long long n, double lr, double alpha, double eps,
                      void* stream);
 int paig_adam_f32(float* p, const float* g, float* m, float* v, long long n, float lr, float b1, float b2, float eps,

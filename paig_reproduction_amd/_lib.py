@@ -71,6 +71,7 @@ SIGNATURES = {
     "paig_frame_sse_bwd": (I, [P, LL, I, LL, P, LL, I, LL, P, P, I, I, P]),
     "paig_rmsprop_f32": (I, [P, P, P, LL, F32, F32, F32, P]),
     "paig_rmsprop_f64": (I, [P, P, P, LL, F64, F64, F64, P]),
+    "paig_rmsprop_mixed": (I, [P, P, P, LL, P, P, P, LL, F64, F64, F64, P]),
     "paig_adam_f32": (I, [P, P, P, P, LL, F32, F32, F32, F32, F32, F32, P]),
     "paig_adam_f64": (I, [P, P, P, P, LL, F64, F64, F64, F64, F64, F64, P]),
     "paig_sgd_f32": (I, [P, P, P, LL, F32, F32, I, P]),

@@ -234,6 +234,29 @@ __global__ void rmsprop_k(T* __restrict__ p, const T* __restrict__ g, T* __restr
   }
 }
 
+// RMSprop over both flat buffers in one launch: the fp32 parameters
+// grid-stride, and block 0 also updates the few fp64 ones (the physics
+// parameters) -- rmsprop_k's arithmetic in each precision
+__global__ void rmsprop_mixed_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ sa, long long n,
+                                float lr, float alpha, float eps, double* __restrict__ pd, const double* __restrict__ gd,
+                                double* __restrict__ sd, long long nd, double lrd, double alphad, double epsd) {
+  if (blockIdx.x == 0)
+    for (long long i = threadIdx.x; i < nd; i += blockDim.x) {
+      const double gi = gd[i];
+      double s = sd[i] * alphad;
+      s = s + (1.0 - alphad) * gi * gi;
+      sd[i] = s;
+      pd[i] = pd[i] - lrd * gi / (sqrt(s) + epsd);
+    }
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    float s = sa[i] * alpha;
+    s = s + (1.f - alpha) * gi * gi;
+    sa[i] = s;
+    p[i] = p[i] - lr * gi / (sqrtf(s) + eps);
+  }
+}
+
 template <typename T>
 __global__ void adam_k(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ m, T* __restrict__ v, long long n,
                        T lr, T b1, T b2, T eps, T bc1, T bc2sqrt) {
@@ -383,6 +406,16 @@ int paig_frame_sse_bwd(const float* a, long long a_fs, int a_grp, long long a_gs
 int paig_rmsprop_f32(float* p, const float* g, float* sa, long long n, float lr, float alpha, float eps, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(rmsprop_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, sa, n, lr, alpha, eps);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_rmsprop_mixed(float* p32, const float* g32, float* s32, long long n32, double* p64, const double* g64,
+                       double* s64, long long n64, double lr, double alpha, double eps, void* stream) {
+  if (n32 <= 0 && n64 <= 0) return 0;
+  const long long nb = n32 > 0 ? n32 : 1;
+  hipLaunchKernelGGL(rmsprop_mixed_k, dim3(grid_for(nb)), dim3(256), 0, (hipStream_t)stream, p32, g32, s32, n32,
+                     (float)lr, (float)alpha, (float)eps, p64, g64, s64, n64, lr, alpha, eps);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

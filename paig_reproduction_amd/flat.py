@@ -207,9 +207,9 @@ class FlatOptimizer:
         n32, n64 = flat.n32, flat.n64
         if self.kind == "rmsprop":
             a, eps = self.hp.get("alpha", 0.99), self.hp.get("eps", 1e-8)
-            L.paig_rmsprop_f32(ptr(flat.p32), ptr(flat.g32), ptr(self._bufs[0]), n32, lr, a, eps, st)
-            if n64:
-                L.paig_rmsprop_f64(ptr(flat.p64), ptr(flat.g64), ptr(self._bufs[1]), n64, lr, a, eps, st)
+            # one launch for both buffers (fp32 hyper-parameters rounded as torch's fp32 math does)
+            L.paig_rmsprop_mixed(ptr(flat.p32), ptr(flat.g32), ptr(self._bufs[0]), n32, ptr(flat.p64),
+                                 ptr(flat.g64), ptr(self._bufs[1]) if n64 else None, n64, lr, a, eps, st)
         elif self.kind == "adam":
             b1, b2 = self.hp.get("betas", (0.9, 0.999))
             eps = self.hp.get("eps", 1e-8)
