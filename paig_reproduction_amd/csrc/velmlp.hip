@@ -12,7 +12,7 @@
 
 namespace {
 
-constexpr int HID = 100, OUT = 2, RB = 8, MAXIN = 16;
+constexpr int HID = 100, OUT = 2, RB = 2, MAXIN = 16;   // RB: backward rows per block (100 blocks at B = 100)
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 // X[r][2t+j] = pos[b][t][2k+j], r = k*B + b (the chunk/cat of blocks.py:43-45)
@@ -149,12 +149,19 @@ velmlp_bwd_k(const float* __restrict__ dvel, const float* __restrict__ X, const 
   // ---- layer 4 (linear): dz2 = (dvel W4) * tanh'(h2);  gW4 = dvel^T h2, gb4 = sum dvel
   if (tid < HID) {
     float g4[OUT] = {0.f, 0.f};
+    // all loads of this phase in flight together (one latency, not RB)
+    float w4[OUT], hvr[RB];
+#pragma unroll
+    for (int j = 0; j < OUT; ++j) w4[j] = W4[j * HID + tid];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) hvr[r] = r < nr ? h2[(long long)(r0 + r) * HID + tid] : 0.f;
+#pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const float hv = r < nr ? h2[(long long)(r0 + r) * HID + tid] : 0.f;
+      const float hv = hvr[r];
       float d = 0.f;
 #pragma unroll
       for (int j = 0; j < OUT; ++j) {
-        d = fmaf(DV[r][j], W4[j * HID + tid], d);
+        d = fmaf(DV[r][j], w4[j], d);
         g4[j] = fmaf(DV[r][j], hv, g4[j]);
       }
       DZ2[r][tid] = d * (1.f - hv * hv);
