@@ -450,13 +450,14 @@ __global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restr
 }
 
 // Split-K factor: the dense layers here are small (M, N <= a few thousand)
-// and latency-bound, so split until ~4 blocks per CU are in flight, keeping
+// and latency-bound, so split until ~2 blocks per CU are in flight (measured
+// best: 4 per CU paid more in partial-slab traffic than it won), keeping
 // >= 1 BK step per split and the partial slabs <= 16 MB.
 static int choose_split(int M, int N, int K) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
   int s = 1;
   if (K < 512) return 1;   // a short K loop costs less than the split-K epilogue launch
-  while (tiles * s < 1024 && cdiv(K, 2 * s) >= BK && (long long)(2 * s) * M * N <= (4ll << 20)) s *= 2;
+  while (tiles * s < 512 && cdiv(K, 2 * s) >= BK && (long long)(2 * s) * M * N <= (4ll << 20)) s *= 2;
   return s;
 }
 
