@@ -672,7 +672,7 @@ class Engine:
                 Hl = H // slvl
                 cin, cout, ks = src[2], dst[2], op["ks"]
                 # weight + bias gradient: per-block partials, then one reduction
-                nblk_max = 768
+                nblk_max = 1024
                 slab = _empty(nblk_max * (cout * cin * ks * ks + cout), dev)
                 nb = ctypes.c_int(0)
                 fl = 2 * F * cin * cout * ks * ks * Hl * Hl
