@@ -724,7 +724,7 @@ dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVi
 template <int K>
 static int dec_launch_fwd(PosView pv, Src S, FViewW out, FView tgt, float* sse, int F, int h, int H, hipStream_t st) {
   const int lds = (K * h * h * 4) * 4;
-  int g = F < 2048 ? F : 2048;
+  int g = (F + 1) / 2 < 1024 ? (F + 1) / 2 : 1024;   // >= 2 frames per block: source staging amortised
   if constexpr (K == 2) {
     if (H == 32) {
       hipLaunchKernelGGL((dec_fwd_reg_k<2, 32>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F);
