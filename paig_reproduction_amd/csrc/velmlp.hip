@@ -21,11 +21,10 @@ __device__ __forceinline__ float packed_in(const float* pos, int B, int Te, int 
   return pos[((long long)b * Te + t) * 2 * K + 2 * k + j];
 }
 
-// forward rows per block: 2 (100 blocks for the 200 rows of spring B=100),
+// forward rows per block: 1 (200 blocks for the 200 rows of spring B=100),
 // so the per-thread hidden-layer loop is short; W2 is staged per block into
 // LDS with an odd row pitch (lanes walk different rows: conflict-free)
-constexpr int FRB = 2, W2P = HID + 1;
-static_assert(FRB == 2, "the hidden-layer loop below is written for 2 rows");
+constexpr int FRB = 1, W2P = HID + 1;
 
 __global__ void __launch_bounds__(128)
 velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const float* __restrict__ W0,
@@ -82,9 +81,8 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
 #pragma unroll 10
     for (int u = 0; u < HID; ++u) {
       const float w = wr[u];
-      const float2 hv = *reinterpret_cast<const float2*>(&H1[u][0]);
-      a[0] = fmaf(hv.x, w, a[0]);
-      a[1] = fmaf(hv.y, w, a[1]);
+#pragma unroll
+      for (int r = 0; r < FRB; ++r) a[r] = fmaf(H1[u][r], w, a[r]);
     }
     for (int r = 0; r < nr; ++r) {
       const float v = tanhf(a[r]);
