@@ -237,8 +237,18 @@ __global__ void upsample_bwd_v_k(FView du, FView s, FViewW ds, int F, int C, int
       if (wy[a] == 0.f) continue;
       const float* rp = dup + y * Wo + 4 * m;
       const float4 v = *reinterpret_cast<const float4*>(rp);
-      const float l = m > 0 ? rp[-1] : 0.f;
-      const float r = 4 * m + 4 < Wo ? rp[4] : 0.f;
+      // the edge columns 4m-1 / 4m+4 are the neighbouring lanes' float4 ends
+      // when a row's P lanes never straddle a wave (P divides 64): lanes i-1 /
+      // i+1 hold m-1 / m+1 of the same row wherever those taps carry weight
+      // (at m = 0 and m = P-1 the weight is zero); else two scalar loads
+      float l, r;
+      if (64 % P == 0) {
+        l = __shfl_up(v.w, 1, 64);
+        r = __shfl_down(v.x, 1, 64);
+      } else {
+        l = m > 0 ? rp[-1] : 0.f;
+        r = 4 * m + 4 < Wo ? rp[4] : 0.f;
+      }
       float row0 = 0.f, row1 = 0.f;
       if (wx0[0] != 0.f) row0 = fmaf(wx0[0], l, row0);
       row0 = fmaf(wx0[1], v.x, row0);
