@@ -389,6 +389,99 @@ __global__ void mask_softmax_bwd_k(const float* __restrict__ lg, FView x, const 
   }
 }
 
+// The same, 4 pixels per thread (float4 loads and stores; frames of HW % 4
+// == 0 pixels, K a template constant): per element the scalar kernel's
+// operation order, so the results are identical.
+typedef float m4 __attribute__((ext_vector_type(4)));
+template <int K>
+__global__ void mask_softmax_fwd_v_k(const float* __restrict__ lg, FView x, float* __restrict__ masks,
+                                     float* __restrict__ objs, int F, int C, int HW) {
+  const int Q = HW / 4;
+  const long long n = (long long)F * Q;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int p = (int)(i % Q) * 4;
+    const int f = (int)(i / Q);
+    m4 l[K], e[K + 1];
+    m4 m = m4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      l[k] = *reinterpret_cast<const m4*>(lg + ((long long)f * K + k) * HW + p);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], l[k][j]);
+    }
+    m4 s = m4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[k][j] = expf(l[k][j] - m[j]);
+      s += e[k];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[K][j] = expf(1.f - m[j]);
+    s += e[K];
+    const float* xp = x.frame(f);
+    m4 xv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (c < C) xv[c] = *reinterpret_cast<const m4*>(xp + c * HW + p);
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+      m4 mk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mk[j] = e[k][j] / s[j];
+      *reinterpret_cast<m4*>(masks + ((long long)f * (K + 1) + k) * HW + p) = mk;
+      if (k < K)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          if (c < C) *reinterpret_cast<m4*>(objs + ((long long)k * F + f) * C * HW + (long long)c * HW + p) = mk * xv[c];
+    }
+  }
+}
+
+template <int K>
+__global__ void mask_softmax_bwd_v_k(const float* __restrict__ lg, FView x, const float* __restrict__ masks,
+                                     const float* __restrict__ dobjs, float* __restrict__ dlg, int F, int C, int HW,
+                                     int flags) {
+  const int Q = HW / 4;
+  const long long n = (long long)F * Q;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int p = (int)(i % Q) * 4;
+    const int f = (int)(i / Q);
+    const float* xp = x.frame(f);
+    m4 xv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (c < C) xv[c] = *reinterpret_cast<const m4*>(xp + c * HW + p);
+    m4 dm[K], mk[K];
+    m4 dot = m4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      m4 a = m4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (c < C) {
+          const m4 d = *reinterpret_cast<const m4*>(dobjs + ((long long)k * F + f) * C * HW + (long long)c * HW + p);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = fmaf(d[j], xv[c][j], a[j]);
+        }
+      dm[k] = a;
+      mk[k] = *reinterpret_cast<const m4*>(masks + ((long long)f * (K + 1) + k) * HW + p);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dot[j] = fmaf(mk[k][j], a[j], dot[j]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      m4 g = mk[k] * (dm[k] - dot);
+      if (flags & 1) {
+        const m4 lv = *reinterpret_cast<const m4*>(lg + ((long long)f * K + k) * HW + p);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g[j] = lv[j] > 0.f ? g[j] : 0.f;
+      }
+      *reinterpret_cast<m4*>(dlg + ((long long)f * K + k) * HW + p) = g;
+    }
+  }
+}
+
 // --------------------------------------------------------- position head ----
 // enc_pos[n][2k+j] = tanh(h3[k*N+n][j]) * (H/2) + H/2
 __global__ void pos_head_fwd_k(const float* __restrict__ h3, float* __restrict__ pos, int N, int K, float half) {
@@ -631,8 +724,18 @@ int paig_mask_softmax_fwd(const float* logits, const float* x, long long x_fs, i
     hipLaunchKernelGGL(mask_softmax_pool_fwd_k, dim3(grid_for((long long)F * (H / 2) * (W / 2))), dim3(256), 0,
                        (hipStream_t)stream, logits, FView{x, x_fs, x_gs, x_grp}, masks, objs, pobjs, F, K, C, H, W);
   } else {
-    hipLaunchKernelGGL(mask_softmax_fwd_k, dim3(grid_for((long long)F * H * W)), dim3(256), 0, (hipStream_t)stream,
-                       logits, FView{x, x_fs, x_gs, x_grp}, masks, objs, F, K, C, H * W);
+    const bool v4 = (H * W) % 4 == 0 && C <= 3 && (K == 2 || K == 3) && x_fs % 4 == 0 && x_gs % 4 == 0 &&
+                    ((uintptr_t)logits | (uintptr_t)x | (uintptr_t)masks | (uintptr_t)objs) % 16 == 0;
+    const dim3 g4(grid_for((long long)F * H * W / 4));
+    if (v4 && K == 2)
+      hipLaunchKernelGGL(mask_softmax_fwd_v_k<2>, g4, dim3(256), 0, (hipStream_t)stream, logits,
+                         FView{x, x_fs, x_gs, x_grp}, masks, objs, F, C, H * W);
+    else if (v4 && K == 3)
+      hipLaunchKernelGGL(mask_softmax_fwd_v_k<3>, g4, dim3(256), 0, (hipStream_t)stream, logits,
+                         FView{x, x_fs, x_gs, x_grp}, masks, objs, F, C, H * W);
+    else
+      hipLaunchKernelGGL(mask_softmax_fwd_k, dim3(grid_for((long long)F * H * W)), dim3(256), 0, (hipStream_t)stream,
+                         logits, FView{x, x_fs, x_gs, x_grp}, masks, objs, F, K, C, H * W);
   }
   PAIG_CHECK_LAUNCH();
   return 0;
@@ -643,8 +746,19 @@ int paig_mask_softmax_bwd(const float* logits, const float* x, long long x_fs, i
                           int flags, void* stream) {
   if (F <= 0) return 0;
   PAIG_REQUIRE(K >= 1 && K <= 7, "mask_softmax: K=%d", K);
-  hipLaunchKernelGGL(mask_softmax_bwd_k, dim3(grid_for((long long)F * H * W)), dim3(256), 0, (hipStream_t)stream,
-                     logits, FView{x, x_fs, x_gs, x_grp}, masks, dobjs, dlogits, F, K, C, H, W, flags);
+  const bool v4 = !(flags & 2) && (H * W) % 4 == 0 && C <= 3 && (K == 2 || K == 3) && x_fs % 4 == 0 &&
+                  x_gs % 4 == 0 &&
+                  ((uintptr_t)logits | (uintptr_t)x | (uintptr_t)masks | (uintptr_t)dobjs | (uintptr_t)dlogits) % 16 == 0;
+  const dim3 g4(grid_for((long long)F * H * W / 4));
+  if (v4 && K == 2)
+    hipLaunchKernelGGL(mask_softmax_bwd_v_k<2>, g4, dim3(256), 0, (hipStream_t)stream, logits,
+                       FView{x, x_fs, x_gs, x_grp}, masks, dobjs, dlogits, F, C, H * W, flags);
+  else if (v4 && K == 3)
+    hipLaunchKernelGGL(mask_softmax_bwd_v_k<3>, g4, dim3(256), 0, (hipStream_t)stream, logits,
+                       FView{x, x_fs, x_gs, x_grp}, masks, dobjs, dlogits, F, C, H * W, flags);
+  else
+    hipLaunchKernelGGL(mask_softmax_bwd_k, dim3(grid_for((long long)F * H * W)), dim3(256), 0, (hipStream_t)stream,
+                       logits, FView{x, x_fs, x_gs, x_grp}, masks, dobjs, dlogits, F, K, C, H, W, flags);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
