@@ -146,7 +146,7 @@ __global__ void vfn_bwd2_k(VfnBwdTasks T) {
 __global__ void loss_reduce_k(const float* __restrict__ sse_rec, const float* __restrict__ sse_roll, int B, int Te,
                               int R, int pred, float ae, float* __restrict__ o_pred, float* __restrict__ o_ext,
                               float* __restrict__ o_rec) {
-  __shared__ float red[3][4];
+  __shared__ float red[3][16];   // one block of up to 1024 threads (16 waves)
   float a = 0.f, b = 0.f, c = 0.f;
   for (int i = threadIdx.x; i < B * R; i += blockDim.x) {
     const int t = i % R;
@@ -166,7 +166,11 @@ __global__ void loss_reduce_k(const float* __restrict__ sse_rec, const float* __
   __syncthreads();
   if (threadIdx.x == 0) {
     float s[3];
-    for (int k = 0; k < 3; ++k) s[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    const int nw = blockDim.x >> 6;
+    for (int k = 0; k < 3; ++k) {
+      s[k] = 0.f;
+      for (int w = 0; w < nw; ++w) s[k] += red[k][w];
+    }
     const float pl = s[0] / (float)(B * pred), rl = s[2] / (float)(B * Te);
     // train = pred (+= ae * recons, physics_models.py:137-141: a separate fp32
     // multiply then add, never contracted into an FMA)
@@ -370,7 +374,7 @@ int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const 
 
 int paig_loss_reduce(const float* sse_rec, const float* sse_roll, int B, int Te, int R, int pred, float ae, float* pred_out,
                      float* extrap_out, float* recons_out, void* stream) {
-  hipLaunchKernelGGL(loss_reduce_k, dim3(1), dim3(256), 0, (hipStream_t)stream, sse_rec, sse_roll, B, Te, R, pred,
+  hipLaunchKernelGGL(loss_reduce_k, dim3(1), dim3(1024), 0, (hipStream_t)stream, sse_rec, sse_roll, B, Te, R, pred,
                      ae, pred_out, extrap_out, recons_out);
   PAIG_CHECK_LAUNCH();
   return 0;
