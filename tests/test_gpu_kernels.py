@@ -273,3 +273,31 @@ def test_pool_upsample():
     torch.cuda.synchronize()
     assert rel_err(ug, u.detach()) <= 1e-6
     assert rel_err(ds, sr.grad * (s > 0)) <= 1e-6
+
+
+@pytest.mark.parametrize("lens,aligned", [([5120, 4096, 36, 0], True), ([64, 100, 7], False), ([3, 8], True)])
+@pytest.mark.parametrize("accumulate", [0, 1])
+def test_slab_reduce_multi(lens, aligned, accumulate):
+    """Batched deterministic slab reductions (vector kernel when every task is
+    float4-shaped and aligned, scalar kernel otherwise) vs a float64 sum."""
+    g = torch.Generator().manual_seed(7)
+    nblks = [1, 300, 129, 2][:len(lens)]
+    srcs, dsts, init = [], [], []
+    for ln, nb in zip(lens, nblks):
+        off = 0 if aligned else 1
+        s = torch.randn(nb * ln + off, generator=g)
+        d = torch.randn(ln + off, generator=g)
+        srcs.append((s.to(DEV), off, s[off:].view(nb, ln) if ln else s[off:].view(nb, 0)))
+        dsts.append((d.to(DEV), off))
+        init.append(d[off:].clone())
+    n = len(lens)
+    L().paig_slab_reduce_multi(n, (ctypes.c_void_p * n)(*[p(s) + o * 4 for s, o, _ in srcs]),
+                               (ctypes.c_int * n)(*nblks), (ctypes.c_int * n)(*lens),
+                               (ctypes.c_void_p * n)(*[p(d) + o * 4 for d, o in dsts]), accumulate, st())
+    torch.cuda.synchronize()
+    for (d, o), (_, _, host), d0 in zip(dsts, srcs, init):
+        want = host.double().sum(0) + (d0.double() if accumulate else 0)
+        got = d.cpu()[o:].double()
+        assert got.shape == want.shape
+        if want.numel():
+            assert float((got - want).abs().max()) <= 1e-4 * max(1.0, float(want.abs().max()))
