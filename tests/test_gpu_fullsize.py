@@ -1,0 +1,75 @@
+"""Size-independent properties of the HIP training step at BASELINE.json's
+full sizes, where the CPU oracle is too slow to run (the golden-vector parity
+tests cover the same kernels at small sizes):
+
+* determinism: two passes over the same weights and batch give bit-identical
+  losses and gradients (every reduction has a fixed order; no atomics);
+* batch additivity: the losses are batch means of per-sequence sums
+  (physics_models.py:119-142), so loss(B) and every gradient equal the average
+  of the two half batches' (what the data-parallel AVG all-reduce relies on).
+  Bar: 1e-5 on losses, GRAD_RTOL on gradients (different summation order);
+  3bp is chaotic (see test_gpu_parity), so its bars are the rollout ones.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+# (task, cell, seq_len, input_steps, pred_steps, frame size, batch): BASELINE.json configs
+FULL = [("spring_color", "spring_ode_cell", 50, 4, 6, 32, 100),
+        ("3bp_color", "gravity_ode_cell", 20, 4, 12, 36, 512),
+        ("mnist_spring_color", "spring_ode_cell", 12, 3, 7, 64, 256),
+        ("bouncing_balls", "bouncing_ode_cell", 100, 4, 6, 32, 1024)]
+GRAD_RTOL = 1e-3
+
+
+def _setup(task, cell, seq_len, ins, pred, size, B):
+    from paig_reproduction_amd.nn.datasets.synth import as_model_input, render_sequences
+    from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = PhysicsNet(task, 100, 1, cell, seq_len, ins, pred, 3.0, False, True, size * size, "conv_encoder",
+                   "conv_st_decoder", device=dev).to(dev)
+    x = torch.from_numpy(as_model_input(render_sequences(task, B, seq_len, seed=3))).to(dev)
+    return m, x
+
+
+def _step(m, x):
+    m.output = m(x)
+    loss, (pred, extrap, recons) = m.compute_loss()
+    m.zero_grad(set_to_none=True)
+    loss.backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    return [float(v.detach()) for v in (loss, extrap, recons)], grads
+
+
+@pytest.mark.parametrize("cfg", FULL, ids=[c[0] for c in FULL])
+def test_full_size_step_is_deterministic(cfg):
+    m, x = _setup(*cfg)
+    l1, g1 = _step(m, x)
+    l2, g2 = _step(m, x)
+    assert all(np.isfinite(l1)), l1
+    assert l1 == l2
+    assert sorted(g1) == sorted(g2) and len(g1) > 0
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+
+
+@pytest.mark.parametrize("cfg", FULL, ids=[c[0] for c in FULL])
+def test_full_size_batch_halves_average(cfg):
+    m, x = _setup(*cfg)
+    B = x.shape[0]
+    lf, gf = _step(m, x)
+    la, ga = _step(m, x[:B // 2].contiguous())
+    lb, gb = _step(m, x[B // 2:].contiguous())
+    chaotic = cfg[0] == "3bp_color"
+    lbar, gbar = (2e-3, 5e-2) if chaotic else (1e-5, GRAD_RTOL)
+    for i, what in enumerate(("train", "extrap", "recons")):
+        bar = 1e-5 if what == "recons" else lbar   # recons does not go through the rollout
+        assert rel_err(np.float64(lf[i]), np.float64((la[i] + lb[i]) / 2)) <= bar, what
+    for k in gf:
+        assert rel_err(gf[k], (ga[k] + gb[k]) / 2) <= gbar, k
