@@ -449,6 +449,56 @@ __global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restr
   }
 }
 
+// Vector form (N % 4 == 0; C, bias, aux and the slabs float4-addressable;
+// S * M * N < 2^31; M * N >= 2^19 so the grid stays wide): 4 consecutive
+// columns per thread, float4 loads of up to 8 partials in flight, 32-bit indexing.  The row sums, if any, take the
+// threads past the element range.  Same per-element order as the scalar form.
+__global__ void __launch_bounds__(256) gemm_splitk_epilogue_v_k(int M, int N, int S, const float* __restrict__ part,
+                                                                float* __restrict__ C, int ldc, float beta,
+                                                                const float* __restrict__ bias, int act, int auxm,
+                                                                const float* __restrict__ aux, int ldaux,
+                                                                const float* __restrict__ rowpart,
+                                                                float* __restrict__ rowsum) {
+  const int n_el = M * N, n4 = n_el >> 2;
+  const int tot = n4 + (rowsum ? M : 0);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
+    if (i >= n4) {
+      const int m = i - n4;
+      rowsum[m] = sum_strided(rowpart + m, M, S);
+      continue;
+    }
+    const int e = i << 2, m = e / N, n = e - m * N;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    int s = 0;
+    for (; s + 8 <= S; s += 8) {   // 8 partial loads in flight, summed in slab order
+      float4 t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = *reinterpret_cast<const float4*>(part + (s + j) * n_el + e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v.x += t[j].x; v.y += t[j].y; v.z += t[j].z; v.w += t[j].w; }
+    }
+    for (; s < S; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(part + s * n_el + e);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    float* c = C + m * ldc + n;
+    if (beta != 0.f) {
+      const float4 o = *reinterpret_cast<const float4*>(c);
+      v.x += beta * o.x; v.y += beta * o.y; v.z += beta * o.z; v.w += beta * o.w;
+    }
+    if (bias) {
+      const float4 b = *reinterpret_cast<const float4*>(bias + n);
+      v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+    }
+    const long long ao = (long long)m * ldaux + n;
+    v.x = epi(v.x, act, auxm, aux, ao);
+    v.y = epi(v.y, act, auxm, aux, ao + 1);
+    v.z = epi(v.z, act, auxm, aux, ao + 2);
+    v.w = epi(v.w, act, auxm, aux, ao + 3);
+    *reinterpret_cast<float4*>(c) = v;
+  }
+}
+
 // Split-K factor: the dense layers here are small (M, N <= a few thousand)
 // and latency-bound, so split until ~2 blocks per CU are in flight (measured
 // best: 4 per CU paid more in partial-slab traffic than it won), keeping
@@ -530,11 +580,19 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
 #undef PAIG_G
   PAIG_CHECK_LAUNCH();
   if (S > 1) {
-    long long n_el = (long long)M * N + (rowsum ? M : 0);
+    const bool v4 = N % 4 == 0 && vec_ok(C, ldc) && (!bias || (uintptr_t)bias % 16 == 0) && (!aux || auxm == AUX_NONE ||
+                    vec_ok(aux, ldaux)) && (uintptr_t)part % 16 == 0 && (long long)S * M * N < (1ll << 31) &&
+                    (long long)M * ldc < (1ll << 31) && (long long)M * ldaux < (1ll << 31) &&
+                    (long long)M * N >= (1 << 19);   // smaller outputs keep the scalar form (4x the threads)
+    long long n_el = (v4 ? (long long)M * N / 4 : (long long)M * N) + (rowsum ? M : 0);
     int g = cdiv(n_el, 256);
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(gemm_splitk_epilogue_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, ldc, beta, bias, act, auxm,
-                       aux, ldaux, rowpart, rowsum);
+    if (v4)
+      hipLaunchKernelGGL(gemm_splitk_epilogue_v_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, (int)ldc, beta, bias,
+                         act, auxm, aux, (int)ldaux, rowpart, rowsum);
+    else
+      hipLaunchKernelGGL(gemm_splitk_epilogue_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, ldc, beta, bias, act,
+                         auxm, aux, ldaux, rowpart, rowsum);
     PAIG_CHECK_LAUNCH();
   }
   return 0;

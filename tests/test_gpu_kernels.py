@@ -222,7 +222,7 @@ GEMM_EX_TOL = {1: 2e-5, 2: 5e-5, 3: 3e-2}
 @pytest.mark.parametrize("math", [1, 2, 3])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(37, 50, 19), (130, 200, 3072), (200, 3072, 130), (6, 2, 200), (1, 513, 200),
-                                   (2000, 200, 3072)])
+                                   (2000, 200, 3072), (200, 3072, 2000)])   # last: float4 split-K epilogue
 def test_gemm_ex(ta, tb, M, N, K, math):
     torch.manual_seed(M + N + K + math)
     A = (torch.randn(K, M) if ta else torch.randn(M, K)) / K ** 0.5
