@@ -64,6 +64,9 @@ def parse():
                     help="committed rocprofv3 FETCH_SIZE/WRITE_SIZE summary (tools/pmc_traffic.py)")
     ap.add_argument("--graph", type=int, default=1, help="capture fwd+loss+bwd in a HIP graph per resident batch")
     ap.add_argument("--probe_steps", type=int, default=5, help="eager steps timing the probed kernel")
+    ap.add_argument("--graph_optimizer", type=int, default=1,
+                    help="at N=1 capture the RMSprop launch in the step graph too (it runs every replay; "
+                         "no all-reduce to order it after, no step counter in RMSprop)")
     ap.add_argument("--split_graph", type=int, default=-1,
                     help="capture the step as two HIP graphs split where the early gradient bucket is final, and "
                          "all-reduce that bucket between the replays, overlapping the U-Net backward "
@@ -171,6 +174,7 @@ def main():
         eager_step(i)
     graphs = None
     split = a.split_graph if a.split_graph >= 0 else int(world > 1)
+    opt_in_graph = bool(a.graph and a.graph_optimizer and world == 1 and not split and m.optimizer.kind == "rmsprop")
     if a.graph:
         # one graph per resident batch (two when split), sharing one memory
         # pool; the optimizer step and the DP all-reduce stay eager
@@ -181,6 +185,8 @@ def main():
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
                     lg = body(x)
+                    if opt_in_graph:
+                        m.optimizer.step()
                 pool = g.pool()
                 graphs.append(((g,), lg))
                 continue
@@ -217,7 +223,8 @@ def main():
         if len(gs) == 2:
             m._flat.allreduce_early()   # overlaps the second graph (U-Net backward)
             gs[1].replay()
-        m.optimizer.step()
+        if not opt_in_graph:
+            m.optimizer.step()
         return lg
 
     step(0)
@@ -279,7 +286,8 @@ def main():
                                    f"B={a.batch}/rank, {size}x{size}x3, seq_len {a.seq_len} "
                                    f"({ins} in / {pred} pred / {a.seq_len - ins - pred} extrap)",
                        "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}",
-                       "conv_math": a.conv_math, "split_graph": bool(a.graph and split)},
+                       "conv_math": a.conv_math, "split_graph": bool(a.graph and split),
+                       "optimizer_in_graph": opt_in_graph},
             "roofline": roof, "cpu_baseline": cpu, "final_loss": round(lossv, 4),
             # whole-step memory-side traffic (committed PMC profile) at this run's step time
             "hbm_step": None if step_bytes is None else {
