@@ -12,7 +12,7 @@
 
 namespace {
 
-constexpr int HID = 100, OUT = 2, RB = 2, MAXIN = 16;   // RB: backward rows per block (100 blocks at B = 100)
+constexpr int HID = 100, OUT = 2, RB = 1, MAXIN = 16;   // RB: backward rows per block (200 blocks at B = 100)
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 // X[r][2t+j] = pos[b][t][2k+j], r = k*B + b (the chunk/cat of blocks.py:43-45)
