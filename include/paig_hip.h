@@ -30,6 +30,13 @@ extern "C" {
 
 const char* paig_last_error(void);
 int paig_abi_version(void);
+/* f16 range guard of paig_gemm_ex math 1, which feeds its operands to the
+ * f16 matrix cores unscaled (|v| < 65504 needed; the step's split path uses
+ * the scaled math 4 and the scaled convs, which have no such limit); a
+ * kernel that meets a larger value sets a device flag.  Synchronises the device, returns 1 if any flag is set
+ * (clear != 0 resets them), 0 if none, < 0 on a HIP error.  (No reference
+ * counterpart: fp32 aten ops have no such limit; the caller raises.) */
+int paig_f16_range_status(int clear);
 
 /* ---- U-Net convolutions -------------------------------------------------
  * replaces aten conv2d / convolution_backward for ShallowUNet and UNet
@@ -41,8 +48,9 @@ int paig_abi_version(void);
  *        MFMA kernel (tests), 32 the input is the 2x bilinear
  *        upsample of the given (H/2 x W/2) planes, formed while staging
  *        (torchvision Resize of blocks.py:260,269 fused, never materialised),
- *        128 split-precision 16-bit MFMA (f16 hi+lo pieces for the forward,
- *        bf16 hi+lo for dgrad: fp32-accurate), 256 bf16 operands (config #2).
+ *        128 split-precision 16-bit MFMA (f16 hi+lo pieces, every operand
+ *        scaled by powers of two: fp32-accurate at any range), 256 bf16
+ *        operands (config #2).
  *        Shapes without a split instantiation fall back to the f32 MFMA /
  *        VALU kernels (same results within fp32 accuracy). */
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
@@ -92,8 +100,10 @@ int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, 
               const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, void* stream);
 /* paig_gemm on the 16-bit matrix cores with split-precision operands
  * (gemm.hip): math 0 = f32-input MFMA (= paig_gemm), 1 = f16 hi+lo pieces
- * (fp32-accurate; operands |v| < 65504), 2 = bf16 hi+lo pieces (fp32 range),
- * 3 = bf16.  rowsum is fused only for ta = 1 (else math falls back to 0). */
+ * (fp32-accurate; operands |v| < 65504, range-guarded), 2 = bf16 hi+lo
+ * pieces (fp32 range, 16 bits), 3 = bf16, 4 = f16 hi+lo with both operands
+ * scaled by running powers of two (any range; fp32-accurate).  rowsum
+ * is fused only for ta = 1 (else math falls back to 0). */
 int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
                  long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
                  const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,

@@ -158,7 +158,7 @@ def st_decoder(cfg, joint, bg, pos):
         theta = torch.stack([one, zero, t2, zero, one, t5], 1).view(-1, 2, 3)
         grid = F.affine_grid(theta, [N, 6, H, H], align_corners=False)
         src = joint[k:k + 1].expand(N, -1, -1, -1)
-        o = F.grid_sample(src, grid.float(), mode="bilinear", padding_mode="zeros", align_corners=False)
+        o = F.grid_sample(src, grid.to(src.dtype), mode="bilinear", padding_mode="zeros", align_corners=False)
         outs.append((o[:, :3], o[:, 3:]))
     masks = torch.stack([t - 5 for t, _ in outs] + [torch.ones_like(outs[0][0])], 1)
     masks = torch.softmax(masks, 1)
@@ -301,6 +301,17 @@ def train_step(state, cfg, x, with_grads=True):
         L["train"].backward()
         grads = {k: P[k].grad for k in live_params(state, cfg) if P[k].grad is not None}
     return out, L, grads
+
+
+def train_step_f64(state, cfg, x, with_grads=True):
+    """The same step in float64 throughout (state, input, constants, grid):
+    the envelope against which fp32 implementations are judged."""
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        return train_step({k: v.double() for k, v in state.items()}, cfg, x.double(), with_grads)
+    finally:
+        torch.set_default_dtype(prev)
 
 
 def rmsprop_step(param, grad, square_avg, lr, alpha=0.99, eps=1e-8):

@@ -11,6 +11,8 @@ import torch  # noqa: F401  (loads torch's HIP runtime first; the .so binds to i
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpaig_hip.so")
+# A/B tooling only (tools/conv_bench.py against an older build): another .so
+AB_PATH = os.environ.get("PAIG_AB_LIB")
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -23,6 +25,7 @@ SZ = ctypes.c_size_t
 SIGNATURES = {
     "paig_last_error": (ctypes.c_char_p, []),
     "paig_abi_version": (I, []),
+    "paig_f16_range_status": (I, [I]),
     "paig_conv2d_fwd": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P]),
     "paig_conv2d_wgrad": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
@@ -97,6 +100,8 @@ class _Lib:
         self.dll = ctypes.CDLL(path)
         self.fns = {}
         for name, (rt, args) in SIGNATURES.items():
+            if path != LIB_PATH and not hasattr(self.dll, name):
+                continue   # an older A/B build
             f = getattr(self.dll, name)
             f.restype = rt
             f.argtypes = args
@@ -127,7 +132,7 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        _lib = _Lib()
+        _lib = _Lib(AB_PATH or LIB_PATH)
     return _lib
 
 

@@ -57,6 +57,9 @@ struct FViewW {
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float uniform_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -68,6 +71,69 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// f16 range guard of the split-precision kernels (conv_split.hip, gemm.hip):
+// their unscaled f16 operands (activations, weights) need |v| < 65504.  A
+// kernel that stages a larger value sets its translation unit's flag (plain
+// vector store; any value, so concurrent writers need no atomics);
+// paig_f16_range_status() reads and clears every unit's flag.
+static __device__ unsigned paig_f16_range_flag;
+constexpr float PAIG_F16_MAX = 65504.f;
+__device__ __forceinline__ void f16_range_note(float rmax) {
+  if (rmax >= PAIG_F16_MAX) *(volatile unsigned*)&paig_f16_range_flag = 1u;
+}
+// host side: read (and clear) this unit's flag; the device must be idle
+#define PAIG_F16_RANGE_ACCESSOR(NAME)                                                     \
+  int NAME(int clear) {                                                                   \
+    unsigned v = 0;                                                                       \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(paig_f16_range_flag), sizeof(v)) != hipSuccess) \
+      return -1;                                                                          \
+    if (clear && v) {                                                                     \
+      const unsigned z = 0;                                                               \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(paig_f16_range_flag), &z, sizeof(z)) != hipSuccess) \
+        return -1;                                                                        \
+    }                                                                                     \
+    return (int)v;                                                                        \
+  }
+int paig_f16_range_conv(int clear);
+int paig_f16_range_gemm(int clear);
+
+// fixed power-of-two scale of the weights in the split-precision convs: f16
+// keeps 22 significant bits for |w| >= 2^-(3 + 8) and overflows at 2^(16 - 8)
+// (range-guarded); per-block weight maxima cost a serial pass per launch
+#define PAIG_W_EXP 8
+
+// power-of-two exponent e with m * 2^e in [2^14, 2^15) (f16's top binade,
+// clear of its 65504 limit); 100 when m == 0 (no constraint); clamped
+// m must be wave-uniform (a block maximum); the exponent is computed in
+// scalar registers
+__device__ __forceinline__ int f16_scale_exp(float m) {
+  const int b = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m));
+  int e = b > 0 ? 14 - (((b >> 23) & 255) - 127) : 100;
+  return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
+
+// max over the wave of v >= 0, returned wave-uniform: DPP within rows of 16
+// (quad swaps, half-row and row mirrors: VALU ops, no LDS round trips), then
+// the four row results read as scalars.  The scale exponents of the
+// split-precision kernels need it once per staged tile.
+template <int CTRL>
+__device__ __forceinline__ float dpp_fmax(float v) {
+  const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false);
+  return fmaxf(v, __builtin_bit_cast(float, o));
+}
+__device__ __forceinline__ float wave_max_u(float v) {
+  v = dpp_fmax<0xB1>(v);    // quad_perm [1,0,3,2]
+  v = dpp_fmax<0x4E>(v);    // quad_perm [2,3,0,1]
+  v = dpp_fmax<0x141>(v);   // row_half_mirror: quads 0<->1, 2<->3
+  v = dpp_fmax<0x140>(v);   // row_mirror: halves of the row
+  const int b = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 
 __device__ __forceinline__ double wave_sum_d(double v) {

@@ -11,15 +11,19 @@
 // so the three-term product does fp32-accurate convolutions at ~5x the f32
 // matrix rate; these layers (3..128 channels) then run at the HBM/LDS
 // roofline instead of the MFMA one.  Precision modes (PM):
-//   0  f16 hi/lo   (22 significant bits: forward activations and weights,
-//                  whose range |v| < 65504 this mode requires; dgrad too,
-//                  each tile's gradients scaled by a power of two into that
-//                  range and the result scaled back exactly)
-//   1  bf16 hi/lo  (16 significant bits, fp32 range: wgrad, whose pixel sums
-//                  span many tiles, so no per-tile scale applies)
+//   0  f16 hi/lo   (22 significant bits).  Activations and weights go in
+//                  unscaled (|v| < 65504 required: the kernels flag a larger
+//                  value, paig_f16_range_status); gradients are scaled by
+//                  powers of two into f16's top binade: per tile in dgrad
+//                  (the tile's outputs are complete, the epilogue scales
+//                  back), by a running block exponent in wgrad (whose pixel
+//                  sums span tiles: a tile needing a smaller exponent first
+//                  rescales the accumulators, exactly)
+//   1  bf16 hi/lo  (16 significant bits, fp32 range; no longer launched:
+//                  its wgrad errors measured 100x the fp32 envelope)
 //   2  bf16 hi only (one MFMA: the bf16 configuration, BASELINE config #2)
-// Measured against the reference's golden vectors (tests/golden): outputs
-// within 1e-6 and gradients within fp32 noise.
+// Measured against a float64 restatement of the step (tests/envelope.py):
+// within ENVELOPE_K times the fp32 reference's own error.
 //
 // forward / dgrad  D[pixel][co] = im2col(X)[pixel][k] * Wt[k][co], with
 //   k = (tap, ci) in 8-channel chunks: the block stages its input tile as an
@@ -34,6 +38,10 @@
 //   16 columns of an N-tile are 4 (tap, 4-channel) quads.  Bias gradients
 //   are summed exactly in fp32 from the staging registers.
 #include "conv_tile.h"
+
+#ifndef PAIG_SCALE_MODE
+#define PAIG_SCALE_MODE 0   // A/B experiments only: 1 no weight scale, 2 no scaling
+#endif
 
 namespace {
 
@@ -63,9 +71,11 @@ constexpr int rows_fit(int n, int w, int cap) {
 // smallest y >= x with y % 16 == r
 constexpr int to_mod16(int x, int r) { return x + ((r - x % 16) + 16) % 16; }
 
+// rmax: running max |v| of the f16-split values (the range guard, common.h)
 template <int PM>
-__device__ __forceinline__ void split(float v, short& h, short& l) {
+__device__ __forceinline__ void split(float v, short& h, short& l, float& rmax) {
   if constexpr (PM == 0) {
+    rmax = fmaxf(rmax, fabsf(v));
     const _Float16 a = (_Float16)v;
     const _Float16 b = (_Float16)(v - (float)a);
     h = __builtin_bit_cast(short, a);
@@ -138,6 +148,17 @@ struct UpStage {
         v1[l] = ok ? u : 0.f;
       }
     }
+  }
+  // max |v| of the prefetched window: a bound on its upsampled values (convex
+  // combinations of window values)
+  __device__ __forceinline__ float amax() const {
+    float m = 0.f;
+#pragma unroll
+    for (int l = 0; l < NLS; ++l) {
+      if constexpr (VS == 4) m = fmaxf(m, fmaxf(fmaxf(fabsf(v[l][0]), fabsf(v[l][1])), fmaxf(fabsf(v[l][2]), fabsf(v[l][3]))));
+      else m = fmaxf(m, fabsf(v1[l]));
+    }
+    return m;
   }
   __device__ __forceinline__ void commit(float* Sl, int tid) const {
 #pragma unroll
@@ -286,27 +307,24 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
   constexpr int NRB = H / RT;
   const int co0 = blockIdx.y * NT * 16;   // this block's COUT slice
+  float rmax = 0.f;                       // f16 range guard of the scaled weights
+  __shared__ float smax[4];
 
   // ---- weights in fragment order: [s][nt][lane][8]; dgrad: transposed + flipped
-  for (int idx = tid; idx < NS * NT * 64; idx += 256) {
+  auto wval = [&](int idx, int j) {
     const int ln = idx & 63, snt = idx >> 6, nt = snt % NT, s = snt / NT;
     const int kc = 4 * s + (ln >> 4), co = co0 + nt * 16 + (ln & 15);
-    s16x8 vh, vl;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = 0.f;
-      if (kc < KC && co < COUT) {
-        const int tap = kc / CC, ci = (kc % CC) * 8 + j;
-        if (ci < CIN) v = DG ? w[(ci * COUT + co) * KK + (KK - 1 - tap)] : w[(co * CIN + ci) * KK + tap];
-      }
-      short h, l;
-      split<PM>(v, h, l);
-      vh[j] = h;
-      vl[j] = l;
+    float v = 0.f;
+    if (kc < KC && co < COUT) {
+      const int tap = kc / CC, ci = (kc % CC) * 8 + j;
+      if (ci < CIN) v = DG ? w[(ci * COUT + co) * KK + (KK - 1 - tap)] : w[(co * CIN + ci) * KK + tap];
     }
-    *reinterpret_cast<s16x8*>(Wh + idx * 8) = vh;
-    if (PM != 2) *reinterpret_cast<s16x8*>(Wl + idx * 8) = vl;
-  }
+    return v;
+  };
+  // PM 0: the weights are scaled by the fixed 2^PAIG_W_EXP (common.h; the
+  // epilogue takes it back out exactly) and range-guarded
+  int ew = 0;
+  float wsc = 1.f;
   // ---- zero the halo columns (never written by the staging)
   if (PADL > 0) {
     for (int i = tid; i < FPT * ROWS * 2 * PADL * CC; i += 256) {
@@ -347,10 +365,10 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       short h, lo;
-      split<PM>(v[c].x, h, lo);
+      split<PM>(v[c].x, h, lo, rmax);
       h0[c] = h;
       l0[c] = lo;
-      split<PM>(v[c].y, h, lo);
+      split<PM>(v[c].y, h, lo, rmax);
       h1[c] = h;
       l1[c] = lo;
     }
@@ -363,9 +381,9 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   };
   float2 pre[UPS ? 1 : NL][8];
   UP up;
-  // dgrad with f16 pieces (PM 0): per-tile scale (see commit)
-  constexpr bool SC = DG && PM == 0;
-  __shared__ float smax[4];
+  // f16 pieces (PM 0): every tile's operand image scaled by one power of two
+  // (tile_max, commit); tinv takes it and the weight exponent back out
+  constexpr bool SC = PM == 0 && PAIG_SCALE_MODE < 2;
   float tsc = 1.f, tinv = 1.f;
   auto issue = [&](int t) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
@@ -397,6 +415,11 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
       __syncthreads();
+      if constexpr (SC) {
+        const int e = f16_scale_exp(fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3])));
+        tsc = __builtin_amdgcn_ldexpf(1.f, e);
+        tinv = __builtin_amdgcn_ldexpf(1.f, -(e + ew));
+      }
 #pragma unroll 1
       for (int i = tid; i < NI; i += 256) {
         const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
@@ -406,29 +429,20 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
         for (int c = 0; c < 8; ++c)
           v[c] = (ok && cc * 8 + c < CIN)
-                     ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp),
-                                   UPX == 2 ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1) : 0.f)
+                     ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp) * tsc,
+                                   UPX == 2 ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1) * tsc : 0.f)
                      : make_float2(0.f, 0.f);
         put_px(i, v);
       }
     } else {
       if constexpr (SC) {
-        // dgrad in f16 pieces: the tile's gradients scaled by one power of
-        // two (max -> [2^14, 2^15)) so they sit in f16's range; the epilogue
-        // undoes it exactly
-        float m = 0.f;
-#pragma unroll
-        for (int l = 0; l < NL; ++l)
-#pragma unroll
-          for (int c = 0; c < 8; ++c) m = fmaxf(m, fmaxf(fabsf(pre[l][c].x), fabsf(pre[l][c].y)));
-        m = wave_max(m);
-        if (lane == 0) smax[wv] = m;
-        __syncthreads();
-        m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
-        int e = 15 - (m > 0.f ? (int)((__builtin_bit_cast(unsigned, m) >> 23) & 255) - 126 : 0);
-        e = e < -100 ? -100 : (e > 100 ? 100 : e);
+        // f16 pieces: the tile's operand (activations, or dgrad's gradients)
+        // scaled by one power of two (max -> [2^14, 2^15)): f16's range and
+        // 22 significant bits for all but negligibly small values; the
+        // epilogue undoes it exactly
+        const int e = f16_scale_exp(fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3])));
         tsc = __builtin_amdgcn_ldexpf(1.f, e);
-        tinv = __builtin_amdgcn_ldexpf(1.f, -e);
+        tinv = __builtin_amdgcn_ldexpf(1.f, -(e + ew));
 #pragma unroll
         for (int l = 0; l < NL; ++l)
 #pragma unroll
@@ -446,11 +460,48 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     }
   };
 
+  // PM 0: this wave's max |operand| of the prefetched tile into smax[wv],
+  // before the loop-top barrier (commit reads it after; the previous tile's
+  // reads finished before the post-commit barrier)
+  auto tile_max = [&]() {
+    float m = 0.f;
+    if constexpr (UPS) {
+      m = up.amax();   // the window bounds its upsampled values
+    } else {
+#pragma unroll
+      for (int l = 0; l < NL; ++l)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) m = fmaxf(m, fmaxf(fabsf(pre[l][c].x), fabsf(pre[l][c].y)));
+    }
+    m = wave_max_u(m);
+    if (lane == 0) smax[wv] = m;
+  };
+
   int lt = blockIdx.x;   // logical tile; xcd_tile() gives the physical one
   if (lt < ntiles) issue(xcd_tile(lt, ntiles));
+  // PM 0: the slice's weights scaled by 2^ew (max |w| into [2^14, 2^15)), so
+  // small weights keep 22 significant bits instead of an f16-subnormal lo
+  // piece; the epilogue takes the exponent back out exactly
+  if constexpr (PM == 0) {
+    ew = PAIG_W_EXP;
+    wsc = __builtin_amdgcn_ldexpf(1.f, ew);
+  }
+  for (int idx = tid; idx < NS * NT * 64; idx += 256) {
+    s16x8 vh, vl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      short h, l;
+      split<PM>(wval(idx, j) * wsc, h, l, rmax);
+      vh[j] = h;
+      vl[j] = l;
+    }
+    *reinterpret_cast<s16x8*>(Wh + idx * 8) = vh;
+    if (PM != 2) *reinterpret_cast<s16x8*>(Wl + idx * 8) = vl;
+  }
   for (; lt < ntiles; lt += gridDim.x) {
     const int tile = xcd_tile(lt, ntiles);
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
+    if constexpr (SC) tile_max();
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
     __syncthreads();
@@ -528,6 +579,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       }
     }
   }
+  if constexpr (PM == 0) f16_range_note(rmax);
 }
 
 // ===================================================================== wgrad
@@ -652,6 +704,16 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
   const int wn = wv % WN, wp = wv / WN;
   constexpr int NRB = H / RT;
+  // PM 0 (f16 pieces): X and dY each scaled by a running power of two (2^ecx,
+  // 2^ecd): a tile's block-wide max |X| / |dY| gives the exponent that puts
+  // it in [2^14, 2^15); when a tile needs a smaller one than the running
+  // exponent, the accumulators (held at scale 2^(ecx + ecd)) are rescaled
+  // first, exactly.  Every element then keeps 22 significant bits or an
+  // absolute error below 2^-40 of the largest (bf16 pieces keep 16 bits; an
+  // unscaled f16 lo piece goes subnormal below |v| = 1/8).
+  int ecx = PAIG_SCALE_MODE < 2 ? 100 : 0, ecd = ecx;
+  float xsc = __builtin_amdgcn_ldexpf(1.f, ecx), dsc = xsc;
+  __shared__ float smax[4], smaxx[4];
 
   auto xplane = [](int cq) { return cq * XPL + ((cq & 1) ? 16 : 0) + ((cq & 2) ? 64 : 0); };
   // ---- zero the halo columns of X (never staged)
@@ -723,13 +785,14 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
     const int o = xplane(cq) + ((fi * ROWS + r) * TWPX + xp + OFFX) * 4;
     s16x8 hv, lv;
+    float xmx = 0.f;   // scaled: below 2^15
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       short h, lo;
-      split<PM>(v[c].x, h, lo);
+      split<PM>(PM == 0 ? v[c].x * xsc : v[c].x, h, lo, xmx);
       hv[c] = h;
       lv[c] = lo;
-      split<PM>(v[c].y, h, lo);
+      split<PM>(PM == 0 ? v[c].y * xsc : v[c].y, h, lo, xmx);
       hv[4 + c] = h;
       lv[4 + c] = lo;
     }
@@ -775,7 +838,93 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
       for (int l = 0; l < NLD; ++l) sd[l] = load_d(t, l);
     }
   };
+  // PM 0 scale exponents.  Operands held in registers before the barrier
+  // (prefetched X / dY, the fused-upsample window) publish their tile max
+  // there (tile_max); the synchronously loaded ones (XSYNC, DSYNC: too many
+  // registers to prefetch) are staged with the running exponent and checked
+  // after the barrier: a tile whose max would overflow f16 at that scale
+  // (the block's first tile, or one > 2x any before) is staged again with
+  // its own exponent.  One pass over the data in the steady state.
+  constexpr bool XSYNC = !UPS && !XPIPE, DSYNC = !DPIPE;
+  __shared__ float srx[4], srd[4];
+  auto rescale = [&](int nx, int nd) {   // block-uniform
+    if (nx + nd < ecx + ecd) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[m][j][r] = __builtin_amdgcn_ldexpf(acc[m][j][r], nx + nd - ecx - ecd);
+    }
+    ecx = nx;
+    ecd = nd;
+    xsc = __builtin_amdgcn_ldexpf(1.f, ecx);
+    dsc = __builtin_amdgcn_ldexpf(1.f, ecd);
+  };
+  // synchronous X staging of tile t (raw max into rx)
+  auto stage_x_sync = [&](int t, float& rx) {
+#pragma unroll 1
+    for (int i = tid; i < NIX; i += 256) {
+      float2 v[4];
+      load_x(t, i, v);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) rx = fmaxf(rx, fmaxf(fabsf(v[c].x), fabsf(v[c].y)));
+      put_x(i, v);
+    }
+  };
+  // dY staging of tile t (raw max into rd; bias partials on the first pass)
+  auto stage_d = [&](int t, float& rd, bool first) {
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int i = tid + l * 256;
+      if (NID % 256 != 0 && i >= NID) break;
+      const int co = i / NPU, pt = DU * (i % NPU);
+      f32x4 dv;
+      if constexpr (DPIPE) dv = sd[l];
+      else dv = load_d(t, l);
+      if (first) bacc[l] += (dv[0] + dv[1]) + (dv[2] + dv[3]);   // zeros past DU; unscaled
+      if constexpr (PM == 0) {
+        if constexpr (DSYNC)
+          rd = fmaxf(rd, fmaxf(fmaxf(fabsf(dv[0]), fabsf(dv[1])), fmaxf(fabsf(dv[2]), fabsf(dv[3]))));
+        dv *= dsc;
+      }
+      s16x4 hv, lv;
+      float dmx = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        short h, lo;
+        split<PM>(dv[e], h, lo, dmx);
+        hv[e] = h;
+        lv[e] = lo;
+      }
+      if constexpr (DU == 4) {
+        *reinterpret_cast<s16x4*>(Dh + co * DP + pt) = hv;
+        if (PM != 2) *reinterpret_cast<s16x4*>(Dl + co * DP + pt) = lv;
+      } else {
+#pragma unroll
+        for (int e = 0; e < DU; ++e) {
+          Dh[co * DP + pt + e] = hv[e];
+          if (PM != 2) Dl[co * DP + pt + e] = lv[e];
+        }
+      }
+    }
+  };
   auto commit = [&](int t) {
+    if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) {
+      // exponents of the register-held operands (published before the
+      // barrier); a smaller one rescales the accumulators exactly
+      int nx = ecx, nd = ecd;
+      if constexpr (!XSYNC) {
+        const int tx = f16_scale_exp(fmaxf(fmaxf(smaxx[0], smaxx[1]), fmaxf(smaxx[2], smaxx[3])));
+        nx = tx < ecx ? tx : ecx;
+      }
+      if constexpr (!DSYNC) {
+        const int td = f16_scale_exp(fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3])));
+        nd = td < ecd ? td : ecd;
+      }
+      if (nx != ecx || nd != ecd) rescale(nx, nd);
+    }
+    float rx = 0.f, rd = 0.f;
     if constexpr (UPS) {
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
@@ -802,49 +951,71 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
         put_x(i, sx[l]);
       }
     } else {
-#pragma unroll 1
-      for (int i = tid; i < NIX; i += 256) {
-        float2 v[4];
-        load_x(t, i, v);
-        put_x(i, v);
+      stage_x_sync(t, rx);
+    }
+    stage_d(t, rd, true);
+    if constexpr (PM == 0 && XSYNC) {
+      rx = wave_max_u(rx);
+      if (lane == 0) srx[wv] = rx;
+    }
+    if constexpr (PM == 0 && DSYNC) {
+      rd = wave_max_u(rd);
+      if (lane == 0) srd[wv] = rd;
+    }
+  };
+  // after the post-commit barrier: re-stage a synchronously loaded operand
+  // whose tile max overflowed f16 at the running scale
+  auto check_sync = [&](int t) {
+    if constexpr (PM == 0 && (XSYNC || DSYNC) && PAIG_SCALE_MODE < 2) {
+      const float mx = XSYNC ? uniform_f(fmaxf(fmaxf(srx[0], srx[1]), fmaxf(srx[2], srx[3]))) : 0.f;
+      const float md = DSYNC ? uniform_f(fmaxf(fmaxf(srd[0], srd[1]), fmaxf(srd[2], srd[3]))) : 0.f;
+      const bool redo_x = XSYNC && mx * xsc >= PAIG_F16_MAX;
+      const bool redo_d = DSYNC && md * dsc >= PAIG_F16_MAX;
+      if (redo_x || redo_d) {   // block-uniform
+        rescale(redo_x ? f16_scale_exp(mx) : ecx, redo_d ? f16_scale_exp(md) : ecd);
+        float r0 = 0.f, r1 = 0.f;
+        if (redo_x) stage_x_sync(t, r0);
+        if (redo_d) stage_d(t, r1, false);
+        __syncthreads();
       }
     }
+  };
+
+  // PM 0: this wave's max |X| / |dY| of tile t for the register-held
+  // operands into smaxx[wv] / smax[wv] (read by commit after the next
+  // barrier; the previous tile's reads finished before the last one)
+  auto tile_max = [&](int t) {
+    if constexpr (!DSYNC) {
+      float m = 0.f;
 #pragma unroll
-    for (int l = 0; l < NLD; ++l) {
-      const int i = tid + l * 256;
-      if (NID % 256 != 0 && i >= NID) break;
-      const int co = i / NPU, pt = DU * (i % NPU);
-      f32x4 dv;
-      if constexpr (DPIPE) dv = sd[l];
-      else dv = load_d(t, l);
-      s16x4 hv, lv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        short h, lo;
-        split<PM>(dv[e], h, lo);
-        hv[e] = h;
-        lv[e] = lo;
-      }
-      bacc[l] += (dv[0] + dv[1]) + (dv[2] + dv[3]);   // zeros past DU
-      if constexpr (DU == 4) {
-        *reinterpret_cast<s16x4*>(Dh + co * DP + pt) = hv;
-        if (PM != 2) *reinterpret_cast<s16x4*>(Dl + co * DP + pt) = lv;
+      for (int l = 0; l < NLD; ++l)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(sd[l][0]), fabsf(sd[l][1])), fmaxf(fabsf(sd[l][2]), fabsf(sd[l][3]))));
+      m = wave_max_u(m);
+      if (lane == 0) smax[wv] = m;
+    }
+    if constexpr (!XSYNC) {
+      float mx = 0.f;
+      if constexpr (UPS) {
+        mx = up.amax();   // the window bounds its upsampled values
       } else {
 #pragma unroll
-        for (int e = 0; e < DU; ++e) {
-          Dh[co * DP + pt + e] = hv[e];
-          if (PM != 2) Dl[co * DP + pt + e] = lv[e];
-        }
+        for (int l = 0; l < NLX; ++l)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) mx = fmaxf(mx, fmaxf(fabsf(sx[l][c].x), fabsf(sx[l][c].y)));
       }
+      mx = wave_max_u(mx);
+      if (lane == 0) smaxx[wv] = mx;
     }
   };
 
   if ((int)blockIdx.x < ntiles) issue(xcd_tile(blockIdx.x, ntiles));
   for (int lt = blockIdx.x; lt < ntiles; lt += gridDim.x) {
     const int tile = xcd_tile(lt, ntiles);
+    if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) tile_max(tile);
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
     __syncthreads();
+    check_sync(tile);
     if (lt + (int)gridDim.x < ntiles) issue(xcd_tile(lt + gridDim.x, ntiles));
 #pragma unroll
     for (int kb = wp; kb < KB; kb += WP) {
@@ -923,6 +1094,7 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
           float v = 0.f;
           for (int p = 0; p < WP; ++p) v += R[((((p * WN + wn) * MT + m) * NTW + j) * 4 + r) * 64 + lane];
           const int co = m * 16 + (lane >> 4) * 4 + r;
+          if constexpr (PM == 0) v = __builtin_amdgcn_ldexpf(v, -(ecx + ecd));   // all waves share them
           if (co < COUTB && cq < NQ && ci < CINB) s[(co0 + co) * NCOL + (ci0 + ci) * KK + tap] = v;
         }
       }
@@ -1066,7 +1238,7 @@ int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nbl
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
     if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
       *rc = b16 ? swg_launch<CI, CO, HH, HH, K, true, 2>(x, dy, slab, nblk_max, nblk_out, F, st)          \
-                : swg_launch<CI, CO, HH, HH, K, true, 1>(x, dy, slab, nblk_max, nblk_out, F, st);         \
+                : swg_launch<CI, CO, HH, HH, K, true, 0>(x, dy, slab, nblk_max, nblk_out, F, st);         \
       return 1;                                                                                           \
     }
     PAIG_SPLIT_UP(PAIG_CASE)
@@ -1076,7 +1248,7 @@ int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nbl
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
   if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                    \
     *rc = b16 ? swg_launch<CI, CO, HH, HH, K, false, 2>(x, dy, slab, nblk_max, nblk_out, F, st)           \
-              : swg_launch<CI, CO, HH, HH, K, false, 1>(x, dy, slab, nblk_max, nblk_out, F, st);          \
+              : swg_launch<CI, CO, HH, HH, K, false, 0>(x, dy, slab, nblk_max, nblk_out, F, st);          \
     return 1;                                                                                             \
   }
   PAIG_SPLIT_WG(PAIG_CASE)
@@ -1103,3 +1275,5 @@ int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks,
 #undef PAIG_CASE
   return 0;
 }
+
+PAIG_F16_RANGE_ACCESSOR(paig_f16_range_conv)

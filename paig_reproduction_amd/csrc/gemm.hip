@@ -216,8 +216,14 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
 // Per K element the three MFMAs cost ~3/16 of the f32-input form, so these
 // GEMMs (K = 3072 / 2000 / 200) fall to the HBM roofline.  math: 1 = f16
 // pieces (22 significant bits; operands must satisfy |v| < 65504: forward
-// activations / weights), 2 = bf16 pieces (16 bits, fp32 range: gradients),
-// 3 = bf16 hi only (the bf16 configuration).
+// activations / weights, range-guarded, see common.h), 4 = f16 pieces with
+// both operands scaled by running block powers of two (each K-tile's max
+// |op(A)| and |op(B)| into [2^14, 2^15); a tile that needs a smaller exponent
+// first rescales the accumulators exactly): any range, and 22 significant
+// bits for every value but the negligibly small (an unscaled f16 lo piece is
+// subnormal below |v| = 1/8); 2 = bf16 pieces (16 bits, fp32 range; kept for the ABI, not used by the
+// step: its gradient errors measured well outside the fp32 envelope), 3 =
+// bf16 hi only (the bf16 configuration).
 // LDS images keep each operand's global orientation: k-contiguous operands
 // as [row][k] (pitch 48, see SPK), row-contiguous operands as [pi(k)][row] (pitch 80) read with
 // ds_read_b64_tr_b16; pi places the 8 k-rows one 32-lane half reads in 8
@@ -243,8 +249,9 @@ __device__ __forceinline__ int kperm(int k) {   // k = 8g + 4h + q
 }
 
 template <int PM>
-__device__ __forceinline__ void gsplit(float v, short& h, short& l) {
-  if constexpr (PM == 1) {
+__device__ __forceinline__ void gsplit(float v, short& h, short& l, float& rmax) {
+  if constexpr (PM == 1 || PM == 4) {
+    rmax = fmaxf(rmax, fabsf(v));
     const _Float16 a = (_Float16)v;
     h = __builtin_bit_cast(short, a);
     l = __builtin_bit_cast(short, (_Float16)(v - (float)a));
@@ -257,7 +264,7 @@ __device__ __forceinline__ void gsplit(float v, short& h, short& l) {
 
 template <int PM>
 __device__ __forceinline__ f32x4 gmma(s16x8 a, s16x8 b, f32x4 c) {
-  if constexpr (PM == 1)
+  if constexpr (PM == 1 || PM == 4)
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
                                                   0, 0);
   else
@@ -265,16 +272,18 @@ __device__ __forceinline__ f32x4 gmma(s16x8 a, s16x8 b, f32x4 c) {
                                                    0, 0, 0);
 }
 
-// 16-bit image of one 64 x BK operand tile (the fp32 Tile registers, split)
+// 16-bit image of one 64 x BK operand tile (the fp32 Tile registers times
+// sc, split)
 template <bool KCONTIG, int PM>
-__device__ __forceinline__ void store16(const Tile<KCONTIG>& t, short* ih, short* il, int tid) {
+__device__ __forceinline__ void store16(const Tile<KCONTIG>& t, short* ih, short* il, int tid, float sc,
+                                        float& rmax) {
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     s16x4 hv, lv;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       short h, l;
-      gsplit<PM>(t.v[e][i], h, l);
+      gsplit<PM>(t.v[e][i] * sc, h, l, rmax);
       hv[i] = h;
       lv[i] = l;
     }
@@ -328,6 +337,10 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 rs4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rmax = 0.f;                                   // f16 range guard (PM 1; PM 4 never trips)
+  int eca = 100, ecb = 100;                           // PM 4: operand scales 2^eca, 2^ecb
+  float asc = PM == 4 ? __builtin_amdgcn_ldexpf(1.f, 100) : 1.f, bsc = asc;
+  __shared__ float smx[8];
 
   // register ring of NS K-tiles: the loads of tile k + NS are issued right
   // after tile k is parked in LDS, so NS-1 tiles stay in flight behind the
@@ -346,9 +359,44 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
     for (int st = 0; st < NS; ++st) {
       const int kk = k0 + st * BK;
       if (kk >= kend) break;
+      if constexpr (PM == 4) {
+        // this K-tile's max |op(A)|, |op(B)|, published before the barrier
+        // (the previous tile's smx reads finished before the last one)
+        float ma = 0.f, mb = 0.f;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            ma = fmaxf(ma, fabsf(ta[st].v[e][i]));
+            mb = fmaxf(mb, fabsf(tb[st].v[e][i]));
+          }
+        ma = wave_max_u(ma);
+        mb = wave_max_u(mb);
+        if (lane == 0) {
+          smx[wv] = ma;
+          smx[4 + wv] = mb;
+        }
+      }
       __syncthreads();
-      store16<!TA, PM>(ta[st], Ah, Al, tid);
-      store16<TB, PM>(tb[st], Bh, Bl, tid);
+      if constexpr (PM == 4) {
+        const int ta_ = f16_scale_exp(fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3])));
+        const int tb_ = f16_scale_exp(fmaxf(fmaxf(smx[4], smx[5]), fmaxf(smx[6], smx[7])));
+        const int na = ta_ < eca ? ta_ : eca, nb = tb_ < ecb ? tb_ : ecb;
+        if (na + nb < eca + ecb) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[i][j][r] = __builtin_amdgcn_ldexpf(acc[i][j][r], na + nb - eca - ecb);
+          eca = na;
+          ecb = nb;
+          asc = __builtin_amdgcn_ldexpf(1.f, eca);
+          bsc = __builtin_amdgcn_ldexpf(1.f, ecb);
+        }
+      }
+      store16<!TA, PM>(ta[st], Ah, Al, tid, asc, rmax);
+      store16<TB, PM>(tb[st], Bh, Bl, tid, bsc, rmax);
       if (do_rs) rs4 += ta[st].v[0] + ta[st].v[1];
       __syncthreads();
       if (kk + NS * BK < kend) {
@@ -401,7 +449,7 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
         const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
         const int n = n0 + wn * 32 + j * 16 + (lane & 15);
         if (m < M && n < N) {
-          float v = alpha * acc[i][j][r];
+          float v = alpha * (PM == 4 ? __builtin_amdgcn_ldexpf(acc[i][j][r], -(eca + ecb)) : acc[i][j][r]);
           if (part) {
             part[((long long)bt.z * M + m) * N + n] = v;
           } else {
@@ -411,6 +459,7 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
           }
         }
       }
+  if constexpr (PM == 1) f16_range_note(rmax);
 }
 
 // sum_{s<S} p[s*ld] in order s = 0..S-1 (deterministic), loads issued 8 at a
@@ -526,6 +575,7 @@ static void launch_gemm(int math, dim3 grid, hipStream_t st, int M, int N, int K
   if (math == 1) PAIG_L((gemm_split_k<TA, TB, 1>));
   else if (math == 2) PAIG_L((gemm_split_k<TA, TB, 2>));
   else if (math == 3) PAIG_L((gemm_split_k<TA, TB, 3>));
+  else if (math == 4) PAIG_L((gemm_split_k<TA, TB, 4>));
   else PAIG_L((gemm_k<TA, TB>));
 #undef PAIG_L
 }
@@ -556,8 +606,8 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
                  const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,
                  void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (math < 0 || math > 3) {
-    paig_set_error("paig_gemm_ex: math must be 0..3, got %d", math);
+  if (math < 0 || math > 4) {
+    paig_set_error("paig_gemm_ex: math must be 0..4, got %d", math);
     return PAIG_E_UNSUPPORTED;
   }
   if (rowsum && !ta) math = 0;   // fused row sums exist on the split path for op(A) = A^T only
@@ -599,3 +649,5 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
 }
 
 }  // extern "C"
+
+PAIG_F16_RANGE_ACCESSOR(paig_f16_range_gemm)

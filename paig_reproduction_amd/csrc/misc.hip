@@ -304,6 +304,23 @@ const char* paig_last_error(void) { return g_err; }
 
 int paig_abi_version(void) { return 1; }
 
+// f16 range guard (common.h): waits for the device, then reads (and with
+// clear != 0 resets) the flags the split-precision kernels set when an
+// unscaled f16 operand reached |v| >= 65504.  1 = flagged, 0 = clean.
+int paig_f16_range_status(int clear) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    paig_set_error("paig_f16_range_status: %s", hipGetErrorString(e));
+    return -(int)e;
+  }
+  const int a = paig_f16_range_conv(clear), b = paig_f16_range_gemm(clear);
+  if (a < 0 || b < 0) {
+    paig_set_error("paig_f16_range_status: flag read failed");
+    return -1;
+  }
+  return (a | b) ? 1 : 0;
+}
+
 // y[P] = W2 tanh(W1 1 + b1) + b2 ; hout[200] ; ypost = sigmoid(y) if non-null
 int paig_vfn_fwd_multi(int n, const float* const* W1, const float* const* b1, const float* const* W2,
                        const float* const* b2, float* const* hout, float* const* y, float* const* ypost, const int* P,

@@ -171,23 +171,25 @@ class Layout:
 
 
 class KernelProbe:
-    """Times every launch of ONE tagged kernel with HIP events recorded on the
-    stream it is launched on (bench.py's roofline numbers)."""
+    """Times every launch of one tagged kernel (``tag``), or of every tagged
+    kernel (``tag=None``), with HIP events recorded on the stream it is
+    launched on: the main stream; the side-stream chains are not tagged
+    (bench.py's roofline numbers)."""
 
     backlog_cycles = 1 << 20
 
     def __init__(self, tag):
         self.tag = tag
-        self.events = []
-        self.flops = 0
-        self.nbytes = 0
+        self.events = {}
+        self.work = {}
 
     def wrap(self, tag, flops, nbytes=0):
         probe = self
+        want = probe.tag is None or tag == probe.tag
 
         class _Ctx:
             def __enter__(self):
-                if tag == probe.tag:
+                if want:
                     self.e0 = torch.cuda.Event(enable_timing=True)
                     self.e1 = torch.cuda.Event(enable_timing=True)
                     # a spin kernel first: the stream is then backlogged when the
@@ -198,22 +200,27 @@ class KernelProbe:
                 return self
 
             def __exit__(self, *exc):
-                if tag == probe.tag:
+                if want:
                     self.e1.record()
-                    probe.events.append((self.e0, self.e1))
-                    probe.flops = flops
-                    probe.nbytes = nbytes
+                    probe.events.setdefault(tag, []).append((self.e0, self.e1))
+                    probe.work[tag] = (flops, nbytes)
                 return False
 
         return _Ctx()
 
-    def summary(self):
-        if not self.events:
-            return None
+    def summaries(self):
+        """{tag: {tag, n, avg_ms, flops, bytes}} (per launch)."""
         torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b in self.events]
-        return {"tag": self.tag, "n": len(ms), "avg_ms": sum(ms) / len(ms), "flops": self.flops,
-                "bytes": self.nbytes}
+        out = {}
+        for tag, evs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            fl, nb = self.work[tag]
+            out[tag] = {"tag": tag, "n": len(ms), "avg_ms": sum(ms) / len(ms), "flops": fl, "bytes": nb}
+        return out
+
+    def summary(self):
+        s = self.summaries()
+        return s.get(self.tag) if self.tag is not None else None
 
 
 class _NoProbe:
@@ -252,15 +259,15 @@ class Engine:
         # (FlatParams.allreduce_early by default; bench.py splits its HIP graph here)
         self.bucket_hook = model._flat.allreduce_early
 
-    # conv arithmetic (include/paig_hip.h flags): "split" = f16 hi/lo forward and
-    # bf16 hi/lo dgrad/wgrad on the 16-bit matrix cores (fp32-accurate: the
-    # north-star 1e-4 bar), "fp32" = f32-input MFMA, "bf16" = bf16 operands
-    # (BASELINE config #2)
+    # conv arithmetic (include/paig_hip.h flags): "split" = f16 hi/lo pieces on
+    # the 16-bit matrix cores, operands scaled by powers of two (fp32-accurate:
+    # within 3x the fp32 reference's own error, tests/test_gpu_envelope.py),
+    # "fp32" = f32-input MFMA, "bf16" = bf16 operands (BASELINE config #2)
     CONV_MATH = {"split": 128, "fp32": 0, "bf16": 256}
 
-    # the same choice for the dense layers (paig_gemm_ex math): forward GEMMs
-    # take f16 pieces, gradient GEMMs bf16 pieces
-    GEMM_MATH = {"split": (1, 2), "fp32": (0, 0), "bf16": (3, 3)}
+    # the same choice for the dense layers (paig_gemm_ex math): f16 pieces with
+    # both operands scaled by powers of two, forward and backward
+    GEMM_MATH = {"split": (4, 4), "fp32": (0, 0), "bf16": (3, 3)}
 
     def gemm_math(self, backward):
         return self.GEMM_MATH[getattr(self.model, "conv_math", "split")][1 if backward else 0]
@@ -270,6 +277,15 @@ class Engine:
         if m not in self.CONV_MATH:
             raise ValueError(f"conv_math must be one of {sorted(self.CONV_MATH)}, got {m!r}")
         return self.CONV_MATH[m]
+
+    @staticmethod
+    def _dec_bytes(n, lay, bwd, slab_floats=0):
+        """Algorithmic HBM bytes of one decoder launch over n frames: the
+        target frames read (fused SSE) and the decoded frames written (fwd) /
+        the position grads and partial source-grad slab rows written (bwd);
+        positions and the step-constant sources (< 100 KB) are negligible."""
+        frames = n * lay.frame * 4
+        return frames + (n * 2 * lay.D * 4 + slab_floats * 4 if bwd else frames)
 
     def _p(self, tag, flops=0, nbytes=0):
         """Probe context of one launch: algorithmic FLOPs and HBM bytes (the
@@ -288,7 +304,7 @@ class Engine:
         """out[rows, O] = act(x[rows, I] W^T + b) ; W = name.weight [O, I]"""
         W, b = self.p(name + ".weight"), self.p(name + ".bias")
         O, I = W.shape
-        with self._p("gemm_fwd:" + name, 2 * rows * O * I):
+        with self._p("gemm_fwd:" + name, 2 * rows * O * I, 4 * (rows * I + O * I + rows * O)):
             self.L.paig_gemm_ex(0, 1, rows, O, I, 1.0, ptr(x), I, ptr(W), I, 0.0, ptr(out), O, ptr(b), act, 0, None,
                                 0, None, ptr(ws), ws.numel() if ws is not None else 0, self.gemm_math(False), st)
 
@@ -298,11 +314,11 @@ class Engine:
         O, I = W.shape
         gW, gb = self.g(name + ".weight"), self.g(name + ".bias")
         n_ws = ws.numel()
-        with self._p("gemm_wgrad:" + name, 2 * rows * O * I):
+        with self._p("gemm_wgrad:" + name, 2 * rows * O * I, 4 * (rows * O + rows * I + O * I + O)):
             self.L.paig_gemm_ex(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
                                 ptr(gb), ptr(ws), n_ws, self.gemm_math(True), st)
         if need_dx:
-            with self._p("gemm_dgrad:" + name, 2 * rows * O * I):
+            with self._p("gemm_dgrad:" + name, 2 * rows * O * I, 4 * (rows * O + O * I + 2 * rows * I)):
                 self.L.paig_gemm_ex(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm,
                                     ptr(aux), I, None, ptr(ws), n_ws, self.gemm_math(True), st)
 
@@ -454,16 +470,18 @@ class Engine:
         L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0), ptr(prm[0]),
                            ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, sst)
         # ---- (main) reconstruction decode (all B*Te frames, SSE vs input fused)
-        L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons), lay.frame,
-                           x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, st)
+        with self._p("dec_fwd:recon", 0, self._dec_bytes(F, lay, False)):
+            L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons), lay.frame,
+                               x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, st)
         self._join(dev)
 
         # ---- rollout decode (all B*R frames in one launch, SSE vs input[:, ins:])
         out = _empty(B * lay.R * lay.frame, dev)
         sse_roll = _empty(B * lay.R, dev)
         tgt_roll = (ptr(x) + lay.ins * lay.frame * 4, T * lay.frame, lay.R, lay.frame)
-        L.paig_decoder_fwd(ptr(pvs) + 2 * D * 4, (lay.R + 1) * 2 * D, 2 * D, lay.R, ptr(tmpl), ptr(cont), ptr(bgp),
-                           ptr(out), lay.frame, *tgt_roll, ptr(sse_roll), B * lay.R, K, h, H, st)
+        with self._p("dec_fwd:rollout", 0, self._dec_bytes(B * lay.R, lay, False)):
+            L.paig_decoder_fwd(ptr(pvs) + 2 * D * 4, (lay.R + 1) * 2 * D, 2 * D, lay.R, ptr(tmpl), ptr(cont),
+                               ptr(bgp), ptr(out), lay.frame, *tgt_roll, ptr(sse_roll), B * lay.R, K, h, H, st)
         S["tgt_roll"] = tgt_roll
         S["x_view"] = x_view
 
@@ -553,9 +571,10 @@ class Engine:
         vparts = [_empty(L.paig_vfn_bwd_blocks(P) * 200, dev) for _, P, _, _ in vfn]
 
         # ---- (main) rollout-frame decoder backward: d rollout positions + partial source grads
-        L.paig_decoder_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
-                           *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
-                           ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, K, h, H, st)
+        with self._p("dec_bwd:rollout", 0, self._dec_bytes(B * R, lay, True, nb_roll * slab_len)):
+            L.paig_decoder_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
+                               *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
+                               ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, K, h, H, st)
 
         sst = self._fork(dev)
         # ---- (side) rollout adjoint -> d pos0, d vel0, physics params
@@ -582,8 +601,10 @@ class Engine:
                 S["extra_slabs"].append((vslab, vblk, vlen, g0))
 
         # ---- (main) reconstruction decoder backward, source-grad reduction, VFN backward
-        L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
-                           ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, K, h, H, st)
+        with self._p("dec_bwd:recon", 0, self._dec_bytes(F, lay, True, nb_rec * slab_len)):
+            L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
+                               ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, K, h,
+                               H, st)
         L.paig_slab_reduce_multi(1, (ctypes.c_void_p * 1)(ptr(slab)), (ctypes.c_int * 1)(nb_rec + nb_roll),
                                  (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, st)
         if d_enc_pos is not None:

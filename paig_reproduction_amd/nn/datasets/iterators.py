@@ -72,7 +72,14 @@ class DeviceDataIterator(DataIterator):
     ``X_u8``: uint8 [N, T, H, W, C] (the npz layout); ``shape``: the per-example
     model shape the bytes are reinterpreted as (Q5: (T, C, H, W)).
     next_batch returns a float32 device tensor [B, *shape] gathered by
-    paig_gather_u8_f32; ``X`` is the device uint8 tensor (``X.shape[0]`` is N)."""
+    paig_gather_u8_f32; ``X`` is the device uint8 tensor (``X.shape[0]`` is N).
+
+    The epoch permutation is drawn on the host exactly as DataIterator draws it
+    (same RNG calls, same batches) and uploaded once per epoch; a batch is then
+    a slice of that device permutation, so a step issues no host-to-device
+    copy at all, only the gather launch.  ``out`` (next_batch / gather_into)
+    lets a caller gather into a fixed buffer, e.g. the input of a captured
+    HIP graph."""
 
     def __init__(self, X_u8, shape, device, seed=None, rank=0, world=1):
         import torch
@@ -80,23 +87,52 @@ class DeviceDataIterator(DataIterator):
         self.row = int(np.prod(X_u8.shape[1:]))
         assert self.row == int(np.prod(self.shape)), (X_u8.shape, shape)
         self.device = torch.device(device)
+        self.idx_d = None
         super().__init__(torch.from_numpy(np.ascontiguousarray(X_u8)).to(self.device), None, seed, rank, world)
 
-    def _gather(self, idx):
+    def reset_iteration(self):
         import torch
-        from paig_reproduction_amd._lib import lib, ptr, stream_handle
-        idx = np.asarray(idx, dtype=np.int64)
-        assert idx.size == 0 or (idx.min() >= 0 and idx.max() < self.num_examples)
-        out = torch.empty((idx.size,) + self.shape, device=self.device)
-        if idx.size:
-            idx_d = torch.from_numpy(idx).pin_memory().to(self.device, non_blocking=True)
-            lib().paig_gather_u8_f32(ptr(self.X), ptr(idx_d), ptr(out), int(idx.size), self.row,
+        super().reset_iteration()
+        # stream-ordered upload of this epoch's permutation (gathers of the
+        # previous epoch that are still queued read their own buffer)
+        self.idx_d = torch.from_numpy(self.indices.astype(np.int64)).pin_memory().to(self.device, non_blocking=True)
+
+    def _launch(self, idx_ptr, n, out):
+        from paig_reproduction_amd._lib import lib, stream_handle
+        if n:
+            lib().paig_gather_u8_f32(self.X.data_ptr(), idx_ptr, out.data_ptr(), int(n), self.row,
                                      stream_handle(self.device))
         return out
 
-    def next_batch(self, batch_size, data_type="train", shuffle=True):
+    def _out(self, n, out):
+        import torch
+        if out is None:
+            return torch.empty((n,) + self.shape, device=self.device)
+        assert out.is_contiguous() and out.dtype == torch.float32 and tuple(out.shape) == (n,) + self.shape, \
+            (tuple(out.shape), out.dtype)
+        return out
+
+    def _gather(self, idx, out=None):
+        """Rows ``idx`` (host indices) -> float32 [len(idx), *shape]."""
+        import torch
+        idx = np.asarray(idx, dtype=np.int64)
+        assert idx.size == 0 or (idx.min() >= 0 and idx.max() < self.num_examples)
+        out = self._out(idx.size, out)
+        if idx.size:
+            idx_d = torch.from_numpy(idx).pin_memory().to(self.device, non_blocking=True)
+            self._launch(idx_d.data_ptr(), idx.size, out)
+        return out
+
+    def next_batch(self, batch_size, data_type="train", shuffle=True, out=None):
         assert data_type in ["train", "val", "test"], "data_type must be 'train', 'val', or 'test'."
-        return self._gather(self._take(batch_size)), None
+        # the same bookkeeping as DataIterator._take, on the device permutation
+        lo = self.start_idx + self.rank * batch_size
+        n = max(0, min(batch_size, self.num_examples - lo))
+        idx_d = self.idx_d
+        out = self._out(n, out)
+        self._launch(idx_d.data_ptr() + 8 * lo, n, out)
+        self._take(batch_size)   # advances start_idx / epoch (may upload the next permutation)
+        return out, None
 
     def sample_random_batch(self, batch_size):
         np.random.randint(0, self.num_examples - batch_size)   # reference quirk (iterators.py:42-47)
