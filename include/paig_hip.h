@@ -183,6 +183,23 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
                      long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
                      float* slab, float* scratch, int F, int K, int h, int H, void* stream);
 
+/* the decoder's per-object intermediates (transf_contents / transf_masks,
+ * physics_models.py:186-196) for positions pos [F][2K] (row stride
+ * pos_inner): contents [K+1][F][3][H][W] (the K warped sigmoid(content_k)
+ * and the tiled background), masks [K+1][F][3][H][W] (softmax weights) */
+int paig_decoder_parts(const float* pos, long long pos_inner, const float* tmpl, const float* cont, const float* bg,
+                       float* contents, float* masks, int F, int K, int h, int H, void* stream);
+/* general affine STN, stn() stn.py:5-16 (affine_grid + grid_sample: bilinear,
+ * zeros padding, align_corners=False): U [N][C][Hi][Wi], theta [N][2][3] ->
+ * out [N][C][Ho][Wo]; the backward writes dU (accumulated: zero it first;
+ * nullable) and dtheta [N][2][3] (nullable) */
+int paig_stn_fwd(const float* U, const float* theta, float* out, int N, int C, int Hi, int Wi, int Ho, int Wo,
+                 void* stream);
+int paig_stn_bwd(const float* U, const float* theta, const float* dout, float* dU, float* dtheta, int N, int C,
+                 int Hi, int Wi, int Ho, int Wo, void* stream);
+/* d *= (y > 0) in place (n elements) */
+int paig_relu_mask(const float* y, float* d, long long n, void* stream);
+
 /* ---- losses (physics_models.py:119-142): means of the per-frame SSE;
  *      extrap is NaN when there are no extrapolation steps (mean of empty) */
 /* pred_out receives train = pred + ae * recons (ae > 0; the reference's

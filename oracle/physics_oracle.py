@@ -166,6 +166,29 @@ def st_decoder(cfg, joint, bg, pos):
     return sum(masks[:, i] * conts[i] for i in range(K + 1))
 
 
+def st_decoder_parts(cfg, joint, bg, pos):
+    """transf_contents / transf_masks of conv_st_decoder
+    (nn/network/physics_models.py:186-196): K warped contents + the tiled
+    background, and the K+1 softmax masks, each [N, 3, H, W]."""
+    K, h, H = cfg.n_objs, cfg.tmpl, cfg.size
+    N = pos.shape[0]
+    outs = []
+    for k in range(K):
+        loc = pos[:, 2 * k:2 * k + 2]
+        one = torch.ones(N, dtype=torch.float64)
+        zero = torch.zeros(N, dtype=torch.float64)
+        t2 = ((H / 2 - loc[:, 0]) / h).double()
+        t5 = ((H / 2 - loc[:, 1]) / h).double()
+        theta = torch.stack([one, zero, t2, zero, one, t5], 1).view(-1, 2, 3)
+        grid = F.affine_grid(theta, [N, 6, H, H], align_corners=False)
+        o = F.grid_sample(joint[k:k + 1].expand(N, -1, -1, -1), grid.to(joint.dtype), mode="bilinear",
+                          padding_mode="zeros", align_corners=False)
+        outs.append((o[:, :3], o[:, 3:]))
+    contents = [c for _, c in outs] + [bg.expand(N, -1, -1, -1)]
+    masks = torch.softmax(torch.stack([t - 5 for t, _ in outs] + [torch.ones_like(outs[0][0])], 1), 1)
+    return contents, torch.unbind(masks, 1)
+
+
 def velocity_encoder(P, cfg, pos_in):
     """VelocityEncoder.forward, nn/network/blocks.py:31-49.  pos_in [B, in, D] -> [B, D]."""
     K, ins = cfg.n_objs, cfg.input_steps
@@ -312,6 +335,77 @@ def train_step_f64(state, cfg, x, with_grads=True):
         return train_step({k: v.double() for k, v in state.items()}, cfg, x.double(), with_grads)
     finally:
         torch.set_default_dtype(prev)
+
+
+def train_trajectory(state, cfg, xs, lr, steps, f64=False):
+    """``steps`` fresh-mode steps with torch.optim.RMSprop semantics
+    (nn/network/base.py:141-152, :14 defaults), batch xs[s % len(xs)].
+    Returns (per-step [train, pred(aliased: = train, Q2), extrap, recons],
+    final state).  f64: the whole loop in float64 (the envelope)."""
+    prev = torch.get_default_dtype()
+    if f64:
+        torch.set_default_dtype(torch.float64)
+        state = {k: v.double() for k, v in state.items()}
+        xs = [x.double() for x in xs]
+    try:
+        state = {k: v.detach().clone() for k, v in state.items()}
+        live = live_params(state, cfg)
+        sq = {k: torch.zeros_like(state[k]) for k in live}
+        losses = []
+        for s in range(steps):
+            x = xs[s % len(xs)]
+            out, L, grads = train_step(state, cfg, x)
+            t = float(L["train"].detach())
+            losses.append([t, t, float(L["extrap"].detach()), float(L["recons"].detach())])
+            with torch.no_grad():
+                for k, g in grads.items():
+                    rmsprop_step(state[k], g, sq[k], lr)
+        return losses, state
+    finally:
+        torch.set_default_dtype(prev)
+
+
+def reference_mode_steps(state, cfg, x_eval, xs, lr):
+    """The reference's ACTUAL training step (quirk Q1, nn/network/base.py:141-143
+    vs :195): ``self.output`` is the last eval forward's (no grad); each train
+    step's loss reads it for pred/extrap while the gradient reaches only the
+    current forward's reconstruction term (encoder + decoder sources; the
+    rollout, velocity MLP and physics parameters get None and RMSprop skips
+    them).  Returns (per-step losses, first step's grads, final state)."""
+    state = {k: v.detach().clone() for k, v in state.items()}
+    live = live_params(state, cfg)
+    sq = {k: torch.zeros_like(state[k]) for k in live}
+    with torch.no_grad():
+        stale = forward(state, cfg, x_eval)["output_seq"]
+    losses, g0 = [], None
+    for x in xs:
+        P = {k: (v.requires_grad_(True) if k in live else v) for k, v in state.items()}
+        out = forward(P, cfg, x)
+        rl = torch.sum(torch.square(x[:, :cfg.Te] - out["recons_out"]), dim=[2, 3, 4]).mean()
+        L = torch.sum(torch.square(x[:, cfg.input_steps:] - stale), dim=[2, 3, 4])
+        pred, extrap = L[:, :cfg.pred_steps].mean(), L[:, cfg.pred_steps:].mean()
+        train = pred + cfg.ae * rl if cfg.ae > 0.0 else pred
+        t = float(train.detach())
+        losses.append([t, t, float(extrap), float(rl.detach())])
+        train.backward()
+        grads = {k: P[k].grad for k in live if P[k].grad is not None}
+        if g0 is None:
+            g0 = {k: g.clone() for k, g in grads.items()}
+        with torch.no_grad():
+            for k, g in grads.items():
+                rmsprop_step(state[k], g, sq[k], lr)
+        state = {k: v.detach() for k, v in state.items()}
+    return losses, g0, state
+
+
+def eval_metrics(state, cfg, x):
+    """eval_performance over ONE whole-set batch (Q15), nn/network/base.py:174-211:
+    {eval_pred_loss (= train, Q2), eval_extrap_loss, eval_recons_loss} and the outputs."""
+    with torch.no_grad():
+        out = forward(state, cfg, x)
+        L = losses(cfg, x, out)
+    return {"eval_pred_loss": float(L["train"]), "eval_extrap_loss": float(L["extrap"]),
+            "eval_recons_loss": float(L["recons"])}, out
 
 
 def rmsprop_step(param, grad, square_avg, lr, alpha=0.99, eps=1e-8):

@@ -68,6 +68,10 @@ SIGNATURES = {
     "paig_decoder_slab_len": (SZ, [I, I, I]),
     "paig_decoder_bwd_scratch": (SZ, [I, I, I, I]),
     "paig_decoder_bwd": (I, [P, LL, LL, I, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, P]),
+    "paig_decoder_parts": (I, [P, LL, P, P, P, P, P, I, I, I, I, P]),
+    "paig_stn_fwd": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "paig_stn_bwd": (I, [P, P, P, P, P, I, I, I, I, I, I, P]),
+    "paig_relu_mask": (I, [P, P, LL, P]),
     "paig_loss_reduce": (I, [P, P, I, I, I, I, F32, P, P, P, P]),
     "paig_loss_bwd": (I, [P, P, P, F32, P, P, I, I, I, I, P]),
     "paig_frame_sse": (I, [P, LL, I, LL, P, LL, I, LL, P, I, I, P]),
@@ -81,7 +85,7 @@ SIGNATURES = {
     "paig_sgd_f64": (I, [P, P, P, LL, F64, F64, I, P]),
 }
 
-_QUERY = {"paig_last_error", "paig_abi_version", "paig_conv2d_mfma_supported", "paig_velmlp_bwd_blocks",
+_QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported", "paig_velmlp_bwd_blocks",
           "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_gemm_workspace", "paig_colsum_workspace",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
           "paig_decoder_bwd_scratch"}

@@ -744,6 +744,144 @@ static int dec_launch_fwd(PosView pv, Src S, FViewW out, FView tgt, float* sse, 
   return 0;
 }
 
+// The reference decoder's intermediate per-object tensors (attributes
+// transf_contents / transf_masks, physics_models.py:186-196): for every frame
+// the K warped contents sigmoid(content_k) o warp_k, the tiled background, and
+// the K+1 compositing masks (softmax over [template_k o warp_k, 1]), each
+// [F][3][H][W] (the mask is the same on the 3 channels, as the reference's
+// 3-channel template makes it).  Off the hot path: computed on request.
+template <int K>
+__global__ void __launch_bounds__(256)
+dec_parts_k(PosView pos, Src S, float* __restrict__ contents, float* __restrict__ masks, int F, int h, int H) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int hh = h * h, HW = H * H;
+  float* T = lds;
+  float* Cn = T + K * hh;
+  __shared__ float cx[K][MAXH], cy[K][MAXH];
+  __shared__ double bc[MAXH];
+  init_base(bc, H);
+  stage_sources<K>(S, h, T, Cn);
+  const long long plane = (long long)F * 3 * HW;   // one [F][3][H][W] tensor
+  for (int f = blockIdx.x; f < F; f += gridDim.x) {
+    __syncthreads();
+    coord_tables<K>(pos.at(f), H, h, cx, cy, bc);
+    __syncthreads();
+    for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+      const int i = p / H, j = p % H;
+      Bil bl[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) bl[k] = bil(cx[k][j], cy[k][i]);
+      float o[3], m[K + 1], cs[K][3];
+      composite<K>(T, Cn, S.bg, HW, p, h, bl, o, m, cs);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const long long at = ((long long)f * 3 + c) * HW + p;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          contents[k * plane + at] = cs[k][c];
+          masks[k * plane + at] = m[k];
+        }
+        contents[K * plane + at] = S.bg[c * HW + p];
+        masks[K * plane + at] = m[K];
+      }
+    }
+  }
+}
+
+// General affine spatial transformer (stn(), nn/network/stn.py:5-16: aten
+// affine_grid + grid_sample, bilinear, zeros padding, align_corners=False)
+// for any theta [N][2][3]: U [N][C][Hi][Wi] -> O [N][C][Ho][Wo].  The grid is
+// formed in fp32 (the reference casts it with .float() before sampling).
+__device__ __forceinline__ float ag_base(int j, int n) {   // affine_grid linspace * (n-1)/n, fp32
+  const float step = 2.f / (float)(n - 1 > 0 ? n - 1 : 1);
+  const float v = n == 1 ? 0.f : ((j < n / 2) ? -1.f + step * (float)j : 1.f - step * (float)(n - 1 - j));
+  return v * (float)(n - 1) / (float)n;
+}
+
+__global__ void __launch_bounds__(256)
+stn_fwd_k(const float* __restrict__ U, const float* __restrict__ th, float* __restrict__ O, int N, int C, int Hi,
+          int Wi, int Ho, int Wo) {
+  const long long total = (long long)N * Ho * Wo;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(t / (Ho * Wo)), p = (int)(t % (Ho * Wo)), i = p / Wo, j = p % Wo;
+    const float* a = th + n * 6;
+    const float xb = ag_base(j, Wo), yb = ag_base(i, Ho);
+    const float gx = a[0] * xb + a[1] * yb + a[2], gy = a[3] * xb + a[4] * yb + a[5];
+    const float ix = ((gx + 1.f) * (float)Wi - 1.f) * 0.5f, iy = ((gy + 1.f) * (float)Hi - 1.f) * 0.5f;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float fx = ix - fx0, fy = iy - fy0;
+    const float w[4] = {(1.f - fx) * (1.f - fy), fx * (1.f - fy), (1.f - fx) * fy, fx * fy};
+    const int xs[4] = {x0, x0 + 1, x0, x0 + 1}, ys[4] = {y0, y0, y0 + 1, y0 + 1};
+    for (int c = 0; c < C; ++c) {
+      const float* u = U + ((long long)n * C + c) * Hi * Wi;
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (xs[q] >= 0 && xs[q] < Wi && ys[q] >= 0 && ys[q] < Hi) v += w[q] * u[ys[q] * Wi + xs[q]];
+      O[((long long)n * C + c) * Ho * Wo + p] = v;
+    }
+  }
+}
+
+// backward: dU by atomics (scatter of the bilinear weights; this general
+// helper is off the training path), dtheta per sample by a block reduction
+// (one block per sample, deterministic)
+__global__ void __launch_bounds__(256)
+stn_bwd_k(const float* __restrict__ U, const float* __restrict__ th, const float* __restrict__ dO, float* __restrict__ dU,
+          float* __restrict__ dth, int N, int C, int Hi, int Wi, int Ho, int Wo) {
+  const int n = blockIdx.x;
+  const float* a = th + n * 6;
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = threadIdx.x; p < Ho * Wo; p += blockDim.x) {
+    const int i = p / Wo, j = p % Wo;
+    const float xb = ag_base(j, Wo), yb = ag_base(i, Ho);
+    const float gx = a[0] * xb + a[1] * yb + a[2], gy = a[3] * xb + a[4] * yb + a[5];
+    const float ix = ((gx + 1.f) * (float)Wi - 1.f) * 0.5f, iy = ((gy + 1.f) * (float)Hi - 1.f) * 0.5f;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float fx = ix - fx0, fy = iy - fy0;
+    float dix = 0.f, diy = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float* u = U + ((long long)n * C + c) * Hi * Wi;
+      float* du = dU ? dU + ((long long)n * C + c) * Hi * Wi : nullptr;
+      const float g = dO[((long long)n * C + c) * Ho * Wo + p];
+      auto tapv = [&](int y, int x) { return (x >= 0 && x < Wi && y >= 0 && y < Hi) ? u[y * Wi + x] : 0.f; };
+      const float nw = tapv(y0, x0), ne = tapv(y0, x0 + 1), sw = tapv(y0 + 1, x0), se = tapv(y0 + 1, x0 + 1);
+      dix += g * ((ne - nw) * (1.f - fy) + (se - sw) * fy);
+      diy += g * ((sw - nw) * (1.f - fx) + (se - ne) * fx);
+      if (du) {
+        const float w[4] = {(1.f - fx) * (1.f - fy), fx * (1.f - fy), (1.f - fx) * fy, fx * fy};
+        const int xs[4] = {x0, x0 + 1, x0, x0 + 1}, ys[4] = {y0, y0, y0 + 1, y0 + 1};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (xs[q] >= 0 && xs[q] < Wi && ys[q] >= 0 && ys[q] < Hi) atomicAdd(du + ys[q] * Wi + xs[q], g * w[q]);
+      }
+    }
+    // ix = ((gx + 1) Wi - 1) / 2 -> dgx = dix * Wi / 2 ; gx = a0 xb + a1 yb + a2
+    const float dgx = dix * (float)Wi * 0.5f, dgy = diy * (float)Hi * 0.5f;
+    acc[0] += dgx * xb;
+    acc[1] += dgx * yb;
+    acc[2] += dgx;
+    acc[3] += dgy * xb;
+    acc[4] += dgy * yb;
+    acc[5] += dgy;
+  }
+  __shared__ float red[4][6];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const float v = wave_sum(acc[q]);
+    if (lane == 0) red[wv][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6 && dth) {
+    float v = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += red[w][threadIdx.x];
+    dth[n * 6 + threadIdx.x] = v;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -809,6 +947,50 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
     paig_set_error("decoder: unsupported n_objs %d", K);
     return PAIG_E_UNSUPPORTED;
   }
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int paig_decoder_parts(const float* pos, long long pos_inner, const float* tmpl, const float* cont, const float* bg,
+                       float* contents, float* masks, int F, int K, int h, int H, void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(H == 2 * h && H <= MAXH, "decoder_parts: H=%d must be 2*tmpl=%d (<= %d)", H, 2 * h, MAXH);
+  PosView pv{pos, 0, pos_inner, 0};
+  Src S{tmpl, cont, bg};
+  hipStream_t st = (hipStream_t)stream;
+  const int g = F < 2048 ? F : 2048;
+  const int lds = (K * h * h * 4) * 4;
+  if (K == 2) hipLaunchKernelGGL((dec_parts_k<2>), dim3(g), dim3(256), lds, st, pv, S, contents, masks, F, h, H);
+  else if (K == 3) hipLaunchKernelGGL((dec_parts_k<3>), dim3(g), dim3(256), lds, st, pv, S, contents, masks, F, h, H);
+  else {
+    paig_set_error("decoder_parts: unsupported n_objs %d", K);
+    return PAIG_E_UNSUPPORTED;
+  }
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_stn_fwd(const float* U, const float* theta, float* out, int N, int C, int Hi, int Wi, int Ho, int Wo,
+                 void* stream) {
+  if (N <= 0) return 0;
+  PAIG_REQUIRE(C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "stn_fwd: bad shape");
+  const long long total = (long long)N * Ho * Wo;
+  const int g = (int)(total / 256 + 1 < 8192 ? total / 256 + 1 : 8192);
+  hipLaunchKernelGGL(stn_fwd_k, dim3(g), dim3(256), 0, (hipStream_t)stream, U, theta, out, N, C, Hi, Wi, Ho, Wo);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_stn_bwd(const float* U, const float* theta, const float* dout, float* dU, float* dtheta, int N, int C,
+                 int Hi, int Wi, int Ho, int Wo, void* stream) {
+  if (N <= 0) return 0;
+  PAIG_REQUIRE(C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "stn_bwd: bad shape");
+  hipLaunchKernelGGL(stn_bwd_k, dim3(N), dim3(256), 0, (hipStream_t)stream, U, theta, dout, dU, dtheta, N, C, Hi, Wi,
+                     Ho, Wo);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

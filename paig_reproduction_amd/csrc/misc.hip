@@ -483,3 +483,22 @@ int paig_sgd_f64(double* p, const double* g, double* buf, long long n, double lr
 }
 
 }  // extern "C"
+
+// d *= (y > 0): the ReLU derivative applied to a gradient in place (the
+// standalone ShallowUNet backward: its last conv's output is ReLU'd, Q13)
+__global__ void relu_mask_k(const float* __restrict__ y, float* __restrict__ d, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    d[i] = y[i] > 0.f ? d[i] : 0.f;
+}
+
+extern "C" {
+
+int paig_relu_mask(const float* y, float* d, long long n, void* stream) {
+  if (n <= 0) return 0;
+  const int g = (int)(n / 256 + 1 < 4096 ? n / 256 + 1 : 4096);
+  hipLaunchKernelGGL(relu_mask_k, dim3(g), dim3(256), 0, (hipStream_t)stream, y, d, n);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -124,7 +124,11 @@ def backward_plan(ops):
 class Layout:
     """Static shapes of one step (from the PhysicsNet config and batch)."""
 
-    def __init__(self, model, B, T):
+    def __init__(self, model, B, T, frames=None, net=None):
+        """frames=N: the encoder alone over N independent frames (the
+        standalone ConvolutionalEncoder / U-Net calls): F = N, no sequence.
+        net: "unet" / "shallow_unet" to plan that U-Net whatever the frame
+        size (both are built, Q8; the live one is chosen by H otherwise)."""
         self.B, self.T = B, T
         self.K = model.n_objs
         self.D = model.coord_units // 2
@@ -133,11 +137,14 @@ class Layout:
         self.ins, self.pred = model.input_steps, model.pred_steps
         self.Te = self.ins + self.pred
         self.R = model.pred_steps + model.extrap_steps
-        assert T == model.seq_len, f"input has {T} frames, model expects seq_len={model.seq_len}"
-        self.F = B * self.Te
+        if frames is None:
+            assert T == model.seq_len, f"input has {T} frames, model expects seq_len={model.seq_len}"
+            self.F = B * self.Te
+        else:
+            self.F = frames
         self.alt_vel = model.alt_vel
         self.cell = {"spring_ode_cell": 0, "bouncing_ode_cell": 1, "gravity_ode_cell": 2}[model.cell_type]
-        self.unet = self.H >= 40
+        self.unet = self.H >= 40 if net is None else net == "unet"
         if self.unet:       # UNet(hidden 16), blocks.py:106-237; c18 not ReLU'd
             self.bufs, self.ops = unet_plan(16, self.K)
             self.prefix = "encoder.unet."
@@ -344,7 +351,7 @@ class Engine:
         x = x.contiguous()
         K, F, HW, H, h, D = lay.K, lay.F, lay.HW, lay.H, lay.h, lay.D
         ws = _empty(self.workspace_floats(lay), dev)
-        S = {"lay": lay, "x": x, "ws": ws}
+        S = {"lay": lay, "x": x, "ws": ws, "dev": dev}
         cm = self.conv_flags()
         S["cm"] = cm
 
@@ -361,74 +368,10 @@ class Engine:
         S["src"] = src
         tmpl, cont, bgp = src["var_net_template"][1], src["var_net_content"][1], src["var_net_background"][2]
 
-        # ---- encoder U-Net over the first Te frames of every sequence
-        x_view = (ptr(x), T * lay.frame, lay.Te, lay.frame)   # frame n = b*Te + t, in place
-        acts = {}
-        for name, (C, lvl) in lay.bufs.items():
-            if name != "X0" and name not in lay.fused_bufs:
-                acts[name] = _empty(F * C * (H // lvl) * (H // lvl), dev)
-        S["acts"] = acts
-
-        def view(region):
-            buf, off, n = region
-            C, lvl = lay.bufs[buf]
-            hw = (H // lvl) ** 2
-            if buf == "X0":
-                return (x_view[0] + off * hw * 4, x_view[1], x_view[2], x_view[3]), lvl
-            t = acts[buf]
-            return (t.data_ptr() + off * hw * 4, C * hw, 0, 0), lvl
-
-        def conv_input(i, op):
-            """(view, level of the conv, extra flags): a fused upsample reads its
-            half-resolution source and forms the 2x bilinear rows while staging."""
-            up = lay.fused_up.get(i)
-            if up is None:
-                v, lvl = view(op["src"])
-                return v, lvl, 0
-            v, lvl = view(up["src"])
-            return v, lvl // 2, 32
-
-        S["view"] = view
-        S["conv_input"] = conv_input
-        for i, op in enumerate(lay.ops):
-            if op["op"] == "up" and op["dst"][0] in lay.fused_bufs:
-                continue   # formed inside the consuming conv's staging
-            dv, dlvl = view(op["dst"])
-            if op["op"] == "conv":
-                sv, clvl, xfl = conv_input(i, op)
-                Hl = H // clvl
-                W_ = self.p(lay.prefix + op["name"] + ".weight")
-                b_ = self.p(lay.prefix + op["name"] + ".bias")
-                fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
-                nbytes = 4 * F * (op["src"][2] * (Hl // (2 if xfl else 1)) ** 2 + op["dst"][2] * Hl * Hl)
-                with self._p("conv_fwd:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_fwd(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
-                                      op["src"][2], op["dst"][2], Hl, Hl, op["ks"], (1 if op["relu"] else 0) | xfl | cm,
-                                      st)
-            elif op["op"] == "pool":
-                sv, slvl = view(op["src"])
-                Hl = H // slvl
-                L.paig_maxpool2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hl, Hl, st)
-            else:
-                sv, slvl = view(op["src"])
-                Hs, Ho = H // slvl, H // dlvl
-                L.paig_upsample2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hs, Hs, Ho, Ho, st)
-
-        # ---- mask softmax + masked objects + localiser MLP + position head
-        masks = _empty(F * (K + 1) * HW, dev)
-        objs = _empty(K * F * 3 * HW, dev)
-        pobjs = _empty(K * F * lay.l1_in, dev) if lay.unet else None
-        L.paig_mask_softmax_fwd(ptr(acts["LG"]), *x_view, ptr(masks), ptr(objs), ptr(pobjs), F, K, 3, H, H, st)
-        l1_x = pobjs if lay.unet else objs
-        h1 = _empty(K * F * 200, dev)
-        h2 = _empty(K * F * 200, dev)
-        h3 = _empty(K * F * 2, dev)
-        self.linear(l1_x, K * F, "encoder.l1", h1, 1, st, ws)
-        self.linear(h1, K * F, "encoder.l2", h2, 1, st, ws)
-        enc_pos = _empty(F * 2 * K, dev)
-        L.paig_head_fwd(ptr(h2), ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
-                        ptr(enc_pos), F, K, 200, float(H / 2), st)
-        S.update(masks=masks, objs=objs, l1_x=l1_x, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
+        # ---- encoder over the first Te frames of every sequence (in place)
+        x_view = (ptr(x), T * lay.frame, lay.Te, lay.frame)   # frame n = b*Te + t
+        self._encoder_forward(S, lay, x_view, ws, st)
+        masks, objs, enc_pos = S["masks"], S["objs"], S["enc_pos"]
 
         # Two independent chains follow the position head; they run concurrently:
         #   side stream: velocity MLP -> physics rollout (one thread per
@@ -499,6 +442,89 @@ class Engine:
             "background_content": bgp.view(1, 3, H, H),
         }
         return res, (S if need_saved else None)
+
+    def _unet_forward(self, S, lay, x_view, st):
+        """The U-Net plan over F frames addressed by x_view (frame view
+        pointer, stride, group, group stride): fills S["acts"] (LG = logits)."""
+        L = self.L
+        F, H = lay.F, lay.H
+        dev = S["dev"]
+        cm = S["cm"]
+        acts = {}
+        for name, (C, lvl) in lay.bufs.items():
+            if name != "X0" and name not in lay.fused_bufs:
+                acts[name] = _empty(F * C * (H // lvl) * (H // lvl), dev)
+        S["acts"] = acts
+
+        def view(region):
+            buf, off, n = region
+            C, lvl = lay.bufs[buf]
+            hw = (H // lvl) ** 2
+            if buf == "X0":
+                return (x_view[0] + off * hw * 4, x_view[1], x_view[2], x_view[3]), lvl
+            t = acts[buf]
+            return (t.data_ptr() + off * hw * 4, C * hw, 0, 0), lvl
+
+        def conv_input(i, op):
+            """(view, level of the conv, extra flags): a fused upsample reads its
+            half-resolution source and forms the 2x bilinear rows while staging."""
+            up = lay.fused_up.get(i)
+            if up is None:
+                v, lvl = view(op["src"])
+                return v, lvl, 0
+            v, lvl = view(up["src"])
+            return v, lvl // 2, 32
+
+        S["view"] = view
+        S["conv_input"] = conv_input
+        for i, op in enumerate(lay.ops):
+            if op["op"] == "up" and op["dst"][0] in lay.fused_bufs:
+                continue   # formed inside the consuming conv's staging
+            dv, dlvl = view(op["dst"])
+            if op["op"] == "conv":
+                sv, clvl, xfl = conv_input(i, op)
+                Hl = H // clvl
+                W_ = self.p(lay.prefix + op["name"] + ".weight")
+                b_ = self.p(lay.prefix + op["name"] + ".bias")
+                fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
+                nbytes = 4 * F * (op["src"][2] * (Hl // (2 if xfl else 1)) ** 2 + op["dst"][2] * Hl * Hl)
+                with self._p("conv_fwd:" + op["name"], fl, nbytes):
+                    L.paig_conv2d_fwd(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
+                                      op["src"][2], op["dst"][2], Hl, Hl, op["ks"], (1 if op["relu"] else 0) | xfl | cm,
+                                      st)
+            elif op["op"] == "pool":
+                sv, slvl = view(op["src"])
+                Hl = H // slvl
+                L.paig_maxpool2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hl, Hl, st)
+            else:
+                sv, slvl = view(op["src"])
+                Hs, Ho = H // slvl, H // dlvl
+                L.paig_upsample2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hs, Hs, Ho, Ho, st)
+
+    def _encoder_forward(self, S, lay, x_view, ws, st):
+        """ConvolutionalEncoder.forward (nn/network/blocks.py:77-103) over the
+        frames of x_view: U-Net, mask softmax x image, l1/l2, position head."""
+        L = self.L
+        F, H, HW, K = lay.F, lay.H, lay.HW, lay.K
+        dev = S["dev"]
+        S["x_view"] = x_view
+        self._unet_forward(S, lay, x_view, st)
+        acts = S["acts"]
+        # ---- mask softmax + masked objects + localiser MLP + position head
+        masks = _empty(F * (K + 1) * HW, dev)
+        objs = _empty(K * F * 3 * HW, dev)
+        pobjs = _empty(K * F * lay.l1_in, dev) if lay.unet else None
+        L.paig_mask_softmax_fwd(ptr(acts["LG"]), *x_view, ptr(masks), ptr(objs), ptr(pobjs), F, K, 3, H, H, st)
+        l1_x = pobjs if lay.unet else objs
+        h1 = _empty(K * F * 200, dev)
+        h2 = _empty(K * F * 200, dev)
+        h3 = _empty(K * F * 2, dev)
+        self.linear(l1_x, K * F, "encoder.l1", h1, 1, st, ws)
+        self.linear(h1, K * F, "encoder.l2", h2, 1, st, ws)
+        enc_pos = _empty(F * 2 * K, dev)
+        L.paig_head_fwd(ptr(h2), ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
+                        ptr(enc_pos), F, K, 200, float(H / 2), st)
+        S.update(masks=masks, objs=objs, l1_x=l1_x, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
 
     # -- a second stream for the latency-bound per-sequence chains ---------
     def _fork(self, dev):
@@ -620,6 +646,18 @@ class Engine:
 
         L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
 
+        self._encoder_backward(S, denc, st)
+
+    def _encoder_backward(self, S, denc, st, hook=True):
+        """ConvolutionalEncoder backward from d enc_pos (denc [F][2K]): position
+        head, l2/l1, mask softmax, U-Net; all its weight gradients."""
+        lay = S["lay"]
+        L = self.L
+        dev = S["dev"]
+        ws = S["ws"]
+        K, F, HW, H = lay.K, lay.F, lay.HW, lay.H
+        x_view = S["x_view"]
+        S.setdefault("extra_slabs", [])
         # ---- position head + localiser MLP backward -> d masked objects
         dh2 = _empty(K * F * 200, dev)
         hblk = L.paig_head_bwd_blocks(K * F)
@@ -635,7 +673,7 @@ class Engine:
         self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
         # every gradient of the flat buffer's early bucket is final (queued on
         # this stream): the data-parallel all-reduce of that bucket may start
-        if self.bucket_hook is not None:
+        if hook and self.bucket_hook is not None:
             self.bucket_hook()
 
         # ---- mask softmax backward (incl. ReLU' of ShallowUNet's c13, Q13, and

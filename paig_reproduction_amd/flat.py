@@ -8,12 +8,35 @@ one kernel launch (nn/network/base.py:12-17, :150-152 in the reference run a
 per-parameter torch optimizer).  The 0-dim float64 physics parameters
 (cells.py:28-29, 92-93; quirk Q9) get a tiny flat fp64 buffer of their own.
 """
+import contextlib
 import math
+import weakref
 
 import torch
 import torch.distributed as dist
 
 from ._lib import lib, ptr, stream_handle
+
+
+# parameter (by id) -> (FlatParams, name): lets a standalone submodule call
+# (nn/network/modules.py) deposit its gradients into the owning flat buffer
+_OWNER = weakref.WeakValueDictionary()
+
+
+def deposit_grad(p, g):
+    """Add gradient g to parameter p with torch semantics (p.grad None ->
+    set, else accumulate).  A parameter that lives in a FlatParams buffer gets
+    it in its flat gradient slot (what FlatOptimizer and the DP all-reduce
+    read); any other parameter gets p.grad directly."""
+    fp = _OWNER.get(id(p))
+    if fp is not None and fp.index and fp._params_by_id().get(id(p)) is not None:
+        fp.deposit({fp._params_by_id()[id(p)]: g})
+        return
+    g = g.detach().reshape(p.shape).to(p.dtype)
+    if p.grad is None:
+        p.grad = g.clone()
+    else:
+        p.grad.add_(g)
 
 
 class FlatParams:
@@ -74,6 +97,8 @@ class FlatParams:
                 else:
                     raise TypeError(f"{n}: unsupported dtype {p.dtype}")
         self.n32, self.n64 = n32, n64
+        for n, p in params:
+            _OWNER[id(p)] = self
         # the early bucket = the leading fp32 parameters named by self.early
         self.n32_early = 0
         for n, p in params:
@@ -83,6 +108,49 @@ class FlatParams:
         self.device = dev
         self._early_work = None
         return True
+
+    def _params_by_id(self):
+        return {id(p): n for n, p in self._params()}
+
+    def deposit(self, grads):
+        """{name: gradient tensor} into the flat gradient slots: copied where
+        p.grad is None (and p.grad set to the slot view), added otherwise."""
+        L = lib()
+        pd = dict(self._params())
+        for n, g in grads.items():
+            kind, off, num, shape = self.index[n]
+            base = self.g32 if kind == 32 else self.g64
+            slot = base[off:off + num]
+            g = g.detach().reshape(-1).to(base.dtype).contiguous()
+            p = pd[n]
+            if p.grad is None:
+                slot.copy_(g)
+                p.grad = slot.view(shape)
+            elif kind == 32:
+                L.paig_axpby(ptr(g), ptr(slot), num, 1.0, 1.0, stream_handle(slot.device))
+            else:
+                slot.add_(g)   # the 0-dim fp64 physics parameters
+
+    @contextlib.contextmanager
+    def partial_backward(self, prefixes):
+        """A backward that writes only the parameters named by ``prefixes``
+        (a standalone submodule call): the engine writes them into a zeroed
+        redirect buffer, from which they are deposited with torch semantics;
+        every other parameter's gradient is left as it was."""
+        self.ensure()
+        prefixes = tuple(prefixes)
+        red = (torch.zeros_like(self.g32), torch.zeros_like(self.g64))
+        self._redirect = red
+        try:
+            yield
+        finally:
+            self._redirect = None
+        grads = {}
+        for n, p in self._params():
+            if n.startswith(prefixes):
+                kind, off, num, shape = self.index[n]
+                grads[n] = (red[0] if kind == 32 else red[1])[off:off + num]
+        self.deposit(grads)
 
     def grad_view(self, name):
         kind, off, num, shape = self.index[name]
@@ -100,7 +168,7 @@ class FlatParams:
             self._redirect[1].zero_()
         return acc
 
-    def end_backward(self, accumulated):
+    def end_backward(self, accumulated, none_prefixes=()):
         if accumulated:
             L = lib()
             st = stream_handle(self.g32.device)
@@ -108,10 +176,16 @@ class FlatParams:
             if self.n64:
                 self.g64.add_(self._redirect[1])  # 2 fp64 scalars
             self._redirect = None
-        self.attach_grads()
+        self.attach_grads(none_prefixes)
 
-    def attach_grads(self):
+    def attach_grads(self, none_prefixes=()):
+        """p.grad = its flat view; parameters the backward did not reach
+        (name prefixes in none_prefixes) keep grad None unless they already
+        had an accumulated gradient."""
+        none_prefixes = tuple(none_prefixes)
         for n, p in self._params():
+            if none_prefixes and n.startswith(none_prefixes) and p.grad is None:
+                continue
             p.grad = self.grad_view(n)
 
     @staticmethod

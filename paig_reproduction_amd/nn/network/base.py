@@ -9,7 +9,13 @@ Differences (documented in DESIGN.md):
     train step's loss reads the stale ``self.output`` of the last eval batch;
   * when torch.distributed is initialised, the optimizer step first averages
     the flat gradient over the group (RCCL), and each rank trains on its own
-    shard of every epoch (DataIterator(rank, world)).
+    shard of every epoch (DataIterator(rank, world)).  The reference has no
+    data parallelism, so its file side effects are made rank-safe here: rank 0
+    alone deletes / creates save_dir, writes log.txt, code.zip, model.ckpt and
+    outputs.npz, with barriers where other ranks read them; eval metrics are
+    example-weighted means over all ranks (one all-reduce), and a set too small
+    for the reference's batch (Q15: < 100 examples, one whole-set batch) is
+    split into one near-equal share per rank instead.
 """
 import logging
 import os
@@ -31,6 +37,22 @@ OPTIMIZERS = {
     "momentum": lambda model, lr: FlatOptimizer(model, "sgd", lr, momentum=0.9),
     "sgd": lambda model, lr: FlatOptimizer(model, "sgd", lr),
 }
+
+
+def _dp():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _rank():
+    import torch.distributed as dist
+    return dist.get_rank() if _dp() else 0
+
+
+def _barrier():
+    if _dp():
+        import torch.distributed as dist
+        dist.barrier()
 
 
 class BaseNetTorch(torch.nn.Module):
@@ -71,24 +93,32 @@ class BaseNetTorch(torch.nn.Module):
 
     def initialize_graph(self, save_dir, use_ckpt, ckpt_dir=""):
         """nn/network/base.py:65-94, including Q14 (an existing save_dir is
-        deleted unless use_ckpt)."""
+        deleted unless use_ckpt).  Data-parallel: every rank decides from what
+        existed before any rank touched the directory; rank 0 alone deletes /
+        creates it; the checkpoint is read after a barrier."""
         self.save_dir = save_dir
-        if os.path.exists(save_dir):
+        existed = os.path.exists(save_dir)
+        _barrier()   # every rank has looked before rank 0 changes anything
+        rank0 = _rank() == 0
+        if existed:
             if use_ckpt:
                 restore = True
                 restore_dir = ckpt_dir if ckpt_dir else save_dir
             else:
-                logger.info("Folder exists, deleting...")
-                shutil.rmtree(save_dir)
-                os.makedirs(save_dir)
+                if rank0:
+                    logger.info("Folder exists, deleting...")
+                    shutil.rmtree(save_dir)
+                    os.makedirs(save_dir)
                 restore = False
         else:
-            os.makedirs(save_dir)
+            if rank0:
+                os.makedirs(save_dir)
             if use_ckpt:
                 restore = True
                 restore_dir = ckpt_dir
             else:
                 restore = False
+        _barrier()
         if restore:
             print(f"Loading model from: {restore_dir + '/model.ckpt'}")
             sd = torch.load(os.path.join(restore_dir, "model.ckpt"), map_location=self.device, weights_only=True)
@@ -103,6 +133,8 @@ class BaseNetTorch(torch.nn.Module):
             return self.test_iterator
 
     def add_train_logger(self):
+        if _rank() != 0:   # one writer of log.txt
+            return
         log_path = os.path.join(self.save_dir, "log.txt")
         fh = logging.FileHandler(log_path)
         fh.setFormatter(logging.Formatter('%(asctime)s - %(name)s - %(message)s'))
@@ -121,7 +153,8 @@ class BaseNetTorch(torch.nn.Module):
         self.train()
         self.batch_size = batch_size
         self.add_train_logger()
-        zipdir(root_path, self.save_dir)
+        if _rank() == 0:
+            zipdir(root_path, self.save_dir)
         logger.info("\n".join(sys.argv))
         step = 0
         if not debug and epochs > 0:
@@ -152,6 +185,8 @@ class BaseNetTorch(torch.nn.Module):
                 self.run_extra_fns("train")
                 if step % print_interval == 0:
                     log_metrics(logger, "train - iter=%s" % step, self.train_metrics)
+                    if hasattr(self, "check_numerics"):
+                        self.check_numerics()
                 step += 1
 
             if ep % eval_every_n_epochs == 0:
@@ -163,14 +198,27 @@ class BaseNetTorch(torch.nn.Module):
                 print("saving")
                 if self._is_rank0():
                     torch.save(self.state_dict(), os.path.join(self.save_dir, "model.ckpt"))
+                _barrier()   # the file is complete before any rank may restore it
 
         test_metrics_results = self.eval_performance(batch_size, type='test')
         log_metrics(logger, "test - epoch=%s" % epochs, test_metrics_results)
 
     @staticmethod
     def _is_rank0():
-        import torch.distributed as dist
-        return not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+        return _rank() == 0
+
+    def _reduce_metrics(self, per_batch, counts):
+        """Example-weighted mean of the per-batch metric values over all
+        batches of all ranks (the reference's np.mean over equal-size batches;
+        exact for the uneven shares of a small set too)."""
+        keys = list(per_batch)
+        local = [sum(float(np.asarray(v).reshape(-1)[0]) * n for v, n in zip(per_batch[k], counts)) for k in keys]
+        t = torch.tensor(local + [float(sum(counts))], dtype=torch.float64, device=self.device)
+        if _dp():
+            import torch.distributed as dist
+            dist.all_reduce(t)
+        t = t.cpu().numpy()
+        return {k: np.float64(t[i] / max(t[-1], 1.0)) for i, k in enumerate(keys)}
 
     def eval_performance(self, batch_size, type='valid'):
         """nn/network/base.py:174-218 (Q15: whole set when it has < 100 examples)."""
@@ -183,10 +231,17 @@ class BaseNetTorch(torch.nn.Module):
             eval_outputs = {"input": [], "output": []}
             eval_iterator = self.get_iterator(type)
             eval_iterator.reset_epoch()
+            counts = []
             while eval_iterator.get_epoch() < 1:
                 if eval_iterator.X.shape[0] < 100:
-                    batch_size = eval_iterator.X.shape[0]
+                    # Q15: the whole set as one batch; data-parallel: one
+                    # near-equal share of it per rank
+                    n, w = eval_iterator.X.shape[0], max(getattr(eval_iterator, "world", 1), 1)
+                    batch_size = -(-n // w)
                 feed_dict, _ = self.get_batch(batch_size, eval_iterator)
+                if len(feed_dict["input"]) == 0:   # more ranks than examples: nothing to evaluate here
+                    continue
+                counts.append(len(feed_dict["input"]))
                 inp = self._to_device(feed_dict["input"], False)
                 self.output = self.conv_feedforward(inp)
                 self.train_loss, self.eval_losses = self.compute_loss()
@@ -200,12 +255,23 @@ class BaseNetTorch(torch.nn.Module):
                 fi = feed_dict["input"]
                 eval_outputs["input"].append(fi.detach().cpu().numpy() if torch.is_tensor(fi) else fi)
                 eval_outputs["output"].append(self.eval_losses)
-            eval_metrics_results = {k: np.mean([i.detach().cpu().numpy() for i in v], axis=0)
-                                    for k, v in eval_metrics_results.items()}
-            if self._is_rank0():
+            if _dp():
+                eval_metrics_results = self._reduce_metrics(
+                    {k: [i.detach().cpu().numpy() for i in v] for k, v in eval_metrics_results.items()}, counts)
+            else:
+                eval_metrics_results = {k: np.mean([i.detach().cpu().numpy() for i in v], axis=0)
+                                        for k, v in eval_metrics_results.items()}
+            ins = [np.asarray(a) for a in eval_outputs["input"]]
+            outs = [[o.detach().cpu().numpy() for o in out] for out in eval_outputs["output"]]
+            if _dp():   # every rank's inputs and per-batch losses, in rank order
+                import torch.distributed as dist
+                got = [None] * dist.get_world_size() if self._is_rank0() else None
+                dist.gather_object((ins, outs), got, dst=0)
+                if self._is_rank0():
+                    ins = [a for g in got for a in g[0]]
+                    outs = [o for g in got for o in g[1]]
+            if self._is_rank0() and ins:
                 np.savez_compressed(os.path.join(self.save_dir, "outputs.npz"),
-                                    input=np.concatenate(eval_outputs["input"], axis=0),
-                                    output=np.array([[o.detach().cpu().numpy() for o in out]
-                                                     for out in eval_outputs["output"]]))
+                                    input=np.concatenate(ins, axis=0), output=np.array(outs))
             self.run_extra_fns(type)
             return eval_metrics_results

@@ -3,19 +3,20 @@ reference module-for-module: same class names, same parameter names, shapes
 and CREATION ORDER (so ``torch.manual_seed`` gives the reference's initial
 weights and reference checkpoints load unchanged).
 
-They hold parameters only.  The arithmetic of the training path runs in the
-HIP kernels driven by ``paig_reproduction_amd.engine`` (the whole PhysicsNet
-step at once), so these modules have no per-module forward on the hot path;
-calling one directly raises with a pointer to the supported entry points.
+The training path runs them fused (``paig_reproduction_amd.engine``: the
+whole PhysicsNet step at once).  Called one at a time, as the reference's
+callers do, each forward below runs on the same HIP kernels through
+``native_modules`` (differentiable; parameter gradients land in the owning
+PhysicsNet's flat gradient buffer).
 """
 import numpy as np
 import torch.nn as pnn
 
+from paig_reproduction_amd.nn.network import native_modules as _nm
+
 
 class _ParamsOnly(pnn.Module):
-    def forward(self, *a, **k):
-        raise RuntimeError(f"{type(self).__name__} is evaluated inside the fused PhysicsNet step "
-                           "(PhysicsNet.forward / conv_st_decoder); it has no standalone forward in this build")
+    pass
 
 
 class VelocityEncoder(_ParamsOnly):
@@ -39,6 +40,10 @@ class VelocityEncoder(_ParamsOnly):
                 pnn.Tanh(),
                 pnn.Linear(100, self.coord_units // self.n_objs // 2),
             )
+
+    def forward(self, inp):
+        """blocks.py:31-49: inp [B, input_steps, coord_units/2] -> [B, coord_units/2]."""
+        return _nm.velocity_forward(self, inp)
 
 
 class UNet(_ParamsOnly):
@@ -72,6 +77,10 @@ class UNet(_ParamsOnly):
         self.c17 = C(hd, hd, kernel_size=3, padding="same")
         self.c18 = C(hd, out_features, kernel_size=1, padding="same")
 
+    def forward(self, x):
+        """blocks.py:172-237: frames [N, 3, H, W] -> logits [N, n_objs, H, W] (c18 not ReLU'd)."""
+        return _nm.unet_forward(self, x, "unet")
+
 
 class ShallowUNet(_ParamsOnly):
     """nn/network/blocks.py:240-276."""
@@ -98,6 +107,10 @@ class ShallowUNet(_ParamsOnly):
         self.c12 = C(hd, hd, kernel_size=3, padding="same")
         self.c13 = C(hd, out_features, kernel_size=1, padding="same")
 
+    def forward(self, x):
+        """blocks.py:278-308: frames [N, 3, H, W] -> ReLU'd logits [N, n_objs, H, W] (Q13)."""
+        return _nm.unet_forward(self, x, "shallow_unet")
+
 
 class ConvolutionalEncoder(_ParamsOnly):
     """nn/network/blocks.py:52-75: builds BOTH U-Nets (quirk Q8: the unused one
@@ -118,6 +131,11 @@ class ConvolutionalEncoder(_ParamsOnly):
         self.l2 = pnn.Linear(hidden_dim, hidden_dim)
         self.l3 = pnn.Linear(hidden_dim, out_features)
 
+    def forward(self, inp):
+        """blocks.py:77-103: frames [N, 3, H, W] -> (enc_pos [N, 2K] in pixels,
+        enc_masks [N, K+1, H, W], masked_objs: K x [N, 3, H, W])."""
+        return _nm.encoder_forward(self, inp)
+
 
 class VariableFromNetwork(_ParamsOnly):
     """nn/network/blocks.py:311-316: l2(tanh(l1(ones[1,10]))) reshaped to `shape`."""
@@ -127,3 +145,7 @@ class VariableFromNetwork(_ParamsOnly):
         self.l1 = pnn.Linear(10, 200)
         self.l2 = pnn.Linear(200, int(np.prod(shape)))
         self.shape = shape
+
+    def forward(self):
+        """blocks.py:318-322: l2(tanh(l1(ones[1, 10]))) reshaped to self.shape."""
+        return _nm.vfn_forward(self)

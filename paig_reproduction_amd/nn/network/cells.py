@@ -29,7 +29,11 @@ class ode_cell(tnn.RNNCell):
         return x_0, v_0
 
     def forward(self, poss, vels):
-        raise RuntimeError(f"{type(self).__name__}: the rollout runs fused in PhysicsNet.forward (paig_rollout_fwd)")
+        """One cell step (5 substeps) on paig_rollout_fwd/bwd with R = 1:
+        poss, vels [B, coord_units/2] -> (poss, vels).  The training path runs
+        all R steps in one launch instead (PhysicsNet.forward)."""
+        from paig_reproduction_amd.nn.network import native_modules as _nm
+        return _nm.cell_forward(self, poss, vels)
 
 
 class spring_ode_cell(ode_cell):

@@ -11,6 +11,9 @@ backward is the explicit HIP backward (paig_reproduction_amd.engine).
 import inspect
 import logging
 import os
+import weakref
+
+import ctypes
 
 import numpy as np
 import torch
@@ -64,7 +67,11 @@ class _PhysicsStep(torch.autograd.Function):
         flat = ctx.engine.model._flat
         acc = flat.begin_backward()
         ctx.engine.backward(ctx.S, d_sse_rec, d_sse_roll, d_out, d_rec, d_enc, d_pvs)
-        flat.end_backward(acc)
+        # nothing reached the rollout branch (quirk Q1: the loss read a stale
+        # output): the velocity encoder and physics parameters are not in the
+        # graph, so like torch they get grad None (their flat slots hold zeros)
+        none = ctx.engine.model.ROLLOUT_PARAMS if d_out is None and d_sse_roll is None and d_pvs is None else ()
+        flat.end_backward(acc, none)
         ctx.S = None
         return None, None, None
 
@@ -103,6 +110,10 @@ class _FrameSSE(torch.autograd.Function):
     def forward(ctx, frames, x, ins):
         B, R = frames.shape[0], frames.shape[1]
         T = x.shape[1]
+        if x.shape[0] != B or tuple(x.shape[2:]) != tuple(frames.shape[2:]) or T - ins != R:
+            # the reference's (input[:, ins:] - output) would not broadcast either
+            raise RuntimeError(f"compute_loss: output {tuple(frames.shape)} does not match input[:, {ins}:] of "
+                               f"{tuple(x.shape)}")
         fr = 3 * frames.shape[-1] * frames.shape[-2]
         frames = frames.contiguous()
         x = x.contiguous()
@@ -187,6 +198,10 @@ class PhysicsNet(BaseNetTorch):
         self.velocity_encoder = VelocityEncoder(self.alt_vel, self.input_steps, self.n_objs, self.coord_units,
                                                 self.device)
         self.rollout_cell = self.cell(self.coord_units // 2, self.coord_units // 2)
+        # the standalone U-Net / encoder forwards run on this model's engine
+        for mod in (self.encoder, self.encoder.shallow_unet, self.encoder.unet):
+            object.__setattr__(mod, "_paig_owner", weakref.ref(self))
+        object.__setattr__(self, "_parts", None)
         self.loss_mode = "fresh"
         # conv arithmetic of the HIP path: "split" (fp32-accurate split-precision
         # 16-bit MFMA, default), "fp32" (f32-input MFMA) or "bf16"
@@ -198,6 +213,8 @@ class PhysicsNet(BaseNetTorch):
     # the localiser's l1/l2: ~97% of the gradient bytes) lead the flat buffer,
     # so their data-parallel all-reduce can start while the U-Net backward runs
     EARLY_GRADS = ("var_net_content.", "var_net_background.", "var_net_template.", "encoder.l1.", "encoder.l2.")
+    # parameters reached only through the rollout branch
+    ROLLOUT_PARAMS = ("velocity_encoder.", "rollout_cell.")
 
     def _live_names(self):
         dead = "encoder.unet." if self.conv_input_shape[1] < 40 else "encoder.shallow_unet."
@@ -266,32 +283,125 @@ class PhysicsNet(BaseNetTorch):
 
     def conv_st_decoder(self, inp):
         """Decode positions [N, coord_units/2] -> frames [N, C, H, W]
-        (physics_models.py:151-199) with the HIP decoder (no gradient through
-        this standalone call; the training path decodes inside forward)."""
+        (physics_models.py:151-199): the three VariableFromNetwork sources and
+        the HIP STN/compositing decoder, differentiable w.r.t. the positions and
+        the sources' parameters.  Sets template / contents / background_content
+        like the reference; transf_contents / transf_masks are formed on request."""
         require_device(inp)
-        eng = self._native()
+        from paig_reproduction_amd.nn.network.native_modules import _STDecoder
+        self._native()
+        out = _STDecoder.apply(inp, self._anchor_for_modules(), self)
+        srcs = self._last_sources
         K, H = self.n_objs, self.conv_input_shape[1]
         h = H // 2
-        N = inp.shape[0]
-        inp = inp.detach().float().contiguous()
-        dev = inp.device
-        L = lib()
-        st = stream_handle(dev)
-        srcs = {}
-        for nm, P, post in (("var_net_template", K * h * h, False), ("var_net_content", K * 3 * h * h, False),
-                            ("var_net_background", 3 * H * H, True)):
-            hv, y = torch.empty(200, device=dev), torch.empty(P, device=dev)
-            yp = torch.empty(P, device=dev) if post else None
-            L.paig_vfn_fwd(ptr(eng.p(nm + ".l1.weight")), ptr(eng.p(nm + ".l1.bias")), ptr(eng.p(nm + ".l2.weight")),
-                           ptr(eng.p(nm + ".l2.bias")), ptr(hv), ptr(y), ptr(yp), P, st)
-            srcs[nm] = yp if post else y
-        out = torch.empty(N, 3, H, H, device=dev)
-        L.paig_decoder_fwd(ptr(inp), 0, 2 * K, 0, ptr(srcs["var_net_template"]), ptr(srcs["var_net_content"]),
-                           ptr(srcs["var_net_background"]), ptr(out), 3 * H * H, None, 0, 0, 0, None, N, K, h, H, st)
-        self.template = srcs["var_net_template"].view(K, 1, h, h)
-        self.contents = srcs["var_net_content"].view(K, 3, h, h)
-        self.background_content = srcs["var_net_background"].view(1, 3, H, H)
+        self.template = srcs["tmpl"].view(K, 1, h, h)
+        self.contents = srcs["cont"].view(K, 3, h, h)
+        self.background_content = srcs["bg"].view(1, 3, H, H)
+        object.__setattr__(self, "_parts", (inp.detach().float().contiguous(), 2 * K, srcs))
         return out
+
+    def check_numerics(self):
+        """Raise if a split-precision kernel flagged an operand outside f16's
+        range since the last check (conv weights are staged at a fixed 2^8
+        scale, so |w| >= 256; every other operand is scaled dynamically).
+        Synchronises the device: BaseNetTorch calls it at log steps only."""
+        if self.conv_math != "split":
+            return
+        rc = lib().paig_f16_range_status(1)
+        if rc != 0:
+            raise FloatingPointError(
+                "split-precision path: a weight reached |w| >= 256, beyond the f16 staging range of the "
+                "fp32-accurate 16-bit matrix-core convolutions; rerun with --conv_math fp32" if rc > 0 else
+                f"paig_f16_range_status failed ({rc})")
+
+    def _anchor_for_modules(self):
+        return torch.zeros((), requires_grad=True)
+
+    _VFN_SRCS = (("var_net_template", "tmpl", 0), ("var_net_content", "cont", 0), ("var_net_background", "bg", 1))
+
+    def _decoder_sources(self, dev, st):
+        """The decoder's step-constant sources (physics_models.py:163-171,
+        185-186): raw template, raw contents, sigmoid(background)."""
+        L = lib()
+        K, H = self.n_objs, self.conv_input_shape[1]
+        h = H // 2
+        sizes = {"tmpl": K * h * h, "cont": K * 3 * h * h, "bg": 3 * H * H}
+        pd = self._param_by_name
+        srcs = {}
+        for nm, key, post in self._VFN_SRCS:
+            P = sizes[key]
+            srcs[nm] = (torch.empty(200, device=dev), torch.empty(P, device=dev),
+                        torch.empty(P, device=dev) if post else None, P)
+        arr = lambda xs: (ctypes.c_void_p * 3)(*xs)   # noqa: E731
+        L.paig_vfn_fwd_multi(3, *[arr([ptr(pd[nm + suf]) for nm, _, _ in self._VFN_SRCS])
+                                  for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                             arr([ptr(srcs[nm][0]) for nm, _, _ in self._VFN_SRCS]),
+                             arr([ptr(srcs[nm][1]) for nm, _, _ in self._VFN_SRCS]),
+                             arr([ptr(srcs[nm][2]) for nm, _, _ in self._VFN_SRCS]),
+                             (ctypes.c_int * 3)(*[srcs[nm][3] for nm, _, _ in self._VFN_SRCS]), st)
+        out = {"tmpl": srcs["var_net_template"][1], "cont": srcs["var_net_content"][1],
+               "bg": srcs["var_net_background"][2], "_vfn": srcs}
+        object.__setattr__(self, "_last_sources", out)
+        return out
+
+    def _decoder_sources_backward(self, srcs, dsrc, st):
+        """dsrc = [d template | d sigmoid(content) | d sigmoid(background)] (the
+        decoder's source gradients) -> the three VariableFromNetworks' parameter
+        gradients, deposited into the flat gradient buffer."""
+        from paig_reproduction_amd.flat import deposit_grad
+        L = lib()
+        dev = dsrc.device
+        v = srcs["_vfn"]
+        pd = self._param_by_name
+        offs, o = [], 0
+        for nm, _, _ in self._VFN_SRCS:
+            offs.append(o)
+            o += v[nm][3]
+        g = {nm: {suf: torch.empty_like(pd[nm + suf]) for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")}
+             for nm, _, _ in self._VFN_SRCS}
+        parts = [torch.empty(L.paig_vfn_bwd_blocks(v[nm][3]) * 200, device=dev) for nm, _, _ in self._VFN_SRCS]
+        arr = lambda xs: (ctypes.c_void_p * 3)(*xs)   # noqa: E731
+        # content and background enter through a sigmoid (sig = 1)
+        L.paig_vfn_bwd_multi(3, arr([ptr(dsrc) + 4 * off for off in offs]),
+                             arr([ptr(v[nm][1]) for nm, _, _ in self._VFN_SRCS]), (ctypes.c_int * 3)(0, 1, 1),
+                             arr([ptr(v[nm][0]) for nm, _, _ in self._VFN_SRCS]),
+                             arr([ptr(pd[nm + ".l2.weight"]) for nm, _, _ in self._VFN_SRCS]),
+                             *[arr([ptr(g[nm][suf]) for nm, _, _ in self._VFN_SRCS])
+                               for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                             arr([ptr(pt) for pt in parts]), (ctypes.c_int * 3)(*[v[nm][3] for nm, _, _ in self._VFN_SRCS]),
+                             st)
+        for nm, _, _ in self._VFN_SRCS:
+            for suf, t in g[nm].items():
+                deposit_grad(pd[nm + suf], t)
+
+    def _transf_parts(self):
+        """(transf_contents, transf_masks) of the last decoder call
+        (physics_models.py:186-196): K warped contents + the tiled background,
+        and the K+1 compositing masks, each [N, 3, H, W] (detached)."""
+        if self._parts is None:
+            raise AttributeError("transf_contents / transf_masks: no decoder call yet")
+        cached = getattr(self, "_parts_cache", None)
+        if cached is not None and cached[0] is self._parts:
+            return cached[1]
+        pos, inner, srcs = self._parts
+        K, H = self.n_objs, self.conv_input_shape[1]
+        N = pos.shape[0]
+        dev = pos.device
+        cont = torch.empty(K + 1, N, 3, H, H, device=dev)
+        masks = torch.empty(K + 1, N, 3, H, H, device=dev)
+        lib().paig_decoder_parts(ptr(pos), inner, ptr(srcs["tmpl"]), ptr(srcs["cont"]), ptr(srcs["bg"]), ptr(cont),
+                                 ptr(masks), N, K, H // 2, H, stream_handle(dev))
+        res = ([cont[k] for k in range(K + 1)], tuple(masks[k] for k in range(K + 1)))
+        object.__setattr__(self, "_parts_cache", (self._parts, res))
+        return res
+
+    @property
+    def transf_contents(self):
+        return self._transf_parts()[0]
+
+    @property
+    def transf_masks(self):
+        return self._transf_parts()[1]
 
     def forward(self, input):
         return self.conv_feedforward(input)
@@ -313,6 +423,10 @@ class PhysicsNet(BaseNetTorch):
         self.masked_objs = eng.last_masked_objs
         self.template, self.contents, self.background_content = tmpl, cont, bg
         self._sse_rec, self._sse_roll = sse_rec, sse_roll
+        # the reference's last decoder call decodes the last rollout step
+        R, D = self.pred_steps + self.extrap_steps, self.coord_units // 2
+        object.__setattr__(self, "_parts", (pvs.detach()[:, R, :D], (R + 1) * 2 * D,
+                                            {"tmpl": tmpl.detach(), "cont": cont.detach(), "bg": bg.detach()}))
         self._fwd_output = out
         return out
 

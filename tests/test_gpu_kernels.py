@@ -215,11 +215,12 @@ def test_gemm(ta, tb, M, N, K):
     assert rel_err(rs, (A.t() if ta else A).sum(1)) <= 2e-5
 
 
-# split-precision GEMM (paig_gemm_ex): math 1 f16 hi/lo, 2 bf16 hi/lo, 3 bf16
-GEMM_EX_TOL = {1: 2e-5, 2: 5e-5, 3: 3e-2}
+# split-precision GEMM (paig_gemm_ex): math 1 f16 hi/lo, 2 bf16 hi/lo, 3 bf16,
+# 4 f16 hi/lo with both operands scaled by running powers of two
+GEMM_EX_TOL = {1: 2e-5, 2: 5e-5, 3: 3e-2, 4: 2e-5}
 
 
-@pytest.mark.parametrize("math", [1, 2, 3])
+@pytest.mark.parametrize("math", [1, 2, 3, 4])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(37, 50, 19), (130, 200, 3072), (200, 3072, 130), (6, 2, 200), (1, 513, 200),
                                    (2000, 200, 3072), (200, 3072, 2000)])   # last: float4 split-K epilogue
@@ -301,3 +302,78 @@ def test_slab_reduce_multi(lens, aligned, accumulate):
         assert got.shape == want.shape
         if want.numel():
             assert float((got - want).abs().max()) <= 1e-4 * max(1.0, float(want.abs().max()))
+
+
+# ---- range: the scaled split-precision paths work at any magnitude; the
+# unscaled f16 operands (conv weights at a fixed 2^8, GEMM math 1) raise the
+# device range flag instead of silently overflowing
+def _range_status():
+    return L().paig_f16_range_status(1)
+
+
+@pytest.mark.parametrize("act_scale,dy_scale", [(1e6, 1.0), (1e-9, 1e-12), (1.0, 1e9), (3e5, 1e-20)])
+def test_conv_split_any_range(act_scale, dy_scale):
+    """Activations far above f16's 65504 (and far below its normal range),
+    gradients at any magnitude: per-tile / running power-of-two scales keep
+    fp32 accuracy (reference: aten fp32 conv2d has no such limit)."""
+    cin, cout, hw, ks, F_ = 16, 16, 16, 3, 5
+    _range_status()
+    torch.manual_seed(5)
+    x = torch.randn(F_, cin, hw, hw) * act_scale
+    w = torch.randn(cout, cin, ks, ks) * 0.2
+    b = torch.randn(cout) * act_scale
+    dy = torch.randn(F_, cout, hw, hw) * dy_scale
+    xr, wr = x.clone().double().requires_grad_(True), w.clone().double().requires_grad_(True)
+    y = F.conv2d(xr, wr, b.double(), padding="same")
+    y.backward(dy.double())
+    xg, wg, bg, dyg = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
+    out = torch.empty(F_, cout, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(xg), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout, hw,
+                        hw, ks, 128, st())
+    dx = torch.empty(F_, cin, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(dyg), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, None, 0, p(wg), None, F_, cout, cin, hw,
+                        hw, ks, 8 | 128, st())
+    nmax = 64
+    slab = torch.empty(nmax * (cout * cin * ks * ks + cout), device=DEV)
+    nb = ctypes.c_int(0)
+    L().paig_conv2d_wgrad(p(xg), cin * hw * hw, 0, 0, p(dyg), cout * hw * hw, p(slab), nmax, ctypes.byref(nb), F_, cin,
+                          cout, hw, hw, ks, 128, st())
+    g = torch.empty(cout * cin * ks * ks + cout, device=DEV)
+    L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
+    torch.cuda.synchronize()
+    assert rel_err(out, y.detach()) <= 1e-5
+    assert rel_err(dx, xr.grad) <= 1e-5
+    assert rel_err(g[:cout * cin * ks * ks].view_as(w), wr.grad) <= 1e-5
+    assert _range_status() == 0
+
+
+def test_conv_split_weight_range_flag():
+    """Conv weights are staged at a fixed 2^8 scale: |w| >= 256 cannot be
+    represented, and the kernel flags it (PhysicsNet raises at its next check)."""
+    cin, cout, hw, F_ = 8, 8, 32, 2
+    _range_status()
+    x = torch.rand(F_, cin, hw, hw, device=DEV)
+    w = torch.randn(cout, cin, 3, 3, device=DEV)
+    w[0, 0, 1, 1] = 300.0
+    b = torch.zeros(cout, device=DEV)
+    out = torch.empty(F_, cout, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(x), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout, hw, hw,
+                        3, 128, st())
+    assert _range_status() == 1
+    assert _range_status() == 0   # cleared by the read
+
+
+def test_gemm_math1_range_flag():
+    M, N, K = 64, 64, 64
+    _range_status()
+    A = torch.randn(M, K, device=DEV) * 1e5
+    Bm = torch.randn(K, N, device=DEV)
+    C = torch.empty(M, N, device=DEV)
+    L().paig_gemm_ex(0, 0, M, N, K, 1.0, p(A), K, p(Bm), N, 0.0, p(C), N, None, 0, 0, None, 0, None, None, 0, 1, st())
+    assert _range_status() == 1
+    # math 4 (scaled) at the same magnitude: exact enough, no flag
+    L().paig_gemm_ex(0, 0, M, N, K, 1.0, p(A), K, p(Bm), N, 0.0, p(C), N, None, 0, 0, None, 0, None, None, 0, 4, st())
+    torch.cuda.synchronize()
+    ref = A.double().cpu() @ Bm.double().cpu()
+    assert rel_err(C, ref) <= 2e-5
+    assert _range_status() == 0

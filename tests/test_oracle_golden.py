@@ -37,3 +37,57 @@ def test_oracle_matches_reference(name):
     grad_checks(z, grads, ROLLOUT_RTOL.get(name, 2e-5))
     # the oracle's live-parameter set is exactly the set the reference grads
     assert sorted(grads) == sorted(str(k) for k in z["grad_keys"])
+
+
+# ---- training loop / test phase fixtures (tests/golden/gen_golden_train.py)
+def _train_fixture(name):
+    import os
+    import numpy as np
+    from helpers import GOLDEN_DIR
+    return np.load(os.path.join(GOLDEN_DIR, f"train_{name}.npz"), allow_pickle=False)
+
+
+def test_oracle_reference_mode_step():
+    """Quirk Q1 (nn/network/base.py:141-143 vs :195) restated: the same losses
+    for both steps, the same first-step gradients and gradient key set."""
+    import numpy as np
+    torch.set_num_threads(4)
+    z = _train_fixture("refmode_spring_s12")
+    cfg, _ = O.cfg_from_golden(z)
+    xs = [O.input_from_u8(z["input_u8_0"]), O.input_from_u8(z["input_u8_1"])]
+    L, g0, _ = O.reference_mode_steps(golden_weights(z), cfg, O.input_from_u8(z["input_u8_eval"]), xs, float(z["lr"]))
+    assert_close(np.array(L), z["losses"], ORACLE_RTOL, "refmode losses")
+    assert sorted(g0) == sorted(str(k) for k in z["grad_keys"])
+    grad_checks(z, g0, 2e-5)
+
+
+@pytest.mark.parametrize("name", ["spring_s30", "3bp_s40"])
+def test_oracle_eval_test_phase(name):
+    """eval_performance at test_seq_len over a whole-set batch (Q15)."""
+    torch.set_num_threads(4)
+    z = _train_fixture("eval_" + name)
+    cfg, _ = O.cfg_from_golden(z)
+    metrics, out = O.eval_metrics(golden_weights(z), cfg, O.input_from_u8(z["input_u8"]))
+    for k, v in metrics.items():
+        assert_close(torch.tensor(v, dtype=torch.float64), z["metric/" + k], ROLLOUT_RTOL.get(name.replace("40", "20"),
+                                                                                          ORACLE_RTOL), k)
+    assert_close(out["output_seq"], z["output_seq"], ROLLOUT_RTOL.get(name.replace("40", "20"), 1e-5), "output_seq")
+
+
+@pytest.mark.parametrize("name", ["spring_s12", "mnist_s12"])
+def test_oracle_rmsprop_trajectory(name):
+    """10 RMSprop steps (base.py:134-160).  Step 0 (before any update) agrees
+    to the fixed bar; afterwards RMSprop's sign-amplified updates of
+    rounding-level gradients make even two CPU fp32 runs drift apart (the GPU
+    test bounds the HIP run by an fp32 ensemble), so the whole trajectory is
+    only held to the drift this restatement was measured at (spring 1.7e-4,
+    mnist 1.2e-2, x3)."""
+    import numpy as np
+    torch.set_num_threads(8)
+    z = _train_fixture("traj_" + name)
+    cfg, _ = O.cfg_from_golden(z)
+    xs = [O.input_from_u8(z["input_u8_0"]), O.input_from_u8(z["input_u8_1"])]
+    L, _ = O.train_trajectory(golden_weights(z), cfg, xs, float(z["lr"]), int(z["steps"]))
+    L = np.array(L)
+    assert_close(L[0], z["losses"][0], ORACLE_RTOL, "step 0 losses")
+    assert_close(L, z["losses"], 5e-4 if name.startswith("spring") else 4e-2, "trajectory losses")
