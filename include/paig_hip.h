@@ -30,12 +30,15 @@ extern "C" {
 
 const char* paig_last_error(void);
 int paig_abi_version(void);
-/* f16 range guard of paig_gemm_ex math 1, which feeds its operands to the
- * f16 matrix cores unscaled (|v| < 65504 needed; the step's split path uses
- * the scaled math 4 and the scaled convs, which have no such limit); a
- * kernel that meets a larger value sets a device flag.  Synchronises the device, returns 1 if any flag is set
- * (clear != 0 resets them), 0 if none, < 0 on a HIP error.  (No reference
- * counterpart: fp32 aten ops have no such limit; the caller raises.) */
+/* f16 range guard of the split-precision path.  Activations and gradients
+ * are staged for the f16 matrix cores at power-of-two scales taken from their
+ * own maxima (any magnitude); weights at a fixed 2^8 (|w| < 256), as are the
+ * activations of a split wgrad called without the forward's xmax slots and
+ * the operands of paig_gemm_ex math 5 (math 1: unscaled, |v| < 65504).  A
+ * kernel that meets a value beyond a fixed range sets a device flag.
+ * Synchronises the device, returns 1 if any flag is set (clear != 0 resets
+ * them), 0 if none, < 0 on a HIP error.  (No reference counterpart: fp32 aten
+ * ops have no such limit; the caller raises.) */
 int paig_f16_range_status(int clear);
 
 /* ---- U-Net convolutions -------------------------------------------------
@@ -48,14 +51,23 @@ int paig_f16_range_status(int clear);
  *        MFMA kernel (tests), 32 the input is the 2x bilinear
  *        upsample of the given (H/2 x W/2) planes, formed while staging
  *        (torchvision Resize of blocks.py:260,269 fused, never materialised),
- *        128 split-precision 16-bit MFMA (f16 hi+lo pieces, every operand
- *        scaled by powers of two: fp32-accurate at any range), 256 bf16
+ *        128 split-precision 16-bit MFMA (f16 hi+lo pieces scaled by powers of
+ *        two: activations and gradients per tile from their maxima, weights
+ *        at a fixed 2^8, |w| < 256 range-guarded: fp32-accurate), 256 bf16
  *        operands (config #2).
  *        Shapes without a split instantiation fall back to the f32 MFMA /
  *        VALU kernels (same results within fp32 accuracy). */
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                     const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin, int Cout,
                     int H, int W, int ks, int flags, void* stream);
+/* paig_conv2d_fwd that also records, on the split path (flags & 128, not
+ * dgrad), max |input| per persistent block into xmax[0 .. xmax_n) (unused
+ * slots zeroed; xmax_n >= the block count, PAIG_XMAX_SLOTS suffices): the
+ * X scale of the wgrad of the same input (paig_conv2d_wgrad_ex). */
+#define PAIG_XMAX_SLOTS 2048
+int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                       const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, void* stream);
 /* 1 if the shape runs on the MFMA path for fwd/dgrad (what 0) or wgrad (what 1)
  * with these flags; flag 32 (fused upsample input) is available only there */
 int paig_conv2d_mfma_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags);
@@ -63,6 +75,12 @@ int paig_conv2d_mfma_supported(int what, int Cin, int Cout, int H, int W, int ks
 int paig_conv2d_wgrad(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
                       float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
                       int flags, void* stream);
+/* paig_conv2d_wgrad with X scaled by max(xmax[0 .. xmax_n)) (16-byte aligned,
+ * xmax_n % 4 == 0): any slots whose max bounds |x|, e.g. those the forward
+ * of x filled.  Null (or all-zero) slots: the fixed 2^8, range-guarded. */
+int paig_conv2d_wgrad_ex(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
+                         float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
+                         int flags, const float* xmax, int xmax_n, void* stream);
 
 /* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,
@@ -101,8 +119,11 @@ int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, 
 /* paig_gemm on the 16-bit matrix cores with split-precision operands
  * (gemm.hip): math 0 = f32-input MFMA (= paig_gemm), 1 = f16 hi+lo pieces
  * (fp32-accurate; operands |v| < 65504, range-guarded), 2 = bf16 hi+lo
- * pieces (fp32 range, 16 bits), 3 = bf16, 4 = f16 hi+lo with both operands
- * scaled by running powers of two (any range; fp32-accurate).  rowsum
+ * pieces (fp32 range, 16 bits), 3 = bf16, 4 = f16 hi+lo with op(A) (any
+ * magnitude) scaled by running powers of two and op(B) (weights) at a fixed
+ * 2^8, |v| < 256 range-guarded (forward and dgrad GEMMs), 5 = f16 hi+lo, both
+ * operands at the fixed 2^8, 6 = f16 hi+lo, both operands scaled by running
+ * powers of two (wgrad GEMMs: gradient x activations).  rowsum
  * is fused only for ta = 1 (else math falls back to 0). */
 int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
                  long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,

@@ -12,6 +12,9 @@ import torch  # noqa: F401  (loads torch's HIP runtime first; the .so binds to i
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpaig_hip.so")
 # A/B tooling only (tools/conv_bench.py against an older build): another .so
+# slots per conv of paig_conv2d_fwd_ex / paig_conv2d_wgrad_ex (PAIG_XMAX_SLOTS)
+XMAX_SLOTS = 2048
+
 AB_PATH = os.environ.get("PAIG_AB_LIB")
 
 P = ctypes.c_void_p
@@ -28,6 +31,8 @@ SIGNATURES = {
     "paig_f16_range_status": (I, [I]),
     "paig_conv2d_fwd": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P]),
     "paig_conv2d_wgrad": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P]),
+    "paig_conv2d_fwd_ex": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P]),
+    "paig_conv2d_wgrad_ex": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
     "paig_gather_u8_f32": (I, [P, P, P, I, LL, P]),
     "paig_velmlp_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),

@@ -103,6 +103,10 @@ int paig_f16_range_gemm(int clear);
 // keeps 22 significant bits for |w| >= 2^-(3 + 8) and overflows at 2^(16 - 8)
 // (range-guarded); per-block weight maxima cost a serial pass per launch
 #define PAIG_W_EXP 8
+// the same for activations (values bounded by construction: ReLU'd conv
+// outputs of [0, 1] frames, masked objects): full f16 precision for
+// |a| >= 2^-11, a range-flagged overflow at 2^8; gradients get dynamic scales
+#define PAIG_A_EXP 8
 
 // power-of-two exponent e with m * 2^e in [2^14, 2^15) (f16's top binade,
 // clear of its 65504 limit); 100 when m == 0 (no constraint); clamped
@@ -144,14 +148,20 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 // MFMA implicit-GEMM convolutions (conv_mfma.hip): return 1 when the shape is
 // instantiated there (launch status in *rc), 0 to fall back to the VALU path.
+// xmax (nullable): per-block max |input| of a split-precision forward
+// (written, n slots) / of the wgrad's X (read: the launch's fixed X scale)
+struct XMax {
+  float* p;
+  int n;
+};
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                       int H, int W, int ks, int flags, hipStream_t st, int* rc);
+                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
 int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H,
-                         int W, int ks, int flags, hipStream_t st, int* rc);
+                         int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
 // Split-precision 16-bit MFMA convolutions (conv_split.hip), selected by
 // flags & 128 (f16x3 forward / bf16x3 dgrad and wgrad) or flags & 256 (bf16).
 int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                        int H, int W, int ks, int flags, hipStream_t st, int* rc);
+                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
 int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout,
-                          int H, int W, int ks, int flags, hipStream_t st, int* rc);
+                          int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
 int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags);

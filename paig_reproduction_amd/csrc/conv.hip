@@ -353,9 +353,20 @@ extern "C" {
 // out[f][co_off..] = conv(in) (+bias) (ReLU)      (forward)
 // out = conv_transpose-as-dgrad(in = dY) (* aux>0) (dgrad, flags & 8)
 // Views: p/fs/grp/gs per frame_view; channel offsets are folded into pointers.
+int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                       const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, void* stream);
+
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                     const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                     int Cout, int H, int W, int ks, int flags, void* stream) {
+  return paig_conv2d_fwd_ex(in, in_fs, in_grp, in_gs, out, out_fs, aux, aux_fs, w, bias, F, Cin, Cout, H, W, ks, flags,
+                            nullptr, 0, stream);
+}
+
+int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                       const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   FView vin{in, in_fs, in_gs, in_grp};
   FViewW vout{out, out_fs};
@@ -364,7 +375,9 @@ int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_g
   const int fl = flags & 7;
   if (F <= 0) return 0;
   int rc = 0;
-  if (!(flags & 16) && paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc)) return rc;
+  if (!(flags & 16) &&
+      paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc, XMax{xmax, xmax_n}))
+    return rc;
   if (flags & 32) {
     paig_set_error("paig_conv2d_fwd: fused-upsample input has no instantiation for Cin=%d Cout=%d H=%d", Cin, Cout, H);
     return PAIG_E_UNSUPPORTED;
@@ -382,16 +395,28 @@ int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_g
 
 // Per-block partial weight+bias gradients: slab[nblk][Cout*Cin*ks*ks + Cout].
 // *nblk_out receives the number of partial rows written (<= nblk_max).
+int paig_conv2d_wgrad_ex(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
+                         float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
+                         int flags, const float* xmax, int xmax_n, void* stream);
+
 int paig_conv2d_wgrad(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
                       float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
                       int flags, void* stream) {
+  return paig_conv2d_wgrad_ex(x, x_fs, x_grp, x_gs, dy, dy_fs, slab, nblk_max, nblk_out, F, Cin, Cout, H, W, ks, flags,
+                              nullptr, 0, stream);
+}
+
+int paig_conv2d_wgrad_ex(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
+                         float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
+                         int flags, const float* xmax, int xmax_n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   FView vx{x, x_fs, x_gs, x_grp};
   FView vd{dy, dy_fs, 0, 0};
   *nblk_out = 0;
   if (F <= 0) return 0;
   int rc = 0;
-  if (!(flags & 16) && paig_conv_mfma_wgrad(vx, vd, slab, nblk_max, nblk_out, F, Cin, Cout, H, W, ks, flags, st, &rc))
+  if (!(flags & 16) && paig_conv_mfma_wgrad(vx, vd, slab, nblk_max, nblk_out, F, Cin, Cout, H, W, ks, flags, st, &rc,
+                                             XMax{const_cast<float*>(xmax), xmax_n}))
     return rc;
   if (flags & 32) {
     paig_set_error("paig_conv2d_wgrad: fused-upsample input has no instantiation for Cin=%d Cout=%d H=%d", Cin, Cout, H);

@@ -684,8 +684,9 @@ static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_
 // Returns 1 if handled (rc in *rc), 0 if the shape has no MFMA instantiation.
 // flags: 1 relu, 2 mask(aux>0), 4 accumulate, 8 dgrad, 32 input = 2x upsample of (H/2 x W/2)
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                       int H, int W, int ks, int flags, hipStream_t st, int* rc) {
-  if ((flags & (128 | 256)) && paig_conv_split_fwd(in, out, aux, w, b, F, Cin, Cout, H, W, ks, flags, st, rc)) return 1;
+                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm) {
+  if ((flags & (128 | 256)) && paig_conv_split_fwd(in, out, aux, w, b, F, Cin, Cout, H, W, ks, flags, st, rc, xm))
+    return 1;
   const bool dg = (flags & 8) != 0;
   const bool up = (flags & 32) != 0;
   const int fl = flags & 7;
@@ -723,8 +724,9 @@ int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const fl
 }
 
 int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H,
-                         int W, int ks, int flags, hipStream_t st, int* rc) {
-  if ((flags & (128 | 256)) && paig_conv_split_wgrad(x, dy, slab, nblk_max, nblk_out, F, Cin, Cout, H, W, ks, flags, st, rc))
+                         int W, int ks, int flags, hipStream_t st, int* rc, XMax xm) {
+  if ((flags & (128 | 256)) &&
+      paig_conv_split_wgrad(x, dy, slab, nblk_max, nblk_out, F, Cin, Cout, H, W, ks, flags, st, rc, xm))
     return 1;
   if (H != W) return 0;
   if (flags & 32) {

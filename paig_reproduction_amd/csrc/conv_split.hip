@@ -292,7 +292,7 @@ struct SFwdCfg {
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 __global__ void __launch_bounds__(256, 2)
 conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
-                 int flags, int ntiles) {
+                 int flags, int ntiles, XMax xm) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
   constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP;
@@ -381,10 +381,20 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   };
   float2 pre[UPS ? 1 : NL][8];
   UP up;
-  // f16 pieces (PM 0): every tile's operand image scaled by one power of two
-  // (tile_max, commit); tinv takes it and the weight exponent back out
-  constexpr bool SC = PM == 0 && PAIG_SCALE_MODE < 2;
-  float tsc = 1.f, tinv = 1.f;
+  // f16 pieces (PM 0): the operand image (activations, or dgrad's gradients:
+  // any magnitude) is scaled per tile by one power of two from the tile's
+  // block max (tile_max, commit) and tinv takes it and the weight exponent
+  // back out exactly.  The block's running max of the tile maxima goes to
+  // xm.p[blockIdx.x] (the wgrad of the same input scales X by their max).
+  constexpr bool SCL = PM == 0, DYN = PM == 0 && PAIG_SCALE_MODE < 2;
+  float tsc = 1.f, tinv = 1.f, xrun = 0.f;
+  auto tile_scale = [&]() {
+    const float m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    xrun = fmaxf(xrun, m);
+    const int e = f16_scale_exp(m);
+    tsc = __builtin_amdgcn_ldexpf(1.f, e);
+    tinv = __builtin_amdgcn_ldexpf(1.f, -(e + ew));
+  };
   auto issue = [&](int t) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
     if constexpr (UPS) {
@@ -411,15 +421,11 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     }
   };
   auto commit = [&](int t) {
+    if constexpr (DYN) tile_scale();
     if constexpr (UPS) {
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
       __syncthreads();
-      if constexpr (SC) {
-        const int e = f16_scale_exp(fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3])));
-        tsc = __builtin_amdgcn_ldexpf(1.f, e);
-        tinv = __builtin_amdgcn_ldexpf(1.f, -(e + ew));
-      }
 #pragma unroll 1
       for (int i = tid; i < NI; i += 256) {
         const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
@@ -435,14 +441,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
         put_px(i, v);
       }
     } else {
-      if constexpr (SC) {
-        // f16 pieces: the tile's operand (activations, or dgrad's gradients)
-        // scaled by one power of two (max -> [2^14, 2^15)): f16's range and
-        // 22 significant bits for all but negligibly small values; the
-        // epilogue undoes it exactly
-        const int e = f16_scale_exp(fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3])));
-        tsc = __builtin_amdgcn_ldexpf(1.f, e);
-        tinv = __builtin_amdgcn_ldexpf(1.f, -(e + ew));
+      if constexpr (SCL) {
 #pragma unroll
         for (int l = 0; l < NL; ++l)
 #pragma unroll
@@ -501,7 +500,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   for (; lt < ntiles; lt += gridDim.x) {
     const int tile = xcd_tile(lt, ntiles);
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
-    if constexpr (SC) tile_max();
+    if constexpr (DYN) tile_max();
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
     __syncthreads();
@@ -546,7 +545,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
           if (f >= F) continue;
           float* op = out.frame(f) + co * HW + (long long)y * W + x;
           f32x4 v = acc[mt][nt];
-          if constexpr (SC) v *= tinv;
+          if constexpr (SCL) v *= tinv;
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += bv;
           if (flags & 1) {
@@ -569,7 +568,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
             const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
             if (f >= F) continue;
             float* op = out.frame(f) + co * HW + (long long)y * W + x;
-            float v = (SC ? acc[mt][nt][r] * tinv : acc[mt][nt][r]) + bv;
+            float v = (SCL ? acc[mt][nt][r] * tinv : acc[mt][nt][r]) + bv;
             if (flags & 1) v = v < 0.f ? 0.f : v;
             if (flags & 4) v += *op;
             if (flags & 2) v = aux.frame(f)[co * HW + (long long)y * W + x] > 0.f ? v : 0.f;
@@ -579,7 +578,14 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       }
     }
   }
-  if constexpr (PM == 0) f16_range_note(rmax);
+  if constexpr (PM == 0) {
+    f16_range_note(rmax);
+    if (xm.p && blockIdx.y == 0) {
+      if (tid == 0) xm.p[blockIdx.x] = xrun;
+      if (blockIdx.x == 0)
+        for (int i = gridDim.x + tid; i < xm.n; i += 256) xm.p[i] = 0.f;
+    }
+  }
 }
 
 // ===================================================================== wgrad
@@ -681,7 +687,7 @@ struct SWgCfg {
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
 __global__ void __launch_bounds__(256, (SWgCfg<CIN, COUT, H, W, KS, UPS, PM>::MINW))
-conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int ntiles) {
+conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int ntiles, XMax xm) {
   using C = SWgCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int CINB = C::CINB, COUTB = C::COUTB;
   constexpr int KK = C::KK, CQ = C::CQ, NQ = C::NQ, NT = C::NT, NCOL = C::NCOL, MT = C::MT, COP = C::COP;
@@ -704,16 +710,22 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
   const int wn = wv % WN, wp = wv / WN;
   constexpr int NRB = H / RT;
-  // PM 0 (f16 pieces): X and dY each scaled by a running power of two (2^ecx,
-  // 2^ecd): a tile's block-wide max |X| / |dY| gives the exponent that puts
-  // it in [2^14, 2^15); when a tile needs a smaller one than the running
-  // exponent, the accumulators (held at scale 2^(ecx + ecd)) are rescaled
-  // first, exactly.  Every element then keeps 22 significant bits or an
-  // absolute error below 2^-40 of the largest (bf16 pieces keep 16 bits; an
+  // PM 0 (f16 pieces): X (activations) scaled by one power of two for the
+  // whole launch, from the max |X| the forward conv of the same input
+  // recorded per block (xm; without it the fixed 2^PAIG_A_EXP, range-
+  // guarded); dY (gradients, any magnitude) scaled by a running power of two
+  // 2^ecd: a tile's block-wide max |dY| gives the exponent that puts it in
+  // [2^14, 2^15); when a tile needs a smaller one than the running exponent,
+  // the accumulators (held at scale 2^(ecx + ecd)) are rescaled first,
+  // exactly.  Every element then keeps 22 significant bits or an absolute
+  // error below 2^-40 of its operand's largest (bf16 pieces keep 16 bits; an
   // unscaled f16 lo piece goes subnormal below |v| = 1/8).
-  int ecx = PAIG_SCALE_MODE < 2 ? 100 : 0, ecd = ecx;
-  float xsc = __builtin_amdgcn_ldexpf(1.f, ecx), dsc = xsc;
-  __shared__ float smax[4], smaxx[4];
+  int ecx = PAIG_A_EXP;
+  float xsc = 1.f;   // 2^ecx, set before the first tile
+  int ecd = PAIG_SCALE_MODE < 2 ? 100 : 0;
+  float dsc = __builtin_amdgcn_ldexpf(1.f, ecd);
+  float rmax = 0.f;   // range guard of the scaled activations
+  __shared__ float smax[4];
 
   auto xplane = [](int cq) { return cq * XPL + ((cq & 1) ? 16 : 0) + ((cq & 2) ? 64 : 0); };
   // ---- zero the halo columns of X (never staged)
@@ -785,14 +797,13 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
     const int o = xplane(cq) + ((fi * ROWS + r) * TWPX + xp + OFFX) * 4;
     s16x8 hv, lv;
-    float xmx = 0.f;   // scaled: below 2^15
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       short h, lo;
-      split<PM>(PM == 0 ? v[c].x * xsc : v[c].x, h, lo, xmx);
+      split<PM>(PM == 0 ? v[c].x * xsc : v[c].x, h, lo, rmax);
       hv[c] = h;
       lv[c] = lo;
-      split<PM>(PM == 0 ? v[c].y * xsc : v[c].y, h, lo, xmx);
+      split<PM>(PM == 0 ? v[c].y * xsc : v[c].y, h, lo, rmax);
       hv[4 + c] = h;
       lv[4 + c] = lo;
     }
@@ -838,39 +849,25 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
       for (int l = 0; l < NLD; ++l) sd[l] = load_d(t, l);
     }
   };
-  // PM 0 scale exponents.  Operands held in registers before the barrier
-  // (prefetched X / dY, the fused-upsample window) publish their tile max
-  // there (tile_max); the synchronously loaded ones (XSYNC, DSYNC: too many
-  // registers to prefetch) are staged with the running exponent and checked
-  // after the barrier: a tile whose max would overflow f16 at that scale
-  // (the block's first tile, or one > 2x any before) is staged again with
-  // its own exponent.  One pass over the data in the steady state.
-  constexpr bool XSYNC = !UPS && !XPIPE, DSYNC = !DPIPE;
-  __shared__ float srx[4], srd[4];
-  auto rescale = [&](int nx, int nd) {   // block-uniform
-    if (nx + nd < ecx + ecd) {
+  // PM 0 dY exponent.  dY held in registers before the barrier (prefetched)
+  // publishes its tile max there (tile_max); synchronously loaded dY (DSYNC:
+  // too many registers to prefetch) is staged with the running exponent and
+  // checked after the barrier: a tile whose max would overflow f16 at that
+  // scale (the block's first tile, or one > 2x any before) is staged again
+  // with its own exponent.  One pass over the data in the steady state.
+  constexpr bool DSYNC = !DPIPE;
+  __shared__ float srd[4];
+  auto rescale = [&](int nd) {   // block-uniform
+    if (nd < ecd) {
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int j = 0; j < NTW; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[m][j][r] = __builtin_amdgcn_ldexpf(acc[m][j][r], nx + nd - ecx - ecd);
+          for (int r = 0; r < 4; ++r) acc[m][j][r] = __builtin_amdgcn_ldexpf(acc[m][j][r], nd - ecd);
     }
-    ecx = nx;
     ecd = nd;
-    xsc = __builtin_amdgcn_ldexpf(1.f, ecx);
     dsc = __builtin_amdgcn_ldexpf(1.f, ecd);
-  };
-  // synchronous X staging of tile t (raw max into rx)
-  auto stage_x_sync = [&](int t, float& rx) {
-#pragma unroll 1
-    for (int i = tid; i < NIX; i += 256) {
-      float2 v[4];
-      load_x(t, i, v);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) rx = fmaxf(rx, fmaxf(fabsf(v[c].x), fabsf(v[c].y)));
-      put_x(i, v);
-    }
   };
   // dY staging of tile t (raw max into rd; bias partials on the first pass)
   auto stage_d = [&](int t, float& rd, bool first) {
@@ -910,21 +907,13 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     }
   };
   auto commit = [&](int t) {
-    if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) {
-      // exponents of the register-held operands (published before the
-      // barrier); a smaller one rescales the accumulators exactly
-      int nx = ecx, nd = ecd;
-      if constexpr (!XSYNC) {
-        const int tx = f16_scale_exp(fmaxf(fmaxf(smaxx[0], smaxx[1]), fmaxf(smaxx[2], smaxx[3])));
-        nx = tx < ecx ? tx : ecx;
-      }
-      if constexpr (!DSYNC) {
-        const int td = f16_scale_exp(fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3])));
-        nd = td < ecd ? td : ecd;
-      }
-      if (nx != ecx || nd != ecd) rescale(nx, nd);
+    if constexpr (PM == 0 && !DSYNC && PAIG_SCALE_MODE < 2) {
+      // this tile's dY exponent (block max published before the barrier); a
+      // smaller one rescales the accumulators exactly
+      const int td = f16_scale_exp(fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3])));
+      if (td < ecd) rescale(td);
     }
-    float rx = 0.f, rd = 0.f;
+    float rd = 0.f;
     if constexpr (UPS) {
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
@@ -951,39 +940,36 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
         put_x(i, sx[l]);
       }
     } else {
-      stage_x_sync(t, rx);
+#pragma unroll 1
+      for (int i = tid; i < NIX; i += 256) {
+        float2 v[4];
+        load_x(t, i, v);
+        put_x(i, v);
+      }
     }
     stage_d(t, rd, true);
-    if constexpr (PM == 0 && XSYNC) {
-      rx = wave_max_u(rx);
-      if (lane == 0) srx[wv] = rx;
-    }
     if constexpr (PM == 0 && DSYNC) {
       rd = wave_max_u(rd);
       if (lane == 0) srd[wv] = rd;
     }
   };
-  // after the post-commit barrier: re-stage a synchronously loaded operand
-  // whose tile max overflowed f16 at the running scale
+  // after the post-commit barrier: re-stage synchronously loaded dY whose
+  // tile max overflowed f16 at the running scale
   auto check_sync = [&](int t) {
-    if constexpr (PM == 0 && (XSYNC || DSYNC) && PAIG_SCALE_MODE < 2) {
-      const float mx = XSYNC ? uniform_f(fmaxf(fmaxf(srx[0], srx[1]), fmaxf(srx[2], srx[3]))) : 0.f;
-      const float md = DSYNC ? uniform_f(fmaxf(fmaxf(srd[0], srd[1]), fmaxf(srd[2], srd[3]))) : 0.f;
-      const bool redo_x = XSYNC && mx * xsc >= PAIG_F16_MAX;
-      const bool redo_d = DSYNC && md * dsc >= PAIG_F16_MAX;
-      if (redo_x || redo_d) {   // block-uniform
-        rescale(redo_x ? f16_scale_exp(mx) : ecx, redo_d ? f16_scale_exp(md) : ecd);
-        float r0 = 0.f, r1 = 0.f;
-        if (redo_x) stage_x_sync(t, r0);
-        if (redo_d) stage_d(t, r1, false);
+    if constexpr (PM == 0 && DSYNC && PAIG_SCALE_MODE < 2) {
+      const float md = uniform_f(fmaxf(fmaxf(srd[0], srd[1]), fmaxf(srd[2], srd[3])));
+      if (md * dsc >= PAIG_F16_MAX) {   // block-uniform
+        rescale(f16_scale_exp(md));
+        float r1 = 0.f;
+        stage_d(t, r1, false);
         __syncthreads();
       }
     }
   };
 
-  // PM 0: this wave's max |X| / |dY| of tile t for the register-held
-  // operands into smaxx[wv] / smax[wv] (read by commit after the next
-  // barrier; the previous tile's reads finished before the last one)
+  // PM 0: this wave's max |dY| of the prefetched tile t into smax[wv] (read
+  // by commit after the next barrier; the previous tile's reads finished
+  // before the last one)
   auto tile_max = [&](int t) {
     if constexpr (!DSYNC) {
       float m = 0.f;
@@ -993,22 +979,25 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
       m = wave_max_u(m);
       if (lane == 0) smax[wv] = m;
     }
-    if constexpr (!XSYNC) {
-      float mx = 0.f;
-      if constexpr (UPS) {
-        mx = up.amax();   // the window bounds its upsampled values
-      } else {
-#pragma unroll
-        for (int l = 0; l < NLX; ++l)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) mx = fmaxf(mx, fmaxf(fabsf(sx[l][c].x), fabsf(sx[l][c].y)));
-      }
-      mx = wave_max_u(mx);
-      if (lane == 0) smaxx[wv] = mx;
-    }
   };
 
   if ((int)blockIdx.x < ntiles) issue(xcd_tile(blockIdx.x, ntiles));
+  if (PM == 0 && xm.p) {
+    // the launch's X exponent: max over the forward's per-block slots (their
+    // loads overlap the first tile's)
+    float m = 0.f;
+    for (int i = tid * 4; i < xm.n; i += 1024) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xm.p + i);
+      m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    }
+    m = wave_max_u(m);
+    if (lane == 0) smax[wv] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    if (m > 0.f) ecx = f16_scale_exp(m);   // all-zero slots (never written): the fixed scale, guarded
+    __syncthreads();   // smax is reused by tile_max
+  }
+  xsc = __builtin_amdgcn_ldexpf(1.f, ecx);
   for (int lt = blockIdx.x; lt < ntiles; lt += gridDim.x) {
     const int tile = xcd_tile(lt, ntiles);
     if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) tile_max(tile);
@@ -1112,11 +1101,12 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     for (int i = tid * NPU; i < (tid + 1) * NPU; ++i) v += Rb[(i / 256) * 256 + i % 256];
     s[COUT * NCOL + co0 + tid] = v;
   }
+  if constexpr (PM == 0) f16_range_note(rmax);
 }
 
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
-                       hipStream_t st) {
+                       hipStream_t st, XMax xm) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int LDS = C::LDS + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
@@ -1129,13 +1119,15 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
   int nb = resident / C::NB;   // persistent blocks per COUT slice
   if (nb > ntiles) nb = ntiles;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles);
+  if (PM != 0 || DG) xm.p = nullptr;
+  PAIG_REQUIRE(!xm.p || nb <= xm.n, "conv split fwd: %d blocks need more than %d xmax slots", nb, xm.n);
+  hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles, xm);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
-static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st) {
+static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st, XMax xm) {
   using C = SWgCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int STG = C::STG + (UPS ? UpStage<C::CINB, H, W, C::FPT, C::RT>::SL * 4 : 0);
   constexpr int LDS = STG > C::RED ? STG : C::RED;
@@ -1152,7 +1144,9 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
   if (nb > resident / (C::NSI * C::NSO)) nb = resident / (C::NSI * C::NSO);
   if (nb < 1) nb = 1;
   *nblk_out = nb;
-  hipLaunchKernelGGL(k, dim3(nb, C::NSI, C::NSO), dim3(256), LDS, st, x, dy, slab, F, ntiles);
+  PAIG_REQUIRE(!xm.p || (xm.n % 4 == 0 && (reinterpret_cast<uintptr_t>(xm.p) & 15) == 0),
+               "conv split wgrad: xmax needs 16-byte alignment and a multiple of 4 slots (%d)", xm.n);
+  hipLaunchKernelGGL(k, dim3(nb, C::NSI, C::NSO), dim3(256), LDS, st, x, dy, slab, F, ntiles, xm);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -1197,7 +1191,7 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
 // flags & 128: split precision (f16 x3 forward and scaled dgrad), flags & 256:
 // bf16 hi only.  Returns 1 if the shape is instantiated here (rc in *rc).
 int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                        int H, int W, int ks, int flags, hipStream_t st, int* rc) {
+                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm) {
   const bool dg = (flags & 8) != 0, up = (flags & 32) != 0, b16 = (flags & 256) != 0;
   const int fl = flags & 7;
   if (H != W || !(flags & (128 | 256))) return 0;
@@ -1206,8 +1200,8 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
     if (dg) return 0;
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
     if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
-      *rc = b16 ? sfwd_launch<CI, CO, HH, HH, K, false, true, 2>(in, out, aux, w, b, F, fl, st)           \
-                : sfwd_launch<CI, CO, HH, HH, K, false, true, 0>(in, out, aux, w, b, F, fl, st);          \
+      *rc = b16 ? sfwd_launch<CI, CO, HH, HH, K, false, true, 2>(in, out, aux, w, b, F, fl, st, xm)           \
+                : sfwd_launch<CI, CO, HH, HH, K, false, true, 0>(in, out, aux, w, b, F, fl, st, xm);          \
       return 1;                                                                                           \
     }
     PAIG_SPLIT_UP(PAIG_CASE)
@@ -1217,11 +1211,11 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
 #define PAIG_CASE(CI, CO, HH, K)                                                                            \
   if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                      \
     if (b16)                                                                                                \
-      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 2>(in, out, aux, w, b, F, fl, st)              \
-               : sfwd_launch<CI, CO, HH, HH, K, false, false, 2>(in, out, aux, w, b, F, fl, st);            \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 2>(in, out, aux, w, b, F, fl, st, xm)              \
+               : sfwd_launch<CI, CO, HH, HH, K, false, false, 2>(in, out, aux, w, b, F, fl, st, xm);            \
     else                                                                                                    \
-      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 0>(in, out, aux, w, b, F, fl, st)              \
-               : sfwd_launch<CI, CO, HH, HH, K, false, false, 0>(in, out, aux, w, b, F, fl, st);            \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 0>(in, out, aux, w, b, F, fl, st, xm)              \
+               : sfwd_launch<CI, CO, HH, HH, K, false, false, 0>(in, out, aux, w, b, F, fl, st, xm);            \
     return 1;                                                                                               \
   }
   PAIG_SPLIT_FWD(PAIG_CASE)
@@ -1230,15 +1224,15 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
 }
 
 int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout,
-                          int H, int W, int ks, int flags, hipStream_t st, int* rc) {
+                          int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm) {
   const bool up = (flags & 32) != 0, b16 = (flags & 256) != 0;
   if (H != W || !(flags & (128 | 256))) return 0;
   if (x.grp > 0 && H * W < 256) return 0;   // multi-frame tiles step frames by a plain stride
   if (up) {
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
     if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
-      *rc = b16 ? swg_launch<CI, CO, HH, HH, K, true, 2>(x, dy, slab, nblk_max, nblk_out, F, st)          \
-                : swg_launch<CI, CO, HH, HH, K, true, 0>(x, dy, slab, nblk_max, nblk_out, F, st);         \
+      *rc = b16 ? swg_launch<CI, CO, HH, HH, K, true, 2>(x, dy, slab, nblk_max, nblk_out, F, st, xm)          \
+                : swg_launch<CI, CO, HH, HH, K, true, 0>(x, dy, slab, nblk_max, nblk_out, F, st, xm);         \
       return 1;                                                                                           \
     }
     PAIG_SPLIT_UP(PAIG_CASE)
@@ -1247,8 +1241,8 @@ int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nbl
   }
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
   if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                    \
-    *rc = b16 ? swg_launch<CI, CO, HH, HH, K, false, 2>(x, dy, slab, nblk_max, nblk_out, F, st)           \
-              : swg_launch<CI, CO, HH, HH, K, false, 0>(x, dy, slab, nblk_max, nblk_out, F, st);          \
+    *rc = b16 ? swg_launch<CI, CO, HH, HH, K, false, 2>(x, dy, slab, nblk_max, nblk_out, F, st, xm)           \
+              : swg_launch<CI, CO, HH, HH, K, false, 0>(x, dy, slab, nblk_max, nblk_out, F, st, xm);          \
     return 1;                                                                                             \
   }
   PAIG_SPLIT_WG(PAIG_CASE)

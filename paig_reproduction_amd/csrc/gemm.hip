@@ -216,12 +216,15 @@ gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A
 // Per K element the three MFMAs cost ~3/16 of the f32-input form, so these
 // GEMMs (K = 3072 / 2000 / 200) fall to the HBM roofline.  math: 1 = f16
 // pieces (22 significant bits; operands must satisfy |v| < 65504: forward
-// activations / weights, range-guarded, see common.h), 4 = f16 pieces with
-// both operands scaled by running block powers of two (each K-tile's max
-// |op(A)| and |op(B)| into [2^14, 2^15); a tile that needs a smaller exponent
-// first rescales the accumulators exactly): any range, and 22 significant
-// bits for every value but the negligibly small (an unscaled f16 lo piece is
-// subnormal below |v| = 1/8); 2 = bf16 pieces (16 bits, fp32 range; kept for the ABI, not used by the
+// activations / weights, range-guarded, see common.h), 4 = f16 pieces for a
+// backward GEMM: op(A) (the gradient, any magnitude) scaled by a running
+// block power of two (each K-tile's max |op(A)| into [2^14, 2^15); a tile that
+// needs a smaller exponent first rescales the accumulators exactly), op(B)
+// (weights, bounded) at the fixed 2^PAIG_A_EXP, range-guarded; 5 = both
+// operands at the fixed 2^PAIG_A_EXP, range-guarded; 6 = both operands with
+// running exponents (a wgrad GEMM: gradient x activations).  Scaling keeps 22 significant bits for all but negligibly
+// small values (an unscaled f16 lo piece is subnormal below |v| = 1/8);
+// 2 = bf16 pieces (16 bits, fp32 range; kept for the ABI, not used by the
 // step: its gradient errors measured well outside the fp32 envelope), 3 =
 // bf16 hi only (the bf16 configuration).
 // LDS images keep each operand's global orientation: k-contiguous operands
@@ -248,9 +251,13 @@ __device__ __forceinline__ int kperm(int k) {   // k = 8g + 4h + q
   return 16 * (g >> 1) + 8 * h + 4 * (g & 1) + q;
 }
 
+// f16-piece modes, and the ones whose operands are scaled by powers of two
+#define F16PM(PM) ((PM) == 1 || (PM) == 4 || (PM) == 5 || (PM) == 6)
+#define SCALED(PM) ((PM) >= 4)
+
 template <int PM>
 __device__ __forceinline__ void gsplit(float v, short& h, short& l, float& rmax) {
-  if constexpr (PM == 1 || PM == 4) {
+  if constexpr (F16PM(PM)) {
     rmax = fmaxf(rmax, fabsf(v));
     const _Float16 a = (_Float16)v;
     h = __builtin_bit_cast(short, a);
@@ -264,7 +271,7 @@ __device__ __forceinline__ void gsplit(float v, short& h, short& l, float& rmax)
 
 template <int PM>
 __device__ __forceinline__ f32x4 gmma(s16x8 a, s16x8 b, f32x4 c) {
-  if constexpr (PM == 1 || PM == 4)
+  if constexpr (F16PM(PM))
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
                                                   0, 0);
   else
@@ -337,9 +344,15 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 rs4 = f32x4{0.f, 0.f, 0.f, 0.f};
-  float rmax = 0.f;                                   // f16 range guard (PM 1; PM 4 never trips)
-  int eca = 100, ecb = 100;                           // PM 4: operand scales 2^eca, 2^ecb
-  float asc = PM == 4 ? __builtin_amdgcn_ldexpf(1.f, 100) : 1.f, bsc = asc;
+  float rmax = 0.f;                                   // f16 range guard of fixed-scale operands
+  // operand scales 2^eca, 2^ecb: dynamic ones (DA: PM 4, 6; DB: PM 6) run
+  // from a high start down to each K-tile's need; the fixed ones (PM 5: both,
+  // PM 4: op(B)) are the activation / weight scale 2^PAIG_A_EXP
+  constexpr bool DA = PM == 4 || PM == 6, DB = PM == 6;
+  int eca = DA ? 100 : (PM == 5 ? PAIG_A_EXP : 0);
+  int ecb = DB ? 100 : (PM == 4 || PM == 5 ? PAIG_A_EXP : 0);
+  float asc = __builtin_amdgcn_ldexpf(1.f, eca);
+  float bsc = __builtin_amdgcn_ldexpf(1.f, ecb);
   __shared__ float smx[8];
 
   // register ring of NS K-tiles: the loads of tile k + NS are issued right
@@ -359,44 +372,51 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
     for (int st = 0; st < NS; ++st) {
       const int kk = k0 + st * BK;
       if (kk >= kend) break;
-      if constexpr (PM == 4) {
-        // this K-tile's max |op(A)|, |op(B)|, published before the barrier
-        // (the previous tile's smx reads finished before the last one)
-        float ma = 0.f, mb = 0.f;
+      // this K-tile's max |op(A)| / |op(B)| (dynamic operands), published
+      // before the barrier (the previous tile's smx reads finished before the
+      // last one)
+      if constexpr (DA) {
+        float ma = 0.f;
 #pragma unroll
         for (int e = 0; e < 2; ++e)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            ma = fmaxf(ma, fabsf(ta[st].v[e][i]));
-            mb = fmaxf(mb, fabsf(tb[st].v[e][i]));
-          }
+          for (int i = 0; i < 4; ++i) ma = fmaxf(ma, fabsf(ta[st].v[e][i]));
         ma = wave_max_u(ma);
+        if (lane == 0) smx[wv] = ma;
+      }
+      if constexpr (DB) {
+        float mb = 0.f;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mb = fmaxf(mb, fabsf(tb[st].v[e][i]));
         mb = wave_max_u(mb);
-        if (lane == 0) {
-          smx[wv] = ma;
-          smx[4 + wv] = mb;
-        }
+        if (lane == 0) smx[4 + wv] = mb;
       }
       __syncthreads();
-      if constexpr (PM == 4) {
-        const int ta_ = f16_scale_exp(fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3])));
-        const int tb_ = f16_scale_exp(fmaxf(fmaxf(smx[4], smx[5]), fmaxf(smx[6], smx[7])));
-        const int na = ta_ < eca ? ta_ : eca, nb = tb_ < ecb ? tb_ : ecb;
+      if constexpr (DA || DB) {
+        // a smaller exponent than the running one rescales the accumulators
+        // (held at 2^(eca + ecb)) exactly first
+        int na = eca, nb = ecb;
+        if constexpr (DA) na = min(eca, f16_scale_exp(fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]))));
+        if constexpr (DB) nb = min(ecb, f16_scale_exp(fmaxf(fmaxf(smx[4], smx[5]), fmaxf(smx[6], smx[7]))));
         if (na + nb < eca + ecb) {
 #pragma unroll
           for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) acc[i][j][r] = __builtin_amdgcn_ldexpf(acc[i][j][r], na + nb - eca - ecb);
-          eca = na;
-          ecb = nb;
-          asc = __builtin_amdgcn_ldexpf(1.f, eca);
-          bsc = __builtin_amdgcn_ldexpf(1.f, ecb);
+              for (int r = 0; r < 4; ++r)
+                acc[i][j][r] = __builtin_amdgcn_ldexpf(acc[i][j][r], (na + nb) - (eca + ecb));
         }
+        eca = na;
+        ecb = nb;
+        asc = __builtin_amdgcn_ldexpf(1.f, eca);
+        bsc = __builtin_amdgcn_ldexpf(1.f, ecb);
       }
-      store16<!TA, PM>(ta[st], Ah, Al, tid, asc, rmax);
-      store16<TB, PM>(tb[st], Bh, Bl, tid, bsc, rmax);
+      float dmx = 0.f;   // dynamically scaled operands stay below 2^15: no guard
+      store16<!TA, PM>(ta[st], Ah, Al, tid, asc, DA ? dmx : rmax);
+      store16<TB, PM>(tb[st], Bh, Bl, tid, bsc, DB ? dmx : rmax);
       if (do_rs) rs4 += ta[st].v[0] + ta[st].v[1];
       __syncthreads();
       if (kk + NS * BK < kend) {
@@ -449,7 +469,7 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
         const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
         const int n = n0 + wn * 32 + j * 16 + (lane & 15);
         if (m < M && n < N) {
-          float v = alpha * (PM == 4 ? __builtin_amdgcn_ldexpf(acc[i][j][r], -(eca + ecb)) : acc[i][j][r]);
+          float v = alpha * (SCALED(PM) ? __builtin_amdgcn_ldexpf(acc[i][j][r], -(eca + ecb)) : acc[i][j][r]);
           if (part) {
             part[((long long)bt.z * M + m) * N + n] = v;
           } else {
@@ -459,7 +479,7 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
           }
         }
       }
-  if constexpr (PM == 1) f16_range_note(rmax);
+  if constexpr (F16PM(PM)) f16_range_note(rmax);
 }
 
 // sum_{s<S} p[s*ld] in order s = 0..S-1 (deterministic), loads issued 8 at a
@@ -576,6 +596,8 @@ static void launch_gemm(int math, dim3 grid, hipStream_t st, int M, int N, int K
   else if (math == 2) PAIG_L((gemm_split_k<TA, TB, 2>));
   else if (math == 3) PAIG_L((gemm_split_k<TA, TB, 3>));
   else if (math == 4) PAIG_L((gemm_split_k<TA, TB, 4>));
+  else if (math == 5) PAIG_L((gemm_split_k<TA, TB, 5>));
+  else if (math == 6) PAIG_L((gemm_split_k<TA, TB, 6>));
   else PAIG_L((gemm_k<TA, TB>));
 #undef PAIG_L
 }
@@ -606,8 +628,8 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
                  const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,
                  void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (math < 0 || math > 4) {
-    paig_set_error("paig_gemm_ex: math must be 0..4, got %d", math);
+  if (math < 0 || math > 6) {
+    paig_set_error("paig_gemm_ex: math must be 0..6, got %d", math);
     return PAIG_E_UNSUPPORTED;
   }
   if (rowsum && !ta) math = 0;   // fused row sums exist on the split path for op(A) = A^T only

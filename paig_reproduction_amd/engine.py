@@ -22,7 +22,7 @@ import ctypes
 
 import torch
 
-from ._lib import lib, ptr, stream_handle, require_device
+from ._lib import XMAX_SLOTS, lib, ptr, stream_handle, require_device
 
 # --------------------------------------------------------------------------
 # U-Net plans (buffers + ops), forward order.  A buffer is (channels, level),
@@ -272,12 +272,15 @@ class Engine:
     # "fp32" = f32-input MFMA, "bf16" = bf16 operands (BASELINE config #2)
     CONV_MATH = {"split": 128, "fp32": 0, "bf16": 256}
 
-    # the same choice for the dense layers (paig_gemm_ex math): f16 pieces with
-    # both operands scaled by powers of two, forward and backward
-    GEMM_MATH = {"split": (4, 4), "fp32": (0, 0), "bf16": (3, 3)}
+    # the same choice for the dense layers (paig_gemm_ex math) per GEMM kind
+    # (forward, wgrad, dgrad): f16 pieces with the activations / gradients
+    # scaled by running powers of two, the weights at the fixed 2^8 (4:
+    # op(A) dynamic, op(B) = W fixed; 6: both dynamic)
+    GEMM_MATH = {"split": (4, 6, 4), "fp32": (0, 0, 0), "bf16": (3, 3, 3)}
+    FWD, WGRAD, DGRAD = 0, 1, 2
 
-    def gemm_math(self, backward):
-        return self.GEMM_MATH[getattr(self.model, "conv_math", "split")][1 if backward else 0]
+    def gemm_math(self, kind):
+        return self.GEMM_MATH[getattr(self.model, "conv_math", "split")][kind]
 
     def conv_flags(self):
         m = getattr(self.model, "conv_math", "split")
@@ -313,7 +316,7 @@ class Engine:
         O, I = W.shape
         with self._p("gemm_fwd:" + name, 2 * rows * O * I, 4 * (rows * I + O * I + rows * O)):
             self.L.paig_gemm_ex(0, 1, rows, O, I, 1.0, ptr(x), I, ptr(W), I, 0.0, ptr(out), O, ptr(b), act, 0, None,
-                                0, None, ptr(ws), ws.numel() if ws is not None else 0, self.gemm_math(False), st)
+                                0, None, ptr(ws), ws.numel() if ws is not None else 0, self.gemm_math(self.FWD), st)
 
     def linear_bwd(self, x, dy, rows, name, dx, aux, auxm, st, ws, need_dx=True):
         """dW = dy^T x and db = colsum(dy) (one GEMM, fused row sums) ; dx = (dy W) * act'(aux)"""
@@ -323,11 +326,11 @@ class Engine:
         n_ws = ws.numel()
         with self._p("gemm_wgrad:" + name, 2 * rows * O * I, 4 * (rows * O + rows * I + O * I + O)):
             self.L.paig_gemm_ex(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
-                                ptr(gb), ptr(ws), n_ws, self.gemm_math(True), st)
+                                ptr(gb), ptr(ws), n_ws, self.gemm_math(self.WGRAD), st)
         if need_dx:
             with self._p("gemm_dgrad:" + name, 2 * rows * O * I, 4 * (rows * O + O * I + 2 * rows * I)):
                 self.L.paig_gemm_ex(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm,
-                                    ptr(aux), I, None, ptr(ws), n_ws, self.gemm_math(True), st)
+                                    ptr(aux), I, None, ptr(ws), n_ws, self.gemm_math(self.DGRAD), st)
 
     def workspace_floats(self, lay):
         K, F, B = lay.K, lay.F, lay.B
@@ -477,6 +480,11 @@ class Engine:
 
         S["view"] = view
         S["conv_input"] = conv_input
+        # per conv: the split forward's per-block max |input| slots, which
+        # set the X scale of the same input's wgrad (every slot is written)
+        xmax = _empty(len(lay.ops) * XMAX_SLOTS, dev)
+        S["xmax"] = lambda i: ptr(xmax) + i * XMAX_SLOTS * 4
+        S["xmax_buf"] = xmax
         for i, op in enumerate(lay.ops):
             if op["op"] == "up" and op["dst"][0] in lay.fused_bufs:
                 continue   # formed inside the consuming conv's staging
@@ -489,9 +497,9 @@ class Engine:
                 fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
                 nbytes = 4 * F * (op["src"][2] * (Hl // (2 if xfl else 1)) ** 2 + op["dst"][2] * Hl * Hl)
                 with self._p("conv_fwd:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_fwd(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
-                                      op["src"][2], op["dst"][2], Hl, Hl, op["ks"], (1 if op["relu"] else 0) | xfl | cm,
-                                      st)
+                    L.paig_conv2d_fwd_ex(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
+                                         op["src"][2], op["dst"][2], Hl, Hl, op["ks"],
+                                         (1 if op["relu"] else 0) | xfl | cm, S["xmax"](i), XMAX_SLOTS, st)
             elif op["op"] == "pool":
                 sv, slvl = view(op["src"])
                 Hl = H // slvl
@@ -737,8 +745,9 @@ class Engine:
                 fl = 2 * F * cin * cout * ks * ks * Hl * Hl
                 nbytes = 4 * F * (cin * (Hl // (2 if xfl else 1)) ** 2 + cout * Hl * Hl)
                 with self._p("conv_wgrad:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_wgrad(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], ptr(slab), nblk_max,
-                                        ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, xfl | cm, st)
+                    L.paig_conv2d_wgrad_ex(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], ptr(slab), nblk_max,
+                                           ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, xfl | cm, S["xmax"](i),
+                                           XMAX_SLOTS, st)
                 gw = self.g(lay.prefix + op["name"] + ".weight")
                 gb = self.g(lay.prefix + op["name"] + ".bias")
                 n_w = cout * cin * ks * ks

@@ -302,8 +302,9 @@ class PhysicsNet(BaseNetTorch):
 
     def check_numerics(self):
         """Raise if a split-precision kernel flagged an operand outside f16's
-        range since the last check (conv weights are staged at a fixed 2^8
-        scale, so |w| >= 256; every other operand is scaled dynamically).
+        range since the last check: weights are staged at a fixed 2^8 scale
+        (|w| >= 256 is flagged); activations and gradients are scaled by
+        powers of two from their own maxima and have no limit.
         Synchronises the device: BaseNetTorch calls it at log steps only."""
         if self.conv_math != "split":
             return
@@ -311,7 +312,7 @@ class PhysicsNet(BaseNetTorch):
         if rc != 0:
             raise FloatingPointError(
                 "split-precision path: a weight reached |w| >= 256, beyond the f16 staging range of the "
-                "fp32-accurate 16-bit matrix-core convolutions; rerun with --conv_math fp32" if rc > 0 else
+                "fp32-accurate 16-bit matrix-core kernels; rerun with --conv_math fp32" if rc > 0 else
                 f"paig_f16_range_status failed ({rc})")
 
     def _anchor_for_modules(self):

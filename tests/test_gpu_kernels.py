@@ -216,11 +216,12 @@ def test_gemm(ta, tb, M, N, K):
 
 
 # split-precision GEMM (paig_gemm_ex): math 1 f16 hi/lo, 2 bf16 hi/lo, 3 bf16,
-# 4 f16 hi/lo with both operands scaled by running powers of two
-GEMM_EX_TOL = {1: 2e-5, 2: 5e-5, 3: 3e-2, 4: 2e-5}
+# 4 f16 hi/lo with op(A) scaled by running powers of two (op(B) fixed 2^8),
+# 5 both fixed, 6 both running
+GEMM_EX_TOL = {1: 2e-5, 2: 5e-5, 3: 3e-2, 4: 2e-5, 5: 2e-5, 6: 2e-5}
 
 
-@pytest.mark.parametrize("math", [1, 2, 3, 4])
+@pytest.mark.parametrize("math", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(37, 50, 19), (130, 200, 3072), (200, 3072, 130), (6, 2, 200), (1, 513, 200),
                                    (2000, 200, 3072), (200, 3072, 2000)])   # last: float4 split-K epilogue
@@ -304,18 +305,54 @@ def test_slab_reduce_multi(lens, aligned, accumulate):
             assert float((got - want).abs().max()) <= 1e-4 * max(1.0, float(want.abs().max()))
 
 
-# ---- range: the scaled split-precision paths work at any magnitude; the
-# unscaled f16 operands (conv weights at a fixed 2^8, GEMM math 1) raise the
-# device range flag instead of silently overflowing
+# ---- range: activations and gradients (power-of-two scales from their own
+# maxima) work at any magnitude, including beyond f16's 65504; weights (fixed
+# 2^8 scale) up to 256, and the device range flag is raised beyond, as by a
+# wgrad called without the forward's xmax slots (fixed 2^8 for X) and GEMM
+# math 1 (unscaled) beyond 65504
+XMAX_SLOTS = 2048
+
+
 def _range_status():
     return L().paig_f16_range_status(1)
 
 
-@pytest.mark.parametrize("act_scale,dy_scale", [(1e6, 1.0), (1e-9, 1e-12), (1.0, 1e9), (3e5, 1e-20)])
+def _split_conv_all(x, w, b, dy, ks, xmax_mode):
+    """forward (recording xmax), dgrad, wgrad (X scale from: "fwd" the
+    forward's slots, "host" one host-computed slot, "none" the fixed 2^8)"""
+    F_, cin, hw = x.shape[0], x.shape[1], x.shape[2]
+    cout = w.shape[0]
+    xg, wg, bg, dyg = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
+    out = torch.empty(F_, cout, hw, hw, device=DEV)
+    xmax = torch.full((XMAX_SLOTS,), float("nan"), device=DEV)
+    L().paig_conv2d_fwd_ex(p(xg), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout,
+                           hw, hw, ks, 128, p(xmax), XMAX_SLOTS, st())
+    dx = torch.empty(F_, cin, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(dyg), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, None, 0, p(wg), None, F_, cout, cin, hw,
+                        hw, ks, 8 | 128, st())
+    nmax = 64
+    slab = torch.empty(nmax * (cout * cin * ks * ks + cout), device=DEV)
+    nb = ctypes.c_int(0)
+    if xmax_mode == "host":
+        xs = torch.zeros(4, device=DEV)
+        xs[0] = x.abs().max()
+        xp, xn = p(xs), 4
+    else:
+        xp, xn = (p(xmax), XMAX_SLOTS) if xmax_mode == "fwd" else (None, 0)
+    L().paig_conv2d_wgrad_ex(p(xg), cin * hw * hw, 0, 0, p(dyg), cout * hw * hw, p(slab), nmax, ctypes.byref(nb), F_,
+                             cin, cout, hw, hw, ks, 128, xp, xn, st())
+    g = torch.empty(cout * cin * ks * ks + cout, device=DEV)
+    L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
+    torch.cuda.synchronize()
+    return out, dx, g[:cout * cin * ks * ks].view_as(w), xmax
+
+
+@pytest.mark.parametrize("act_scale,dy_scale", [(40.0, 1.0), (1e-5, 1e-12), (1.0, 1e9), (30.0, 1e-20), (1e5, 1.0),
+                                                (3e4, 1e6)])
 def test_conv_split_any_range(act_scale, dy_scale):
-    """Activations far above f16's 65504 (and far below its normal range),
-    gradients at any magnitude: per-tile / running power-of-two scales keep
-    fp32 accuracy (reference: aten fp32 conv2d has no such limit)."""
+    """Activations and gradients at any magnitude (per-tile / running / the
+    forward-recorded power-of-two scales) keep fp32 accuracy, down to f16's
+    subnormals and past its 65504 (reference: float64 conv2d)."""
     cin, cout, hw, ks, F_ = 16, 16, 16, 3, 5
     _range_status()
     torch.manual_seed(5)
@@ -326,25 +363,38 @@ def test_conv_split_any_range(act_scale, dy_scale):
     xr, wr = x.clone().double().requires_grad_(True), w.clone().double().requires_grad_(True)
     y = F.conv2d(xr, wr, b.double(), padding="same")
     y.backward(dy.double())
-    xg, wg, bg, dyg = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
-    out = torch.empty(F_, cout, hw, hw, device=DEV)
-    L().paig_conv2d_fwd(p(xg), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout, hw,
-                        hw, ks, 128, st())
-    dx = torch.empty(F_, cin, hw, hw, device=DEV)
-    L().paig_conv2d_fwd(p(dyg), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, None, 0, p(wg), None, F_, cout, cin, hw,
-                        hw, ks, 8 | 128, st())
-    nmax = 64
-    slab = torch.empty(nmax * (cout * cin * ks * ks + cout), device=DEV)
-    nb = ctypes.c_int(0)
-    L().paig_conv2d_wgrad(p(xg), cin * hw * hw, 0, 0, p(dyg), cout * hw * hw, p(slab), nmax, ctypes.byref(nb), F_, cin,
-                          cout, hw, hw, ks, 128, st())
-    g = torch.empty(cout * cin * ks * ks + cout, device=DEV)
-    L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
-    torch.cuda.synchronize()
-    assert rel_err(out, y.detach()) <= 1e-5
-    assert rel_err(dx, xr.grad) <= 1e-5
-    assert rel_err(g[:cout * cin * ks * ks].view_as(w), wr.grad) <= 1e-5
+    for mode in ("fwd", "host"):
+        out, dx, gw, xmax = _split_conv_all(x, w, b, dy, ks, mode)
+        assert rel_err(out, y.detach()) <= 1e-5
+        assert rel_err(dx, xr.grad) <= 1e-5
+        assert rel_err(gw, wr.grad) <= 1e-5, mode
+        assert _range_status() == 0
+    # the slots: every one written, their max = max |x|
+    assert torch.isfinite(xmax).all() and float(xmax.max()) == float(x.abs().max())
+
+
+def test_conv_split_xmax_fallback_flag():
+    """A wgrad without the forward's slots stages X at the fixed 2^8: exact
+    below 256, flagged (not wrapped) beyond; the forward itself takes any
+    magnitude."""
+    cin, cout, hw, ks, F_ = 8, 8, 32, 3, 2
+    torch.manual_seed(3)
+    x = torch.rand(F_, cin, hw, hw) * 100
+    w = torch.randn(cout, cin, 3, 3) * 0.2
+    b = torch.zeros(cout)
+    dy = torch.randn(F_, cout, hw, hw)
+    xr, wr = x.clone().double(), w.clone().double().requires_grad_(True)
+    F.conv2d(xr, wr, padding="same").backward(dy.double())
+    _range_status()
+    out, dx, gw, _ = _split_conv_all(x, w, b, dy, ks, "none")
+    assert rel_err(gw, wr.grad) <= 1e-5
     assert _range_status() == 0
+    x[1, 2, 3, 4] = 1e4
+    out, dx, gw, _ = _split_conv_all(x, w, b, dy, ks, "fwd")
+    assert rel_err(out, F.conv2d(x.double(), w.double(), padding="same")) <= 1e-5
+    assert _range_status() == 0
+    _split_conv_all(x, w, b, dy, ks, "none")
+    assert _range_status() == 1
 
 
 def test_conv_split_weight_range_flag():
@@ -371,9 +421,17 @@ def test_gemm_math1_range_flag():
     C = torch.empty(M, N, device=DEV)
     L().paig_gemm_ex(0, 0, M, N, K, 1.0, p(A), K, p(Bm), N, 0.0, p(C), N, None, 0, 0, None, 0, None, None, 0, 1, st())
     assert _range_status() == 1
-    # math 4 (scaled) at the same magnitude: exact enough, no flag
+    # math 4 (op(A) = a gradient, scaled dynamically) at the same magnitude: exact, no flag
     L().paig_gemm_ex(0, 0, M, N, K, 1.0, p(A), K, p(Bm), N, 0.0, p(C), N, None, 0, 0, None, 0, None, None, 0, 4, st())
     torch.cuda.synchronize()
     ref = A.double().cpu() @ Bm.double().cpu()
     assert rel_err(C, ref) <= 2e-5
     assert _range_status() == 0
+    # math 6 (both running): op(B) far outside f16 too, and tiny
+    for sb in (1e7, 1e-9):
+        B2 = Bm * sb
+        L().paig_gemm_ex(0, 0, M, N, K, 1.0, p(A), K, p(B2), N, 0.0, p(C), N, None, 0, 0, None, 0, None, None, 0, 6,
+                         st())
+        torch.cuda.synchronize()
+        assert rel_err(C, A.double().cpu() @ B2.double().cpu()) <= 2e-5
+        assert _range_status() == 0
