@@ -120,25 +120,51 @@ __device__ __forceinline__ int f16_scale_exp(float m) {
 
 // max over the wave of v >= 0, returned wave-uniform: DPP within rows of 16
 // (quad swaps, half-row and row mirrors: VALU ops, no LDS round trips), then
-// the four row results read as scalars.  The scale exponents of the
-// split-precision kernels need it once per staged tile.
+// the four row results read as scalars.  Non-negative floats order as their
+// bit patterns, so the steps are integer maxima (no NaN canonicalisation).
+// The scale exponents of the split-precision kernels need it once per tile.
 template <int CTRL>
-__device__ __forceinline__ float dpp_fmax(float v) {
-  const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false);
-  return fmaxf(v, __builtin_bit_cast(float, o));
+__device__ __forceinline__ unsigned dpp_umax(unsigned v) {
+  const unsigned o = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+  return v > o ? v : o;
 }
-__device__ __forceinline__ float wave_max_u(float v) {
-  v = dpp_fmax<0xB1>(v);    // quad_perm [1,0,3,2]
-  v = dpp_fmax<0x4E>(v);    // quad_perm [2,3,0,1]
-  v = dpp_fmax<0x141>(v);   // row_half_mirror: quads 0<->1, 2<->3
-  v = dpp_fmax<0x140>(v);   // row_mirror: halves of the row
-  const int b = __builtin_bit_cast(int, v);
-  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
-  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
-  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
-  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
-  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+__device__ __forceinline__ float wave_max_u(float f) {
+  unsigned v = __builtin_bit_cast(unsigned, f);
+  v = dpp_umax<0xB1>(v);    // quad_perm [1,0,3,2]
+  v = dpp_umax<0x4E>(v);    // quad_perm [2,3,0,1]
+  v = dpp_umax<0x141>(v);   // row_half_mirror: quads 0<->1, 2<->3
+  v = dpp_umax<0x140>(v);   // row_mirror: halves of the row
+  const unsigned r0 = __builtin_amdgcn_readlane((int)v, 0), r1 = __builtin_amdgcn_readlane((int)v, 16);
+  const unsigned r2 = __builtin_amdgcn_readlane((int)v, 32), r3 = __builtin_amdgcn_readlane((int)v, 48);
+  const unsigned a = r0 > r1 ? r0 : r1, b = r2 > r3 ? r2 : r3;
+  return __builtin_bit_cast(float, a > b ? a : b);
 }
+
+// Source of the zeros a branch-free staging load reads for an out-of-range
+// element: selecting the ADDRESS (instead of the loaded data) keeps the load
+// unconsumed until its use, so a prefetch really stays in flight behind the
+// MFMAs; a data select made the compiler wait for it right after issue.
+static __device__ __attribute__((aligned(16))) float paig_zeros[4];   // never written
+// zero planes for staging units that read several channel planes from one
+// base address (8 channels of up to 64 x 64 pixels, + one float2 beyond)
+static __device__ __attribute__((aligned(16))) float paig_zero_planes[8 * 4096 + 4];
+
+// f16 hi + lo pieces of two fp32 values already scaled into f16's range,
+// each pair packed (a in the low half): one packed RNE conversion per piece
+// and a packed residual, ~3 VALU ops per value
+typedef float pf32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 pf16x2 __attribute__((ext_vector_type(2)));
+struct HiLo {
+  unsigned h, l;
+};
+__device__ __forceinline__ HiLo split_pk(float a, float b) {
+  const pf32x2 v = {a, b};
+  const pf16x2 hh = __builtin_convertvector(v, pf16x2);
+  const pf16x2 ll = __builtin_convertvector(v - __builtin_convertvector(hh, pf32x2), pf16x2);
+  return HiLo{__builtin_bit_cast(unsigned, hh), __builtin_bit_cast(unsigned, ll)};
+}
+// m = max(m, |a|, |b|): one v_max3 with abs modifiers (m stays canonical)
+__device__ __forceinline__ float amax2(float m, float a, float b) { return fmaxf(fmaxf(m, fabsf(a)), fabsf(b)); }
 
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll

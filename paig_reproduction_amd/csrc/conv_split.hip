@@ -50,6 +50,8 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int rup(int a, int b) { return ceil_div(a, b) * b; }
 
@@ -139,14 +141,9 @@ struct UpStage {
       const int q = i % QS, sr = (i / QS) % SRN, c = (i / (QS * SRN)) % CIN, fi = i / (QS * SRN * CIN);
       const int srow = y0 / 2 - 1 + sr;
       const bool ok = i < NSU && f0 + fi < F && srow >= 0 && srow < HS;
-      const int off = ok ? fi * (int)x.fs + c * HS * WS + srow * WS + VS * q : 0;
-      if constexpr (VS == 4) {
-        const f32x4 u = *reinterpret_cast<const f32x4*>(x.frame(f0) + off);
-        v[l] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        const float u = x.frame(f0)[off];
-        v1[l] = ok ? u : 0.f;
-      }
+      const float* src = ok ? x.frame(f0) + fi * (int)x.fs + c * HS * WS + srow * WS + VS * q : paig_zeros;
+      if constexpr (VS == 4) v[l] = *reinterpret_cast<const f32x4*>(src);
+      else v1[l] = *src;
     }
   }
   // max |v| of the prefetched window: a bound on its upsampled values (convex
@@ -155,7 +152,7 @@ struct UpStage {
     float m = 0.f;
 #pragma unroll
     for (int l = 0; l < NLS; ++l) {
-      if constexpr (VS == 4) m = fmaxf(m, fmaxf(fmaxf(fabsf(v[l][0]), fabsf(v[l][1])), fmaxf(fabsf(v[l][2]), fabsf(v[l][3]))));
+      if constexpr (VS == 4) m = amax2(amax2(m, v[l][0], v[l][1]), v[l][2], v[l][3]);
       else m = fmaxf(m, fabsf(v1[l]));
     }
     return m;
@@ -358,19 +355,36 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
   float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::IMG + C::WIMG));
   constexpr int UPX = C::UPX;
-  auto put_px = [&](int i, const float2* v) {
+  auto put_px = [&](int i, const float2* v, float sc) {
     const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
     const int o = ((fi * ROWS + r) * RP + (xp + PADL) * PS + cc) * 8;
     s16x8 h0, l0, h1, l1;
+    if constexpr (PM == 0) {
+      // scaled by sc (packed multiplies), split pairwise along the channels
+      pf32x2 sv[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      short h, lo;
-      split<PM>(v[c].x, h, lo, rmax);
-      h0[c] = h;
-      l0[c] = lo;
-      split<PM>(v[c].y, h, lo, rmax);
-      h1[c] = h;
-      l1[c] = lo;
+      for (int c = 0; c < 8; ++c) sv[c] = pf32x2{v[c].x, v[c].y} * sc;
+      u32x4 a0, b0, a1, b1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        { const HiLo q_ = split_pk(sv[2 * k].x, sv[2 * k + 1].x); a0[k] = q_.h; b0[k] = q_.l; }
+        { const HiLo q_ = split_pk(sv[2 * k].y, sv[2 * k + 1].y); a1[k] = q_.h; b1[k] = q_.l; }
+      }
+      h0 = __builtin_bit_cast(s16x8, a0);
+      l0 = __builtin_bit_cast(s16x8, b0);
+      h1 = __builtin_bit_cast(s16x8, a1);
+      l1 = __builtin_bit_cast(s16x8, b1);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        short h, lo;
+        split<PM>(v[c].x, h, lo, rmax);
+        h0[c] = h;
+        l0[c] = lo;
+        split<PM>(v[c].y, h, lo, rmax);
+        h1[c] = h;
+        l1[c] = lo;
+      }
     }
     *reinterpret_cast<s16x8*>(Xh + o) = h0;
     if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = l0;
@@ -410,12 +424,14 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
         const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
         const int gy = y0 + r - PADL;
         const bool ok = i < NI && f0 + fi < F && gy >= 0 && gy < H;
-        const int off = ok ? fi * (int)in.fs + cc * 8 * (int)PLANE + gy * W + xp : 0;
+        const int off = fi * (int)in.fs + cc * 8 * (int)PLANE + gy * W + xp;
+        static_assert(8 * PLANE <= 8 * 4096, "paig_zero_planes covers the unit");
+        const float* base = ok ? fb + off : paig_zero_planes;   // one address per unit
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          const float* q = fb + off + (cc * 8 + c < CIN ? c : 0) * (int)PLANE;
-          const float2 v = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
-          pre[l][c] = (ok && cc * 8 + c < CIN) ? v : make_float2(0.f, 0.f);
+          // channels past CIN (CIN % 8 != 0 only) read a zero of their own
+          const float* q = CIN % 8 == 0 || cc * 8 + c < CIN ? base + c * (int)PLANE : paig_zeros;
+          pre[l][c] = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
         }
       }
     }
@@ -435,26 +451,17 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
         for (int c = 0; c < 8; ++c)
           v[c] = (ok && cc * 8 + c < CIN)
-                     ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp) * tsc,
-                                   UPX == 2 ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1) * tsc : 0.f)
+                     ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp),
+                                   UPX == 2 ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1) : 0.f)
                      : make_float2(0.f, 0.f);
-        put_px(i, v);
+        put_px(i, v, tsc);
       }
     } else {
-      if constexpr (SCL) {
-#pragma unroll
-        for (int l = 0; l < NL; ++l)
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            pre[l][c].x *= tsc;
-            pre[l][c].y *= tsc;
-          }
-      }
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         const int i = tid + l * 256;
         if (NI % 256 != 0 && i >= NI) break;
-        put_px(i, pre[l]);
+        put_px(i, pre[l], tsc);
       }
     }
   };
@@ -470,14 +477,18 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
       for (int l = 0; l < NL; ++l)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) m = fmaxf(m, fmaxf(fabsf(pre[l][c].x), fabsf(pre[l][c].y)));
+        for (int c = 0; c < 8; ++c) m = amax2(m, pre[l][c].x, pre[l][c].y);
     }
     m = wave_max_u(m);
     if (lane == 0) smax[wv] = m;
   };
 
-  int lt = blockIdx.x;   // logical tile; xcd_tile() gives the physical one
-  if (lt < ntiles) issue(xcd_tile(lt, ntiles));
+  // logical tile lt; xcd_tile() gives the physical one; past the last tile,
+  // tile ntiles lies beyond frame F and every lane reads paig_zeros (the
+  // prefetch stays unconditional: branch-free for the load counting)
+  int lt = blockIdx.x;
+  auto tile_of = [&](int l) { return l < ntiles ? xcd_tile(l, ntiles) : ntiles; };
+  issue(tile_of(lt));
   // PM 0: the slice's weights scaled by 2^ew (max |w| into [2^14, 2^15)), so
   // small weights keep 22 significant bits instead of an f16-subnormal lo
   // piece; the epilogue takes the exponent back out exactly
@@ -497,6 +508,14 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     *reinterpret_cast<s16x8*>(Wh + idx * 8) = vh;
     if (PM != 2) *reinterpret_cast<s16x8*>(Wl + idx * 8) = vl;
   }
+  // the bias of this lane's output channels (block constant)
+  float bvs[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int co = co0 + nt * 16 + (lane & 15);
+    bvs[nt] = *(bias && co < COUT ? bias + co : paig_zeros);
+    asm volatile("" ::"v"(bvs[nt]));   // arrived before the loop: no wait on it behind a prefetch
+  }
   for (; lt < ntiles; lt += gridDim.x) {
     const int tile = xcd_tile(lt, ntiles);
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
@@ -504,7 +523,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
     __syncthreads();
-    if (lt + (int)gridDim.x < ntiles) issue(xcd_tile(lt + gridDim.x, ntiles));
+    issue(tile_of(lt + gridDim.x));
     f32x4 acc[MW][NT];
 #pragma unroll
     for (int mt = 0; mt < MW; ++mt)
@@ -533,7 +552,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     for (int nt = 0; nt < NT; ++nt) {
       const int co = co0 + nt * 16 + (lane & 15);
       if (co >= COUT) continue;
-      const float bv = bias ? bias[co] : 0.f;
+      const float bv = bvs[nt];
 #pragma unroll
       for (int mt = 0; mt < MW; ++mt) {
         const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
@@ -785,27 +804,43 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     const int gy = y0 + r - PADL;
     const bool ok = i < NIX && f0 + fi < F && gy >= 0 && gy < H;
     const float* fb = x.frame(f0);
-    const int off = ok ? fi * (int)x.fs + cq * 4 * (int)PLANE + gy * W + xp : 0;
+    const int off = fi * (int)x.fs + cq * 4 * (int)PLANE + gy * W + xp;
+    const float* base = ok ? fb + off : paig_zero_planes;   // one address per unit
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float* q = fb + off + (cq * 4 + c < CINB ? c : 0) * (int)PLANE;
-      const float2 u = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
-      v[c] = (ok && cq * 4 + c < CINB) ? u : make_float2(0.f, 0.f);
+      const float* q = CINB % 4 == 0 || cq * 4 + c < CINB ? base + c * (int)PLANE : paig_zeros;
+      v[c] = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
     }
   };
   auto put_x = [&](int i, const float2* v) {
     const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
     const int o = xplane(cq) + ((fi * ROWS + r) * TWPX + xp + OFFX) * 4;
     s16x8 hv, lv;
+    if constexpr (PM == 0) {
+      pf32x2 sv[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      short h, lo;
-      split<PM>(PM == 0 ? v[c].x * xsc : v[c].x, h, lo, rmax);
-      hv[c] = h;
-      lv[c] = lo;
-      split<PM>(PM == 0 ? v[c].y * xsc : v[c].y, h, lo, rmax);
-      hv[4 + c] = h;
-      lv[4 + c] = lo;
+      for (int c = 0; c < 4; ++c) {
+        sv[c] = pf32x2{v[c].x, v[c].y} * xsc;
+        rmax = amax2(rmax, sv[c].x, sv[c].y);
+      }
+      u32x4 a, b;
+      { const HiLo q_ = split_pk(sv[0].x, sv[1].x); a[0] = q_.h; b[0] = q_.l; }
+      { const HiLo q_ = split_pk(sv[2].x, sv[3].x); a[1] = q_.h; b[1] = q_.l; }
+      { const HiLo q_ = split_pk(sv[0].y, sv[1].y); a[2] = q_.h; b[2] = q_.l; }
+      { const HiLo q_ = split_pk(sv[2].y, sv[3].y); a[3] = q_.h; b[3] = q_.l; }
+      hv = __builtin_bit_cast(s16x8, a);
+      lv = __builtin_bit_cast(s16x8, b);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        short h, lo;
+        split<PM>(v[c].x, h, lo, rmax);
+        hv[c] = h;
+        lv[c] = lo;
+        split<PM>(v[c].y, h, lo, rmax);
+        hv[4 + c] = h;
+        lv[4 + c] = lo;
+      }
     }
     if constexpr (UPX == 2) {
       *reinterpret_cast<s16x8*>(Xh + o) = hv;
@@ -880,19 +915,24 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
       if constexpr (DPIPE) dv = sd[l];
       else dv = load_d(t, l);
       if (first) bacc[l] += (dv[0] + dv[1]) + (dv[2] + dv[3]);   // zeros past DU; unscaled
-      if constexpr (PM == 0) {
-        if constexpr (DSYNC)
-          rd = fmaxf(rd, fmaxf(fmaxf(fabsf(dv[0]), fabsf(dv[1])), fmaxf(fabsf(dv[2]), fabsf(dv[3]))));
-        dv *= dsc;
-      }
       s16x4 hv, lv;
-      float dmx = 0.f;
+      if constexpr (PM == 0) {
+        if constexpr (DSYNC) rd = amax2(amax2(rd, dv[0], dv[1]), dv[2], dv[3]);
+        const pf32x2 d0 = pf32x2{dv[0], dv[1]} * dsc, d1 = pf32x2{dv[2], dv[3]} * dsc;
+        u32x2 a, b;
+        { const HiLo q_ = split_pk(d0.x, d0.y); a[0] = q_.h; b[0] = q_.l; }
+        { const HiLo q_ = split_pk(d1.x, d1.y); a[1] = q_.h; b[1] = q_.l; }
+        hv = __builtin_bit_cast(s16x4, a);
+        lv = __builtin_bit_cast(s16x4, b);
+      } else {
+        float dmx = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        short h, lo;
-        split<PM>(dv[e], h, lo, dmx);
-        hv[e] = h;
-        lv[e] = lo;
+        for (int e = 0; e < 4; ++e) {
+          short h, lo;
+          split<PM>(dv[e], h, lo, dmx);
+          hv[e] = h;
+          lv[e] = lo;
+        }
       }
       if constexpr (DU == 4) {
         *reinterpret_cast<s16x4*>(Dh + co * DP + pt) = hv;
@@ -974,8 +1014,7 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     if constexpr (!DSYNC) {
       float m = 0.f;
 #pragma unroll
-      for (int l = 0; l < NLD; ++l)
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(sd[l][0]), fabsf(sd[l][1])), fmaxf(fabsf(sd[l][2]), fabsf(sd[l][3]))));
+      for (int l = 0; l < NLD; ++l) m = amax2(amax2(m, sd[l][0], sd[l][1]), sd[l][2], sd[l][3]);
       m = wave_max_u(m);
       if (lane == 0) smax[wv] = m;
     }
@@ -1005,7 +1044,9 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     commit(tile);
     __syncthreads();
     check_sync(tile);
-    if (lt + (int)gridDim.x < ntiles) issue(xcd_tile(lt + gridDim.x, ntiles));
+    // unconditional (branch-free for the load counting): past the last tile,
+    // tile ntiles lies beyond frame F and every lane reads paig_zeros
+    issue(lt + (int)gridDim.x < ntiles ? xcd_tile(lt + gridDim.x, ntiles) : ntiles);
 #pragma unroll
     for (int kb = wp; kb < KB; kb += WP) {
       // k-block kb: 32 consecutive tile pixels, all in one frame

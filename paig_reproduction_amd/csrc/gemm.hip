@@ -43,6 +43,9 @@ __device__ __forceinline__ float epi(float v, int act, int auxm, const float* au
   return v;
 }
 
+// the source of out-of-range operand elements (Tile::load_bf)
+__device__ __attribute__((aligned(16))) float zero16[4];   // zero-initialised, never written
+
 // One operand tile (64 rows x BK k) as 2 float4 per thread.
 //  KCONTIG: element (r, k) at p[(r0 + r) * ld + k0 + k]   -> image [r][k]
 // !KCONTIG: element (r, k) at p[(k0 + k) * ld + r0 + r]   -> image [k][r]
@@ -76,6 +79,36 @@ struct Tile {
         }
       }
       v[e] = x;
+    }
+  }
+  // Branch-free form (split kernels): every lane issues its loads, and an
+  // out-of-range element reads a zero from zero16 instead (the address is
+  // selected, not the data, so nothing waits on the load before its use):
+  // the compiler counts the loads in flight and the register ring really
+  // overlaps them (branchy or data-selected loads made it wait for all).
+  // VEC: float4 along the contiguous dimension, which must then be a multiple
+  // of 4 with 16-byte aligned rows.
+  template <bool VEC>
+  __device__ __forceinline__ void load_bf(const float* __restrict__ p, long long ld, int r0, int k0, int R, int K,
+                                          int tid) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      int r, k;
+      if (KCONTIG) { r = (tid >> 3) + 32 * e; k = (tid & 7) * 4; }
+      else { k = (tid >> 4) + 16 * e; r = (tid & 15) * 4; }
+      const int gr = r0 + r, gk = k0 + k;
+      if constexpr (VEC) {
+        const bool ok = gr < R && gk < K;
+        const float* q = ok ? p + (KCONTIG ? (long long)gr * ld + gk : (long long)gk * ld + gr) : zero16;
+        v[e] = *reinterpret_cast<const f32x4*>(q);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rr = KCONTIG ? gr : gr + i, kk = KCONTIG ? gk + i : gk;
+          const bool ok = rr < R && kk < K;
+          v[e][i] = *(ok ? p + (KCONTIG ? (long long)rr * ld + kk : (long long)kk * ld + rr) : zero16);
+        }
+      }
     }
   }
   __device__ __forceinline__ void store(float* img, int tid) const {
@@ -236,6 +269,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 // [row][k] pitch (16-bit elements): 6 16-B slots.  ds_read_b128 serves a
 // wave in lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): 8 rows at
@@ -287,12 +321,23 @@ __device__ __forceinline__ void store16(const Tile<KCONTIG>& t, short* ih, short
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     s16x4 hv, lv;
+    if constexpr (F16PM(PM)) {
+      // packed multiplies and conversions (split_pk), pairs of consecutive elements
+      const pf32x2 a = pf32x2{t.v[e][0], t.v[e][1]} * sc, b = pf32x2{t.v[e][2], t.v[e][3]} * sc;
+      rmax = amax2(amax2(rmax, a.x, a.y), b.x, b.y);
+      u32x2 h, l;
+      { const HiLo q_ = split_pk(a.x, a.y); h[0] = q_.h; l[0] = q_.l; }
+      { const HiLo q_ = split_pk(b.x, b.y); h[1] = q_.h; l[1] = q_.l; }
+      hv = __builtin_bit_cast(s16x4, h);
+      lv = __builtin_bit_cast(s16x4, l);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      short h, l;
-      gsplit<PM>(t.v[e][i] * sc, h, l, rmax);
-      hv[i] = h;
-      lv[i] = l;
+      for (int i = 0; i < 4; ++i) {
+        short h, l;
+        gsplit<PM>(t.v[e][i] * sc, h, l, rmax);
+        hv[i] = h;
+        lv[i] = l;
+      }
     }
     int o;
     if (KCONTIG) o = ((tid >> 3) + 32 * e) * SPK + (tid & 7) * 4;
@@ -314,7 +359,7 @@ __device__ __forceinline__ s16x8 frag16(const short* img, int r0, int lane) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <bool TA, bool TB, int PM>
+template <bool TA, bool TB, int PM, bool VEC>
 __global__ void __launch_bounds__(256)
 gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
              const float* __restrict__ B, long long ldb, int vecb, float* __restrict__ C, long long ldc, float beta,
@@ -362,11 +407,10 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
   Tile<!TA> ta[NS];
   Tile<TB> tb[NS];
 #pragma unroll
-  for (int st = 0; st < NS; ++st)
-    if (kbeg + st * BK < kend) {
-      ta[st].load(A, lda, m0, kbeg + st * BK, M, kend, veca, tid);
-      tb[st].load(B, ldb, n0, kbeg + st * BK, N, kend, vecb, tid);
-    }
+  for (int st = 0; st < NS; ++st) {   // (tiles past kend load as zeros)
+    ta[st].template load_bf<VEC>(A, lda, m0, kbeg + st * BK, M, kend, tid);
+    tb[st].template load_bf<VEC>(B, ldb, n0, kbeg + st * BK, N, kend, tid);
+  }
   for (int k0 = kbeg; k0 < kend; k0 += NS * BK) {
 #pragma unroll
     for (int st = 0; st < NS; ++st) {
@@ -378,18 +422,14 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
       if constexpr (DA) {
         float ma = 0.f;
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) ma = fmaxf(ma, fabsf(ta[st].v[e][i]));
+        for (int e = 0; e < 2; ++e) ma = amax2(amax2(ma, ta[st].v[e][0], ta[st].v[e][1]), ta[st].v[e][2], ta[st].v[e][3]);
         ma = wave_max_u(ma);
         if (lane == 0) smx[wv] = ma;
       }
       if constexpr (DB) {
         float mb = 0.f;
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) mb = fmaxf(mb, fabsf(tb[st].v[e][i]));
+        for (int e = 0; e < 2; ++e) mb = amax2(amax2(mb, tb[st].v[e][0], tb[st].v[e][1]), tb[st].v[e][2], tb[st].v[e][3]);
         mb = wave_max_u(mb);
         if (lane == 0) smx[4 + wv] = mb;
       }
@@ -419,10 +459,8 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
       store16<TB, PM>(tb[st], Bh, Bl, tid, bsc, DB ? dmx : rmax);
       if (do_rs) rs4 += ta[st].v[0] + ta[st].v[1];
       __syncthreads();
-      if (kk + NS * BK < kend) {
-        ta[st].load(A, lda, m0, kk + NS * BK, M, kend, veca, tid);
-        tb[st].load(B, ldb, n0, kk + NS * BK, N, kend, vecb, tid);
-      }
+      ta[st].template load_bf<VEC>(A, lda, m0, kk + NS * BK, M, kend, tid);
+      tb[st].template load_bf<VEC>(B, ldb, n0, kk + NS * BK, N, kend, tid);
       s16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -592,13 +630,21 @@ static void launch_gemm(int math, dim3 grid, hipStream_t st, int M, int N, int K
 #define PAIG_L(KERN)                                                                                          \
   hipLaunchKernelGGL(KERN, grid, dim3(256), 0, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, \
                      bias, act, auxm, aux, ldaux, part, rowsum, rowpart)
-  if (math == 1) PAIG_L((gemm_split_k<TA, TB, 1>));
-  else if (math == 2) PAIG_L((gemm_split_k<TA, TB, 2>));
-  else if (math == 3) PAIG_L((gemm_split_k<TA, TB, 3>));
-  else if (math == 4) PAIG_L((gemm_split_k<TA, TB, 4>));
-  else if (math == 5) PAIG_L((gemm_split_k<TA, TB, 5>));
-  else if (math == 6) PAIG_L((gemm_split_k<TA, TB, 6>));
+  // the split kernels' branch-free loads: float4 when both operands allow
+  const bool v = va && vb;
+#define PAIG_S(PM_) \
+  do {                                              \
+    if (v) PAIG_L((gemm_split_k<TA, TB, PM_, true>)); \
+    else PAIG_L((gemm_split_k<TA, TB, PM_, false>));  \
+  } while (0)
+  if (math == 1) PAIG_S(1);
+  else if (math == 2) PAIG_S(2);
+  else if (math == 3) PAIG_S(3);
+  else if (math == 4) PAIG_S(4);
+  else if (math == 5) PAIG_S(5);
+  else if (math == 6) PAIG_S(6);
   else PAIG_L((gemm_k<TA, TB>));
+#undef PAIG_S
 #undef PAIG_L
 }
 
@@ -641,7 +687,10 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
   dim3 grid(cdiv(N, BN), cdiv(M, BM), S);
   float* part = S > 1 ? ws : nullptr;
   float* rowpart = (S > 1 && rowsum) ? ws + (size_t)S * M * N : nullptr;
-  const int va = vec_ok(A, lda), vb = vec_ok(B, ldb);
+  // float4 operand loads: aligned rows and a contiguous extent that is a
+  // multiple of 4 (op(A) is k-contiguous unless ta, op(B) when tb)
+  const int va = vec_ok(A, lda) && (ta ? M % 4 == 0 : K % 4 == 0);
+  const int vb = vec_ok(B, ldb) && (tb ? K % 4 == 0 : N % 4 == 0);
 #define PAIG_G(TA_, TB_)                                                                                       \
   launch_gemm<TA_, TB_>(math, grid, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, bias, act, auxm, \
                         aux, ldaux, part, rowsum, rowpart)

@@ -36,3 +36,22 @@ def test_device_batches_match_host(rank, world):
         assert dx.dtype == torch.float32 and tuple(dx.shape) == (3, T, C, H, W)
         assert np.array_equal(dx.cpu().numpy(), hx.astype(np.float32))
         assert host.get_epoch() == dev.get_epoch()
+
+
+@pytest.mark.gpu
+def test_gather_every_byte_value():
+    """v / 255 of every byte value bit for bit as numpy's float32 division."""
+    N, T, H, W, C = 4, 2, 8, 8, 3
+    u8 = (np.arange(N * T * H * W * C) % 256).astype(np.uint8).reshape(N, T, H, W, C)
+    want = u8.astype(np.float32).reshape(N, T, C, H, W) / 255
+    dev = DeviceDataIterator(u8, (T, C, H, W), "cuda:0", seed=0)
+    for _ in range(2):
+        dx, _ = dev.next_batch(2)
+        torch.cuda.synchronize()
+        for row in dx.cpu().numpy():
+            assert any(np.array_equal(row, w) for w in want)
+    dx = torch.empty(N, T, C, H, W, device="cuda:0")
+    dev.reset_iteration()
+    dev.next_batch(N, out=dx)
+    torch.cuda.synchronize()
+    assert sorted(map(bytes, dx.cpu().numpy())) == sorted(map(bytes, want))   # all 256 values, every sequence

@@ -14,6 +14,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from paig_reproduction_amd._lib import lib  # noqa: E402
 
+XS = int(os.environ.get("PAIG_XMAX_SLOTS", "2048"))
 MODES = {"split": 128, "fp32": 0, "bf16": 256}
 # (name, Cin, Cout, H, ks, fused-upsample input): ShallowUNet(hidden 8) at 32x32
 LAYERS = [("c1", 3, 8, 32, 3, 0), ("c2", 8, 8, 32, 3, 0), ("c3", 8, 16, 16, 3, 0), ("c4", 16, 16, 16, 3, 0),
@@ -43,17 +44,26 @@ def main():
         dx = torch.empty(F, cin, H, H, device=dev)
         aux = torch.rand(F, cin, H, H, device=dev)
         slab = torch.empty(768 * (cout * cin * ks * ks + cout), device=dev)
+        xmax = torch.zeros(XS, device=dev)   # the forward's per-block max |x| slots (ex entry points)
+        ex = hasattr(L, "paig_conv2d_fwd_ex")
         nb = ctypes.c_int(0)
         fl = 2 * F * cin * cout * ks * ks * H * H
         for mode in modes:
             m = MODES[mode]
             runs = {
-                "fwd": lambda: L.paig_conv2d_fwd(x.data_ptr(), cin * Hin * Hin, 0, 0, y.data_ptr(), cout * H * H, None,
-                                                 0, w.data_ptr(), b.data_ptr(), F, cin, cout, H, H, ks,
-                                                 1 | (32 if up else 0) | m, st),
-                "wgrad": lambda: L.paig_conv2d_wgrad(x.data_ptr(), cin * Hin * Hin, 0, 0, dy.data_ptr(), cout * H * H,
-                                                     slab.data_ptr(), 768, ctypes.byref(nb), F, cin, cout, H, H, ks,
-                                                     (32 if up else 0) | m, st),
+                "fwd": (lambda: L.paig_conv2d_fwd_ex(x.data_ptr(), cin * Hin * Hin, 0, 0, y.data_ptr(), cout * H * H,
+                                                     None, 0, w.data_ptr(), b.data_ptr(), F, cin, cout, H, H, ks,
+                                                     1 | (32 if up else 0) | m, xmax.data_ptr(), XS, st)) if ex else
+                       (lambda: L.paig_conv2d_fwd(x.data_ptr(), cin * Hin * Hin, 0, 0, y.data_ptr(), cout * H * H,
+                                                  None, 0, w.data_ptr(), b.data_ptr(), F, cin, cout, H, H, ks,
+                                                  1 | (32 if up else 0) | m, st)),
+                "wgrad": (lambda: L.paig_conv2d_wgrad_ex(x.data_ptr(), cin * Hin * Hin, 0, 0, dy.data_ptr(),
+                                                         cout * H * H, slab.data_ptr(), 768, ctypes.byref(nb), F, cin,
+                                                         cout, H, H, ks, (32 if up else 0) | m, xmax.data_ptr(), XS,
+                                                         st)) if ex else
+                         (lambda: L.paig_conv2d_wgrad(x.data_ptr(), cin * Hin * Hin, 0, 0, dy.data_ptr(), cout * H * H,
+                                                      slab.data_ptr(), 768, ctypes.byref(nb), F, cin, cout, H, H, ks,
+                                                      (32 if up else 0) | m, st)),
             }
             if name != "c1":
                 runs["dgrad"] = lambda: L.paig_conv2d_fwd(dy.data_ptr(), cout * H * H, 0, 0, dx.data_ptr(),
