@@ -858,8 +858,9 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     const int co = i / NPU, pt = DU * (i % NPU);
     const int fi = pt / (RT * W), y = (pt / W) % RT, xx = pt % W;
     const bool ok = i < NID && f0 + fi < F;
+    // (a tile past the last one has f0 >= F: its lanes read frame 0)
     const int off = ok ? fi * (int)dy.fs + co * (int)HW + (y0 + y) * W + xx : 0;
-    const float* q = dy.frame(f0) + off;
+    const float* q = dy.frame(f0 < F ? f0 : 0) + off;
     f32x4 v;
     if constexpr (DU == 4) v = *reinterpret_cast<const f32x4*>(q);
     else if constexpr (DU == 2) {
