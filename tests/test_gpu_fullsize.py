@@ -8,7 +8,8 @@ tests cover the same kernels at small sizes):
   (physics_models.py:119-142), so loss(B) and every gradient equal the average
   of the two half batches' (what the data-parallel AVG all-reduce relies on).
   Bar: 1e-5 on losses, GRAD_RTOL on gradients (different summation order);
-  3bp is chaotic (see test_gpu_parity), so its bars are the rollout ones.
+  3bp is chaotic (see test_gpu_parity), so its rollout losses get the
+  rollout bar.
 """
 import numpy as np
 import pytest
@@ -23,7 +24,8 @@ FULL = [("spring_color", "spring_ode_cell", 50, 4, 6, 32, 100),
         ("3bp_color", "gravity_ode_cell", 20, 4, 12, 36, 512),
         ("mnist_spring_color", "spring_ode_cell", 12, 3, 7, 64, 256),
         ("bouncing_balls", "bouncing_ode_cell", 100, 4, 6, 32, 1024)]
-GRAD_RTOL = 1e-3
+# ~3x the worst measured (round 2: 1.9e-6 mnist c15, <= 9.4e-7 elsewhere, 3bp included)
+GRAD_RTOL = 6e-6
 
 
 def _setup(task, cell, seq_len, ins, pred, size, B):
@@ -67,9 +69,11 @@ def test_full_size_batch_halves_average(cfg):
     la, ga = _step(m, x[:B // 2].contiguous())
     lb, gb = _step(m, x[B // 2:].contiguous())
     chaotic = cfg[0] == "3bp_color"
-    lbar, gbar = (2e-3, 5e-2) if chaotic else (1e-5, GRAD_RTOL)
+    lbar, gbar = (2e-3, GRAD_RTOL) if chaotic else (1e-5, GRAD_RTOL)
     for i, what in enumerate(("train", "extrap", "recons")):
         bar = 1e-5 if what == "recons" else lbar   # recons does not go through the rollout
         assert rel_err(np.float64(lf[i]), np.float64((la[i] + lb[i]) / 2)) <= bar, what
-    for k in gf:
-        assert rel_err(gf[k], (ga[k] + gb[k]) / 2) <= gbar, k
+    errs = {k: rel_err(gf[k], (ga[k] + gb[k]) / 2) for k in gf}
+    print(cfg[0], "worst grad", max(errs.items(), key=lambda kv: kv[1]))
+    for k, e in errs.items():
+        assert e <= gbar, (k, e)

@@ -18,16 +18,18 @@ from helpers import GOLDEN, load_golden, golden_weights, rel_err, grad_checks, R
 
 pytestmark = pytest.mark.gpu
 
-GRAD_RTOL = 1e-3
+# gradient bars: ~3x the worst error measured against the fixtures (round 2,
+# both conv arithmetics alike; `pytest -s` prints it as "worst grad"):
+#   ShallowUNet configs (spring / bouncing / altvel): <= 3.1e-5
+#   3bp (gravity, 16 rollout steps): 1.0e-5
+#   mnist (UNet over 64x64 frames, 3 max-pools): 5.3e-4 -- near-tie max-pool
+#   / ReLU decisions of this fixture flip under one-ulp changes, so even fp32
+#   oracle runs on one-ulp-perturbed weights differ from it by 3.9e-4
+#   (tests/test_gpu_envelope.py bounds every config against that spread)
+GRAD_RTOL = 1e-4
+GRAD_RTOL_3BP = 3e-5
+GRAD_RTOL_MNIST = 1.6e-3
 ROLLOUT_RTOL_3BP = 2e-3
-# mnist (UNet, 3 max-pools over 64x64 frames of clipped-noise background) in
-# split mode: outputs stay within ~2e-6 of the fixture, but the f16 hi/lo
-# forward's ~1e-6 activation differences move more near-tie max-pool/ReLU
-# decisions than exact fp32 does, and the rerouted gradient shows in a few
-# summed-gradient checks (c10: 1.5e-3).  Measured with tools/grad_errs.py: the
-# same step with the exact-fp32 forward and the split dgrad/wgrad stays at the
-# fp32 mode's 5.2e-4, so the backward arithmetic is not the cause.
-GRAD_RTOL_MNIST_SPLIT = 2.5e-3
 SUPPORTED = list(GOLDEN)
 
 
@@ -48,8 +50,8 @@ def _input(z, device):
     return torch.from_numpy(x).to(device)
 
 
-# conv arithmetic: "split" (default: f16 hi/lo forward, bf16 hi/lo backward on
-# the 16-bit matrix cores) and "fp32" (f32-input MFMA) both meet the fp32 bar
+# conv arithmetic: "split" (default: f16 hi/lo pieces scaled by powers of two
+# on the 16-bit matrix cores) and "fp32" (f32-input MFMA) both meet the fp32 bar
 @pytest.mark.parametrize("conv_math", ["split", "fp32"])
 @pytest.mark.parametrize("name", SUPPORTED)
 def test_step_matches_reference(name, conv_math):
@@ -82,8 +84,7 @@ def test_step_matches_reference(name, conv_math):
     for k in ("output_seq", "pos_vel_seq", "loss_extrap", "loss_train", "loss_pred_aliased"):
         assert errs[k] <= rt, (k, errs[k])
     grads = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
-    bar = 5e-2 if name.startswith("3bp") else (
-        GRAD_RTOL_MNIST_SPLIT if name.startswith("mnist") and conv_math == "split" else GRAD_RTOL)
+    bar = GRAD_RTOL_3BP if name.startswith("3bp") else (GRAD_RTOL_MNIST if name.startswith("mnist") else GRAD_RTOL)
     gerr = grad_checks(z, grads, bar, prefix=name + ": ")
     worst = max(gerr.items(), key=lambda kv: kv[1])
     print(name, "worst grad", worst)
