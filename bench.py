@@ -290,11 +290,14 @@ def main():
             graph = ((g1, g2), lg)
         torch.cuda.synchronize()
 
+    replays = [0]
+
     def step():
         if graph is None:
             return eager_step()
         gs, lg = graph
         it.next_batch(a.batch, out=xbuf)   # get_batch: one gather launch, no H2D
+        replays[0] += 1
         gs[0].replay()
         if len(gs) == 2:
             m._flat.allreduce_early()   # overlaps the second graph (U-Net backward)
@@ -318,6 +321,10 @@ def main():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    if opt_in_graph:
+        # the captured RMSprop step ran Python once, at capture: count its
+        # replays (its lr is the captured constant; RMSprop only, see above)
+        m.optimizer.steps += replays[0]
     lossv = float(loss.item())
     # roofline probes: every tagged main-stream launch timed with HIP events
     # on its stream, over eager steps of the same workload after the timed region

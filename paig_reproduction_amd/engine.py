@@ -610,6 +610,10 @@ class Engine:
                                *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
                                ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, K, h, H, st)
 
+        # the side chain's inputs exist before the fork (a temporary made after
+        # it could be recycled by a main-stream allocation while the side
+        # kernel still reads it)
+        d_pvs_c = d_pvs.contiguous() if d_pvs is not None else None
         sst = self._fork(dev)
         # ---- (side) rollout adjoint -> d pos0, d vel0, physics params
         prm = self.cell_params(lay)
@@ -618,7 +622,7 @@ class Engine:
             gk, gq = self.g("rollout_cell.k"), self.g("rollout_cell.equil")
         elif lay.cell == 2:
             gk = self.g("rollout_cell.g")
-        L.paig_rollout_bwd(lay.cell, ptr(pvs), ptr(dpos_roll), ptr(d_pvs.contiguous() if d_pvs is not None else None),
+        L.paig_rollout_bwd(lay.cell, ptr(pvs), ptr(dpos_roll), ptr(d_pvs_c),
                            ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(dpos0), ptr(dvel0), ptr(rpart), ptr(gk), ptr(gq),
                            0, B, D, R, sst)
         # ---- (side) velocity encoder backward -> d packed inputs
@@ -651,6 +655,7 @@ class Engine:
                                for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
                              _parr([ptr(pt) for pt in vparts]), _iarr([P for _, P, _, _ in vfn]), st)
         self._join(dev)
+        del d_pvs_c   # (kept alive across the side chain)
 
         L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
 

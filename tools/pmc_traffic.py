@@ -29,7 +29,9 @@ def load(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        k = short(r["Kernel_Name"])
+        # launches of one kernel with different grids (e.g. the decoder over
+        # rollout and reconstruction frames) are kept apart: "name @grid"
+        k = short(r["Kernel_Name"]) + " @" + r["Grid_Size"]
         per[k].append(float(r["Counter_Value"]) * 1024.0)
         meta[k] = {"vgpr": int(r["VGPR_Count"]), "agpr": int(r["Accum_VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
                    "lds": int(r["LDS_Block_Size"]), "wg": int(r["Workgroup_Size"])}
@@ -45,7 +47,9 @@ def main():
     ap.add_argument("--task", default="spring_color")
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--seq_len", type=int, default=50)
-    ap.add_argument("--probe", action="append", default=[], help="TAG=KERNEL: bench.py probe tag -> kernel name")
+    ap.add_argument("--conv_math", default="split")
+    ap.add_argument("--probe", action="append", default=[],
+                    help="TAG=KERNEL @GRID: bench.py probe tag -> kernel name and grid (a key of 'kernels')")
     ap.add_argument("--command", default="")
     a = ap.parse_args()
     f, meta = load(a.fetch, "FETCH_SIZE")
@@ -58,7 +62,7 @@ def main():
                   "traffic_bytes": fr + wr, **meta.get(k, {})}
     probes = dict(p.split("=", 1) for p in a.probe)
     json.dump({"correction": "fetch x2 (gfx950 FETCH_SIZE halving), KiB -> bytes", "command": a.command,
-               "config": {"task": a.task, "batch": a.batch, "seq_len": a.seq_len}, "steps_profiled": a.steps,
+               "config": {"task": a.task, "batch": a.batch, "seq_len": a.seq_len, "conv_math": a.conv_math}, "steps_profiled": a.steps,
                "probe_kernels": probes, "kernels": res}, open(a.out, "w"), indent=1, sort_keys=True)
     for k, v in sorted(res.items(), key=lambda kv: -kv[1]["traffic_bytes"] * kv[1]["launches"])[:25]:
         print("%-70s n=%4d  fetch %9.2f MB  write %9.2f MB" % (k[:70], v["launches"], v["fetch_bytes"] / 1e6,

@@ -3,7 +3,7 @@
 #   graph-mode and eager-mode rocprofv3 kernel stats, FETCH_SIZE / WRITE_SIZE
 #   PMC passes (one counter per run).  Output: gpurun_out/prof_<tag>/
 set -e
-TAG=${1:-r01}
+TAG=${1:-r02}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
