@@ -359,7 +359,9 @@ def main():
         gbs = kd["bytes"] / sec / 1e9
         return {"bound": "hbm", "kernel": kd["tag"], "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_tflops": round(tflops, 2),
-                "avg_us": round(kd["avg_ms"] * 1e3, 2), "launches": kd["n"], "algorithmic_flops": kd["flops"],
+                "avg_us": round(kd["avg_ms"] * 1e3, 2), "avg_us_events_raw": round(kd["avg_ms_raw"] * 1e3, 2),
+                "event_overhead_us": round(kd["overhead_ms"] * 1e3, 2), "launches": kd["n"],
+                "algorithmic_flops": kd["flops"],
                 "algorithmic_bytes": kd["bytes"]}
 
     roof = None

@@ -215,14 +215,34 @@ class KernelProbe:
 
         return _Ctx()
 
-    def summaries(self):
-        """{tag: {tag, n, avg_ms, flops, bytes}} (per launch)."""
+    def overhead_ms(self, n=20):
+        """The event pair's own cost around one dispatch: the same bracket
+        (backlogged stream, start event, launch, end event) around a spin
+        kernel of zero cycles.  Subtracted from the probed intervals so they
+        compare with rocprof's kernel start-to-end durations."""
+        pairs = []
+        for _ in range(n):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(self.backlog_cycles)
+            e0.record()
+            torch.cuda._sleep(0)
+            e1.record()
+            pairs.append((e0, e1))
         torch.cuda.synchronize()
+        return min(a.elapsed_time(b) for a, b in pairs)
+
+    def summaries(self):
+        """{tag: {tag, n, avg_ms, avg_ms_raw, flops, bytes}} (per launch;
+        avg_ms net of the event bracket's overhead)."""
+        torch.cuda.synchronize()
+        ovh = self.overhead_ms() if self.events else 0.0
         out = {}
         for tag, evs in self.events.items():
             ms = [a.elapsed_time(b) for a, b in evs]
             fl, nb = self.work[tag]
-            out[tag] = {"tag": tag, "n": len(ms), "avg_ms": sum(ms) / len(ms), "flops": fl, "bytes": nb}
+            raw = sum(ms) / len(ms)
+            out[tag] = {"tag": tag, "n": len(ms), "avg_ms": max(raw - ovh, 1e-6), "avg_ms_raw": raw,
+                        "overhead_ms": ovh, "flops": fl, "bytes": nb}
         return out
 
     def summary(self):
