@@ -87,7 +87,7 @@ def test_rmsprop_trajectory(name):
     for s in range(steps):
         m.output = m(xs[s % 2])
         tl, (p, e, r) = m.compute_loss()
-        losses.append([float(tl), float(p), float(e), float(r)])
+        losses.append([float(v.detach()) for v in (tl, p, e, r)])
         m.optimizer.zero_grad(set_to_none=True)
         tl.backward()
         m.optimizer.step()
@@ -133,7 +133,7 @@ def test_reference_loss_mode():
     for s in range(2):
         m.forward(_x(z["input_u8_%d" % s], dev))    # result discarded (base.py:142)
         tl, (p, e, r) = m.compute_loss()
-        losses.append([float(tl), float(p), float(e), float(r)])
+        losses.append([float(v.detach()) for v in (tl, p, e, r)])
         m.optimizer.zero_grad(set_to_none=True)
         tl.backward()
         if s == 0:
