@@ -12,7 +12,6 @@
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // v / 255 correctly rounded (= IEEE division, as numpy) for v in 0..255:
 // the reciprocal product plus one fma correction of its exact residual
@@ -23,22 +22,36 @@ __device__ __forceinline__ float div255(float v) {
   return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, v), r, q);
 }
 
+// One 4-byte word -> one float4 per lane: each wave instruction reads 256
+// contiguous bytes and writes 1 KB contiguous (the 16-byte-word-per-lane form
+// wrote 16 B at a 64-B lane stride, four partial passes over every line).
 __global__ void __launch_bounds__(256)
 gather_u8_f32_k(const uint8_t* __restrict__ src, const long long* __restrict__ idx, float* __restrict__ out,
                 long long row) {
   const int b = blockIdx.y;
-  const uint8_t* s = src + idx[b] * row;
-  float* o = out + (long long)b * row;
-  const long long n16 = row / 16;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x) {
-    const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + i * 16));
+  const unsigned* s = reinterpret_cast<const unsigned*>(src + idx[b] * row);
+  f32x4* o = reinterpret_cast<f32x4*>(out + (long long)b * row);
+  const long long n4 = row / 4;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  for (; i + 3 * step < n4; i += 4 * step) {   // four words in flight per lane
+    unsigned w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int k = 0; k < 4; ++k) w[k] = __builtin_nontemporal_load(s + i + k * step);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
       f32x4 f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) f[e] = div255((float)((w[j] >> (8 * e)) & 0xffu));
-      *reinterpret_cast<f32x4*>(o + i * 16 + 4 * j) = f;
+      for (int e = 0; e < 4; ++e) f[e] = div255((float)((w[k] >> (8 * e)) & 0xffu));
+      o[i + k * step] = f;
     }
+  }
+  for (; i < n4; i += step) {
+    const unsigned w = __builtin_nontemporal_load(s + i);
+    f32x4 f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = div255((float)((w >> (8 * e)) & 0xffu));
+    o[i] = f;
   }
 }
 
@@ -51,7 +64,7 @@ int paig_gather_u8_f32(const unsigned char* src, const long long* idx, float* ou
   if (B <= 0 || row <= 0) return 0;
   PAIG_REQUIRE(((uintptr_t)src % 16) == 0 && ((uintptr_t)out % 16) == 0 && row % 16 == 0,
                "gather_u8_f32: src/out must be 16-byte aligned and row (%lld) a multiple of 16", row);
-  long long per = (row / 16 + 255) / 256;
+  long long per = (row / 16 + 255) / 256;   // blocks for four words per lane
   const unsigned gx = (unsigned)(per < 64 ? per : 64);
   hipLaunchKernelGGL(gather_u8_f32_k, dim3(gx, B), dim3(256), 0, (hipStream_t)stream, src, idx, out, row);
   PAIG_CHECK_LAUNCH();
