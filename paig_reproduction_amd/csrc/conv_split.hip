@@ -235,14 +235,19 @@ constexpr int sfwd_vgprs(int CIN, int H, int W, int KS, bool UPS, int tpxm, int 
 // fits the LDS and the registers; wide layers (UNet, 48..128 channels) split
 // COUT over blocks (grid.y; each slice's weights resident) and/or take
 // smaller pixel tiles.  At most 4 output tiles per block.
+// Pass 0 keeps two blocks per CU (LDS <= half the CU's): one 256-thread
+// block is one wave per SIMD, which leaves the staging VALU work and the
+// MFMAs serialised (the UNet's 32..128-channel layers: 1.2-1.7x faster).
+// Not for the fused upsample (its 64 x 64 layer measured 1.2x slower on
+// 64-pixel tiles).
 constexpr int sfwd_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM) {
   const int base = W == 8 ? 128 : 256, NT = ceil_div(COUT, 16);
-  for (int pass = 0; pass < 2; ++pass)
+  for (int pass = UPS ? 1 : 0; pass < 3; ++pass)
     for (int nb = 1; nb <= NT; ++nb) {
       if (NT % nb != 0 || NT / nb > 4) continue;
-      for (int tp = base; tp >= (pass == 0 ? base / 2 : 64); tp /= 2)
-        if (sfwd_lds(CIN, H, W, KS, UPS, PM, tp, NT / nb) <= LDS_MAX &&
-            sfwd_vgprs(CIN, H, W, KS, UPS, tp, NT / nb) <= 264)
+      for (int tp = base; tp >= (pass == 1 ? base / 2 : 64); tp /= 2)
+        if (sfwd_lds(CIN, H, W, KS, UPS, PM, tp, NT / nb) <= (pass == 0 ? LDS_MAX / 2 : LDS_MAX) &&
+            sfwd_vgprs(CIN, H, W, KS, UPS, tp, NT / nb) <= 264 && (pass > 0 || tp >= base / 2))
           return tp * 256 + nb;
     }
   return 0;
@@ -442,19 +447,43 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
       __syncthreads();
+if constexpr (W % 4 == 0) {
+        // units of 4 pixels x 8 channels: one row4 per channel (shared taps
+        // and source reads), stored as two 2-pixel staging units
+        constexpr int W4 = W / 4;
 #pragma unroll 1
-      for (int i = tid; i < NI; i += 256) {
-        const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
-        const int gy = y0 + r - PADL;
-        const bool ok = f0 + fi < F && gy >= 0 && gy < H;
-        float2 v[8];
+        for (int i = tid; i < NI / 2; i += 256) {
+          const int q = i % W4, r = (i / W4) % ROWS, cc = (i / (W4 * ROWS)) % CC, fi = i / (W4 * ROWS * CC);
+          const int gy = y0 + r - PADL;
+          const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+          f32x4 o[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
-          v[c] = (ok && cc * 8 + c < CIN)
-                     ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp),
-                                   UPX == 2 ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1) : 0.f)
-                     : make_float2(0.f, 0.f);
-        put_px(i, v, tsc);
+          for (int c = 0; c < 8; ++c)
+            o[c] = (ok && cc * 8 + c < CIN) ? UP::row4(Sl, fi, cc * 8 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const int ia = ((fi * CC + cc) * ROWS + r) * W2 + 2 * q;
+          float2 v[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) v[c] = make_float2(o[c][0], o[c][1]);
+          put_px(ia, v, tsc);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) v[c] = make_float2(o[c][2], o[c][3]);
+          put_px(ia + 1, v, tsc);
+        }
+      } else {
+#pragma unroll 1
+        for (int i = tid; i < NI; i += 256) {
+          const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
+          const int gy = y0 + r - PADL;
+          const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+          float2 v[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            v[c] = (ok && cc * 8 + c < CIN)
+                       ? make_float2(UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp),
+                                     UPX == 2 ? UP::px1(Sl, fi, cc * 8 + c, gy, y0, xp + 1) : 0.f)
+                       : make_float2(0.f, 0.f);
+          put_px(i, v, tsc);
+        }
       }
     } else {
 #pragma unroll
@@ -628,23 +657,29 @@ constexpr int swg_lds(int CINB, int COUTB, int H, int W, int KS, bool UPS, int P
 // and staging fit; wide layers take the slice with the most work per block.
 constexpr int swg_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM) {
   const int ci[] = {CIN, 128, 64, 32, 16, 8}, oc[] = {COUT, 128, 64, 32, 16};
-  int best = 0, bw = 0, bs = 0;
-  for (int cb : ci) {
-    if (cb > CIN || CIN % cb != 0 || (cb != CIN && cb % 4 != 0)) continue;
-    for (int ob : oc) {
-      if (ob > COUT || COUT % ob != 0 || (UPS && ob > 16)) continue;   // UPS: dY staging registers
-      const int MT = ceil_div(ob, 16), NT = ceil_div(KS * KS * ceil_div(cb, 4), 4);
-      if (MT * ceil_div(NT, 4) * 4 > 40 || swg_lds(cb, ob, H, W, KS, UPS, PM) > LDS_MAX) continue;
-      // ties: the fewest staged channels
-      const int sc = cb + ob;
-      if (cb * ob > bw || (cb * ob == bw && sc < bs)) {
-        bw = cb * ob;
-        bs = sc;
-        best = cb * 4096 + ob;
+  // pass 0: two blocks per CU (see sfwd_pick; not for the 64 x 64 fused
+  // upsample, whose halved channel slices measured 4% slower)
+  for (int pass = UPS && H * W >= 4096 ? 1 : 0; pass < 2; ++pass) {
+    int best = 0, bw = 0, bs = 0;
+    for (int cb : ci) {
+      if (cb > CIN || CIN % cb != 0 || (cb != CIN && cb % 4 != 0)) continue;
+      for (int ob : oc) {
+        if (ob > COUT || COUT % ob != 0 || (UPS && ob > 16)) continue;   // UPS: dY staging registers
+        const int MT = ceil_div(ob, 16), NT = ceil_div(KS * KS * ceil_div(cb, 4), 4);
+        if (MT * ceil_div(NT, 4) * 4 > 40 || swg_lds(cb, ob, H, W, KS, UPS, PM) > (pass == 0 ? LDS_MAX / 2 : LDS_MAX))
+          continue;
+        // ties: the fewest staged channels
+        const int sc = cb + ob;
+        if (cb * ob > bw || (cb * ob == bw && sc < bs)) {
+          bw = cb * ob;
+          bs = sc;
+          best = cb * 4096 + ob;
+        }
       }
     }
+    if (best) return best;
   }
-  return best;
+  return 0;
 }
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
@@ -691,7 +726,10 @@ struct SWgCfg {
   static constexpr int UPX = W % 2 == 0 ? 2 : 1;              // X units: UPX pixels x 4 channels
   static constexpr int W2 = W / UPX;
   static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = (NIX + 255) / 256;
-  static constexpr int DU = W % 4 == 0 ? 4 : (W % 2 == 0 ? 2 : 1);   // dY units: DU pixels x 1 channel
+  // dY units: DU pixels (of one row) x 1 channel; 3 for 3bp's 9 x 9 level
+  // (1-pixel units there need 31 units per thread, and as many bias partial
+  // registers: the kernel spilled 88 VGPRs)
+  static constexpr int DU = W % 4 == 0 ? 4 : (W % 2 == 0 ? 2 : (W % 3 == 0 ? 3 : 1));
   static constexpr int NPU = TPXV / DU;                       // dY units per channel
   static constexpr int NID = COUTB * NPU, NLD = (NID + 255) / 256;
   static constexpr int SLAB = COUT * NCOL + COUT;
@@ -866,6 +904,8 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     else if constexpr (DU == 2) {
       const float2 u = *reinterpret_cast<const float2*>(q);
       v = f32x4{u.x, u.y, 0.f, 0.f};
+    } else if constexpr (DU == 3) {
+      v = f32x4{q[0], q[1], q[2], 0.f};
     } else {
       v = f32x4{*q, 0.f, 0.f, 0.f};
     }
@@ -959,19 +999,42 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
       __syncthreads();
+if constexpr (W % 4 == 0) {
+        // units of 4 pixels x 4 channels (row4: shared taps and source reads)
+        constexpr int W4 = W / 4;
 #pragma unroll 1
-      for (int i = tid; i < NIX; i += 256) {
-        const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
-        const int gy = y0 + r - PADL;
-        const bool ok = f0 + fi < F && gy >= 0 && gy < H;
-        float2 v[4];
+        for (int i = tid; i < NIX / 2; i += 256) {
+          const int q = i % W4, r = (i / W4) % ROWS, cq = (i / (W4 * ROWS)) % CQ, fi = i / (W4 * ROWS * CQ);
+          const int gy = y0 + r - PADL;
+          const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+          f32x4 o[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          v[c] = (ok && cq * 4 + c < CINB)
-                     ? make_float2(UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp),
-                                   UPX == 2 ? UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp + 1) : 0.f)
-                     : make_float2(0.f, 0.f);
-        put_x(i, v);
+          for (int c = 0; c < 4; ++c)
+            o[c] = (ok && cq * 4 + c < CINB) ? UP::row4(Sl, fi, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const int ia = ((fi * CQ + cq) * ROWS + r) * W2 + 2 * q;
+          float2 v[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][0], o[c][1]);
+          put_x(ia, v);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][2], o[c][3]);
+          put_x(ia + 1, v);
+        }
+      } else {
+#pragma unroll 1
+        for (int i = tid; i < NIX; i += 256) {
+          const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+          const int gy = y0 + r - PADL;
+          const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+          float2 v[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            v[c] = (ok && cq * 4 + c < CINB)
+                       ? make_float2(UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp),
+                                     UPX == 2 ? UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp + 1) : 0.f)
+                       : make_float2(0.f, 0.f);
+          put_x(i, v);
+        }
       }
     } else if constexpr (XPIPE) {
 #pragma unroll

@@ -351,7 +351,7 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
 
 // ---------------------------------------------------------------------------
 // Register-resident variants for the small frames of the headline workloads
-// ((K, H) = (2, 32) spring/bouncing; the forward also (3, 36) 3bp).  Every
+// ((K, H) = (2, 32) spring/bouncing, (3, 36) 3bp).  Every
 // thread owns the same PPT pixels and SPT source texels in every frame, so
 //   * the background values it composites are loaded once per block,
 //   * its background / template / content gradients accumulate in registers
@@ -939,6 +939,8 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
   float* gs = need_scratch ? scratch : nullptr;
   if (K == 2 && H == 32 && !need_scratch)
     hipLaunchKernelGGL((dec_bwd_reg_k<2, 32>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, F);
+  else if (K == 3 && H == 36 && !need_scratch)
+    hipLaunchKernelGGL((dec_bwd_reg_k<3, 36>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, F);
   else if (K == 2)
     hipLaunchKernelGGL((dec_bwd_k<2>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);
   else if (K == 3)
