@@ -104,6 +104,21 @@ int paig_mask_softmax_fwd(const float* logits, const float* x, long long x_fs, i
 int paig_mask_softmax_bwd(const float* logits, const float* x, long long x_fs, int x_grp, long long x_gs,
                           const float* masks, const float* dobjs, float* dlogits, int F, int K, int C, int H, int W,
                           int flags, void* stream);
+/* ---- ShallowUNet c13 (1x1 conv 8 -> K, ReLU'd, Q13; blocks.py:276,307) fused
+ *      with the mask softmax (blocks.py:84-93); K in {2, 3}, H*W % 4 == 0.
+ * fwd: masks, masked objects from c12's output x12 [F][8][H][W]; the logits are
+ *      formed in registers (fp32 FMAs) and not stored.
+ * bwd: dx12 = c13's input gradient with c12's ReLU' applied; slab receives one
+ *      row of K*8 weight + K bias partial gradients per block
+ *      (paig_head_mask_blocks(F, H, W) rows), reduced like a conv wgrad slab.
+ *      Replaces c13's conv fwd / dgrad / wgrad and paig_mask_softmax_fwd/bwd
+ *      on the ShallowUNet path. */
+int paig_head_mask_blocks(int F, int H, int W);
+int paig_head_mask_fwd(const float* x12, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                       long long x_gs, float* masks, float* objs, int F, int K, int H, int W, void* stream);
+int paig_head_mask_bwd(const float* x12, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                       long long x_gs, const float* masks, const float* dobjs, float* dx12, float* slab, int F, int K,
+                       int H, int W, void* stream);
 int paig_pos_head_fwd(const float* h3, float* pos, int N, int K, float half, void* stream);
 int paig_pos_head_bwd(const float* h3, const float* dpos, float* dh3, int N, int K, float half, void* stream);
 

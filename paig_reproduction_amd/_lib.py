@@ -48,6 +48,9 @@ SIGNATURES = {
     "paig_upsample2_bwd": (I, [P, LL, P, LL, P, LL, I, I, I, I, I, I, I, P]),
     "paig_mask_softmax_fwd": (I, [P, P, LL, I, LL, P, P, P, I, I, I, I, I, P]),
     "paig_mask_softmax_bwd": (I, [P, P, LL, I, LL, P, P, P, I, I, I, I, I, I, P]),
+    "paig_head_mask_blocks": (I, [I, I, I]),
+    "paig_head_mask_fwd": (I, [P, P, P, P, LL, I, LL, P, P, I, I, I, I, P]),
+    "paig_head_mask_bwd": (I, [P, P, P, P, LL, I, LL, P, P, P, P, I, I, I, I, P]),
     "paig_pos_head_fwd": (I, [P, P, I, I, F32, P]),
     "paig_pos_head_bwd": (I, [P, P, P, I, I, F32, P]),
     "paig_gemm_workspace": (SZ, [I, I, I]),
@@ -91,7 +94,7 @@ SIGNATURES = {
 }
 
 _QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported", "paig_velmlp_bwd_blocks",
-          "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_gemm_workspace", "paig_colsum_workspace",
+          "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_mask_blocks", "paig_gemm_workspace", "paig_colsum_workspace",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
           "paig_decoder_bwd_scratch"}
 

@@ -22,6 +22,9 @@
 // (deterministic).
 #include "common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace {
 
 constexpr int BM = 64, BN = 64, BK = 32;
@@ -520,6 +523,261 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
   if constexpr (F16PM(PM)) f16_range_note(rmax);
 }
 
+// ------------------------------------------------- wide tiles (512 threads)
+// The same split-precision contract on 64 x 256 or 256 x 64 block tiles, for
+// the encoder projection's shapes (l1: 2000 x 200 x 3072 forward, 200 x 3072
+// x 2000 wgrad, 2000 x 3072 x 200 dgrad): one block spans the whole narrow
+// dimension (<= 256), so the wide operand is loaded, scaled and split ONCE
+// instead of once per 64-column tile (the 64 x 64 form converts the 24.6 MB
+// activation operand 4x and re-reads it from L2 4x), and each wave's K step
+// carries 2-3x the MFMAs per fragment read and barrier.  8 waves as WM x WN,
+// each a (BMT/WM) x (BNT/WN) patch of 16 x 16 MFMA tiles.
+template <bool KCONTIG, int ROWS>
+struct WTile {
+  static constexpr int NTHR = 512;
+  static constexpr int E = ROWS * BK / (4 * NTHR);   // float4 per thread: 64 rows -> 1, 256 -> 4
+  static constexpr int RQ = ROWS / 4;                // !KCONTIG: float4 per k-row
+  f32x4 v[E];
+  static __device__ __forceinline__ void rk(int tid, int e, int& r, int& k) {
+    if (KCONTIG) { r = (tid >> 3) + (NTHR / 8) * e; k = (tid & 7) * 4; }
+    else { r = (tid % RQ) * 4; k = tid / RQ + (NTHR / RQ) * e; }
+  }
+  template <bool VEC>
+  __device__ __forceinline__ void load_bf(const float* __restrict__ p, long long ld, int r0, int k0, int R, int K,
+                                          int tid) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      int r, k;
+      rk(tid, e, r, k);
+      const int gr = r0 + r, gk = k0 + k;
+      if constexpr (VEC) {
+        const bool ok = gr < R && gk < K;
+        const float* q = ok ? p + (KCONTIG ? (long long)gr * ld + gk : (long long)gk * ld + gr) : zero16;
+        v[e] = *reinterpret_cast<const f32x4*>(q);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rr = KCONTIG ? gr : gr + i, kk = KCONTIG ? gk + i : gk;
+          const bool ok = rr < R && kk < K;
+          v[e][i] = *(ok ? p + (KCONTIG ? (long long)rr * ld + kk : (long long)kk * ld + rr) : zero16);
+        }
+      }
+    }
+  }
+  // [pi(k)][row] pitch: ROWS + 16 shorts = an odd multiple of 32 B, so the
+  // 8 image rows a half-wave's ds_read_b64_tr_b16 reads hit 8 distinct 32-B
+  // bank groups (64 rows: 160 B, 256 rows: 544 B = 32 mod 256)
+  static constexpr int SPRW = ROWS + 16;
+  static constexpr int IMG = ROWS * SPK > BK * SPRW ? ROWS * SPK : BK * SPRW;
+  template <int PM>
+  __device__ __forceinline__ void store16(short* ih, short* il, int tid, float sc, float& rmax) const {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const pf32x2 a = pf32x2{v[e][0], v[e][1]} * sc, b = pf32x2{v[e][2], v[e][3]} * sc;
+      s16x4 hv, lv;
+      if constexpr (F16PM(PM)) {
+        rmax = amax2(amax2(rmax, a.x, a.y), b.x, b.y);
+        u32x2 h, l;
+        { const HiLo q_ = split_pk(a.x, a.y); h[0] = q_.h; l[0] = q_.l; }
+        { const HiLo q_ = split_pk(b.x, b.y); h[1] = q_.h; l[1] = q_.l; }
+        hv = __builtin_bit_cast(s16x4, h);
+        lv = __builtin_bit_cast(s16x4, l);
+      } else {
+        const float t[4] = {a.x, a.y, b.x, b.y};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          short hh, ll;
+          gsplit<PM>(t[i], hh, ll, rmax);
+          hv[i] = hh;
+          lv[i] = ll;
+        }
+      }
+      int r, k;
+      rk(tid, e, r, k);
+      const int o = KCONTIG ? r * SPK + k : kperm(k) * SPRW + r;
+      *reinterpret_cast<s16x4*>(ih + o) = hv;
+      if (PM != 3) *reinterpret_cast<s16x4*>(il + o) = lv;
+    }
+  }
+  __device__ __forceinline__ float amax() const {
+    float m = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) m = amax2(amax2(m, v[e][0], v[e][1]), v[e][2], v[e][3]);
+    return m;
+  }
+  static __device__ __forceinline__ s16x8 frag(const short* img, int r0, int lane) {
+    if (KCONTIG) return *reinterpret_cast<const s16x8*>(img + (r0 + (lane & 15)) * SPK + 8 * (lane >> 4));
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const short* b0 = img + kperm(8 * g + q) * SPRW + r0 + 4 * p;
+    const short* b1 = img + kperm(8 * g + 4 + q) * SPRW + r0 + 4 * p;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)b0);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)b1);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+};
+
+template <bool TA, bool TB, int PM, bool VEC, int BMT, int BNT>
+__global__ void __launch_bounds__(512)
+gemm_split_w_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
+               const float* __restrict__ B, long long ldb, int vecb, float* __restrict__ C, long long ldc, float beta,
+               const float* __restrict__ bias, int act, int auxm, const float* __restrict__ aux, long long ldaux,
+               float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart) {
+  constexpr int WM = BMT == 64 ? 2 : 4, WN = 8 / WM;
+  constexpr int PMW = BMT / WM, PNW = BNT / WN;          // wave patch
+  constexpr int MI = PMW / 16, NJ = PNW / 16;
+  using TTA = WTile<!TA, BMT>;
+  using TTB = WTile<TB, BNT>;
+  constexpr int IA = TTA::IMG, IB = TTB::IMG;
+  __shared__ __attribute__((aligned(16))) short S16[2 * IA + 2 * IB];
+  short* Ah = S16;
+  short* Al = S16 + IA;
+  short* Bh = S16 + 2 * IA;
+  short* Bl = Bh + IB;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int wm = wv / WN, wn = wv % WN;
+  const TileId bt = xcd_tile();
+  const int m0 = bt.y * BMT, n0 = bt.x * BNT;
+  const int kbeg = bt.z * kchunk;
+  int kend = kbeg + kchunk;
+  if (kend > K) kend = K;
+  const bool do_rs = TA && rowsum != nullptr && bt.x == 0;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 rs4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rmax = 0.f;
+  constexpr bool DA = PM == 4 || PM == 6, DB = PM == 6;
+  int eca = DA ? 100 : (PM == 5 ? PAIG_A_EXP : 0);
+  int ecb = DB ? 100 : (PM == 4 || PM == 5 ? PAIG_A_EXP : 0);
+  float asc = __builtin_amdgcn_ldexpf(1.f, eca);
+  float bsc = __builtin_amdgcn_ldexpf(1.f, ecb);
+  __shared__ float smx[16];
+
+  constexpr int NS = 3;
+  TTA ta[NS];
+  TTB tb[NS];
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    ta[st].template load_bf<VEC>(A, lda, m0, kbeg + st * BK, M, kend, tid);
+    tb[st].template load_bf<VEC>(B, ldb, n0, kbeg + st * BK, N, kend, tid);
+  }
+  for (int k0 = kbeg; k0 < kend; k0 += NS * BK) {
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      const int kk = k0 + st * BK;
+      if (kk >= kend) break;
+      if constexpr (DA) {
+        const float ma = wave_max_u(ta[st].amax());
+        if (lane == 0) smx[wv] = ma;
+      }
+      if constexpr (DB) {
+        const float mb = wave_max_u(tb[st].amax());
+        if (lane == 0) smx[8 + wv] = mb;
+      }
+      __syncthreads();
+      if constexpr (DA || DB) {
+        int na = eca, nb = ecb;
+        if constexpr (DA) {
+          float m = smx[0];
+#pragma unroll
+          for (int w = 1; w < 8; ++w) m = fmaxf(m, smx[w]);
+          na = min(eca, f16_scale_exp(m));
+        }
+        if constexpr (DB) {
+          float m = smx[8];
+#pragma unroll
+          for (int w = 9; w < 16; ++w) m = fmaxf(m, smx[w]);
+          nb = min(ecb, f16_scale_exp(m));
+        }
+        if (na + nb < eca + ecb) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                acc[i][j][r] = __builtin_amdgcn_ldexpf(acc[i][j][r], (na + nb) - (eca + ecb));
+        }
+        eca = na;
+        ecb = nb;
+        asc = __builtin_amdgcn_ldexpf(1.f, eca);
+        bsc = __builtin_amdgcn_ldexpf(1.f, ecb);
+      }
+      float dmx = 0.f;
+      ta[st].template store16<PM>(Ah, Al, tid, asc, DA ? dmx : rmax);
+      tb[st].template store16<PM>(Bh, Bl, tid, bsc, DB ? dmx : rmax);
+      if (do_rs) {
+#pragma unroll
+        for (int e = 0; e < TTA::E; ++e) rs4 += ta[st].v[e];
+      }
+      __syncthreads();
+      ta[st].template load_bf<VEC>(A, lda, m0, kk + NS * BK, M, kend, tid);
+      tb[st].template load_bf<VEC>(B, ldb, n0, kk + NS * BK, N, kend, tid);
+      s16x8 ah[MI], al[MI], bh[NJ], bl[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        ah[i] = TTA::frag(Ah, wm * PMW + i * 16, lane);
+        al[i] = PM != 3 ? TTA::frag(Al, wm * PMW + i * 16, lane) : ah[i];
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        bh[j] = TTB::frag(Bh, wn * PNW + j * 16, lane);
+        bl[j] = PM != 3 ? TTB::frag(Bl, wn * PNW + j * 16, lane) : bh[j];
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if constexpr (PM != 3) {
+            acc[i][j] = gmma<PM>(al[i], bh[j], acc[i][j]);
+            acc[i][j] = gmma<PM>(ah[i], bl[j], acc[i][j]);
+          }
+          acc[i][j] = gmma<PM>(ah[i], bh[j], acc[i][j]);
+        }
+    }
+  }
+  if (do_rs) {
+    // op(A) = A^T is the !KCONTIG tile: thread rows (tid % RQ)*4 .. +3; the
+    // NTHR / RQ threads of one row group are combined in a fixed order
+    constexpr int RQ = TTA::RQ, G = 512 / RQ;
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(S16);   // [G][BMT]
+    *reinterpret_cast<f32x4*>(red + (tid / RQ) * BMT + (tid % RQ) * 4) = rs4;
+    __syncthreads();
+    if (tid < BMT && m0 + tid < M) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < G; ++k) v += red[k * BMT + tid];
+      if (rowpart) rowpart[(long long)bt.z * M + m0 + tid] = alpha * v;
+      else rowsum[m0 + tid] = alpha * v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * PMW + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * PNW + j * 16 + (lane & 15);
+        if (m < M && n < N) {
+          float v = alpha * (SCALED(PM) ? __builtin_amdgcn_ldexpf(acc[i][j][r], -(eca + ecb)) : acc[i][j][r]);
+          if (part) {
+            part[((long long)bt.z * M + m) * N + n] = v;
+          } else {
+            if (beta != 0.f) v += beta * C[(long long)m * ldc + n];
+            if (bias) v += bias[n];
+            C[(long long)m * ldc + n] = epi(v, act, auxm, aux, (long long)m * ldaux + n);
+          }
+        }
+      }
+  if constexpr (F16PM(PM)) f16_range_note(rmax);
+}
+
 // sum_{s<S} p[s*ld] in order s = 0..S-1 (deterministic), loads issued 8 at a
 // time so the partial slabs stream instead of one dependent load per split
 __device__ __forceinline__ float sum_strided(const float* __restrict__ p, long long ld, int S) {
@@ -618,12 +876,46 @@ static int choose_split(int M, int N, int K) {
   return s;
 }
 
+// Tile plan: 0 = 64 x 64 (256 threads), 1 = 64 x 256, 2 = 256 x 64 (wide,
+// 512 threads, split-precision maths only).  A wide tile spans a narrow
+// dimension of 129..256 whole, when the grid still has >= 128 blocks.
+// PAIG_GEMM_TILE=0 in the environment forces the 64 x 64 form (A/B runs).
+struct GemmPlan {
+  int tile, S;
+};
+static int gemm_tile_env() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("PAIG_GEMM_TILE");
+    v = e ? atoi(e) : -1;
+  }
+  return v;
+}
+static GemmPlan plan_gemm(int M, int N, int K, int math) {
+  GemmPlan p{0, K > 0 ? choose_split(M, N, K) : 1};
+  if (!(math == 3 || math == 4 || math == 6) || gemm_tile_env() == 0 || K <= 0) return p;
+  // measured (tools/gemm_bench.py): the 64 x 256 tile wins where it holds the
+  // whole N and K is split (the projection forward, 34.8 -> 28.6 us); the
+  // l1 dgrad (N = 3072, K = 200) and the 256 x 64 wgrad tile fill fewer CUs
+  // and lost 20% each, so they keep the 64 x 64 form
+  int tile = 0;
+  if (N > 128 && N <= 256 && M >= 512 && K >= 512) tile = 1;
+  if (!tile) return p;
+  // the split depends on K alone (~12 K-steps per block), so a row's sum
+  // order does not change with M: a half batch reproduces the full batch's
+  // rows exactly (the data-parallel AVG identity, tests/test_gpu_fullsize.py)
+  int S = 1;
+  while (K / (2 * S) >= 384) S *= 2;
+  if ((long long)S * M * N > (8ll << 20) || cdiv(M, 64) * S < 128) return p;
+  return GemmPlan{tile, S};
+}
+
 static inline bool vec_ok(const float* p, long long ld) {
   return ((uintptr_t)p % 16 == 0) && (ld % 4 == 0);
 }
 
 template <bool TA, bool TB>
-static void launch_gemm(int math, dim3 grid, hipStream_t st, int M, int N, int K, int kchunk, float alpha,
+static void launch_gemm(int math, int tile, dim3 grid, hipStream_t st, int M, int N, int K, int kchunk, float alpha,
                         const float* A, long long lda, int va, const float* B, long long ldb, int vb, float* C,
                         long long ldc, float beta, const float* bias, int act, int auxm, const float* aux,
                         long long ldaux, float* part, float* rowsum, float* rowpart) {
@@ -632,19 +924,31 @@ static void launch_gemm(int math, dim3 grid, hipStream_t st, int M, int N, int K
                      bias, act, auxm, aux, ldaux, part, rowsum, rowpart)
   // the split kernels' branch-free loads: float4 when both operands allow
   const bool v = va && vb;
+#define PAIG_W(KERN) \
+  hipLaunchKernelGGL(KERN, grid, dim3(512), 0, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, \
+                     bias, act, auxm, aux, ldaux, part, rowsum, rowpart)
 #define PAIG_S(PM_) \
   do {                                              \
     if (v) PAIG_L((gemm_split_k<TA, TB, PM_, true>)); \
     else PAIG_L((gemm_split_k<TA, TB, PM_, false>));  \
   } while (0)
+  // wide tiles: the step's maths (3, 4, 6) with float4 operands (plan_gemm)
+#define PAIG_SW(PM_) \
+  do {                                                                  \
+    if (tile == 1) PAIG_W((gemm_split_w_k<TA, TB, PM_, true, 64, 256>)); \
+    else if (tile == 2) PAIG_W((gemm_split_w_k<TA, TB, PM_, true, 256, 64>)); \
+    else PAIG_S(PM_);                                                   \
+  } while (0)
   if (math == 1) PAIG_S(1);
   else if (math == 2) PAIG_S(2);
-  else if (math == 3) PAIG_S(3);
-  else if (math == 4) PAIG_S(4);
+  else if (math == 3) PAIG_SW(3);
+  else if (math == 4) PAIG_SW(4);
   else if (math == 5) PAIG_S(5);
-  else if (math == 6) PAIG_S(6);
+  else if (math == 6) PAIG_SW(6);
   else PAIG_L((gemm_k<TA, TB>));
+#undef PAIG_SW
 #undef PAIG_S
+#undef PAIG_W
 #undef PAIG_L
 }
 
@@ -658,8 +962,13 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
                  void* stream);
 
 size_t paig_gemm_workspace(int M, int N, int K) {
-  int s = choose_split(M, N, K);
-  return s > 1 ? (size_t)s * M * N + (size_t)s * M : 0;
+  // the larger of the two plans (fp32 math always takes the 64 x 64 tiles)
+  size_t need = 0;
+  for (int math : {0, 4}) {   // 64 x 64 plan, wide plan
+    const GemmPlan p = plan_gemm(M, N, K, math);
+    if (p.S > 1) need = std::max(need, (size_t)p.S * M * N + (size_t)p.S * M);
+  }
+  return need;
 }
 
 int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
@@ -680,19 +989,23 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
   }
   if (rowsum && !ta) math = 0;   // fused row sums exist on the split path for op(A) = A^T only
   if (M <= 0 || N <= 0) return 0;
-  int S = K > 0 ? choose_split(M, N, K) : 1;
-  if (S > 1 && (ws == nullptr || ws_floats < (size_t)S * M * N + (size_t)S * M)) S = 1;
-  const int kchunk = S > 1 ? cdiv(cdiv(K, S), BK) * BK : (K > 0 ? K : 1);
-  S = K > 0 ? cdiv(K, kchunk) : 1;
-  dim3 grid(cdiv(N, BN), cdiv(M, BM), S);
-  float* part = S > 1 ? ws : nullptr;
-  float* rowpart = (S > 1 && rowsum) ? ws + (size_t)S * M * N : nullptr;
   // float4 operand loads: aligned rows and a contiguous extent that is a
   // multiple of 4 (op(A) is k-contiguous unless ta, op(B) when tb)
   const int va = vec_ok(A, lda) && (ta ? M % 4 == 0 : K % 4 == 0);
   const int vb = vec_ok(B, ldb) && (tb ? K % 4 == 0 : N % 4 == 0);
+  GemmPlan plan = plan_gemm(M, N, K, math);
+  if (plan.tile && !(va && vb)) plan = GemmPlan{0, K > 0 ? choose_split(M, N, K) : 1};
+  const int tile = plan.tile;
+  int S = plan.S;
+  if (S > 1 && (ws == nullptr || ws_floats < (size_t)S * M * N + (size_t)S * M)) S = 1;
+  const int kchunk = S > 1 ? cdiv(cdiv(K, S), BK) * BK : (K > 0 ? K : 1);
+  S = K > 0 ? cdiv(K, kchunk) : 1;
+  const int bm = tile == 2 ? 256 : BM, bn = tile == 1 ? 256 : BN;
+  dim3 grid(cdiv(N, bn), cdiv(M, bm), S);
+  float* part = S > 1 ? ws : nullptr;
+  float* rowpart = (S > 1 && rowsum) ? ws + (size_t)S * M * N : nullptr;
 #define PAIG_G(TA_, TB_)                                                                                       \
-  launch_gemm<TA_, TB_>(math, grid, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, bias, act, auxm, \
+  launch_gemm<TA_, TB_>(math, tile, grid, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, bias, act, auxm, \
                         aux, ldaux, part, rowsum, rowpart)
   if (ta && tb) PAIG_G(true, true);
   else if (ta) PAIG_G(true, false);

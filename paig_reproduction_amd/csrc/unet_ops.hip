@@ -482,6 +482,167 @@ __global__ void mask_softmax_bwd_v_k(const float* __restrict__ lg, FView x, cons
   }
 }
 
+// ------------------------------------- fused ShallowUNet head + mask softmax ----
+// ShallowUNet's last layer c13 (1x1 conv, 8 -> K, ReLU'd, Q13; blocks.py:276,
+// 307) fused into the mask softmax (blocks.py:84-93): the logits are formed
+// per pixel in fp32 FMAs from c12's output and never stored.  Forward: logits
+// -> softmax -> masks, masked objects.  Backward: the softmax backward, the
+// c13 ReLU' (the logits recomputed with the forward's exact operation order),
+// c13's input gradient with c12's ReLU' (dX12, the c12 backward's dY) and
+// c13's weight/bias gradient as one slab row per block (deterministic order,
+// reduced with the U-Net's slabs).  Replaces the c13 conv fwd/dgrad/wgrad and
+// the separate softmax kernels: the logits' write and re-reads, and 3 launches.
+constexpr int HEAD_CI = 8;   // ShallowUNet hidden width (c13's input channels)
+
+template <int K>
+__device__ __forceinline__ void head_logits(const float* __restrict__ w, const float* __restrict__ b, const m4* xv,
+                                            m4* l) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    m4 a = m4{b[k], b[k], b[k], b[k]};
+#pragma unroll
+    for (int c = 0; c < HEAD_CI; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = fmaf(w[k * HEAD_CI + c], xv[c][j], a[j]);
+    l[k] = a;
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) head_mask_fwd_k(const float* __restrict__ x12, const float* __restrict__ w,
+                                                       const float* __restrict__ b, FView x, float* __restrict__ masks,
+                                                       float* __restrict__ objs, int F, int HW) {
+  const int Q = HW / 4;
+  const long long n = (long long)F * Q;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int p = (int)(i % Q) * 4;
+    const int f = (int)(i / Q);
+    m4 hv[HEAD_CI];
+#pragma unroll
+    for (int c = 0; c < HEAD_CI; ++c) hv[c] = *reinterpret_cast<const m4*>(x12 + ((long long)f * HEAD_CI + c) * HW + p);
+    const float* xp = x.frame(f);
+    m4 xv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) xv[c] = *reinterpret_cast<const m4*>(xp + c * HW + p);
+    m4 l[K], e[K + 1];
+    head_logits<K>(w, b, hv, l);
+    m4 m = m4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        l[k][j] = l[k][j] < 0.f ? 0.f : l[k][j];   // c13's ReLU (Q13)
+        m[j] = fmaxf(m[j], l[k][j]);
+      }
+    m4 s = m4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[k][j] = expf(l[k][j] - m[j]);
+      s += e[k];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[K][j] = expf(1.f - m[j]);
+    s += e[K];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+      m4 mk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mk[j] = e[k][j] / s[j];
+      *reinterpret_cast<m4*>(masks + ((long long)f * (K + 1) + k) * HW + p) = mk;
+      if (k < K)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          *reinterpret_cast<m4*>(objs + ((long long)k * F + f) * 3 * HW + (long long)c * HW + p) = mk * xv[c];
+    }
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) head_mask_bwd_k(const float* __restrict__ x12, const float* __restrict__ w,
+                                                       const float* __restrict__ b, FView x,
+                                                       const float* __restrict__ masks, const float* __restrict__ dobjs,
+                                                       float* __restrict__ dx12, float* __restrict__ slab, int F,
+                                                       int HW) {
+  constexpr int NW = K * HEAD_CI + K;   // slab row: dW[k][c], then db[k]
+  const int Q = HW / 4;
+  const long long n = (long long)F * Q;
+  float acc[NW];
+#pragma unroll
+  for (int t = 0; t < NW; ++t) acc[t] = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int p = (int)(i % Q) * 4;
+    const int f = (int)(i / Q);
+    m4 hv[HEAD_CI];
+#pragma unroll
+    for (int c = 0; c < HEAD_CI; ++c) hv[c] = *reinterpret_cast<const m4*>(x12 + ((long long)f * HEAD_CI + c) * HW + p);
+    const float* xp = x.frame(f);
+    m4 xv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) xv[c] = *reinterpret_cast<const m4*>(xp + c * HW + p);
+    // softmax backward (mask_softmax_bwd_v_k's order)
+    m4 dm[K], mk[K];
+    m4 dot = m4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      m4 a = m4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const m4 d = *reinterpret_cast<const m4*>(dobjs + ((long long)k * F + f) * 3 * HW + (long long)c * HW + p);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = fmaf(d[j], xv[c][j], a[j]);
+      }
+      dm[k] = a;
+      mk[k] = *reinterpret_cast<const m4*>(masks + ((long long)f * (K + 1) + k) * HW + p);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dot[j] = fmaf(mk[k][j], a[j], dot[j]);
+    }
+    m4 l[K], g[K];
+    head_logits<K>(w, b, hv, l);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      g[k] = mk[k] * (dm[k] - dot);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[k][j] = l[k][j] > 0.f ? g[k][j] : 0.f;   // c13's ReLU'
+    }
+    // c13 input gradient (c12's ReLU' applied) and the weight / bias partials
+#pragma unroll
+    for (int c = 0; c < HEAD_CI; ++c) {
+      m4 d = m4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = fmaf(w[k * HEAD_CI + c], g[k][j], d[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = hv[c][j] > 0.f ? d[j] : 0.f;
+      *reinterpret_cast<m4*>(dx12 + ((long long)f * HEAD_CI + c) * HW + p) = d;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int c = 0; c < HEAD_CI; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[k * HEAD_CI + c] = fmaf(g[k][j], hv[c][j], acc[k * HEAD_CI + c]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[K * HEAD_CI + k] += g[k][j];
+    }
+  }
+  // block reduction in a fixed order: wave butterflies, then the 4 waves
+  __shared__ float red[4][NW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int t = 0; t < NW; ++t) {
+    float v = acc[t];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wv][t] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < NW)
+    slab[(long long)blockIdx.x * NW + threadIdx.x] =
+        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
 // --------------------------------------------------------- position head ----
 // enc_pos[n][2k+j] = tanh(h3[k*N+n][j]) * (H/2) + H/2
 __global__ void pos_head_fwd_k(const float* __restrict__ h3, float* __restrict__ pos, int N, int K, float half) {
@@ -820,6 +981,51 @@ int paig_mask_softmax_bwd(const float* logits, const float* x, long long x_fs, i
   else
     hipLaunchKernelGGL(mask_softmax_bwd_k, dim3(grid_for((long long)F * H * W)), dim3(256), 0, (hipStream_t)stream,
                        logits, FView{x, x_fs, x_gs, x_grp}, masks, dobjs, dlogits, F, K, C, H, W, flags);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+static bool head_mask_ok(const void* a, const void* b, const void* c, const void* d, const void* e, long long x_fs,
+                         long long x_gs, int K, int H, int W) {
+  return (H * W) % 4 == 0 && (K == 2 || K == 3) && x_fs % 4 == 0 && x_gs % 4 == 0 &&
+         ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)d | (uintptr_t)e) % 16 == 0;
+}
+
+int paig_head_mask_blocks(int F, int H, int W) {
+  const long long n = (long long)F * H * W / 4;
+  long long g = (n + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
+}
+
+int paig_head_mask_fwd(const float* x12, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                       long long x_gs, float* masks, float* objs, int F, int K, int H, int W, void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(head_mask_ok(x12, x, masks, objs, nullptr, x_fs, x_gs, K, H, W),
+               "head_mask_fwd: needs K in {2,3}, H*W %% 4 == 0 and 16-byte aligned buffers (K=%d H=%d W=%d)", K, H, W);
+  const dim3 g(grid_for((long long)F * H * W / 4));
+  if (K == 2)
+    hipLaunchKernelGGL(head_mask_fwd_k<2>, g, dim3(256), 0, (hipStream_t)stream, x12, w, b, FView{x, x_fs, x_gs, x_grp},
+                       masks, objs, F, H * W);
+  else
+    hipLaunchKernelGGL(head_mask_fwd_k<3>, g, dim3(256), 0, (hipStream_t)stream, x12, w, b, FView{x, x_fs, x_gs, x_grp},
+                       masks, objs, F, H * W);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_head_mask_bwd(const float* x12, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                       long long x_gs, const float* masks, const float* dobjs, float* dx12, float* slab, int F, int K,
+                       int H, int W, void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(head_mask_ok(x12, x, masks, dobjs, dx12, x_fs, x_gs, K, H, W),
+               "head_mask_bwd: needs K in {2,3}, H*W %% 4 == 0 and 16-byte aligned buffers (K=%d H=%d W=%d)", K, H, W);
+  const dim3 g(paig_head_mask_blocks(F, H, W));
+  if (K == 2)
+    hipLaunchKernelGGL(head_mask_bwd_k<2>, g, dim3(256), 0, (hipStream_t)stream, x12, w, b, FView{x, x_fs, x_gs, x_grp},
+                       masks, dobjs, dx12, slab, F, H * W);
+  else
+    hipLaunchKernelGGL(head_mask_bwd_k<3>, g, dim3(256), 0, (hipStream_t)stream, x12, w, b, FView{x, x_fs, x_gs, x_grp},
+                       masks, dobjs, dx12, slab, F, H * W);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

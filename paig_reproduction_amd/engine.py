@@ -175,6 +175,12 @@ class Layout:
                 self.fused_bufs.add(op["dst"][0])
         self.HW = self.H * self.H
         self.frame = 3 * self.HW
+        # ShallowUNet: c13 (1x1, 8 -> K) is fused into the mask softmax
+        # (paig_head_mask_fwd/bwd) in the encoder; the standalone U-Net call
+        # keeps it as a conv (its logits are the output)
+        last = self.ops[-1]
+        self.fuse_head = (not self.unet and last["name"] == "c13" and last["ks"] == 1 and last["src"][2] == 8
+                          and self.K in (2, 3) and self.HW % 4 == 0)
 
 
 class KernelProbe:
@@ -466,15 +472,21 @@ class Engine:
         }
         return res, (S if need_saved else None)
 
-    def _unet_forward(self, S, lay, x_view, st):
+    def _unet_forward(self, S, lay, x_view, st, fuse_head=False):
         """The U-Net plan over F frames addressed by x_view (frame view
-        pointer, stride, group, group stride): fills S["acts"] (LG = logits)."""
+        pointer, stride, group, group stride): fills S["acts"] (LG = logits).
+        fuse_head: stop before the last op (ShallowUNet's c13), which the
+        encoder runs fused into the mask softmax (no LG buffer)."""
         L = self.L
         F, H = lay.F, lay.H
         dev = S["dev"]
         cm = S["cm"]
         acts = {}
+        S["head_fused"] = fuse_head
+        ops = lay.ops[:-1] if fuse_head else lay.ops
         for name, (C, lvl) in lay.bufs.items():
+            if fuse_head and name == "LG":
+                continue
             if name != "X0" and name not in lay.fused_bufs:
                 acts[name] = _empty(F * C * (H // lvl) * (H // lvl), dev)
         S["acts"] = acts
@@ -505,7 +517,7 @@ class Engine:
         xmax = _empty(len(lay.ops) * XMAX_SLOTS, dev)
         S["xmax"] = lambda i: ptr(xmax) + i * XMAX_SLOTS * 4
         S["xmax_buf"] = xmax
-        for i, op in enumerate(lay.ops):
+        for i, op in enumerate(ops):
             if op["op"] == "up" and op["dst"][0] in lay.fused_bufs:
                 continue   # formed inside the consuming conv's staging
             dv, dlvl = view(op["dst"])
@@ -536,13 +548,17 @@ class Engine:
         F, H, HW, K = lay.F, lay.H, lay.HW, lay.K
         dev = S["dev"]
         S["x_view"] = x_view
-        self._unet_forward(S, lay, x_view, st)
+        self._unet_forward(S, lay, x_view, st, fuse_head=lay.fuse_head)
         acts = S["acts"]
         # ---- mask softmax + masked objects + localiser MLP + position head
         masks = _empty(F * (K + 1) * HW, dev)
         objs = _empty(K * F * 3 * HW, dev)
         pobjs = _empty(K * F * lay.l1_in, dev) if lay.unet else None
-        L.paig_mask_softmax_fwd(ptr(acts["LG"]), *x_view, ptr(masks), ptr(objs), ptr(pobjs), F, K, 3, H, H, st)
+        if lay.fuse_head:   # c13 + cat(ones) + softmax + mask x image, one launch
+            L.paig_head_mask_fwd(ptr(acts["A12"]), ptr(self.p(lay.prefix + "c13.weight")),
+                                 ptr(self.p(lay.prefix + "c13.bias")), *x_view, ptr(masks), ptr(objs), F, K, H, H, st)
+        else:
+            L.paig_mask_softmax_fwd(ptr(acts["LG"]), *x_view, ptr(masks), ptr(objs), ptr(pobjs), F, K, 3, H, H, st)
         l1_x = pobjs if lay.unet else objs
         h1 = _empty(K * F * 200, dev)
         h2 = _empty(K * F * 200, dev)
@@ -713,11 +729,27 @@ class Engine:
         # the AvgPool2d backward of the UNet path)
         acts = S["acts"]
         dacts = {}
-        dLG = _empty(F * K * HW, dev)
-        L.paig_mask_softmax_bwd(ptr(acts["LG"]), x_view[0], x_view[1], x_view[2], x_view[3], ptr(S["masks"]),
-                                ptr(dobjs), ptr(dLG), F, K, 3, H, H, (1 if lay.lg_relu else 0) | (2 if lay.unet else 0),
-                                st)
-        dacts["LG"] = dLG
+        if S.get("head_fused"):
+            # fused c13 + softmax backward: c12's dY (ReLU' applied) and c13's
+            # weight/bias partials (one slab row per block)
+            c = lay.ops[-1]["src"][2]
+            dX12 = _empty(F * c * HW, dev)
+            nb = L.paig_head_mask_blocks(F, H, H)
+            nw = K * c + K
+            hs = _empty(nb * nw, dev)
+            L.paig_head_mask_bwd(ptr(acts["A12"]), ptr(self.p(lay.prefix + "c13.weight")),
+                                 ptr(self.p(lay.prefix + "c13.bias")), *x_view, ptr(S["masks"]), ptr(dobjs), ptr(dX12),
+                                 ptr(hs), F, K, H, H, st)
+            g13 = self.g(lay.prefix + "c13.weight")
+            assert self.g(lay.prefix + "c13.bias").data_ptr() == g13.data_ptr() + K * c * 4, "c13 grads not contiguous"
+            S["extra_slabs"].append((hs, nb, nw, g13))
+            dacts["A12"] = dX12
+        else:
+            dLG = _empty(F * K * HW, dev)
+            L.paig_mask_softmax_bwd(ptr(acts["LG"]), x_view[0], x_view[1], x_view[2], x_view[3], ptr(S["masks"]),
+                                    ptr(dobjs), ptr(dLG), F, K, 3, H, H,
+                                    (1 if lay.lg_relu else 0) | (2 if lay.unet else 0), st)
+            dacts["LG"] = dLG
         self._unet_backward(S, dacts, st)
 
     def _unet_backward(self, S, dacts, st):
@@ -727,7 +759,10 @@ class Engine:
         acts = S["acts"]
         view = S["view"]
         F, H = lay.F, lay.H
-        written = {"LG": [(0, lay.K)]}
+        fused = S.get("head_fused", False)
+        # the fused head wrote c12's dY (dacts["A12"]); otherwise dLG is the start
+        written = {"A12": [(0, lay.ops[-1]["src"][2])]} if fused else {"LG": [(0, lay.K)]}
+        nops = len(lay.ops) - 1 if fused else len(lay.ops)
         cm = S["cm"]
 
         def dview(region):
@@ -753,7 +788,7 @@ class Engine:
             written.setdefault(region[0], []).append((region[1], region[2]))
 
         slabs = []
-        for i in range(len(lay.ops) - 1, -1, -1):
+        for i in range(nops - 1, -1, -1):
             op = lay.ops[i]
             fin = lay.fin[i]
             relu_fin = [r for r, relu in fin if relu]

@@ -224,7 +224,8 @@ GEMM_EX_TOL = {1: 2e-5, 2: 5e-5, 3: 3e-2, 4: 2e-5, 5: 2e-5, 6: 2e-5}
 @pytest.mark.parametrize("math", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(37, 50, 19), (130, 200, 3072), (200, 3072, 130), (6, 2, 200), (1, 513, 200),
-                                   (2000, 200, 3072), (200, 3072, 2000)])   # last: float4 split-K epilogue
+                                   (2000, 200, 3072), (200, 3072, 2000),    # float4 split-K epilogue
+                                   (2000, 3072, 200), (600, 136, 1000)])    # + the 64x256 / 256x64 wide tiles
 def test_gemm_ex(ta, tb, M, N, K, math):
     torch.manual_seed(M + N + K + math)
     A = (torch.randn(K, M) if ta else torch.randn(M, K)) / K ** 0.5
@@ -435,3 +436,46 @@ def test_gemm_math1_range_flag():
         torch.cuda.synchronize()
         assert rel_err(C, A.double().cpu() @ B2.double().cpu()) <= 2e-5
         assert _range_status() == 0
+
+
+@pytest.mark.parametrize("K,hw,F_", [(2, 32, 37), (3, 36, 5)])
+def test_head_mask_fused(K, hw, F_):
+    """paig_head_mask_fwd/bwd (ShallowUNet c13 1x1 + ReLU, cat(ones), softmax,
+    mask x image; blocks.py:84-93,276,307) against the same ops in fp32 torch:
+    masks, masked objects, c12's input gradient (c12's ReLU' applied) and
+    c13's weight / bias gradients (slab rows summed on the host)."""
+    torch.manual_seed(K * 100 + hw)
+    HW = hw * hw
+    x12 = torch.relu(torch.randn(F_, 8, hw, hw))
+    x12[:, :, :3] = 0.0   # dead pixels: ReLU' of c12 must zero them
+    img = torch.rand(F_, 3, hw, hw)
+    w = torch.randn(K, 8) * 0.5
+    b = torch.randn(K) * 0.2
+    dobjs = torch.randn(K, F_, 3, hw, hw)
+    # reference
+    xr = x12.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    lg = torch.relu(F.conv2d(xr, wr.view(K, 8, 1, 1), br))
+    masks_ref = torch.softmax(torch.cat([lg, torch.ones(F_, 1, hw, hw)], 1), 1)   # blocks.py:84-90
+    objs_ref = torch.stack([masks_ref[:, k:k + 1] * img for k in range(K)], 0)
+    (objs_ref * dobjs).sum().backward()
+    dx_ref = xr.grad * (x12 > 0)
+    # device
+    g = {n: t.to(DEV).contiguous() for n, t in dict(x12=x12, img=img, w=w, b=b, dobjs=dobjs).items()}
+    masks = torch.empty(F_, K + 1, hw, hw, device=DEV)
+    objs = torch.empty(K, F_, 3, hw, hw, device=DEV)
+    assert L().paig_head_mask_fwd(p(g["x12"]), p(g["w"]), p(g["b"]), p(g["img"]), 3 * HW, 0, 0, p(masks), p(objs), F_, K,
+                                  hw, hw, st()) == 0
+    nb = L().paig_head_mask_blocks(F_, hw, hw)
+    slab = torch.empty(nb, K * 8 + K, device=DEV)
+    dx = torch.empty(F_, 8, hw, hw, device=DEV)
+    assert L().paig_head_mask_bwd(p(g["x12"]), p(g["w"]), p(g["b"]), p(g["img"]), 3 * HW, 0, 0, p(masks), p(g["dobjs"]),
+                                  p(dx), p(slab), F_, K, hw, hw, st()) == 0
+    torch.cuda.synchronize()
+    part = slab.sum(0).cpu()
+    assert rel_err(masks, masks_ref.detach()) <= 1e-6
+    assert rel_err(objs, objs_ref.detach()) <= 1e-6
+    assert rel_err(dx, dx_ref) <= 1e-5
+    assert rel_err(part[:K * 8].view(K, 8), wr.grad) <= 1e-5
+    assert rel_err(part[K * 8:], br.grad) <= 1e-5

@@ -1,7 +1,7 @@
 """Per-launch timing of paig_gemm_ex at the train step's dense-layer shapes
 (HIP events around N back-to-back launches on one stream).
 
-usage: python tools/gemm_bench.py [maths=4,6,0,3] [reps=50] [rows=2000]
+usage: python tools/gemm_bench.py [maths=4,6,0,3] [reps=50] [rows=2000] [shape names, e.g. l1_fwd,l1_wgrad]
 Prints one line per (shape, math): microseconds per launch (split-K
 epilogue included) and the rate of the compulsory operand/result bytes.
 """
@@ -24,10 +24,13 @@ def main():
     maths = [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "4,6,0,3").split(",")]
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     rows = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
+    only = set(sys.argv[4].split(",")) if len(sys.argv) > 4 else None
     L = lib()
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     for name, ta, tb, M, N, K in shapes(rows):
+        if only and name not in only:
+            continue
         A = torch.randn(K, M, device=dev) if ta else torch.randn(M, K, device=dev)
         B = torch.randn(N, K, device=dev) if tb else torch.randn(K, N, device=dev)
         C = torch.empty(M, N, device=dev)
