@@ -68,6 +68,22 @@ int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_g
 int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, void* stream);
+/* paig_conv2d_fwd_ex with the kernel's weight images prepared beforehand by
+ * paig_conv_wprep (nullable: then staged from w in the kernel, same values).
+ * Used on the split path (flags & 128) only; w and bias are still read. */
+int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                       const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, const void* wprep,
+                       void* stream);
+/* Weight images of the split forward / dgrad kernels, once per step for n
+ * convs in one launch: job i reads the layer weight w[i] and writes the
+ * images for a kernel with cin[i] input / cout[i] output channels (dgrad,
+ * dg[i] = 1: cin = the layer's Cout, cout = the layer's Cin) to out[i]
+ * (16-byte aligned, paig_conv_wprep_size(cin, cout, ks) 16-bit elements).
+ * Fixed 2^8 weight scale, f16 hi/lo, |w| < 256 range-guarded (as in-kernel). */
+long long paig_conv_wprep_size(int cin, int cout, int ks);
+int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
+                    void* const* out, void* stream);
 /* 1 if the shape runs on the MFMA path for fwd/dgrad (what 0) or wgrad (what 1)
  * with these flags; flag 32 (fused upsample input) is available only there */
 int paig_conv2d_mfma_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags);

@@ -32,6 +32,9 @@ SIGNATURES = {
     "paig_conv2d_fwd": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P]),
     "paig_conv2d_wgrad": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P]),
     "paig_conv2d_fwd_ex": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P]),
+    "paig_conv2d_fwd_pw": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P, P]),
+    "paig_conv_wprep_size": (LL, [I, I, I]),
+    "paig_conv_wprep": (I, [I, P, P, P, P, P, P, P]),
     "paig_conv2d_wgrad_ex": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
     "paig_gather_u8_f32": (I, [P, P, P, I, LL, P]),
@@ -94,7 +97,7 @@ SIGNATURES = {
 }
 
 _QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported", "paig_velmlp_bwd_blocks",
-          "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_mask_blocks", "paig_gemm_workspace", "paig_colsum_workspace",
+          "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_mask_blocks", "paig_conv_wprep_size", "paig_gemm_workspace", "paig_colsum_workspace",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
           "paig_decoder_bwd_scratch"}
 

@@ -357,16 +357,29 @@ int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long i
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, void* stream);
 
+int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                       const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, const void* wprep,
+                       void* stream);
+
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                     const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                     int Cout, int H, int W, int ks, int flags, void* stream) {
-  return paig_conv2d_fwd_ex(in, in_fs, in_grp, in_gs, out, out_fs, aux, aux_fs, w, bias, F, Cin, Cout, H, W, ks, flags,
-                            nullptr, 0, stream);
+  return paig_conv2d_fwd_pw(in, in_fs, in_grp, in_gs, out, out_fs, aux, aux_fs, w, bias, F, Cin, Cout, H, W, ks, flags,
+                            nullptr, 0, nullptr, stream);
 }
 
 int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, void* stream) {
+  return paig_conv2d_fwd_pw(in, in_fs, in_grp, in_gs, out, out_fs, aux, aux_fs, w, bias, F, Cin, Cout, H, W, ks, flags,
+                            xmax, xmax_n, nullptr, stream);
+}
+
+int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                       const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, const void* wprep,
+                       void* stream) {
   hipStream_t st = (hipStream_t)stream;
   FView vin{in, in_fs, in_gs, in_grp};
   FViewW vout{out, out_fs};
@@ -376,7 +389,7 @@ int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long i
   if (F <= 0) return 0;
   int rc = 0;
   if (!(flags & 16) &&
-      paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc, XMax{xmax, xmax_n}))
+      paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc, XMax{xmax, xmax_n}, wprep))
     return rc;
   if (flags & 32) {
     paig_set_error("paig_conv2d_fwd: fused-upsample input has no instantiation for Cin=%d Cout=%d H=%d", Cin, Cout, H);

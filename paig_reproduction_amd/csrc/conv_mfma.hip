@@ -684,8 +684,8 @@ static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_
 // Returns 1 if handled (rc in *rc), 0 if the shape has no MFMA instantiation.
 // flags: 1 relu, 2 mask(aux>0), 4 accumulate, 8 dgrad, 32 input = 2x upsample of (H/2 x W/2)
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm) {
-  if ((flags & (128 | 256)) && paig_conv_split_fwd(in, out, aux, w, b, F, Cin, Cout, H, W, ks, flags, st, rc, xm))
+                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp) {
+  if ((flags & (128 | 256)) && paig_conv_split_fwd(in, out, aux, w, b, F, Cin, Cout, H, W, ks, flags, st, rc, xm, wp))
     return 1;
   const bool dg = (flags & 8) != 0;
   const bool up = (flags & 32) != 0;

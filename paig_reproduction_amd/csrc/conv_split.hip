@@ -294,7 +294,7 @@ struct SFwdCfg {
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 __global__ void __launch_bounds__(256, 2)
 conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
-                 int flags, int ntiles, XMax xm) {
+                 int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
   constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP;
@@ -525,17 +525,29 @@ if constexpr (W % 4 == 0) {
     ew = PAIG_W_EXP;
     wsc = __builtin_amdgcn_ldexpf(1.f, ew);
   }
-  for (int idx = tid; idx < NS * NT * 64; idx += 256) {
-    s16x8 vh, vl;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      short h, l;
-      split<PM>(wval(idx, j) * wsc, h, l, rmax);
-      vh[j] = h;
-      vl[j] = l;
+  if (PM == 0 && wp != nullptr) {
+    // pre-split images of the whole COUT (paig_conv_wprep, once per step):
+    // this slice's NT tiles of every k-step, coalesced 16-byte copies
+    constexpr int NTT = NT * C::NB, WLO = NS * NTT * 64;
+    for (int idx = tid; idx < NS * NT * 64; idx += 256) {
+      const int s = idx / (NT * 64), r = idx - s * (NT * 64);
+      const int src = (s * NTT + blockIdx.y * NT) * 64 + r;
+      *reinterpret_cast<s16x8*>(Wh + idx * 8) = wp[src];
+      *reinterpret_cast<s16x8*>(Wl + idx * 8) = wp[WLO + src];
     }
-    *reinterpret_cast<s16x8*>(Wh + idx * 8) = vh;
-    if (PM != 2) *reinterpret_cast<s16x8*>(Wl + idx * 8) = vl;
+  } else {
+    for (int idx = tid; idx < NS * NT * 64; idx += 256) {
+      s16x8 vh, vl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        short h, l;
+        split<PM>(wval(idx, j) * wsc, h, l, rmax);
+        vh[j] = h;
+        vl[j] = l;
+      }
+      *reinterpret_cast<s16x8*>(Wh + idx * 8) = vh;
+      if (PM != 2) *reinterpret_cast<s16x8*>(Wl + idx * 8) = vl;
+    }
   }
   // the bias of this lane's output channels (block constant)
   float bvs[NT];
@@ -1211,7 +1223,7 @@ if constexpr (W % 4 == 0) {
 
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
-                       hipStream_t st, XMax xm) {
+                       hipStream_t st, XMax xm, const void* wp) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int LDS = C::LDS + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
@@ -1226,7 +1238,8 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
   if (nb < 1) nb = 1;
   if (PM != 0 || DG) xm.p = nullptr;
   PAIG_REQUIRE(!xm.p || nb <= xm.n, "conv split fwd: %d blocks need more than %d xmax slots", nb, xm.n);
-  hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles, xm);
+  hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles, xm,
+                     PM == 0 ? static_cast<const s16x8*>(wp) : nullptr);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -1296,7 +1309,7 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
 // flags & 128: split precision (f16 x3 forward and scaled dgrad), flags & 256:
 // bf16 hi only.  Returns 1 if the shape is instantiated here (rc in *rc).
 int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm) {
+                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp) {
   const bool dg = (flags & 8) != 0, up = (flags & 32) != 0, b16 = (flags & 256) != 0;
   const int fl = flags & 7;
   if (H != W || !(flags & (128 | 256))) return 0;
@@ -1305,8 +1318,8 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
     if (dg) return 0;
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
     if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
-      *rc = b16 ? sfwd_launch<CI, CO, HH, HH, K, false, true, 2>(in, out, aux, w, b, F, fl, st, xm)           \
-                : sfwd_launch<CI, CO, HH, HH, K, false, true, 0>(in, out, aux, w, b, F, fl, st, xm);          \
+      *rc = b16 ? sfwd_launch<CI, CO, HH, HH, K, false, true, 2>(in, out, aux, w, b, F, fl, st, xm, wp)           \
+                : sfwd_launch<CI, CO, HH, HH, K, false, true, 0>(in, out, aux, w, b, F, fl, st, xm, wp);          \
       return 1;                                                                                           \
     }
     PAIG_SPLIT_UP(PAIG_CASE)
@@ -1316,11 +1329,11 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
 #define PAIG_CASE(CI, CO, HH, K)                                                                            \
   if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                      \
     if (b16)                                                                                                \
-      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 2>(in, out, aux, w, b, F, fl, st, xm)              \
-               : sfwd_launch<CI, CO, HH, HH, K, false, false, 2>(in, out, aux, w, b, F, fl, st, xm);            \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 2>(in, out, aux, w, b, F, fl, st, xm, wp)              \
+               : sfwd_launch<CI, CO, HH, HH, K, false, false, 2>(in, out, aux, w, b, F, fl, st, xm, wp);            \
     else                                                                                                    \
-      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 0>(in, out, aux, w, b, F, fl, st, xm)              \
-               : sfwd_launch<CI, CO, HH, HH, K, false, false, 0>(in, out, aux, w, b, F, fl, st, xm);            \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 0>(in, out, aux, w, b, F, fl, st, xm, wp)              \
+               : sfwd_launch<CI, CO, HH, HH, K, false, false, 0>(in, out, aux, w, b, F, fl, st, xm, wp);            \
     return 1;                                                                                               \
   }
   PAIG_SPLIT_FWD(PAIG_CASE)
@@ -1374,5 +1387,86 @@ int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks,
 #undef PAIG_CASE
   return 0;
 }
+
+// ----------------------------------------------------------- weight prep
+// The forward / dgrad kernels' weight images, built once per step for every
+// conv (the same values and split as the in-kernel staging: scaled by the
+// fixed 2^PAIG_W_EXP, f16 hi / lo, range-guarded), in fragment order over
+// the whole COUT: entry (s, nt, lane) = 8 channels of k-chunk 4s + lane/16
+// for output channel 16 nt + lane%16; the lo image follows the hi one.  A
+// block then stages its slice with coalesced 16-byte copies instead of one
+// scattered 4-byte weight load (and split) per value, which measured
+// 0.4-8 us per launch (the most on the small-frame, wide-channel layers).
+struct WPrepJob {
+  const float* w;
+  s16x8* out;
+  int cin, cout, ks, dg, entries;
+};
+constexpr int WPREP_MAX = 64;
+struct WPrepJobs {
+  WPrepJob j[WPREP_MAX];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) conv_wprep_k(WPrepJobs jobs) {
+  float rmax = 0.f;
+  for (int q = 0; q < jobs.n; ++q) {
+    const WPrepJob jb = jobs.j[q];
+    const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16;
+    const float wsc = __builtin_amdgcn_ldexpf(1.f, PAIG_W_EXP);
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < jb.entries; e += gridDim.x * 256) {
+      const int s = e / (NTT * 64), rem = e - s * NTT * 64, ln = rem & 63, ntg = rem >> 6;
+      const int kc = 4 * s + (ln >> 4), co = ntg * 16 + (ln & 15);
+      s16x8 vh, vl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = 0.f;
+        if (kc < KC && co < jb.cout) {
+          const int tap = kc / CC, ci = (kc % CC) * 8 + j;
+          if (ci < jb.cin)
+            v = jb.dg ? jb.w[(ci * jb.cout + co) * KK + (KK - 1 - tap)] : jb.w[(co * jb.cin + ci) * KK + tap];
+        }
+        short h, l;
+        split<0>(v * wsc, h, l, rmax);
+        vh[j] = h;
+        vl[j] = l;
+      }
+      jb.out[e] = vh;
+      jb.out[jb.entries + e] = vl;
+    }
+  }
+  f16_range_note(rmax);
+}
+
+extern "C" {
+
+// 16-bit elements of one prepped weight image pair (hi + lo) for a
+// forward / dgrad kernel with cin input and cout output channels
+long long paig_conv_wprep_size(int cin, int cout, int ks) {
+  const int KC = ks * ks * ((cin + 7) / 8), NS = (KC + 3) / 4, NTT = (cout + 15) / 16;
+  return 2ll * NS * NTT * 64 * 8;
+}
+
+int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
+                    void* const* out, void* stream) {
+  for (int b = 0; b < n; b += WPREP_MAX) {
+    WPrepJobs jobs{};
+    jobs.n = n - b < WPREP_MAX ? n - b : WPREP_MAX;
+    int most = 0;
+    for (int q = 0; q < jobs.n; ++q) {
+      const int i = b + q;
+      PAIG_REQUIRE(w[i] && out[i] && cin[i] > 0 && cout[i] > 0 && ks[i] > 0, "conv_wprep: job %d", i);
+      PAIG_REQUIRE(((uintptr_t)out[i] & 15) == 0, "conv_wprep: job %d output not 16-byte aligned", i);
+      const int e = (int)(paig_conv_wprep_size(cin[i], cout[i], ks[i]) / 16);
+      jobs.j[q] = WPrepJob{w[i], static_cast<s16x8*>(out[i]), cin[i], cout[i], ks[i], dg[i], e};
+      if (e > most) most = e;
+    }
+    hipLaunchKernelGGL(conv_wprep_k, dim3(cdiv(most, 256)), dim3(256), 0, (hipStream_t)stream, jobs);
+    PAIG_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // extern "C"
 
 PAIG_F16_RANGE_ACCESSOR(paig_f16_range_conv)

@@ -517,6 +517,33 @@ class Engine:
         xmax = _empty(len(lay.ops) * XMAX_SLOTS, dev)
         S["xmax"] = lambda i: ptr(xmax) + i * XMAX_SLOTS * 4
         S["xmax_buf"] = xmax
+        # split path: every conv's forward and dgrad weight images, pre-split
+        # in one launch per step (paig_conv_wprep) and copied by the kernels
+        wp = {}
+        if cm == self.CONV_MATH["split"]:
+            jobs = []
+            for i, op in enumerate(ops):
+                if op["op"] != "conv":
+                    continue
+                W_ = self.p(lay.prefix + op["name"] + ".weight")
+                cin, cout, ks = op["src"][2], op["dst"][2], op["ks"]
+                jobs.append((i, 0, W_, cin, cout, ks))
+                if op["src"][0] != "X0":   # the dgrad kernel's images (Q10: none for the input)
+                    jobs.append((i, 1, W_, cout, cin, ks))
+            sizes = [int(L.paig_conv_wprep_size(j[3], j[4], j[5])) for j in jobs]
+            buf = torch.empty(sum(sizes), dtype=torch.int16, device=dev)
+            outs, off = [], 0
+            for j, n in zip(jobs, sizes):
+                wp[(j[0], j[1])] = buf.data_ptr() + 2 * off
+                outs.append(wp[(j[0], j[1])])
+                off += n
+            n = len(jobs)
+            L.paig_conv_wprep(n, (ctypes.c_void_p * n)(*[ptr(j[2]) for j in jobs]),
+                              (ctypes.c_int * n)(*[j[3] for j in jobs]), (ctypes.c_int * n)(*[j[4] for j in jobs]),
+                              (ctypes.c_int * n)(*[j[5] for j in jobs]), (ctypes.c_int * n)(*[j[1] for j in jobs]),
+                              (ctypes.c_void_p * n)(*outs), st)
+            S["wprep_buf"] = buf
+        S["wprep"] = wp
         for i, op in enumerate(ops):
             if op["op"] == "up" and op["dst"][0] in lay.fused_bufs:
                 continue   # formed inside the consuming conv's staging
@@ -529,9 +556,10 @@ class Engine:
                 fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
                 nbytes = 4 * F * (op["src"][2] * (Hl // (2 if xfl else 1)) ** 2 + op["dst"][2] * Hl * Hl)
                 with self._p("conv_fwd:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_fwd_ex(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
+                    L.paig_conv2d_fwd_pw(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
                                          op["src"][2], op["dst"][2], Hl, Hl, op["ks"],
-                                         (1 if op["relu"] else 0) | xfl | cm, S["xmax"](i), XMAX_SLOTS, st)
+                                         (1 if op["relu"] else 0) | xfl | cm, S["xmax"](i), XMAX_SLOTS,
+                                         wp.get((i, 0)), st)
             elif op["op"] == "pool":
                 sv, slvl = view(op["src"])
                 Hl = H // slvl
@@ -827,8 +855,8 @@ class Engine:
                 W_ = self.p(lay.prefix + op["name"] + ".weight")
                 nbytes = 4 * F * Hl * Hl * (cout + cin * (1 + (1 if flags & 2 else 0) + (1 if flags & 4 else 0)))
                 with self._p("conv_dgrad:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_fwd(dyv[0], dyv[1], 0, 0, dxv[0], dxv[1], aux[0] or None, aux[1], ptr(W_), None, F,
-                                      cout, cin, Hl, Hl, ks, flags | cm, st)
+                    L.paig_conv2d_fwd_pw(dyv[0], dyv[1], 0, 0, dxv[0], dxv[1], aux[0] or None, aux[1], ptr(W_), None,
+                                         F, cout, cin, Hl, Hl, ks, flags | cm, None, 0, S["wprep"].get((i, 1)), st)
                 mark(src)
             elif op["op"] == "pool":
                 sv, slvl = view(src)

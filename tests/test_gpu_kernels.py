@@ -479,3 +479,43 @@ def test_head_mask_fused(K, hw, F_):
     assert rel_err(dx, dx_ref) <= 1e-5
     assert rel_err(part[:K * 8].view(K, 8), wr.grad) <= 1e-5
     assert rel_err(part[K * 8:], br.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,hw,ks,up", [(8, 8, 32, 3, 0), (32, 32, 8, 3, 0), (24, 8, 32, 3, 0), (8, 24, 32, 3, 0),
+                                               (64, 128, 16, 3, 0), (32, 16, 16, 3, 1), (8, 2, 32, 1, 0)])
+def test_conv_wprep_bit_identical(cin, cout, hw, ks, up):
+    """Split forward / dgrad with weight images from paig_conv_wprep (one
+    launch per step) give bit-identical results to the in-kernel staging,
+    including a multi-slice COUT (64 -> 128 at 16x16, grid.y > 1)."""
+    torch.manual_seed(cin + cout + hw)
+    hin = hw // 2 if up else hw
+    x = torch.randn(3, cin, hin, hin, device=DEV)
+    w = torch.randn(cout, cin, ks, ks, device=DEV) * 0.2
+    b = torch.randn(cout, device=DEV)
+    dy = torch.randn(3, cout, hw, hw, device=DEV)
+    fl = 128 | (32 if up else 0)
+    jobs = [(cin, cout, 0)] + ([] if up else [(cout, cin, 1)])
+    sizes = [int(L().paig_conv_wprep_size(a, c, ks)) for a, c, _ in jobs]
+    bufs = [torch.empty(n, dtype=torch.int16, device=DEV) for n in sizes]
+    n = len(jobs)
+    L().paig_conv_wprep(n, (ctypes.c_void_p * n)(*[p(w)] * n), (ctypes.c_int * n)(*[j[0] for j in jobs]),
+                        (ctypes.c_int * n)(*[j[1] for j in jobs]), (ctypes.c_int * n)(*[ks] * n),
+                        (ctypes.c_int * n)(*[j[2] for j in jobs]), (ctypes.c_void_p * n)(*[p(t) for t in bufs]), st())
+    outs = []
+    for wpp in (None, p(bufs[0])):
+        o = torch.empty(3, cout, hw, hw, device=DEV)
+        L().paig_conv2d_fwd_pw(p(x), cin * hin * hin, 0, 0, p(o), cout * hw * hw, None, 0, p(w), p(b), 3, cin, cout,
+                               hw, hw, ks, 1 | fl, None, 0, wpp, st())
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    if not up:
+        aux = torch.relu(torch.randn(3, cin, hw, hw, device=DEV))
+        dxs = []
+        for wpp in (None, p(bufs[1])):
+            dx = torch.full((3, cin, hw, hw), 0.5, device=DEV)
+            L().paig_conv2d_fwd_pw(p(dy), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, p(aux), cin * hw * hw, p(w), None,
+                                   3, cout, cin, hw, hw, ks, 8 | 4 | 2 | 128, None, 0, wpp, st())
+            dxs.append(dx)
+        torch.cuda.synchronize()
+        assert torch.equal(dxs[0], dxs[1])
