@@ -1405,16 +1405,22 @@ struct WPrepJob {
 constexpr int WPREP_MAX = 64;
 struct WPrepJobs {
   WPrepJob j[WPREP_MAX];
+  int blk0[WPREP_MAX + 1];   // first block of each job (WPREP_T entries per block)
   int n;
 };
+constexpr int WPREP_T = 128;
 
-__global__ void __launch_bounds__(256) conv_wprep_k(WPrepJobs jobs) {
+// one entry (8 values) per thread; the blocks of every job in one grid
+__global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
   float rmax = 0.f;
-  for (int q = 0; q < jobs.n; ++q) {
+  int q = 0;
+  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.blk0[q + 1]) ++q;
+  {
     const WPrepJob jb = jobs.j[q];
     const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16;
     const float wsc = __builtin_amdgcn_ldexpf(1.f, PAIG_W_EXP);
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < jb.entries; e += gridDim.x * 256) {
+    const int e = ((int)blockIdx.x - jobs.blk0[q]) * WPREP_T + threadIdx.x;
+    if (e < jb.entries) {
       const int s = e / (NTT * 64), rem = e - s * NTT * 64, ln = rem & 63, ntg = rem >> 6;
       const int kc = 4 * s + (ln >> 4), co = ntg * 16 + (ln & 15);
       s16x8 vh, vl;
@@ -1452,16 +1458,18 @@ int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cou
   for (int b = 0; b < n; b += WPREP_MAX) {
     WPrepJobs jobs{};
     jobs.n = n - b < WPREP_MAX ? n - b : WPREP_MAX;
-    int most = 0;
+    int blocks = 0;
     for (int q = 0; q < jobs.n; ++q) {
       const int i = b + q;
       PAIG_REQUIRE(w[i] && out[i] && cin[i] > 0 && cout[i] > 0 && ks[i] > 0, "conv_wprep: job %d", i);
       PAIG_REQUIRE(((uintptr_t)out[i] & 15) == 0, "conv_wprep: job %d output not 16-byte aligned", i);
       const int e = (int)(paig_conv_wprep_size(cin[i], cout[i], ks[i]) / 16);
       jobs.j[q] = WPrepJob{w[i], static_cast<s16x8*>(out[i]), cin[i], cout[i], ks[i], dg[i], e};
-      if (e > most) most = e;
+      jobs.blk0[q] = blocks;
+      blocks += cdiv(e, WPREP_T);
     }
-    hipLaunchKernelGGL(conv_wprep_k, dim3(cdiv(most, 256)), dim3(256), 0, (hipStream_t)stream, jobs);
+    jobs.blk0[jobs.n] = blocks;
+    hipLaunchKernelGGL(conv_wprep_k, dim3(blocks), dim3(WPREP_T), 0, (hipStream_t)stream, jobs);
     PAIG_CHECK_LAUNCH();
   }
   return 0;

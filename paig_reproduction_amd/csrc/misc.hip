@@ -111,16 +111,30 @@ __global__ void __launch_bounds__(256) vfn_bwd1_k(VfnBwdTasks T) {
   int p1 = p0 + VROWS;
   if (p1 > P) p1 = P;
   const float hj = j < VH ? T.h[k][j] : 0.f;
+  // every load of the block's rows is issued before the first store (the
+  // stores through T's pointers could alias them: loads interleaved with
+  // stores ran one memory latency per row)
+  float gr[VROWS], yv[VROWS], w2[VROWS];
+#pragma unroll
+  for (int r = 0; r < VROWS; ++r) {
+    const int p = p0 + r < p1 ? p0 + r : p0;
+    gr[r] = d[p];
+    yv[r] = sig ? T.y[k][p] : 0.f;
+    w2[r] = j < VH ? W2[(long long)p * VH + j] : 0.f;
+  }
   float acc = 0.f;
-  for (int p = p0; p < p1; ++p) {
-    float g = d[p];
+#pragma unroll
+  for (int r = 0; r < VROWS; ++r) {
+    const int p = p0 + r;
+    if (p >= p1) break;
+    float g = gr[r];
     if (sig) {
-      const float s = 1.f / (1.f + expf(-T.y[k][p]));
+      const float s = 1.f / (1.f + expf(-yv[r]));
       g = g * (s * (1.f - s));
     }
     if (j < VH) {
       dW2[(long long)p * VH + j] = g * hj;
-      acc = fmaf(W2[(long long)p * VH + j], g, acc);
+      acc = fmaf(w2[r], g, acc);
     }
     if (j == 0) T.db2[k][p] = g;
   }

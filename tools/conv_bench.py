@@ -43,7 +43,9 @@ def main():
         y = torch.empty(F, cout, H, H, device=dev)
         dx = torch.empty(F, cin, H, H, device=dev)
         aux = torch.rand(F, cin, H, H, device=dev)
-        slab = torch.empty(768 * (cout * cin * ks * ks + cout), device=dev)
+        NMAX = int(os.environ.get("PAIG_WG_NMAX", "768"))   # wgrad slab rows (blocks) allowed
+        slab = torch.empty(NMAX * (cout * cin * ks * ks + cout), device=dev)
+        gsum = torch.empty(cout * cin * ks * ks + cout, device=dev)
         xmax = torch.zeros(XS, device=dev)   # the forward's per-block max |x| slots (ex entry points)
         ex = hasattr(L, "paig_conv2d_fwd_ex")
         nb = ctypes.c_int(0)
@@ -58,13 +60,17 @@ def main():
                                                   None, 0, w.data_ptr(), b.data_ptr(), F, cin, cout, H, H, ks,
                                                   1 | (32 if up else 0) | m, st)),
                 "wgrad": (lambda: L.paig_conv2d_wgrad_ex(x.data_ptr(), cin * Hin * Hin, 0, 0, dy.data_ptr(),
-                                                         cout * H * H, slab.data_ptr(), 768, ctypes.byref(nb), F, cin,
+                                                         cout * H * H, slab.data_ptr(), NMAX, ctypes.byref(nb), F, cin,
                                                          cout, H, H, ks, (32 if up else 0) | m, xmax.data_ptr(), XS,
                                                          st)) if ex else
                          (lambda: L.paig_conv2d_wgrad(x.data_ptr(), cin * Hin * Hin, 0, 0, dy.data_ptr(), cout * H * H,
-                                                      slab.data_ptr(), 768, ctypes.byref(nb), F, cin, cout, H, H, ks,
+                                                      slab.data_ptr(), NMAX, ctypes.byref(nb), F, cin, cout, H, H, ks,
                                                       (32 if up else 0) | m, st)),
             }
+            # the wgrad with the reduction of its slab rows (the engine batches
+            # these into one launch per step; timed here per layer)
+            runs["wgred"] = lambda: (runs["wgrad"]() or L.paig_slab_reduce(slab.data_ptr(), nb.value, gsum.numel(),
+                                                                            gsum.numel(), gsum.data_ptr(), 0, st))
             if name != "c1":
                 runs["dgrad"] = lambda: L.paig_conv2d_fwd(dy.data_ptr(), cout * H * H, 0, 0, dx.data_ptr(),
                                                           cin * H * H, aux.data_ptr(), cin * H * H, w.data_ptr(), None,
@@ -85,7 +91,7 @@ def main():
                 xin = F * cin * Hin * Hin * 4
                 byts = {"fwd": xin + F * cout * H * H * 4,
                         "dgrad": F * cout * H * H * 4 + 2 * F * cin * H * H * 4,
-                        "wgrad": xin + F * cout * H * H * 4}[pas]
+                        "wgrad": xin + F * cout * H * H * 4, "wgred": xin + F * cout * H * H * 4}[pas]
                 print(f"{name:4s} {pas:5s} {mode:5s} {us:8.1f} us  {byts / us / 1e3:7.0f} GB/s  "
                       f"{fl / us / 1e6:6.1f} TF", flush=True)
 
