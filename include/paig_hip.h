@@ -69,12 +69,16 @@ int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long i
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, void* stream);
 /* paig_conv2d_fwd_ex with the kernel's weight images prepared beforehand by
- * paig_conv_wprep (nullable: then staged from w in the kernel, same values).
- * Used on the split path (flags & 128) only; w and bias are still read. */
+ * paig_conv_wprep (nullable: then staged from w in the kernel, same values;
+ * used on the split path, flags & 128, only; w and bias are still read), and
+ * flags & 64: the output's 2x2 max pool (nn.MaxPool2d((2,2)), blocks.py:250,
+ * 254) also written to pool_out [F][Cout][H/2][W/2] (frame stride pool_fs),
+ * bit-identical to paig_maxpool2_fwd; forward split shapes for which
+ * paig_conv2d_mfma_supported(0, .., flags | 64) says 1. */
 int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
-                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, const void* wprep,
-                       void* stream);
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, float* pool_out,
+                       long long pool_fs, const void* wprep, void* stream);
 /* Weight images of the split forward / dgrad kernels, once per step for n
  * convs in one launch: job i reads the layer weight w[i] and writes the
  * images for a kernel with cin[i] input / cout[i] output channels (dgrad,

@@ -32,7 +32,7 @@ SIGNATURES = {
     "paig_conv2d_fwd": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P]),
     "paig_conv2d_wgrad": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P]),
     "paig_conv2d_fwd_ex": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P]),
-    "paig_conv2d_fwd_pw": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P, P]),
+    "paig_conv2d_fwd_pw": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P, LL, P, P]),
     "paig_conv_wprep_size": (LL, [I, I, I]),
     "paig_conv_wprep": (I, [I, P, P, P, P, P, P, P]),
     "paig_conv2d_wgrad_ex": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),

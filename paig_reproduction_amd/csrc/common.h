@@ -181,13 +181,13 @@ struct XMax {
   int n;
 };
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr);
+                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr, FViewW pout = FViewW{nullptr, 0});
 int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H,
                          int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
 // Split-precision 16-bit MFMA convolutions (conv_split.hip), selected by
 // flags & 128 (f16x3 forward / bf16x3 dgrad and wgrad) or flags & 256 (bf16).
 int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr);
+                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr, FViewW pout = FViewW{nullptr, 0});
 int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout,
                           int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
 int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags);

@@ -359,27 +359,27 @@ int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long i
 
 int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
-                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, const void* wprep,
-                       void* stream);
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, float* pool_out,
+                       long long pool_fs, const void* wprep, void* stream);
 
 int paig_conv2d_fwd(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                     const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                     int Cout, int H, int W, int ks, int flags, void* stream) {
   return paig_conv2d_fwd_pw(in, in_fs, in_grp, in_gs, out, out_fs, aux, aux_fs, w, bias, F, Cin, Cout, H, W, ks, flags,
-                            nullptr, 0, nullptr, stream);
+                            nullptr, 0, nullptr, 0, nullptr, stream);
 }
 
 int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, void* stream) {
   return paig_conv2d_fwd_pw(in, in_fs, in_grp, in_gs, out, out_fs, aux, aux_fs, w, bias, F, Cin, Cout, H, W, ks, flags,
-                            xmax, xmax_n, nullptr, stream);
+                            xmax, xmax_n, nullptr, 0, nullptr, stream);
 }
 
 int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
-                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, const void* wprep,
-                       void* stream) {
+                       int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, float* pool_out,
+                       long long pool_fs, const void* wprep, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   FView vin{in, in_fs, in_gs, in_grp};
   FViewW vout{out, out_fs};
@@ -388,8 +388,13 @@ int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long i
   const int fl = flags & 7;
   if (F <= 0) return 0;
   int rc = 0;
+  if ((flags & 64) && (flags & 16)) {
+    paig_set_error("paig_conv2d_fwd: the fused pool (flags & 64) needs the split path");
+    return PAIG_E_UNSUPPORTED;
+  }
   if (!(flags & 16) &&
-      paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc, XMax{xmax, xmax_n}, wprep))
+      paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc, XMax{xmax, xmax_n}, wprep,
+                         FViewW{pool_out, pool_fs}))
     return rc;
   if (flags & 32) {
     paig_set_error("paig_conv2d_fwd: fused-upsample input has no instantiation for Cin=%d Cout=%d H=%d", Cin, Cout, H);

@@ -684,9 +684,16 @@ static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_
 // Returns 1 if handled (rc in *rc), 0 if the shape has no MFMA instantiation.
 // flags: 1 relu, 2 mask(aux>0), 4 accumulate, 8 dgrad, 32 input = 2x upsample of (H/2 x W/2)
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp) {
-  if ((flags & (128 | 256)) && paig_conv_split_fwd(in, out, aux, w, b, F, Cin, Cout, H, W, ks, flags, st, rc, xm, wp))
+                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp,
+                       FViewW pout) {
+  if ((flags & (128 | 256)) &&
+      paig_conv_split_fwd(in, out, aux, w, b, F, Cin, Cout, H, W, ks, flags, st, rc, xm, wp, pout))
     return 1;
+  if (flags & 64) {
+    paig_set_error("paig_conv2d_fwd: the fused pool (flags & 64) needs a split-path shape");
+    *rc = PAIG_E_UNSUPPORTED;
+    return 1;
+  }
   const bool dg = (flags & 8) != 0;
   const bool up = (flags & 32) != 0;
   const int fl = flags & 7;
@@ -755,6 +762,7 @@ int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk
 // the host uses this to decide which upsamples it may fuse.
 extern "C" int paig_conv2d_mfma_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags) {
   if ((flags & (128 | 256)) && paig_conv_split_supported(what, Cin, Cout, H, W, ks, flags)) return 1;
+  if (flags & 64) return 0;   // the fused pool exists on the split path only
   if (H != W) return 0;
   const bool up = (flags & 32) != 0, dg = (flags & 8) != 0;
 #define PAIG_CASE(CI, CO, HH, K) \

@@ -289,12 +289,29 @@ struct SFwdCfg {
   static constexpr int NL = (NI + 255) / 256;
   static constexpr bool VEC4 = W % 4 == 0;                   // 4-pixel epilogue stores stay in one row
   static_assert(H % RT == 0, "RT divides H");
+  // fused 2x2 max pool of the output (flags & 64): a lane's 4 pixels of row y
+  // (M-tile mt) and of row y + 1 (M-tile mt + PO) are in the same lane when
+  // rows are whole 16-pixel M-tiles and a wave holds whole row pairs
+  static constexpr int PO = W / 16;
+  static constexpr bool POOLOK = !UPS && VEC4 && W % 16 == 0 && PO >= 1 && MW % (2 * PO) == 0 &&
+                                 (MW * 16) % (2 * W) == 0 && TPXV % (2 * W) == 0 && RT % 2 == 0;
 };
 
-template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
+// aten max_pool2d's window scan (rows, then columns; a later value replaces
+// the running max only if greater, or NaN), so the pooled values are
+// bit-identical to maxpool_fwd_v_k's
+__device__ __forceinline__ float pool4(float a, float b, float c, float d) {
+  float m = a;
+  if (b > m || b != b) m = b;
+  if (c > m || c != c) m = c;
+  if (d > m || d != d) m = d;
+  return m;
+}
+
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false>
 __global__ void __launch_bounds__(256, 2)
 conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
-                 int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp) {
+                 int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp, FViewW pout) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
   constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP;
@@ -594,6 +611,7 @@ if constexpr (W % 4 == 0) {
       const int co = co0 + nt * 16 + (lane & 15);
       if (co >= COUT) continue;
       const float bv = bvs[nt];
+      f32x4 vv[MW];   // the stored values (fused pool)
 #pragma unroll
       for (int mt = 0; mt < MW; ++mt) {
         const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
@@ -619,6 +637,7 @@ if constexpr (W % 4 == 0) {
             for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
           }
           *reinterpret_cast<f32x4*>(op) = v;
+          if constexpr (POOL) vv[mt] = v;
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -633,6 +652,23 @@ if constexpr (W % 4 == 0) {
             if (flags & 4) v += *op;
             if (flags & 2) v = aux.frame(f)[co * HW + (long long)y * W + x] > 0.f ? v : 0.f;
             *op = v;
+          }
+        }
+      }
+      if constexpr (POOL) {
+        {
+          // rows y (M-tile mt) and y + 1 (mt + PO) -> pooled row y / 2, columns x/2, x/2 + 1
+#pragma unroll
+          for (int mt = 0; mt < MW; ++mt) {
+            if ((mt / C::PO) % 2 != 0) continue;
+            const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+            if (pix >= C::TPXV) continue;
+            const int fi = pix / (RT * W), rem = pix % (RT * W);
+            const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
+            if (f >= F) continue;
+            const f32x4 a = vv[mt], b = vv[mt + C::PO];
+            const float2 o = make_float2(pool4(a[0], a[1], b[0], b[1]), pool4(a[2], a[3], b[2], b[3]));
+            *reinterpret_cast<float2*>(pout.frame(f) + (long long)co * (HW / 4) + (y / 2) * (W / 2) + x / 2) = o;
           }
         }
       }
@@ -1223,23 +1259,29 @@ if constexpr (W % 4 == 0) {
 
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
-                       hipStream_t st, XMax xm, const void* wp) {
+                       hipStream_t st, XMax xm, const void* wp, FViewW pout) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int LDS = C::LDS + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
-  auto k = conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM>;
-  static int resident = 0;
-  if (!resident) {
+  // the fused-pool variant (its own instantiation: keeping the stored tile
+  // live for the pool costs ~20 VGPRs, which the other launches must not pay)
+  constexpr bool POOLABLE = C::POOLOK && !DG;
+  auto k = (POOLABLE && (flags & 64)) ? conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, POOLABLE>
+                                      : conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, false>;
+  static int resident[2] = {0, 0};
+  const int kv = (POOLABLE && (flags & 64)) ? 1 : 0;
+  if (!resident[kv]) {
     if (LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    resident = persistent_grid((const void*)k, LDS);
+    resident[kv] = persistent_grid((const void*)k, LDS);
   }
-  int nb = resident / C::NB;   // persistent blocks per COUT slice
+  int nb = resident[kv] / C::NB;   // persistent blocks per COUT slice
   if (nb > ntiles) nb = ntiles;
   if (nb < 1) nb = 1;
   if (PM != 0 || DG) xm.p = nullptr;
   PAIG_REQUIRE(!xm.p || nb <= xm.n, "conv split fwd: %d blocks need more than %d xmax slots", nb, xm.n);
+  if (flags & 64) PAIG_REQUIRE(C::POOLOK && pout.p, "conv split fwd: no fused pool for Cin=%d Cout=%d H=%d", CIN, COUT, H);
   hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles, xm,
-                     PM == 0 ? static_cast<const s16x8*>(wp) : nullptr);
+                     PM == 0 ? static_cast<const s16x8*>(wp) : nullptr, pout);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -1309,17 +1351,18 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
 // flags & 128: split precision (f16 x3 forward and scaled dgrad), flags & 256:
 // bf16 hi only.  Returns 1 if the shape is instantiated here (rc in *rc).
 int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp) {
+                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp,
+                        FViewW pout) {
   const bool dg = (flags & 8) != 0, up = (flags & 32) != 0, b16 = (flags & 256) != 0;
-  const int fl = flags & 7;
+  const int fl = flags & (7 | 64);
   if (H != W || !(flags & (128 | 256))) return 0;
   if (in.grp > 0 && H * W < 256) return 0;   // multi-frame tiles step frames by a plain stride
   if (up) {
     if (dg) return 0;
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
     if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
-      *rc = b16 ? sfwd_launch<CI, CO, HH, HH, K, false, true, 2>(in, out, aux, w, b, F, fl, st, xm, wp)           \
-                : sfwd_launch<CI, CO, HH, HH, K, false, true, 0>(in, out, aux, w, b, F, fl, st, xm, wp);          \
+      *rc = b16 ? sfwd_launch<CI, CO, HH, HH, K, false, true, 2>(in, out, aux, w, b, F, fl, st, xm, wp, pout)           \
+                : sfwd_launch<CI, CO, HH, HH, K, false, true, 0>(in, out, aux, w, b, F, fl, st, xm, wp, pout);          \
       return 1;                                                                                           \
     }
     PAIG_SPLIT_UP(PAIG_CASE)
@@ -1329,11 +1372,11 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
 #define PAIG_CASE(CI, CO, HH, K)                                                                            \
   if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                      \
     if (b16)                                                                                                \
-      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 2>(in, out, aux, w, b, F, fl, st, xm, wp)              \
-               : sfwd_launch<CI, CO, HH, HH, K, false, false, 2>(in, out, aux, w, b, F, fl, st, xm, wp);            \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 2>(in, out, aux, w, b, F, fl, st, xm, wp, pout)              \
+               : sfwd_launch<CI, CO, HH, HH, K, false, false, 2>(in, out, aux, w, b, F, fl, st, xm, wp, pout);            \
     else                                                                                                    \
-      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 0>(in, out, aux, w, b, F, fl, st, xm, wp)              \
-               : sfwd_launch<CI, CO, HH, HH, K, false, false, 0>(in, out, aux, w, b, F, fl, st, xm, wp);            \
+      *rc = dg ? sfwd_launch<CI, CO, HH, HH, K, true, false, 0>(in, out, aux, w, b, F, fl, st, xm, wp, pout)              \
+               : sfwd_launch<CI, CO, HH, HH, K, false, false, 0>(in, out, aux, w, b, F, fl, st, xm, wp, pout);            \
     return 1;                                                                                               \
   }
   PAIG_SPLIT_FWD(PAIG_CASE)
@@ -1372,6 +1415,16 @@ int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nbl
 int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags) {
   if (H != W) return 0;
   const bool up = (flags & 32) != 0, dg = (flags & 8) != 0;
+  if (flags & 64) {   // forward with the fused 2x2 max pool of its output
+    if (what != 0 || up || dg || !(flags & (128 | 256))) return 0;
+    const bool b16 = (flags & 256) != 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                                         \
+    if (Cin == CI && Cout == CO && H == HH && ks == K)                                                   \
+      return b16 ? SFwdCfg<CI, CO, HH, HH, K, false, 2>::POOLOK : SFwdCfg<CI, CO, HH, HH, K, false, 0>::POOLOK;
+    PAIG_SPLIT_FWD(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
 #define PAIG_CASE(CI, CO, HH, K) \
   if (Cin == CI && Cout == CO && H == HH && ks == K) return 1;
   if (up) {

@@ -544,13 +544,25 @@ class Engine:
                               (ctypes.c_void_p * n)(*outs), st)
             S["wprep_buf"] = buf
         S["wprep"] = wp
+        pooled = set()   # pools written by their producing conv's epilogue
         for i, op in enumerate(ops):
             if op["op"] == "up" and op["dst"][0] in lay.fused_bufs:
                 continue   # formed inside the consuming conv's staging
+            if i in pooled:
+                continue
             dv, dlvl = view(op["dst"])
             if op["op"] == "conv":
                 sv, clvl, xfl = conv_input(i, op)
                 Hl = H // clvl
+                # a 2x2 max pool of exactly this output, next in the plan, is
+                # fused into the conv's epilogue where the split kernel has it
+                pool_v = (None, 0)
+                nxt = ops[i + 1] if i + 1 < len(ops) else None
+                if (nxt is not None and nxt["op"] == "pool" and nxt["src"] == op["dst"] and not xfl and cm
+                        and L.paig_conv2d_mfma_supported(0, op["src"][2], op["dst"][2], Hl, Hl, op["ks"], cm | 64)):
+                    pv, _ = view(nxt["dst"])
+                    pool_v = (pv[0], pv[1])
+                    pooled.add(i + 1)
                 W_ = self.p(lay.prefix + op["name"] + ".weight")
                 b_ = self.p(lay.prefix + op["name"] + ".bias")
                 fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
@@ -558,8 +570,8 @@ class Engine:
                 with self._p("conv_fwd:" + op["name"], fl, nbytes):
                     L.paig_conv2d_fwd_pw(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
                                          op["src"][2], op["dst"][2], Hl, Hl, op["ks"],
-                                         (1 if op["relu"] else 0) | xfl | cm, S["xmax"](i), XMAX_SLOTS,
-                                         wp.get((i, 0)), st)
+                                         (1 if op["relu"] else 0) | xfl | cm | (64 if pool_v[0] else 0),
+                                         S["xmax"](i), XMAX_SLOTS, pool_v[0], pool_v[1], wp.get((i, 0)), st)
             elif op["op"] == "pool":
                 sv, slvl = view(op["src"])
                 Hl = H // slvl
@@ -856,7 +868,8 @@ class Engine:
                 nbytes = 4 * F * Hl * Hl * (cout + cin * (1 + (1 if flags & 2 else 0) + (1 if flags & 4 else 0)))
                 with self._p("conv_dgrad:" + op["name"], fl, nbytes):
                     L.paig_conv2d_fwd_pw(dyv[0], dyv[1], 0, 0, dxv[0], dxv[1], aux[0] or None, aux[1], ptr(W_), None,
-                                         F, cout, cin, Hl, Hl, ks, flags | cm, None, 0, S["wprep"].get((i, 1)), st)
+                                         F, cout, cin, Hl, Hl, ks, flags | cm, None, 0, None, 0,
+                                         S["wprep"].get((i, 1)), st)
                 mark(src)
             elif op["op"] == "pool":
                 sv, slvl = view(src)

@@ -505,7 +505,7 @@ def test_conv_wprep_bit_identical(cin, cout, hw, ks, up):
     for wpp in (None, p(bufs[0])):
         o = torch.empty(3, cout, hw, hw, device=DEV)
         L().paig_conv2d_fwd_pw(p(x), cin * hin * hin, 0, 0, p(o), cout * hw * hw, None, 0, p(w), p(b), 3, cin, cout,
-                               hw, hw, ks, 1 | fl, None, 0, wpp, st())
+                               hw, hw, ks, 1 | fl, None, 0, None, 0, wpp, st())
         outs.append(o)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
@@ -515,7 +515,34 @@ def test_conv_wprep_bit_identical(cin, cout, hw, ks, up):
         for wpp in (None, p(bufs[1])):
             dx = torch.full((3, cin, hw, hw), 0.5, device=DEV)
             L().paig_conv2d_fwd_pw(p(dy), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, p(aux), cin * hw * hw, p(w), None,
-                                   3, cout, cin, hw, hw, ks, 8 | 4 | 2 | 128, None, 0, wpp, st())
+                                   3, cout, cin, hw, hw, ks, 8 | 4 | 2 | 128, None, 0, None, 0, wpp, st())
             dxs.append(dx)
         torch.cuda.synchronize()
         assert torch.equal(dxs[0], dxs[1])
+
+
+@pytest.mark.parametrize("cin,cout,hw,mode", [(8, 8, 32, 128), (16, 16, 16, 128), (8, 8, 32, 256), (3, 8, 32, 128)])
+def test_conv_fused_pool(cin, cout, hw, mode):
+    """Split forward with the fused 2x2 max pool (flags & 64): the conv output
+    is unchanged and the pooled output is bit-identical to paig_maxpool2_fwd
+    on it (aten's window scan order; ReLU zeros and ties included)."""
+    torch.manual_seed(cin * 7 + hw)
+    F_ = 5
+    x = torch.randn(F_, cin, hw, hw, device=DEV)
+    w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.2
+    b = torch.randn(cout, device=DEV)
+    assert L().paig_conv2d_mfma_supported(0, cin, cout, hw, hw, 3, mode | 64) == 1
+    h2 = hw // 2
+    y0 = torch.empty(F_, cout, hw, hw, device=DEV)
+    y1 = torch.empty(F_, cout, hw, hw, device=DEV)
+    pool = torch.full((F_, cout, h2, h2), float("nan"), device=DEV)
+    ref = torch.empty(F_, cout, h2, h2, device=DEV)
+    L().paig_conv2d_fwd_pw(p(x), cin * hw * hw, 0, 0, p(y0), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout, hw, hw,
+                           3, 1 | mode, None, 0, None, 0, None, st())
+    L().paig_conv2d_fwd_pw(p(x), cin * hw * hw, 0, 0, p(y1), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout, hw, hw,
+                           3, 1 | mode | 64, None, 0, p(pool), cout * h2 * h2, None, st())
+    L().paig_maxpool2_fwd(p(y0), cout * hw * hw, p(ref), cout * h2 * h2, F_, cout, hw, hw, st())
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert torch.equal(pool, ref)
+    assert L().paig_conv2d_mfma_supported(0, cin, cout, 36, 36, 3, mode | 64) == 0   # 36-wide rows: no in-lane windows
