@@ -1461,7 +1461,7 @@ struct WPrepJobs {
   int blk0[WPREP_MAX + 1];   // first block of each job (WPREP_T entries per block)
   int n;
 };
-constexpr int WPREP_T = 128;
+constexpr int WPREP_T = 64;
 
 // one entry (8 values) per thread; the blocks of every job in one grid
 __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
