@@ -384,16 +384,14 @@ class Engine:
         cm = self.conv_flags()
         S["cm"] = cm
 
-        # ---- VariableFromNetwork sources (once per step, Q12)
+        # ---- VariableFromNetwork sources (once per step, Q12): allocated here,
+        # computed on the main stream while the side stream runs the velocity
+        # MLP + rollout (only the decoders read them)
         src = {}
         vf = (("var_net_template", K * h * h, False), ("var_net_content", K * 3 * h * h, False),
               ("var_net_background", 3 * HW, True))
         for nm, P, post in vf:
             src[nm] = (_empty(200, dev), _empty(P, dev), _empty(P, dev) if post else None)
-        L.paig_vfn_fwd_multi(3, *[_parr([ptr(self.p(nm + suf)) for nm, _, _ in vf])
-                                  for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
-                             _parr([ptr(src[nm][0]) for nm, _, _ in vf]), _parr([ptr(src[nm][1]) for nm, _, _ in vf]),
-                             _parr([ptr(src[nm][2]) for nm, _, _ in vf]), _iarr([P for _, P, _ in vf]), st)
         S["src"] = src
         tmpl, cont, bgp = src["var_net_template"][1], src["var_net_content"][1], src["var_net_background"][2]
 
@@ -441,7 +439,12 @@ class Engine:
         # ---- (side) physics rollout (all R steps in one launch)
         L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0), ptr(prm[0]),
                            ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, sst)
-        # ---- (main) reconstruction decode (all B*Te frames, SSE vs input fused)
+        # ---- (main) VariableFromNetwork sources, then the reconstruction decode
+        # (all B*Te frames, SSE vs input fused)
+        L.paig_vfn_fwd_multi(3, *[_parr([ptr(self.p(nm + suf)) for nm, _, _ in vf])
+                                  for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                             _parr([ptr(src[nm][0]) for nm, _, _ in vf]), _parr([ptr(src[nm][1]) for nm, _, _ in vf]),
+                             _parr([ptr(src[nm][2]) for nm, _, _ in vf]), _iarr([P for _, P, _ in vf]), st)
         with self._p("dec_fwd:recon", 0, self._dec_bytes(F, lay, False)):
             L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons), lay.frame,
                                x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, st)
