@@ -1461,38 +1461,32 @@ struct WPrepJobs {
   int blk0[WPREP_MAX + 1];   // first block of each job (WPREP_T entries per block)
   int n;
 };
-constexpr int WPREP_T = 64;
+constexpr int WPREP_T = 256;
 
-// one entry (8 values) per thread; the blocks of every job in one grid
+// one value per thread (entry e = t / 8, channel j = t % 8): one scattered
+// weight load each, the 8 lanes of an entry store its 16 bytes together
 __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
   float rmax = 0.f;
   int q = 0;
   while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.blk0[q + 1]) ++q;
-  {
-    const WPrepJob jb = jobs.j[q];
-    const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16;
-    const float wsc = __builtin_amdgcn_ldexpf(1.f, PAIG_W_EXP);
-    const int e = ((int)blockIdx.x - jobs.blk0[q]) * WPREP_T + threadIdx.x;
-    if (e < jb.entries) {
-      const int s = e / (NTT * 64), rem = e - s * NTT * 64, ln = rem & 63, ntg = rem >> 6;
-      const int kc = 4 * s + (ln >> 4), co = ntg * 16 + (ln & 15);
-      s16x8 vh, vl;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = 0.f;
-        if (kc < KC && co < jb.cout) {
-          const int tap = kc / CC, ci = (kc % CC) * 8 + j;
-          if (ci < jb.cin)
-            v = jb.dg ? jb.w[(ci * jb.cout + co) * KK + (KK - 1 - tap)] : jb.w[(co * jb.cin + ci) * KK + tap];
-        }
-        short h, l;
-        split<0>(v * wsc, h, l, rmax);
-        vh[j] = h;
-        vl[j] = l;
-      }
-      jb.out[e] = vh;
-      jb.out[jb.entries + e] = vl;
+  const WPrepJob jb = jobs.j[q];
+  const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16;
+  const float wsc = __builtin_amdgcn_ldexpf(1.f, PAIG_W_EXP);
+  const int t = ((int)blockIdx.x - jobs.blk0[q]) * WPREP_T + threadIdx.x;
+  const int e = t >> 3, j = t & 7;
+  if (e < jb.entries) {
+    const int s = e / (NTT * 64), rem = e - s * NTT * 64, ln = rem & 63, ntg = rem >> 6;
+    const int kc = 4 * s + (ln >> 4), co = ntg * 16 + (ln & 15);
+    float v = 0.f;
+    if (kc < KC && co < jb.cout) {
+      const int tap = kc / CC, ci = (kc % CC) * 8 + j;
+      if (ci < jb.cin) v = jb.dg ? jb.w[(ci * jb.cout + co) * KK + (KK - 1 - tap)] : jb.w[(co * jb.cin + ci) * KK + tap];
     }
+    short h, l;
+    split<0>(v * wsc, h, l, rmax);
+    short* o = reinterpret_cast<short*>(jb.out);
+    o[(long long)e * 8 + j] = h;
+    o[((long long)jb.entries + e) * 8 + j] = l;
   }
   f16_range_note(rmax);
 }
@@ -1519,7 +1513,7 @@ int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cou
       const int e = (int)(paig_conv_wprep_size(cin[i], cout[i], ks[i]) / 16);
       jobs.j[q] = WPrepJob{w[i], static_cast<s16x8*>(out[i]), cin[i], cout[i], ks[i], dg[i], e};
       jobs.blk0[q] = blocks;
-      blocks += cdiv(e, WPREP_T);
+      blocks += cdiv(8ll * e, WPREP_T);
     }
     jobs.blk0[jobs.n] = blocks;
     hipLaunchKernelGGL(conv_wprep_k, dim3(blocks), dim3(WPREP_T), 0, (hipStream_t)stream, jobs);
