@@ -116,6 +116,11 @@ def parse():
                     help="U-Net conv arithmetic: split = f16/bf16 hi+lo operands on the 16-bit matrix cores, "
                          "fp32-accurate (meets the 1e-4 parity bar; default); fp32 = f32-input MFMA; "
                          "bf16 = bf16 operands (config #2)")
+    ap.add_argument("--legs", type=int, default=1, help="also time BASELINE configs #2-#5 (LEGS) in the same line")
+    ap.add_argument("--leg_steps", type=int, default=10)
+    ap.add_argument("--leg_warmup", type=int, default=3)
+    ap.add_argument("--leg_render", type=int, default=64,
+                    help="distinct synthetic sequences rendered per leg (tiled to the resident dataset)")
     ap.add_argument("--cpu_baseline", type=int, default=1)
     ap.add_argument("--cpu_seconds", type=float, default=10.0, help="CPU time budget per cpu_baseline sample")
     return ap.parse_args()
@@ -184,6 +189,117 @@ def cpu_baseline(task, u8, ae, budget_s, seq_lens):
     return out
 
 
+# BASELINE.json configs #2-#5 (runners/torch_run_physics.py:49-75 presets),
+# timed as extra legs of the same run, B per rank
+LEGS = [
+    ("config2_spring_bf16", "spring_color", 512, 50, "bf16"),
+    ("config3_3bp", "3bp_color", 512, 20, "split"),
+    ("config4_mnist", "mnist_spring_color", 256, 12, "split"),
+    ("config5_bouncing_r96", "bouncing_balls", 1024, 100, "split"),
+]
+# task -> (cell, input_steps, pred_steps, frame size): runners/torch_run_physics.py:49-75
+TASKS = {"spring_color": ("spring_ode_cell", 4, 6, 32), "spring_color_half": ("spring_ode_cell", 4, 6, 32),
+         "bouncing_balls": ("bouncing_ode_cell", 4, 6, 32), "3bp_color": ("gravity_ode_cell", 4, 12, 36),
+         "mnist_spring_color": ("spring_ode_cell", 3, 7, 64)}
+
+
+def run_workload(a, world, rank, dev, task, batch, seq_len, conv_math, steps, warmup, probe_steps, n_render):
+    """One timed training workload: returns seqs/s over all ranks, the step
+    time, the final loss, the per-kernel probe summaries and the dataset."""
+    from paig_reproduction_amd.nn.datasets.synth import render_sequences
+    from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
+    from paig_reproduction_amd.nn.datasets.iterators import DeviceDataIterator
+    from paig_reproduction_amd import engine as E
+    from paig_reproduction_amd.graph_step import GraphStep
+
+    cell, ins, pred, size = TASKS[task]
+    torch.manual_seed(0)
+    m = PhysicsNet(task, 100, 1, cell, seq_len, ins, pred, a.ae, False, True, size * size,
+                   "conv_encoder", "conv_st_decoder", device=dev).to(dev)
+    m.conv_math = conv_math
+    m.build_optimizer(a.lr, "rmsprop", True)
+    if world > 1:
+        for t in m.state_dict().values():
+            dist.broadcast(t, 0)
+
+    # resident synthetic dataset (this rank's shard): n_render rendered
+    # sequences tiled to a.dataset batches; every step gathers the next B of a
+    # shuffled epoch into the graph's fixed input buffer (get_batch)
+    u8 = render_sequences(task, n_render, seq_len, seed=1000 * rank + 1)
+    reps = max(1, -(-a.dataset * batch // n_render)) if n_render < 2 * batch else max(1, a.dataset // 2)
+    u8 = np.concatenate([u8] * reps, 0)
+    it = DeviceDataIterator(u8, (seq_len, 3, size, size), dev, seed=rank)
+    xbuf = torch.empty((batch, seq_len, 3, size, size), device=dev)
+
+    gstep = GraphStep(m, xbuf, world, split=None if a.split_graph < 0 else bool(a.split_graph), graph=bool(a.graph),
+                      optimizer_in_graph=bool(a.graph_optimizer))
+    eng = gstep.eng
+
+    def eager_step():
+        it.next_batch(batch, out=xbuf)
+        return gstep.eager()
+
+    for i in range(warmup):
+        eager_step()
+    gstep.capture()
+
+    def step():
+        it.next_batch(batch, out=xbuf)   # get_batch: one gather launch, no H2D
+        return gstep()
+
+    step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    gstep.finish()
+    lossv = float(loss.item())
+    # roofline probes: every tagged main-stream launch timed with HIP events
+    # on its stream, over eager steps of the same workload after the timed region
+    probe = E.KernelProbe(None)
+    eng.probe = probe
+    for i in range(probe_steps):
+        eager_step()
+    eng.probe = None
+    kds = probe.summaries()
+    res = {"value": world * batch * steps / el, "el": el, "loss": lossv, "kds": kds, "split": gstep.split,
+           "opt_in_graph": gstep.opt_in_graph, "dataset_seqs": int(u8.shape[0]), "ins": ins, "pred": pred, "size": size,
+           "u8_head": u8[:100]}
+    del gstep, m, eng, it, xbuf
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
+
+
+def roof_of(kd, conv_math):
+    sec = kd["avg_ms"] * 1e-3
+    tflops = kd["flops"] / sec / 1e12
+    if conv_math == "fp32" and kd["tag"].split(":")[0] in ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm_fwd",
+                                                           "gemm_wgrad", "gemm_dgrad"):
+        # f32-input MFMA: bounded by the fp32 matrix rate
+        return {"bound": "mfma", "kernel": kd["tag"], "achieved": round(tflops, 3), "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4), "avg_us": round(kd["avg_ms"] * 1e3, 2),
+                "launches": kd["n"], "algorithmic_flops": kd["flops"], "algorithmic_bytes": kd["bytes"]}
+    # 16-bit matrix cores / VALU kernels: HBM-bound; achieved = algorithmic
+    # bytes per launch / launch time
+    gbs = kd["bytes"] / sec / 1e9
+    return {"bound": "hbm", "kernel": kd["tag"], "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_tflops": round(tflops, 2),
+            "avg_us": round(kd["avg_ms"] * 1e3, 2), "avg_us_events_raw": round(kd["avg_ms_raw"] * 1e3, 2),
+            "event_overhead_us": round(kd["overhead_ms"] * 1e3, 2), "launches": kd["n"],
+            "algorithmic_flops": kd["flops"], "algorithmic_bytes": kd["bytes"]}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -201,142 +317,11 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
 
-    from paig_reproduction_amd.nn.datasets.synth import render_sequences, as_model_input
-    from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
-    from paig_reproduction_amd import engine as E
-
-    # task -> (cell, input_steps, pred_steps, frame size): runners/torch_run_physics.py:49-75
-    tasks = {"spring_color": ("spring_ode_cell", 4, 6, 32), "spring_color_half": ("spring_ode_cell", 4, 6, 32),
-             "bouncing_balls": ("bouncing_ode_cell", 4, 6, 32), "3bp_color": ("gravity_ode_cell", 4, 12, 36),
-             "mnist_spring_color": ("spring_ode_cell", 3, 7, 64)}
-    cell, ins, pred, size = tasks[a.task]
-    torch.manual_seed(0)
-    m = PhysicsNet(a.task, 100, 1, cell, a.seq_len, ins, pred, a.ae, False, True, size * size,
-                   "conv_encoder", "conv_st_decoder", device=dev).to(dev)
-    m.conv_math = a.conv_math
-    m.build_optimizer(a.lr, "rmsprop", True)
-    if world > 1:
-        for t in m.state_dict().values():
-            dist.broadcast(t, 0)
-
-    # resident synthetic dataset (this rank's shard): 2B rendered sequences
-    # tiled to a.dataset batches; every step gathers the next B of a
-    # shuffled epoch into the graph's fixed input buffer (get_batch)
-    from paig_reproduction_amd.nn.datasets.iterators import DeviceDataIterator
-    u8 = render_sequences(a.task, 2 * a.batch, a.seq_len, seed=1000 * rank + 1)
-    u8 = np.concatenate([u8] * max(1, a.dataset // 2), 0)
-    it = DeviceDataIterator(u8, (a.seq_len, 3, size, size), dev, seed=rank)
-    xbuf = torch.empty((a.batch, a.seq_len, 3, size, size), device=dev)
-
-    eng = m._native()
-    seed_grad = {}
-
-    def body(x):
-        m.output = m(x)
-        loss, _ = m.compute_loss()
-        m.optimizer.zero_grad(set_to_none=True)
-        # d loss / d loss = 1 from a persistent tensor (made before any graph
-        # capture): autograd's implicit ones_like would be a fill kernel per step
-        if "one" not in seed_grad:
-            seed_grad["one"] = torch.ones_like(loss)
-        loss.backward(seed_grad["one"])
-        return loss
-
-    def eager_step():
-        it.next_batch(a.batch, out=xbuf)
-        loss = body(xbuf)
-        m.optimizer.step()
-        return loss
-
-    for i in range(a.warmup):
-        eager_step()
-    graph = None
-    split = a.split_graph if a.split_graph >= 0 else int(world > 1)
-    opt_in_graph = bool(a.graph and a.graph_optimizer and world == 1 and not split and m.optimizer.kind == "rmsprop")
-    if a.graph:
-        # fwd+loss+bwd (+RMSprop at N=1) captured once on the fixed input
-        # buffer (two graphs when split); the gather, the DP all-reduce and
-        # (N>1) the optimizer step stay eager
-        torch.cuda.synchronize()
-        if not split:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                lg = body(xbuf)
-                if opt_in_graph:
-                    m.optimizer.step()
-            graph = ((g,), lg)
-        else:
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            seen = []
-
-            def cut():   # engine.bucket_hook: the early bucket is final here
-                g1.capture_end()
-                g2.capture_begin(pool=g1.pool(), capture_error_mode="relaxed")
-                seen.append(1)
-
-            cap = torch.cuda.Stream()
-            cap.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(cap):
-                # relaxed: the cut runs on the autograd engine's device thread
-                g1.capture_begin(capture_error_mode="relaxed")
-                eng.bucket_hook = cut
-                try:
-                    lg = body(xbuf)
-                finally:
-                    eng.bucket_hook = m._flat.allreduce_early
-                g2.capture_end()
-            torch.cuda.current_stream().wait_stream(cap)
-            assert seen == [1], "backward did not reach the bucket split point"
-            graph = ((g1, g2), lg)
-        torch.cuda.synchronize()
-
-    replays = [0]
-
-    def step():
-        if graph is None:
-            return eager_step()
-        gs, lg = graph
-        it.next_batch(a.batch, out=xbuf)   # get_batch: one gather launch, no H2D
-        replays[0] += 1
-        gs[0].replay()
-        if len(gs) == 2:
-            m._flat.allreduce_early()   # overlaps the second graph (U-Net backward)
-            gs[1].replay()
-        if not opt_in_graph:
-            m.optimizer.step()
-        return lg
-
-    step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    if opt_in_graph:
-        # the captured RMSprop step ran Python once, at capture: count its
-        # replays (its lr is the captured constant; RMSprop only, see above)
-        m.optimizer.steps += replays[0]
-    lossv = float(loss.item())
-    # roofline probes: every tagged main-stream launch timed with HIP events
-    # on its stream, over eager steps of the same workload after the timed region
-    probe = E.KernelProbe(None)
-    eng.probe = probe
-    for i in range(a.probe_steps):
-        eager_step()
-    eng.probe = None
-    kds = probe.summaries()
-
-    seqs = world * a.batch * a.steps
-    value = seqs / el
+    r = run_workload(a, world, rank, dev, a.task, a.batch, a.seq_len, a.conv_math, a.steps, a.warmup, a.probe_steps,
+                     2 * a.batch)
+    el, kds = r["el"], r["kds"]
+    ins, pred, size = r["ins"], r["pred"], r["size"]
+    value = r["value"]
     top_kernel, top_src = summary_top()
     fam = tag_family(top_kernel)
     if a.probe != "auto":
@@ -345,43 +330,44 @@ def main():
         cands = [t for t in kds if fam and t.startswith(fam)] or list(kds)
         tag = max(cands, key=lambda t: kds[t]["avg_ms"]) if cands else None
 
-    def roof_of(kd):
-        sec = kd["avg_ms"] * 1e-3
-        tflops = kd["flops"] / sec / 1e12
-        if a.conv_math == "fp32" and kd["tag"].split(":")[0] in ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm_fwd",
-                                                               "gemm_wgrad", "gemm_dgrad"):
-            # f32-input MFMA: bounded by the fp32 matrix rate
-            return {"bound": "mfma", "kernel": kd["tag"], "achieved": round(tflops, 3), "peak": PEAK_FP32_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4), "avg_us": round(kd["avg_ms"] * 1e3, 2),
-                    "launches": kd["n"], "algorithmic_flops": kd["flops"], "algorithmic_bytes": kd["bytes"]}
-        # 16-bit matrix cores / VALU kernels: HBM-bound; achieved = algorithmic
-        # bytes per launch / launch time
-        gbs = kd["bytes"] / sec / 1e9
-        return {"bound": "hbm", "kernel": kd["tag"], "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_tflops": round(tflops, 2),
-                "avg_us": round(kd["avg_ms"] * 1e3, 2), "avg_us_events_raw": round(kd["avg_ms_raw"] * 1e3, 2),
-                "event_overhead_us": round(kd["overhead_ms"] * 1e3, 2), "launches": kd["n"],
-                "algorithmic_flops": kd["flops"],
-                "algorithmic_bytes": kd["bytes"]}
-
     roof = None
-    traffic_path = a.traffic or os.path.join(PROFILES, "r02_pmc_traffic.json")
+    traffic_path = a.traffic or default_traffic()
     traffic, step_bytes = pmc_traffic(traffic_path, tag, {"task": a.task, "batch": a.batch, "seq_len": a.seq_len,
                                                            "conv_math": a.conv_math})
     if tag in kds:
-        roof = roof_of(kds[tag])
+        roof = roof_of(kds[tag], a.conv_math)
         roof.update({"traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (PMC)",
+                     "traffic_source": os.path.relpath(traffic_path, REPO) if traffic else None,
                      "summary_top_kernel": top_kernel, "summary": top_src})
     # the other large kernel families, for the record
     others = {}
-    for want in ("dec_bwd:rollout", "dec_fwd:rollout", "gemm_fwd:encoder.l1", "gemm_dgrad:encoder.l2",
+    for want in ("dec_bwd:rollout", "dec_bwd:recon", "dec_fwd:rollout", "gemm_fwd:encoder.l1", "gemm_dgrad:encoder.l2",
                  "conv_wgrad:c11", "conv_fwd:c11", "conv_dgrad:c2"):
         if want in kds and want != tag:
-            r = roof_of(kds[want])
-            others[want] = {k: r[k] for k in ("bound", "achieved", "unit", "frac", "avg_us")}
+            rr = roof_of(kds[want], a.conv_math)
+            others[want] = {k: rr[k] for k in ("bound", "achieved", "unit", "frac", "avg_us")}
+    # BASELINE configs #2-#5 as extra legs (per-rank B, the same DP path)
+    legs = {}
+    if a.legs:
+        for name, task, batch, seq_len, cm in LEGS:
+            lr_ = run_workload(a, world, rank, dev, task, batch, seq_len, cm, a.leg_steps, a.leg_warmup,
+                               a.probe_steps, min(2 * batch, a.leg_render))
+            lk = lr_["kds"]
+            # the leg's own top kernel: the probed main-stream launch family with the most time per step
+            top = max(lk, key=lambda t: lk[t]["avg_ms"] * lk[t]["n"]) if lk else None
+            ci, cp, cs = lr_["ins"], lr_["pred"], lr_["size"]
+            legs[name] = {
+                "metric": f"video-seqs/sec (train step) {task} B={batch}", "value": round(lr_["value"], 2),
+                "unit": "video-seqs/s", "n_gpus": world, "steps": a.leg_steps, "warmup": a.leg_warmup,
+                "ms_per_step": round(lr_["el"] / a.leg_steps * 1e3, 3), "dtype": "bf16" if cm == "bf16" else "fp32",
+                "config": {"workload": f"{task} B={batch}/rank, {cs}x{cs}x3, seq_len {seq_len} ({ci} in / {cp} pred / "
+                                       f"{seq_len - ci - cp} extrap)", "global_batch": world * batch,
+                           "seq_len": seq_len, "parallelism": f"dp{world}", "conv_math": cm,
+                           "dataset_seqs": lr_["dataset_seqs"]},
+                "roofline": roof_of(lk[top], cm) if top else None, "final_loss": round(lr_["loss"], 4)}
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:
-        cpu = cpu_baseline(a.task, u8[:100], a.ae, a.cpu_seconds, [a.seq_len] + ([12] if a.seq_len != 12 else []))
+        cpu = cpu_baseline(a.task, r["u8_head"], a.ae, a.cpu_seconds, [a.seq_len] + ([12] if a.seq_len != 12 else []))
     if rank == 0:
         line = {
             "metric": METRIC if (a.task, a.batch) == ("spring_color", 100) else
@@ -394,17 +380,25 @@ def main():
                                    f"B={a.batch}/rank, {size}x{size}x3, seq_len {a.seq_len} "
                                    f"({ins} in / {pred} pred / {a.seq_len - ins - pred} extrap)",
                        "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}",
-                       "conv_math": a.conv_math, "split_graph": bool(a.graph and split),
-                       "optimizer_in_graph": opt_in_graph, "dataset_seqs": int(u8.shape[0])},
-            "roofline": roof, "roofline_others": others, "cpu_baseline": cpu, "final_loss": round(lossv, 4),
+                       "conv_math": a.conv_math, "split_graph": r["split"],
+                       "optimizer_in_graph": r["opt_in_graph"], "dataset_seqs": r["dataset_seqs"]},
+            "roofline": roof, "roofline_others": others, "cpu_baseline": cpu, "final_loss": round(r["loss"], 4),
             # whole-step memory-side traffic (committed PMC profile) at this run's step time
             "hbm_step": None if step_bytes is None else {
                 "bytes_per_step": round(step_bytes), "achieved_GBs": round(step_bytes / (el / a.steps) / 1e9, 1),
                 "peak_GBs": PEAK_HBM_GBS, "frac": round(step_bytes / (el / a.steps) / 1e9 / PEAK_HBM_GBS, 4)},
+            "legs": legs,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def default_traffic():
+    """The newest committed whole-step PMC traffic summary (profiles/rNN_pmc_traffic.json)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(PROFILES, "r*_pmc_traffic.json")))
+    return paths[-1] if paths else os.path.join(PROFILES, "r02_pmc_traffic.json")
 
 
 if __name__ == "__main__":

@@ -231,13 +231,18 @@ int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner,
                      const float* cont, const float* bg, float* out, long long out_fs, const float* tgt,
                      long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F, int K, int h, int H,
                      void* stream);
-int paig_decoder_bwd_blocks(int F);
+/* backward over F frames grouped in sequences of pos_grp (0: ungrouped) of
+ * which only the first `live` per sequence carry gradient (0: all; the
+ * rollout decode's pred_steps, physics_models.py:129-139): the others get
+ * dpos = 0 and are not read.  Partial source gradients: one slab row of
+ * paig_decoder_slab_len floats per block, paig_decoder_bwd_blocks rows. */
+int paig_decoder_bwd_blocks(int F, int pos_grp, int live, int K, int h, int H);
 size_t paig_decoder_slab_len(int K, int h, int H);
 size_t paig_decoder_bwd_scratch(int F, int K, int h, int H);
 int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
                      const float* cont, const float* bg, const float* tgt, long long tgt_fs, int tgt_grp,
                      long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
-                     float* slab, float* scratch, int F, int K, int h, int H, void* stream);
+                     float* slab, float* scratch, int F, int live, int K, int h, int H, void* stream);
 
 /* the decoder's per-object intermediates (transf_contents / transf_masks,
  * physics_models.py:186-196) for positions pos [F][2K] (row stride

@@ -75,10 +75,10 @@ SIGNATURES = {
     "paig_rollout_bwd_blocks": (I, [I]),
     "paig_rollout_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P]),
     "paig_decoder_fwd": (I, [P, LL, LL, I, P, P, P, P, LL, P, LL, I, LL, P, I, I, I, I, P]),
-    "paig_decoder_bwd_blocks": (I, [I]),
+    "paig_decoder_bwd_blocks": (I, [I, I, I, I, I, I]),
     "paig_decoder_slab_len": (SZ, [I, I, I]),
     "paig_decoder_bwd_scratch": (SZ, [I, I, I, I]),
-    "paig_decoder_bwd": (I, [P, LL, LL, I, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, P]),
+    "paig_decoder_bwd": (I, [P, LL, LL, I, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, I, P]),
     "paig_decoder_parts": (I, [P, LL, P, P, P, P, P, I, I, I, I, P]),
     "paig_stn_fwd": (I, [P, P, P, I, I, I, I, I, I, P]),
     "paig_stn_bwd": (I, [P, P, P, P, P, I, I, I, I, I, I, P]),

@@ -172,6 +172,48 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// fp64 wave sum without LDS round trips (the __shfl_xor form above issues two
+// ds_bpermute per step): DPP within rows of 16 (quad swaps, half-row and row
+// mirrors; a + b and b + a round alike, so every lane of a row holds the same
+// row sum), then the four row sums read as scalars and added in a fixed
+// order.  Returned wave-uniform; deterministic.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  // every lane reads a valid source lane in these patterns: bound_ctrl, no
+  // "old" operand to initialise
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)b, CTRL, 0xF, 0xF, true);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+// N independent fp64 sums within each row of 16 lanes, the DPP stages
+// interleaved across the N values (ILP): afterwards every lane of a row holds
+// that row's sums
+template <int N>
+__device__ __forceinline__ void row_sums_dpp_d(double* v) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_d<0xB1>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_d<0x4E>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_d<0x141>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_d<0x140>(v[i]);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+__device__ __forceinline__ double wave_sum_dpp_d(double v) {
+  v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);   // row_half_mirror
+  v += dpp_d<0x140>(v);   // row_mirror
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
 // MFMA implicit-GEMM convolutions (conv_mfma.hip): return 1 when the shape is
 // instantiated there (launch status in *rc), 0 to fall back to the VALU path.
 // xmax (nullable): per-block max |input| of a split-precision forward

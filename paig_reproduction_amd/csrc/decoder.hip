@@ -350,7 +350,7 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
 }
 
 // ---------------------------------------------------------------------------
-// Register-resident variants for the small frames of the headline workloads
+// Register-resident forward for the small frames of the headline workloads
 // ((K, H) = (2, 32) spring/bouncing, (3, 36) 3bp).  Every
 // thread owns the same PPT pixels and SPT source texels in every frame, so
 //   * the background values it composites are loaded once per block,
@@ -360,9 +360,8 @@ dec_bwd_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView d
 //   * the next frame's target pixels are prefetched behind the current frame,
 //   * the bilinear tap weights (and their d/dix, d/diy) are formed once per
 //     (pixel, object) and shared by the template and the 3 content planes,
-//   * the backward's source-gradient gather walks per-frame weight tables
-//     (at most 5 contributing output rows / columns per texel).
-// The generic kernels above remain for the large (mnist 64x64) frames.
+// The backward of these shapes is dec_bwd_cu_k below; the generic kernels
+// above remain for the large (mnist 64x64) frames.
 struct Taps {
   int o[4];      // offsets of nw, ne, sw, se in an h x h plane (0 when out of range)
   float w[4];    // bilinear weights (0 for out-of-range taps: zero padding)
@@ -515,209 +514,532 @@ dec_fwd_reg_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse
   }
 }
 
-// Per-frame gather tables of the backward: for source column xs (row ys) of
-// object k, the output columns (rows) j0 .. j0+4 and their bilinear weights
-// (nonzero where floor(c[j]) == s: 1 - frac, or floor(c[j]) + 1 == s: frac).
-// With the 2x upsampling warp at most 4 output indices contribute.
+// Per-frame gather table entry of the backward: for source column (row) s of
+// an object at position l on that axis, the first output index j0 of a
+// 5-wide window of output columns (rows) and their bilinear weights on s
+// (nonzero where floor(c[j]) == s: 1 - frac, or floor(c[j]) + 1 == s: frac;
+// c[j] = the sample coordinate of output index j, as coord_tables() forms
+// it from the fp64 base coordinates bc[]).  With the 2x upsampling warp at
+// most 4 output indices contribute (5 with rounding at both ends).  The
+// coordinates are evaluated directly (no scan over a coordinate table): c is
+// j/2 + c[0] up to fp32 rounding (~1e-6), so the first j with floor(c[j]) >=
+// s-1 is one of three candidates around that estimate.
 constexpr int GW = 5;
-template <int K, int H>
-__device__ __forceinline__ void gather_tables(const float (*cx)[MAXH], const float (*cy)[MAXH], int (*j0)[2][H / 2],
-                                              float (*wt)[2][H / 2][GW]) {
-  constexpr int h = H / 2;
-  for (int t = threadIdx.x; t < K * 2 * h; t += blockDim.x) {
-    const int k = t / (2 * h), ax = (t / h) & 1, s = t % h;
-    const float* c = ax ? cy[k] : cx[k];
-    // first output index whose sample lies at or right of s-1
-    int j = (int)floorf(2.f * ((float)s - 1.f - c[0])) - 2;
-    if (j < 0) j = 0;
-    while (j < H && floorf(c[j]) < (float)(s - 1)) ++j;
-    j0[k][ax][s] = j;
+__device__ __forceinline__ void gather_entry(float l, const double* bc, int H, int h, int s, int* j0, float* wt) {
+  const double tt = (double)(((float)H / 2.f - l) / (float)h);
+  const float c0 = src_coord(bc[0], tt, h);
+  const int je = (int)ceilf(2.f * ((float)s - 1.f - c0)) - 1;
+  int j = je;
 #pragma unroll
-    for (int b = 0; b < GW; ++b) {
-      const int jj = j + b;
-      float w = 0.f;
-      if (jj < H) {
-        const float v = c[jj], f0 = floorf(v);
-        const int x0 = (int)f0;
-        const float fr = v - f0;
-        w = (x0 == s ? 1.f - fr : 0.f) + (x0 + 1 == s ? fr : 0.f);
-      }
-      wt[k][ax][s][b] = w;
-    }
+  for (int i = 0; i < 3; ++i) {
+    const int jj = je + i;
+    const float c = jj < 0 ? -1e30f : (jj >= H ? 1e30f : src_coord(bc[jj], tt, h));
+    if (floorf(c) < (float)(s - 1)) j = jj + 1;
+  }
+  // the window stays inside [0, H): indices before the first contributor get
+  // their (zero) weights like any other, so no gather needs an index clamp
+  if (j < 0) j = 0;
+  if (j > H - GW) j = H - GW;
+  *j0 = j;
+#pragma unroll
+  for (int b = 0; b < GW; ++b) {
+    const float v = src_coord(bc[j + b], tt, h), f0 = floorf(v);
+    const int x0 = (int)f0;
+    const float fr = v - f0;
+    wt[b] = (x0 == s ? 1.f - fr : 0.f) + (x0 + 1 == s ? fr : 0.f);
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decoder backward, one CU per block (1024 / 768 threads), the headline
+// shapes ((K, H) = (2, 32) spring/bouncing, (3, 36) 3bp).
+//
+// Work list: the LIVE frames only.  Frames are grouped in sequences of R
+// (= pos.grp; the rollout decode) of which the first Rl carry a loss weight
+// (the reference trains on loss[:, :pred_steps] only, physics_models.py:
+// 129-139): compact frame n -> f = (n / Rl) * R + n % Rl.  The dead frames'
+// position gradients are zeroed by a grid-stride pass; nothing else of theirs
+// is read.  Each block walks a contiguous run of >= DEC_FPB_MIN live frames,
+// so the partial source-gradient slab (one row per block) stays a fraction
+// of the target bytes.
+//
+// Per frame, one thread per output pixel (H = 36: a second pixel slot for
+// 528 of the 768):
+//   pass 1: sample the K objects' template + 3 content planes (value and
+//     d/dix, d/diy from one padded float4 texel image: 4 ds_read_b128 per
+//     object), composite, dL/dout = 2 dsse[f] (out - target) (+ dense dout);
+//     background grads accumulate in registers (the thread's pixels are
+//     fixed), the per-object pixel gradients (dT, dC0..2) go to an LDS image
+//     G, the position-gradient sums to a per-wave fp64 reduction (Q9);
+//   pass 2: every source texel gathers its <= 5 x 5 contributing pixels from
+//     G through per-frame separable weight tables (no atomics: a fixed
+//     order); for K = 2 an item is a texel's plane pair, so all 1024 threads
+//     take one.
+// Frames are software-pipelined over ONE barrier each: iteration it forms
+// the axis and gather tables of frame it+1, runs pass 2 of frame it-1 and
+// pass 1 of frame it (double / triple buffers for G, the fp64 partials and
+// the tables).  The position gradients reduce as fp64 DPP row
+// sums per wave, finished by one wave each in the next iteration.  Every global load of frame it+1 (its
+// positions, its loss weight, its targets) is issued one iteration ahead,
+// so no wave waits on memory inside the loop.
+constexpr int DEC_FPB_MIN = 4, DEC_CU_MAX_BLOCKS = 256;
+
 template <int K, int H>
-__global__ void __launch_bounds__(256)
-dec_bwd_reg_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
-              float* __restrict__ slab, int F) {
-  constexpr int h = H / 2, hh = h * h, HW = H * H, PPT = (HW + 255) / 256, SPT = (K * hh + 255) / 256;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* T = lds;
-  float* Cn = T + K * hh;
-  float* G = Cn + K * 3 * hh;   // [K][4][HW] per-frame pixel-gradient image
-  __shared__ double redd[4][2 * K];
-  __shared__ float cx[K][MAXH], cy[K][MAXH];
-  __shared__ double bc[MAXH];
-  init_base(bc, H);
-  __shared__ int j0[K][2][h];
-  __shared__ float wt[K][2][h][GW];
+struct DecCu {
+  // threads per block: 16 waves (4 per SIMD, <= 128 VGPRs); 12 for K = 3,
+  // whose per-pixel state needs more registers (<= 168 VGPRs) and whose
+  // 1296 pixels then fall into 768 + 528 slots
+  static constexpr int NT = K >= 3 ? 768 : 1024, NW = NT / 64;
+  static constexpr int h = H / 2, hp = h + 2, hh = h * h, HW = H * H;
+  static constexpr int PS = (HW + NT - 1) / NT;          // pixel slots per thread
+  static constexpr int PL = K == 2 ? 2 : 4;              // planes per pass-2 item
+  static constexpr int NI = K * hh * (4 / PL);           // pass-2 items
+  static constexpr int NIT = (NI + NT - 1) / NT;         // pass-2 items per thread
+  // G (per-pixel dT, dC0 | dC1, dC2) as two float2 images, each row laid out
+  // even columns first, then odd ones: a pass-2 half-wave reads 16 texels'
+  // pixels 2 apart = 16 consecutive float2s; the row pitch (float2s, = 8
+  // mod 16 where LDS allows) puts the next texel row's reads on the other
+  // 128 B of the banks
+  static constexpr int GPITCH = K == 2 ? H + 8 : H;
+  static constexpr int NC = K * 2 * H, NG = K * 2 * h;   // axis / gather table entries
+  // their threads: the waves right after the 2K that finish the position
+  // gradients (old waves: the scheduler favours them, so the extra work
+  // does not become the barrier's tail)
+  static constexpr int TC0 = 64 * 2 * K, TG0 = TC0 + NC;
+  static_assert(TG0 + NG <= NT, "tables need more threads");
+  // fp64 partials per position gradient: the 4 row sums of every wave, or
+  // (K = 3, LDS budget) the 2 half-wave sums
+  static constexpr int RPW = K >= 3 ? 2 : 4, NR = NW * RPW;
+  static_assert(NR <= 64, "one wave finishes a position gradient");
+};
+
+// slot of output column j in a G row (even columns first)
+template <int H>
+__device__ __forceinline__ int gslot(int j) { return (j & 1) * (H / 2) + (j >> 1); }
+
+// Compact live frame -> real frame and its position / target addresses,
+// advanced incrementally (no per-frame integer divisions).  Grouped mode
+// (the rollout decode): positions and targets are both grouped by R, the
+// first Rl steps of each sequence live.  Otherwise frame n = n, each view
+// keeping its own (group, step) counter.
+struct DecCursor {
+  int f, pq, pr, tq, tr;
+};
+
+// separable bilinear setup of one axis: tap index (padded source), masked
+// weights of the two taps and their d/dcoord (0 for out-of-range taps)
+struct Ax {
+  int c;            // padded index of the first tap, in [0, h]
+  float w0, w1;     // interpolation weights
+  float d0, d1;     // d w / d coord: -1 / +1, or 0 when the tap is padding
+};
+__device__ __forceinline__ Ax axis(float ic, int h) {
+  const float f0 = floorf(ic);
+  const int i0 = (int)f0;
+  const float fr = ic - f0;
+  const bool v0 = (unsigned)i0 < (unsigned)h, v1 = (unsigned)(i0 + 1) < (unsigned)h;
+  Ax a;
+  a.c = (i0 < -1 ? -1 : (i0 > h - 1 ? h - 1 : i0)) + 1;
+  a.w0 = v0 ? 1.f - fr : 0.f;
+  a.w1 = v1 ? fr : 0.f;
+  a.d0 = v0 ? -1.f : 0.f;
+  a.d1 = v1 ? 1.f : 0.f;
+  return a;
+}
+
+// Diagnostic build only (-DPAIG_DEC_STAMPS, tools/dec_stamps.sh): s_memtime
+// at the phase boundaries of blocks 0-3, every wave, the first 32
+// iterations, stored by lane 0 (vector stores) for tools/dec_stamps.py.
+#ifdef PAIG_DEC_STAMPS
+__device__ unsigned long long paig_dec_stamps[4][16][33][6];
+#define DEC_STAMP(it, ph)                                                                     \
+  do {                                                                                        \
+    if (blockIdx.x < 4 && (threadIdx.x & 63) == 0 && (it) < 33)                               \
+      paig_dec_stamps[blockIdx.x][threadIdx.x >> 6][(it)][(ph)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define DEC_STAMP(it, ph) \
+  do {                    \
+  } while (0)
+#endif
+
+template <int K, int H>
+__global__ void __launch_bounds__((DecCu<K, H>::NT))
+dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
+             float* __restrict__ slab, int F, int Rl, int FPB) {
+  using C = DecCu<K, H>;
+  constexpr int h = C::h, hp = C::hp, hh = C::hh, HW = C::HW, PS = C::PS, NIT = C::NIT, GPITCH = C::GPITCH;
+  constexpr int NT = C::NT, PL = C::PL, NI = C::NI, NC = C::NC, NG = C::NG, TC0 = C::TC0, TG0 = C::TG0, NR = C::NR;
+  __shared__ float4 SRC[K][hp * hp];              // (template + 5, sigmoid(content) x 3), zero border
+  __shared__ float2 G[2][2][K][H * GPITCH];       // [frame parity][plane pair][object][row][slot]
+  __shared__ float4 AXW[2][K][2][H];              // per output column (0) / row (1): tap weights w0, w1 and
+  __shared__ int AXC[2][K][2][H];                 //   their d/dcoord d0, d1; padded index of the first tap
+  __shared__ int J0[3][K][2][h];                  // gather tables (3 frames in flight): first index
+  __shared__ float WT[3][K][2][h][GW];            //   of the 5-wide window and its weights
+  __shared__ double RED[2][2 * K][NR];            // fp64 position-gradient partials (RPW per wave)
+  __shared__ double BC[H];                        // affine_grid base coordinates (fp64, frame-invariant)
+
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  stage_sources<K>(S, h, T, Cn);
-  float bgv[PPT][3], gbg[PPT][3], tn[PPT][3], gsrc[SPT][4];
+  const int R = pos.grp;
+  const bool grouped = R > 0 && Rl > 0 && Rl < R;
+  const int NL = grouped ? (F / R) * Rl : F;
+  // dead frames (steps Rl..R-1 of every sequence): zero position gradients
+  if (grouped) {
+    const long long per = (long long)(R - Rl) * 2 * K, nd = (long long)(F / R) * per;
+    for (long long e = (long long)blockIdx.x * NT + tid; e < nd; e += (long long)gridDim.x * NT) {
+      const long long b = e / per, rem = e % per;
+      dpos[(b * R + Rl + rem / (2 * K)) * 2 * K + rem % (2 * K)] = 0.f;
+    }
+  }
+  const int first = blockIdx.x * FPB;
+  const int nf = first < NL ? (NL - first < FPB ? NL - first : FPB) : 0;
+
+  // ---- frame cursors (wave-uniform)
+  auto cur_at = [&](int n) {
+    DecCursor c;
+    if (grouped) {
+      c.pq = c.tq = n / Rl;
+      c.pr = c.tr = n % Rl;
+      c.f = c.pq * R + c.pr;
+    } else {
+      c.f = n;
+      c.pq = pos.grp > 0 ? n / pos.grp : 0;
+      c.pr = pos.grp > 0 ? n % pos.grp : 0;
+      c.tq = tgt.grp > 0 ? n / tgt.grp : 0;
+      c.tr = tgt.grp > 0 ? n % tgt.grp : 0;
+    }
+    return c;
+  };
+  auto advance = [&](DecCursor c) {
+    if (grouped) {
+      if (++c.pr == Rl) {
+        c.pr = 0;
+        ++c.pq;
+      }
+      c.tq = c.pq;
+      c.tr = c.pr;
+      c.f = c.pq * R + c.pr;
+    } else {
+      ++c.f;
+      if (pos.grp > 0 && ++c.pr == pos.grp) {
+        c.pr = 0;
+        ++c.pq;
+      }
+      if (tgt.grp > 0 && ++c.tr == tgt.grp) {
+        c.tr = 0;
+        ++c.tq;
+      }
+    }
+    return c;
+  };
+  auto pos_of = [&](const DecCursor& c) {
+    return pos.grp > 0 ? pos.p + (long long)c.pq * pos.outer + (long long)c.pr * pos.inner
+                       : pos.p + (long long)c.f * pos.inner;
+  };
+  auto tgt_of = [&](const DecCursor& c) {
+    return tgt.grp > 0 ? tgt.p + (long long)c.tq * tgt.fs + (long long)c.tr * tgt.gs : tgt.p + (long long)c.f * tgt.fs;
+  };
+
+  // ---- prologue: sources, background, frame 0's tables / weight / targets
+  for (int t = tid; t < K * hp * hp; t += NT) {
+    const int k = t / (hp * hp), q = t % (hp * hp), y = q / hp - 1, x = q % hp - 1;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)h) {
+      const int o = y * h + x;
+      v.x = S.tmpl[k * hh + o] + 5.f;
+      v.y = 1.f / (1.f + expf(-S.cont[(k * 3 + 0) * hh + o]));
+      v.z = 1.f / (1.f + expf(-S.cont[(k * 3 + 1) * hh + o]));
+      v.w = 1.f / (1.f + expf(-S.cont[(k * 3 + 2) * hh + o]));
+    }
+    SRC[k][q] = v;
+  }
+  float bgv[PS][3], gbg[PS][3], tn[PS][3];
+  float gsrc[NIT][PL];
 #pragma unroll
-  for (int j = 0; j < PPT; ++j) {
-    const int p = tid + 256 * j;
+  for (int s = 0; s < PS; ++s) {
+    const int p = tid + NT * s;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      bgv[j][c] = (p < HW) ? S.bg[c * HW + p] : 0.f;
-      gbg[j][c] = 0.f;
+      bgv[s][c] = p < HW ? S.bg[c * HW + p] : 0.f;
+      gbg[s][c] = 0.f;
+      tn[s][c] = 0.f;
     }
   }
 #pragma unroll
-  for (int j = 0; j < SPT; ++j)
+  for (int u = 0; u < NIT; ++u)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) gsrc[j][c] = 0.f;
-  auto fetch = [&](int f) {
-    const float* tf = tgt.frame(f);
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-      const int p = tid + 256 * j;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) tn[j][c] = (p < HW) ? tf[c * HW + p] : 0.f;
+    for (int q = 0; q < PL; ++q) gsrc[u][q] = 0.f;
+  for (int j = tid; j < H; j += NT) BC[j] = base_coord(j, H);
+  // this thread's table entry: an axis entry (tid in [TC0, TC0 + NC)) or a
+  // gather entry (tid in [TG0, TG0 + NG)); (ck, cax) = the object / axis
+  // whose position it reads
+  const int tc = tid - TC0, tg = tid - TG0;
+  const bool is_c = tc >= 0 && tc < NC, is_g = tg >= 0 && tg < NG;
+  const int ck = is_c ? tc / (2 * H) : (is_g ? tg / (2 * h) : 0);
+  const int cax = is_c ? (tc / H) & 1 : (is_g ? (tg / h) & 1 : 0);
+  const int cj = is_c ? tc % H : (is_g ? tg % h : 0);
+  // the tables of a frame from this thread's position value l (BC complete)
+  auto tables = [&](float l, int aslot, int gslot_) {
+    if (is_c) {
+      const Ax x = axis(src_coord(BC[cj], (double)(((float)H / 2.f - l) / (float)h), h), h);
+      AXW[aslot][ck][cax][cj] = make_float4(x.w0, x.w1, x.d0, x.d1);
+      AXC[aslot][ck][cax][cj] = x.c;
+    } else if (is_g) {
+      gather_entry(l, BC, H, h, cj, &J0[gslot_][ck][cax][cj], WT[gslot_][ck][cax][cj]);
     }
   };
-  // frames with no loss weight and no dense gradient contribute nothing (the
-  // extrapolation frames of the rollout decode): walk only the live ones
-  auto live = [&](int f) { return (dsse && dsse[f] != 0.f) || dout.p != nullptr; };
-  if ((int)blockIdx.x < F) fetch(blockIdx.x);
-  for (int f = blockIdx.x; f < F; f += gridDim.x) {
-    float tc[PPT][3];
+  auto fetch = [&](const DecCursor& c) {   // targets -> tn (no SSE weight: none read)
+    if (dsse == nullptr) return;
+    const float* tf = tgt_of(c);
 #pragma unroll
-    for (int j = 0; j < PPT; ++j)
+    for (int s = 0; s < PS; ++s) {
+      const int p = tid + NT * s;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) tc[j][c] = tn[j][c];
-    if (f + (int)gridDim.x < F) fetch(f + gridDim.x);
-    const float w_f = dsse ? 2.f * dsse[f] : 0.f;
-    if (!live(f)) {   // uniform across the block
-      if (tid < 2 * K) dpos[(long long)f * 2 * K + tid] = 0.f;
-      continue;
+      for (int ch = 0; ch < 3; ++ch) tn[s][ch] = p < HW ? tf[ch * HW + p] : 0.f;
     }
-    const float* dof = dout.p ? dout.frame(f) : nullptr;
-    __syncthreads();   // previous frame's pass 2 done with G and the tables
-    coord_tables<K>(pos.at(f), H, h, cx, cy, bc);
-    __syncthreads();
-    gather_tables<K, H>(cx, cy, j0, wt);   // read only after the barrier below
-    double sx[K], sy[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) sx[k] = sy[k] = 0.0;
-    // ---- pass 1: per-pixel gradients
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-      const int p = tid + 256 * j;
-      if (p >= HW) break;
-      const int i = p / H, jj = p % H;
-      Taps tp[K];
-      float sv[K][4], sdx[K][4], sdy[K][4], o[3], m[K + 1];
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        tp[k] = make_taps(bil(cx[k][jj], cy[k][i]), h);
-        sample4<true>(T + k * hh, Cn + k * 3 * hh, hh, tp[k], sv[k], sdx[k], sdy[k]);
-      }
-      blend<K>(sv, bgv[j], o, m);
-      float g[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        g[c] = w_f * (o[c] - tc[j][c]);
-        if (dof) g[c] += dof[c * HW + p];
-        gbg[j][c] = fmaf(m[K], g[c], gbg[j][c]);
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float dT = 0.f;
-        float dC[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          dC[c] = m[k] * g[c];
-          dT = fmaf(g[c], sv[k][1 + c] - o[c], dT);
-        }
-        dT *= m[k];
-        G[(k * 4 + 0) * HW + p] = dT;
-        float gx = dT * sdx[k][0], gy = dT * sdy[k][0];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          G[(k * 4 + 1 + c) * HW + p] = dC[c];
-          gx = fmaf(dC[c], sdx[k][1 + c], gx);
-          gy = fmaf(dC[c], sdy[k][1 + c], gy);
-        }
-        sx[k] += (double)gx;
-        sy[k] += (double)gy;
-      }
-    }
-    // ---- per-frame dpos reduction (fp64)
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double a = wave_sum_d(sx[k]), b = wave_sum_d(sy[k]);
-      if (lane == 0) {
-        redd[wv][2 * k] = a;
-        redd[wv][2 * k + 1] = b;
-      }
-    }
-    __syncthreads();   // G, redd and the gather tables complete
-    if (tid < 2 * K) {
-      const double s = (redd[0][tid] + redd[1][tid]) + (redd[2][tid] + redd[3][tid]);
-      const float dth = (float)(s * (double)h * 0.5);
-      dpos[(long long)f * 2 * K + tid] = -dth / (float)h;
-    }
-    // ---- pass 2: gather this thread's source texels from the pixel-gradient image
-#pragma unroll
-    for (int jt = 0; jt < SPT; ++jt) {
-      const int s = tid + 256 * jt;
-      if (s >= K * hh) break;
-      const int k = s / hh, q = s % hh, ys = q / h, xs = q % h;
-      const int i0 = j0[k][1][ys], c0 = j0[k][0][xs];
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int a = 0; a < GW; ++a) {
-        const float wy = wt[k][1][ys][a];
-        if (wy == 0.f) continue;
-        const int row = (i0 + a) * H;
-        float r4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int b = 0; b < GW; ++b) {
-          const float wx = wt[k][0][xs][b];
-          const int col = c0 + b < H ? c0 + b : H - 1;   // weight is 0 past the edge
-#pragma unroll
-          for (int c = 0; c < 4; ++c) r4[c] = fmaf(wx, G[(k * 4 + c) * HW + row + col], r4[c]);
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = fmaf(wy, r4[c], acc[c]);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) gsrc[jt][c] += acc[c];
-    }
+  };
+  auto is_active = [&](float w) { return w != 0.f || dout.p != nullptr; };
+  // cursors: ccur = frame it, c1 = frame it+1, c2 = frame it+2 (clamped to the block's last)
+  DecCursor cprev{}, ccur = cur_at(first < NL ? first : 0);
+  DecCursor c1 = nf > 1 ? advance(ccur) : ccur;
+  DecCursor c2 = nf > 2 ? advance(c1) : c1;
+  float w_cur = 0.f, p0 = 0.f, ppos = 0.f;
+  bool act_cur = false, act_prev = false;
+  if (nf > 0) {
+    p0 = pos_of(ccur)[2 * ck + cax];
+    ppos = pos_of(c1)[2 * ck + cax];
+    w_cur = dsse != nullptr ? uniform_f(dsse[ccur.f]) : 0.f;
+    act_cur = is_active(w_cur);
+    fetch(ccur);
   }
-  // ---- this block's partial source gradients -> its slab row (every element
-  // owned by exactly one thread; written once)
+  __syncthreads();   // BC
+  if (nf > 0) tables(p0, 0, 0);
+  __syncthreads();
+  DEC_STAMP(0, 0);
+
+  for (int it = 0; it <= nf; ++it) {
+    // tables of frame it+1 (its positions arrived during the last iteration),
+    // then the loads of frame it+2's positions and frame it+1's weight
+    // (clamped to a valid frame on the last iterations: issued
+    // unconditionally, so the memory-counter waits stay exact)
+    if (it + 1 < nf) tables(ppos, (it + 1) & 1, (it + 1) % 3);
+    ppos = pos_of(c2)[2 * ck + cax];
+    const float wnext = dsse != nullptr ? dsse[c1.f] : 0.f;
+    DEC_STAMP(it, 1);
+    // ---- pass 2 of frame it-1: source texels gather from G; its position gradients
+    if (it >= 1 && act_prev) {
+      const int sl = (it - 1) & 1, gs = (it - 1) % 3;
+      if (wv < 2 * K) {   // wave e finishes position gradient e from the NR row partials
+        const double v = lane < NR ? RED[sl][wv][lane] : 0.0;
+        const double tot = wave_sum_dpp_d(v);
+        const float dth = (float)(tot * (double)h * 0.5);
+        if (lane == 0) dpos[(long long)cprev.f * 2 * K + wv] = -dth / (float)h;
+      }
+#pragma unroll
+      for (int u = 0; u < NIT; ++u) {
+        const int t = tid + NT * u;
+        if (NIT == 1 || t < NI) {
+          // item t: texel tx = t % (K hh), plane pair hf (PL = 2) or all 4 planes
+          const int tx = t % (K * hh), hf = PL == 2 ? t / (K * hh) : 0;
+          const int k = tx / hh, q = tx % hh, ys = q / h, xs = q % h;
+          const int i0 = J0[gs][k][1][ys], c0 = J0[gs][k][0][xs];
+          float wy[GW], wx[GW];
+#pragma unroll
+          for (int a2 = 0; a2 < GW; ++a2) {
+            wy[a2] = WT[gs][k][1][ys][a2];
+            wx[a2] = WT[gs][k][0][xs][a2];
+          }
+          // columns c0 + b: the even b share c0's parity (consecutive slots
+          // from gslot(c0)), the odd b the other one: every read below is an
+          // immediate offset from one of two bases
+          const int be = i0 * GPITCH + gslot<H>(c0), bo = i0 * GPITCH + gslot<H>(c0 + 1);
+          const float2* ge[2] = {&G[sl][hf][k][be], &G[sl][1][k][be]};
+          const float2* go[2] = {&G[sl][hf][k][bo], &G[sl][1][k][bo]};
+          float acc[PL];
+#pragma unroll
+          for (int q2 = 0; q2 < PL; ++q2) acc[q2] = 0.f;
+#pragma unroll
+          for (int b = 0; b < GW; ++b) {
+            float r[PL];
+#pragma unroll
+            for (int q2 = 0; q2 < PL; ++q2) r[q2] = 0.f;
+#pragma unroll
+            for (int a2 = 0; a2 < GW; ++a2) {   // rows i0 .. i0+4
+              const int o = a2 * GPITCH + (b >> 1);
+              const float2 v = (b & 1) ? go[0][o] : ge[0][o];
+              r[0] = fmaf(wy[a2], v.x, r[0]);
+              r[1] = fmaf(wy[a2], v.y, r[1]);
+              if constexpr (PL == 4) {
+                const float2 v2 = (b & 1) ? go[1][o] : ge[1][o];
+                r[2] = fmaf(wy[a2], v2.x, r[2]);
+                r[3] = fmaf(wy[a2], v2.y, r[3]);
+              }
+            }
+#pragma unroll
+            for (int q2 = 0; q2 < PL; ++q2) acc[q2] = fmaf(wx[b], r[q2], acc[q2]);
+          }
+#pragma unroll
+          for (int q2 = 0; q2 < PL; ++q2) gsrc[u][q2] += acc[q2];
+        }
+      }
+    } else if (it >= 1 && tid < 2 * K) {
+      dpos[(long long)cprev.f * 2 * K + tid] = 0.f;
+    }
+    DEC_STAMP(it, 2);
+    // ---- pass 1 of frame it
+    if (it < nf && act_cur) {
+      const int sl = it & 1;
+      const float w_f = 2.f * w_cur;
+      const float* dof = dout.p ? dout.p + (long long)ccur.f * dout.fs : nullptr;
+      double sx[K], sy[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) sx[k] = sy[k] = 0.0;
+#pragma unroll
+      for (int s = 0; s < PS; ++s) {
+        const int p = tid + NT * s;
+        if (PS > 1 && p >= HW) break;
+        const int i = p / H, j = p % H;
+        // K >= 3: the derivative planes are re-formed from the texels after
+        // the blend instead of being held across it (register budget)
+        constexpr bool HOLD = K < 3;
+        float sv[K][4], sdx[HOLD ? K : 1][4], sdy[HOLD ? K : 1][4];
+        float4 wxa[K], wya[K];
+        int base[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          wxa[k] = AXW[sl][k][0][j];
+          wya[k] = AXW[sl][k][1][i];
+          base[k] = AXC[sl][k][1][i] * hp + AXC[sl][k][0][j];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float4 ax = wxa[k], ay = wya[k];
+          const int bs = base[k];
+          const float4 a = SRC[k][bs], b = SRC[k][bs + 1], c = SRC[k][bs + hp], d = SRC[k][bs + hp + 1];
+          const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+          const float cv[4] = {c.x, c.y, c.z, c.w}, dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float top = fmaf(ax.y, bv[q], ax.x * av[q]), bot = fmaf(ax.y, dv[q], ax.x * cv[q]);
+            sv[k][q] = fmaf(ay.y, bot, ay.x * top);
+            if constexpr (HOLD) {
+              const float dtop = fmaf(ax.w, bv[q], ax.z * av[q]), dbot = fmaf(ax.w, dv[q], ax.z * cv[q]);
+              sdx[k][q] = fmaf(ay.y, dbot, ay.x * dtop);
+              sdy[k][q] = fmaf(ay.w, bot, ay.z * top);
+            }
+          }
+        }
+        float o[3], m[K + 1];
+        blend<K>(sv, bgv[s], o, m);
+        float g[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          g[c] = w_f * (o[c] - tn[s][c]);
+          if (dof) g[c] += dof[c * HW + p];
+          gbg[s][c] = fmaf(m[K], g[c], gbg[s][c]);
+        }
+        const int gof = i * GPITCH + gslot<H>(j);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          float dT = 0.f;
+          float dC[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            dC[c] = m[k] * g[c];
+            dT = fmaf(g[c], sv[k][1 + c] - o[c], dT);
+          }
+          dT *= m[k];
+          G[sl][0][k][gof] = make_float2(dT, dC[0]);
+          G[sl][1][k][gof] = make_float2(dC[1], dC[2]);
+          const float gq[4] = {dT, dC[0], dC[1], dC[2]};
+          float gx = 0.f, gy = 0.f;
+          if constexpr (HOLD) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              gx = fmaf(gq[q], sdx[k][q], gx);
+              gy = fmaf(gq[q], sdy[k][q], gy);
+            }
+          } else {
+            const float4 ax = wxa[k], ay = wya[k];
+            const int bs = base[k];
+            const float4 a = SRC[k][bs], b = SRC[k][bs + 1], c = SRC[k][bs + hp], d = SRC[k][bs + hp + 1];
+            const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+            const float cv[4] = {c.x, c.y, c.z, c.w}, dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float top = fmaf(ax.y, bv[q], ax.x * av[q]), bot = fmaf(ax.y, dv[q], ax.x * cv[q]);
+              const float dtop = fmaf(ax.w, bv[q], ax.z * av[q]), dbot = fmaf(ax.w, dv[q], ax.z * cv[q]);
+              gx = fmaf(gq[q], fmaf(ay.y, dbot, ay.x * dtop), gx);
+              gy = fmaf(gq[q], fmaf(ay.w, bot, ay.z * top), gy);
+            }
+          }
+          sx[k] += (double)gx;
+          sy[k] += (double)gy;
+        }
+      }
+      double sv2[2 * K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        sv2[2 * k] = sx[k];
+        sv2[2 * k + 1] = sy[k];
+      }
+      row_sums_dpp_d<2 * K>(sv2);
+      if constexpr (C::RPW == 2) {
+#pragma unroll
+        for (int e = 0; e < 2 * K; ++e) sv2[e] += __shfl_xor(sv2[e], 16, 64);   // rows 0+1, 2+3
+        if ((lane & 31) == 0)
+#pragma unroll
+          for (int e = 0; e < 2 * K; ++e) RED[sl][e][wv * 2 + (lane >> 5)] = sv2[e];
+      } else {
+        if ((lane & 15) == 0)
+#pragma unroll
+          for (int e = 0; e < 2 * K; ++e) RED[sl][e][wv * 4 + (lane >> 4)] = sv2[e];
+      }
+    }
+    DEC_STAMP(it, 3);
+    // ---- frame it+1: targets (in flight across the barrier and pass 2) and loss weight
+    cprev = ccur;
+    act_prev = act_cur;
+    if (it + 1 < nf) {
+      ccur = c1;
+      c1 = c2;
+      if (it + 3 < nf) c2 = advance(c2);
+      fetch(ccur);
+      w_cur = uniform_f(wnext);
+      act_cur = is_active(w_cur);
+    } else {
+      act_cur = false;
+    }
+    DEC_STAMP(it, 4);
+    __syncthreads();
+    DEC_STAMP(it, 5);
+  }
+  // ---- this block's partial source gradients -> its slab row (each element
+  // owned by exactly one thread, written once)
   float* srow = slab + (long long)blockIdx.x * ((long long)K * hh * 4 + 3LL * HW);
   float* s_tm = srow;
   float* s_ct = srow + K * hh;
   float* s_bg = s_ct + K * 3 * hh;
 #pragma unroll
-  for (int jt = 0; jt < SPT; ++jt) {
-    const int s = tid + 256 * jt;
-    if (s >= K * hh) break;
-    const int k = s / hh, q = s % hh;
-    s_tm[s] = gsrc[jt][0];
+  for (int u = 0; u < NIT; ++u) {
+    const int t = tid + NT * u;
+    if (t < NI) {
+      const int tx = t % (K * hh), pq = PL == 2 ? (t / (K * hh)) * 2 : 0;
+      const int k = tx / hh, q = tx % hh;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) s_ct[(k * 3 + c) * hh + q] = gsrc[jt][1 + c];
+      for (int q2 = 0; q2 < PL; ++q2) {
+        const int pl = pq + q2;   // 0: template, 1..3: content channel pl-1
+        if (pl == 0) s_tm[tx] = gsrc[u][q2];
+        else s_ct[(k * 3 + pl - 1) * hh + q] = gsrc[u][q2];
+      }
+    }
   }
 #pragma unroll
-  for (int j = 0; j < PPT; ++j) {
-    const int p = tid + 256 * j;
-    if (p >= HW) break;
+  for (int s = 0; s < PS; ++s) {
+    const int p = tid + NT * s;
+    if (p < HW)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) s_bg[c * HW + p] = gbg[j][c];
+      for (int c = 0; c < 3; ++c) s_bg[c * HW + p] = gbg[s][c];
   }
 }
 
@@ -886,8 +1208,30 @@ stn_bwd_k(const float* __restrict__ U, const float* __restrict__ th, const float
 
 extern "C" {
 
-// Decoder grid size used by paig_decoder_bwd (the slab has that many rows).
-int paig_decoder_bwd_blocks(int F) {
+// Launch geometry of paig_decoder_bwd: the one-CU-per-block kernel for the
+// headline shapes, the generic kernels otherwise.
+static bool dec_cu_shape(int K, int h, int H) { return H == 2 * h && ((K == 2 && H == 32) || (K == 3 && H == 36)); }
+
+static int dec_live(int F, int grp, int live) {
+  return (grp > 0 && live > 0 && live < grp) ? (F / grp) * live : F;
+}
+
+// frames per block of the one-CU kernel: >= DEC_FPB_MIN (the slab row of a
+// block is ~1.7 frames of targets), at most DEC_CU_MAX_BLOCKS blocks
+static int dec_cu_fpb(int NL) {
+  int fpb = cdiv(NL, DEC_CU_MAX_BLOCKS);
+  return fpb < DEC_FPB_MIN ? DEC_FPB_MIN : fpb;
+}
+
+// Slab rows (= blocks) of paig_decoder_bwd over F frames grouped by grp
+// (0: ungrouped) of which the first `live` per group are processed (0: all).
+int paig_decoder_bwd_blocks(int F, int grp, int live, int K, int h, int H) {
+  if (F <= 0) return 1;
+  if (dec_cu_shape(K, h, H)) {
+    const int NL = dec_live(F, grp, live);
+    const int g = NL > 0 ? cdiv(NL, dec_cu_fpb(NL)) : 1;
+    return g < 1 ? 1 : g;
+  }
   int g = (F + 1) / 2;
   if (g > 768) g = 768;   // ~3 blocks per CU: latency hiding for the per-frame passes
   if (g < 1) g = 1;
@@ -899,9 +1243,10 @@ size_t paig_decoder_slab_len(int K, int h, int H) { return (size_t)K * h * h * 4
 // Global scratch (floats) needed when the per-frame pixel-gradient image does
 // not fit LDS; 0 when it does.
 size_t paig_decoder_bwd_scratch(int F, int K, int h, int H) {
+  if (dec_cu_shape(K, h, H)) return 0;
   size_t lds = ((size_t)K * h * h * 4 + (size_t)K * 4 * H * H) * 4;
   if (lds <= 120 * 1024) return 0;
-  return (size_t)paig_decoder_bwd_blocks(F) * K * 4 * H * H;
+  return (size_t)paig_decoder_bwd_blocks(F, 0, 0, K, h, H) * K * 4 * H * H;
 }
 
 int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
@@ -924,24 +1269,38 @@ int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner,
 int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
                      const float* cont, const float* bg, const float* tgt, long long tgt_fs, int tgt_grp,
                      long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
-                     float* slab, float* scratch, int F, int K, int h, int H, void* stream) {
+                     float* slab, float* scratch, int F, int live, int K, int h, int H, void* stream) {
   if (F <= 0) return 0;
   PAIG_REQUIRE(H == 2 * h, "decoder: H=%d must be 2*tmpl=%d", H, 2 * h);
+  PAIG_REQUIRE(live >= 0 && (live == 0 || pos_grp > 0), "decoder_bwd: live=%d needs grouped frames (pos_grp=%d)", live,
+               pos_grp);
+  PAIG_REQUIRE(pos_grp <= 0 || F % pos_grp == 0, "decoder_bwd: F=%d is not a multiple of the group %d", F, pos_grp);
+  PAIG_REQUIRE(pos_grp <= 0 || tgt_grp == pos_grp || live == 0,
+               "decoder_bwd: target group %d must equal the position group %d", tgt_grp, pos_grp);
   PosView pv{pos, pos_outer, pos_inner, pos_grp};
   Src S{tmpl, cont, bg};
   FView t{tgt, tgt_fs, tgt_gs, tgt_grp};
   FView d{dout, dout_fs, 0, 0};
   hipStream_t st = (hipStream_t)stream;
-  const int g = paig_decoder_bwd_blocks(F);
+  if (dec_cu_shape(K, h, H)) {
+    const int NL = dec_live(F, pos_grp, live);
+    const int fpb = dec_cu_fpb(NL > 0 ? NL : 1);
+    const int g = paig_decoder_bwd_blocks(F, pos_grp, live, K, h, H);
+    const int rl = dec_live(F, pos_grp, live) == F ? 0 : live;
+    if (K == 2)
+      hipLaunchKernelGGL((dec_bwd_cu_k<2, 32>), dim3(g), dim3(DecCu<2, 32>::NT), 0, st, pv, S, t, dsse, d, dpos, slab, F, rl, fpb);
+    else
+      hipLaunchKernelGGL((dec_bwd_cu_k<3, 36>), dim3(g), dim3(DecCu<3, 36>::NT), 0, st, pv, S, t, dsse, d, dpos, slab, F, rl, fpb);
+    PAIG_CHECK_LAUNCH();
+    return 0;
+  }
+  // generic kernels: every frame is walked (dead ones skipped by their zero weight)
+  const int g = paig_decoder_bwd_blocks(F, 0, 0, K, h, H);
   const bool need_scratch = paig_decoder_bwd_scratch(F, K, h, H) > 0;
   PAIG_REQUIRE(!need_scratch || scratch, "decoder_bwd: scratch required");
   const int lds = (K * h * h * 4 + (need_scratch ? 0 : K * 4 * H * H)) * 4;
   float* gs = need_scratch ? scratch : nullptr;
-  if (K == 2 && H == 32 && !need_scratch)
-    hipLaunchKernelGGL((dec_bwd_reg_k<2, 32>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, F);
-  else if (K == 3 && H == 36 && !need_scratch)
-    hipLaunchKernelGGL((dec_bwd_reg_k<3, 36>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, F);
-  else if (K == 2)
+  if (K == 2)
     hipLaunchKernelGGL((dec_bwd_k<2>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);
   else if (K == 3)
     hipLaunchKernelGGL((dec_bwd_k<3>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);
@@ -998,3 +1357,9 @@ int paig_stn_bwd(const float* U, const float* theta, const float* dout, float* d
 }
 
 }  // extern "C"
+
+#ifdef PAIG_DEC_STAMPS
+extern "C" int paig_dec_stamps_read(void* host, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(paig_dec_stamps), bytes);
+}
+#endif

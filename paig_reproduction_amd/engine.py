@@ -315,13 +315,20 @@ class Engine:
         return self.CONV_MATH[m]
 
     @staticmethod
-    def _dec_bytes(n, lay, bwd, slab_floats=0):
-        """Algorithmic HBM bytes of one decoder launch over n frames: the
-        target frames read (fused SSE) and the decoded frames written (fwd) /
-        the position grads and partial source-grad slab rows written (bwd);
+    def _dec_bytes(n, lay):
+        """Algorithmic HBM bytes of one decoder forward over n frames: the
+        target frames read (fused SSE) and the decoded frames written;
         positions and the step-constant sources (< 100 KB) are negligible."""
-        frames = n * lay.frame * 4
-        return frames + (n * 2 * lay.D * 4 + slab_floats * 4 if bwd else frames)
+        return 2 * n * lay.frame * 4
+
+    @staticmethod
+    def _dec_bwd_bytes(live, n, lay, dense):
+        """Algorithmic HBM bytes of one decoder backward: the targets of the
+        `live` frames that carry a loss weight (+ their dense dL/dout when
+        given) read, the position gradients of all n frames and the source
+        gradients (one slab_len vector) written.  The partial-gradient slab
+        rows are the kernel's own overhead, not algorithmic."""
+        return live * lay.frame * 4 * (2 if dense else 1) + n * 2 * lay.D * 4 + (4 * lay.K * lay.h * lay.h + 3 * lay.HW) * 4
 
     def _p(self, tag, flops=0, nbytes=0):
         """Probe context of one launch: algorithmic FLOPs and HBM bytes (the
@@ -445,7 +452,7 @@ class Engine:
                                   for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
                              _parr([ptr(src[nm][0]) for nm, _, _ in vf]), _parr([ptr(src[nm][1]) for nm, _, _ in vf]),
                              _parr([ptr(src[nm][2]) for nm, _, _ in vf]), _iarr([P for _, P, _ in vf]), st)
-        with self._p("dec_fwd:recon", 0, self._dec_bytes(F, lay, False)):
+        with self._p("dec_fwd:recon", 0, self._dec_bytes(F, lay)):
             L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons), lay.frame,
                                x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, st)
         self._join(dev)
@@ -454,7 +461,7 @@ class Engine:
         out = _empty(B * lay.R * lay.frame, dev)
         sse_roll = _empty(B * lay.R, dev)
         tgt_roll = (ptr(x) + lay.ins * lay.frame * 4, T * lay.frame, lay.R, lay.frame)
-        with self._p("dec_fwd:rollout", 0, self._dec_bytes(B * lay.R, lay, False)):
+        with self._p("dec_fwd:rollout", 0, self._dec_bytes(B * lay.R, lay)):
             L.paig_decoder_fwd(ptr(pvs) + 2 * D * 4, (lay.R + 1) * 2 * D, 2 * D, lay.R, ptr(tmpl), ptr(cont),
                                ptr(bgp), ptr(out), lay.frame, *tgt_roll, ptr(sse_roll), B * lay.R, K, h, H, st)
         S["tgt_roll"] = tgt_roll
@@ -639,8 +646,13 @@ class Engine:
         return dt, None, None
 
     # -- backward --------------------------------------------------------
-    def backward(self, S, d_sse_rec=None, d_sse_roll=None, d_out=None, d_recons=None, d_enc_pos=None, d_pvs=None):
-        """Writes every live parameter gradient into the model's flat grad buffer."""
+    def backward(self, S, d_sse_rec=None, d_sse_roll=None, d_out=None, d_recons=None, d_enc_pos=None, d_pvs=None,
+                 roll_live=0):
+        """Writes every live parameter gradient into the model's flat grad buffer.
+        roll_live > 0: only the first roll_live rollout steps of every
+        sequence have a loss weight (the others' d_sse_roll entries are zero
+        and there is no dense d_out): the rollout decoder backward reads only
+        those frames."""
         lay = S["lay"]
         L = self.L
         x = S["x"]
@@ -661,8 +673,10 @@ class Engine:
         # ---- buffers of the whole decoder / rollout / velocity backward (all
         # allocated on the main stream before the fork below)
         slab_len = int(L.paig_decoder_slab_len(K, h, H))
-        nb_rec = L.paig_decoder_bwd_blocks(F)
-        nb_roll = L.paig_decoder_bwd_blocks(B * R)
+        roll_live = roll_live if (d_out is None and 0 < roll_live < R) else 0
+        S["roll_live"] = roll_live
+        nb_rec = L.paig_decoder_bwd_blocks(F, 0, 0, K, h, H)
+        nb_roll = L.paig_decoder_bwd_blocks(B * R, R, roll_live, K, h, H)
         slab = _empty((nb_rec + nb_roll) * slab_len, dev)
         scr_n = max(L.paig_decoder_bwd_scratch(F, K, h, H), L.paig_decoder_bwd_scratch(B * R, K, h, H))
         scratch = _empty(scr_n, dev) if scr_n else None
@@ -684,10 +698,11 @@ class Engine:
         vparts = [_empty(L.paig_vfn_bwd_blocks(P) * 200, dev) for _, P, _, _ in vfn]
 
         # ---- (main) rollout-frame decoder backward: d rollout positions + partial source grads
-        with self._p("dec_bwd:rollout", 0, self._dec_bytes(B * R, lay, True, nb_roll * slab_len)):
+        live_frames = B * roll_live if roll_live else B * R
+        with self._p("dec_bwd:rollout", 0, self._dec_bwd_bytes(live_frames, B * R, lay, d_out is not None)):
             L.paig_decoder_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
                                *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
-                               ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, K, h, H, st)
+                               ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, roll_live, K, h, H, st)
 
         # the side chain's inputs exist before the fork (a temporary made after
         # it could be recycled by a main-stream allocation while the side
@@ -718,10 +733,10 @@ class Engine:
                 S["extra_slabs"].append((vslab, vblk, vlen, g0))
 
         # ---- (main) reconstruction decoder backward, source-grad reduction, VFN backward
-        with self._p("dec_bwd:recon", 0, self._dec_bytes(F, lay, True, nb_rec * slab_len)):
+        with self._p("dec_bwd:recon", 0, self._dec_bwd_bytes(F, F, lay, d_recons is not None)):
             L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
-                               ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, K, h,
-                               H, st)
+                               ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, 0, K,
+                               h, H, st)
         L.paig_slab_reduce_multi(1, (ctypes.c_void_p * 1)(ptr(slab)), (ctypes.c_int * 1)(nb_rec + nb_roll),
                                  (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, st)
         if d_enc_pos is not None:

@@ -162,11 +162,22 @@ class FlatParams:
     def begin_backward(self):
         """Returns True if gradients must accumulate (grads not zeroed since the
         last backward, the torch semantics the reference relies on)."""
-        acc = any(p.grad is not None for _, p in self._params())
+        params = self._params()
+        acc = any(p.grad is not None for _, p in params)
         if acc:
             self._redirect = (torch.empty_like(self.g32), torch.empty_like(self.g64))
             self._redirect[1].zero_()
+            # a parameter whose grad is None gets this backward's gradient, not
+            # that plus whatever its slot still holds from before zero_grad
+            for n, p in params:
+                if p.grad is None:
+                    self.slot(n).zero_()
         return acc
+
+    def slot(self, name):
+        """The flat gradient slot of a parameter (1-D view)."""
+        kind, off, num, _ = self.index[name]
+        return (self.g32 if kind == 32 else self.g64)[off:off + num]
 
     def end_backward(self, accumulated, none_prefixes=()):
         if accumulated:
@@ -247,7 +258,8 @@ class FlatOptimizer:
         self.param_groups = [{"params": [p for _, p in model._flat._params()], "lr": lr, **hp}]
         self.hp = hp
         self.state = {}
-        self.steps = 0
+        self.steps = 0        # steps taken by every parameter (the fused path)
+        self._psteps = None   # per-parameter steps once a step skipped some (grad None), as torch counts them
         self._bufs = None
 
     def _ensure_state(self):
@@ -260,6 +272,7 @@ class FlatOptimizer:
             else:
                 self._bufs = (z32(), z64())
             self.steps = 0
+            self._psteps = None
 
     def zero_grad(self, set_to_none=True):
         for _, p in self.model._flat._params():
@@ -274,43 +287,87 @@ class FlatOptimizer:
         flat.ensure()
         self._ensure_state()
         flat.allreduce_grads()
+        params = flat._params()
+        have = [p.grad is not None for _, p in params]
+        if all(have) and self._psteps is None:
+            # every parameter has a gradient and the same step count: one
+            # fused launch per dtype over the whole flat buffers
+            self.steps += 1
+            if self.kind == "rmsprop":   # both dtypes in one launch
+                a, eps = self.hp.get("alpha", 0.99), self.hp.get("eps", 1e-8)
+                lib().paig_rmsprop_mixed(ptr(flat.p32), ptr(flat.g32), ptr(self._bufs[0]), flat.n32, ptr(flat.p64),
+                                         ptr(flat.g64), ptr(self._bufs[1]) if flat.n64 else None, flat.n64,
+                                         float(self.param_groups[0]["lr"]), a, eps, stream_handle(flat.p32.device))
+                return None
+            self._launch(32, 0, flat.n32, self.steps)
+            if flat.n64:
+                self._launch(64, 0, flat.n64, self.steps)
+            return None
+        # torch semantics: a parameter whose grad is None is skipped (no
+        # update, no state change, no step count)
+        if self._psteps is None:
+            self._psteps = {n: self.steps for n, _ in params}
+        for (n, _), h in zip(params, have):
+            if h:
+                self._psteps[n] += 1
+                kind, off, num, _ = flat.index[n]
+                self._launch(kind, off, num, self._psteps[n])
+        if len(set(self._psteps.values())) == 1:   # back in lockstep: the fused path again
+            self.steps = next(iter(self._psteps.values()))
+            self._psteps = None
+        return None
+
+    def _launch(self, kind, off, num, step):
+        """The update of flat elements [off, off + num) of one dtype."""
+        flat = self.model._flat
         L = lib()
         st = stream_handle(flat.p32.device)
         lr = float(self.param_groups[0]["lr"])
-        self.steps += 1
-        n32, n64 = flat.n32, flat.n64
+        e32, e64 = 4 * off, 8 * off
+
+        def at(t, e):
+            return ptr(t) + e if t is not None else None
+
         if self.kind == "rmsprop":
             a, eps = self.hp.get("alpha", 0.99), self.hp.get("eps", 1e-8)
-            # one launch for both buffers (fp32 hyper-parameters rounded as torch's fp32 math does)
-            L.paig_rmsprop_mixed(ptr(flat.p32), ptr(flat.g32), ptr(self._bufs[0]), n32, ptr(flat.p64),
-                                 ptr(flat.g64), ptr(self._bufs[1]) if n64 else None, n64, lr, a, eps, st)
+            # one launch for both dtypes when called for the whole buffers
+            # (fp32 hyper-parameters rounded as torch's fp32 math does)
+            if kind == 32:
+                L.paig_rmsprop_mixed(at(flat.p32, e32), at(flat.g32, e32), at(self._bufs[0], e32), num, None, None,
+                                     None, 0, lr, a, eps, st)
+            else:
+                L.paig_rmsprop_mixed(None, None, None, 0, at(flat.p64, e64), at(flat.g64, e64), at(self._bufs[1], e64),
+                                     num, lr, a, eps, st)
         elif self.kind == "adam":
             b1, b2 = self.hp.get("betas", (0.9, 0.999))
             eps = self.hp.get("eps", 1e-8)
-            bc1 = 1 - b1 ** self.steps
-            bc2s = math.sqrt(1 - b2 ** self.steps)
-            L.paig_adam_f32(ptr(flat.p32), ptr(flat.g32), ptr(self._bufs[0]), ptr(self._bufs[1]), n32, lr, b1, b2,
-                            eps, bc1, bc2s, st)
-            if n64:
-                L.paig_adam_f64(ptr(flat.p64), ptr(flat.g64), ptr(self._bufs[2]), ptr(self._bufs[3]), n64, lr, b1,
-                                b2, eps, bc1, bc2s, st)
+            bc1 = 1 - b1 ** step
+            bc2s = math.sqrt(1 - b2 ** step)
+            if kind == 32:
+                L.paig_adam_f32(at(flat.p32, e32), at(flat.g32, e32), at(self._bufs[0], e32), at(self._bufs[1], e32),
+                                num, lr, b1, b2, eps, bc1, bc2s, st)
+            else:
+                L.paig_adam_f64(at(flat.p64, e64), at(flat.g64, e64), at(self._bufs[2], e64), at(self._bufs[3], e64),
+                                num, lr, b1, b2, eps, bc1, bc2s, st)
         else:  # sgd / momentum
             mom = self.hp.get("momentum", 0.0)
-            b32 = self._bufs[0] if mom else None
-            b64 = self._bufs[1] if mom else None
-            first = int(self.steps == 1)
-            L.paig_sgd_f32(ptr(flat.p32), ptr(flat.g32), ptr(b32), n32, lr, mom, first, st)
-            if n64:
-                L.paig_sgd_f64(ptr(flat.p64), ptr(flat.g64), ptr(b64), n64, lr, mom, first, st)
-        return None
+            first = int(step == 1)
+            if kind == 32:
+                L.paig_sgd_f32(at(flat.p32, e32), at(flat.g32, e32), at(self._bufs[0], e32) if mom else None, num, lr,
+                               mom, first, st)
+            else:
+                L.paig_sgd_f64(at(flat.p64, e64), at(flat.g64, e64), at(self._bufs[1], e64) if mom else None, num, lr,
+                               mom, first, st)
 
     def state_dict(self):
-        return {"kind": self.kind, "steps": self.steps, "param_groups": [
+        return {"kind": self.kind, "steps": self.steps, "psteps": None if self._psteps is None else dict(self._psteps),
+                "param_groups": [
             {k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
             "bufs": [b.detach().cpu() for b in (self._bufs or ())]}
 
     def load_state_dict(self, sd):
         self.steps = sd["steps"]
+        self._psteps = dict(sd["psteps"]) if sd.get("psteps") else None
         for g, s in zip(self.param_groups, sd["param_groups"]):
             g.update(s)
         if sd.get("bufs"):

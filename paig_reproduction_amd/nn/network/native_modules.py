@@ -285,7 +285,7 @@ class _STDecoder(torch.autograd.Function):
         N = pos.shape[0]
         dout = dout.float().contiguous()
         slab_len = int(L.paig_decoder_slab_len(K, h, H))
-        nb = L.paig_decoder_bwd_blocks(N)
+        nb = L.paig_decoder_bwd_blocks(N, 0, 0, K, h, H)
         slab = torch.empty(nb * slab_len, device=dev)
         scr_n = L.paig_decoder_bwd_scratch(N, K, h, H)
         scratch = torch.empty(scr_n, device=dev) if scr_n else None
@@ -293,7 +293,7 @@ class _STDecoder(torch.autograd.Function):
         # no target frames: the SSE weight is null and dL/dout comes dense
         # (the target pointer must still address N valid frames; dout does)
         L.paig_decoder_bwd(ptr(pos), 0, 2 * K, 0, ptr(srcs["tmpl"]), ptr(srcs["cont"]), ptr(srcs["bg"]), ptr(dout),
-                           3 * H * H, 0, 0, None, ptr(dout), 3 * H * H, ptr(dpos), ptr(slab), ptr(scratch), N, K, h, H,
+                           3 * H * H, 0, 0, None, ptr(dout), 3 * H * H, ptr(dpos), ptr(slab), ptr(scratch), N, 0, K, h, H,
                            st)
         dsrc = torch.empty(slab_len, device=dev)
         L.paig_slab_reduce(ptr(slab), nb, slab_len, slab_len, ptr(dsrc), 0, st)

@@ -66,7 +66,8 @@ class _PhysicsStep(torch.autograd.Function):
             raise RuntimeError("PhysicsNet step was run without saving activations")
         flat = ctx.engine.model._flat
         acc = flat.begin_backward()
-        ctx.engine.backward(ctx.S, d_sse_rec, d_sse_roll, d_out, d_rec, d_enc, d_pvs)
+        live = getattr(d_sse_roll, "_paig_live_steps", 0) if d_out is None else 0
+        ctx.engine.backward(ctx.S, d_sse_rec, d_sse_roll, d_out, d_rec, d_enc, d_pvs, roll_live=live)
         # nothing reached the rollout branch (quirk Q1: the loss read a stale
         # output): the velocity encoder and physics parameters are not in the
         # graph, so like torch they get grad None (their flat slots hold zeros)
@@ -99,6 +100,13 @@ class _LossReduce(torch.autograd.Function):
         wroll = torch.empty(B * R, device=ctx.dev)
         lib().paig_loss_bwd(ptr(dt), ptr(de), ptr(dr), ae, ptr(wrec), ptr(wroll), B, Te, R, pred,
                             stream_handle(ctx.dev))
+        if de is None:
+            # no extrapolation loss in the graph: only the first pred steps of
+            # every sequence carry a weight (physics_models.py:129-139), so the
+            # rollout decoder backward walks those frames only.  A gradient
+            # that autograd accumulates with another one loses the mark and
+            # falls back to every frame.
+            wroll._paig_live_steps = pred
         return wrec, wroll, None, None, None, None, None
 
 

@@ -50,7 +50,9 @@ def test_library_loads_and_exports_every_symbol():
     assert L.paig_abi_version() == 1
     # size queries are host-only and safe without a GPU
     assert L.paig_decoder_slab_len(2, 16, 32) == 2 * 16 * 16 * 4 + 3 * 32 * 32
-    assert L.paig_decoder_bwd_blocks(1600) >= 1
+    assert L.paig_decoder_bwd_blocks(1600, 0, 0, 2, 16, 32) >= 1
+    # live rollout frames only: 100 sequences x 6 of 46 steps, >= 4 frames per block
+    assert L.paig_decoder_bwd_blocks(4600, 46, 6, 2, 16, 32) == 150
     assert L.paig_vfn_bwd_blocks(3072) == 384
 
 

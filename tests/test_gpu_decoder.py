@@ -1,0 +1,170 @@
+"""Decoder backward (paig_decoder_bwd) vs autograd through the oracle's
+restatement of conv_st_decoder (nn/network/physics_models.py:151-199,
+stn.py:5-16: affine_grid in fp64 from the fp32 translation, grid_sample in
+fp32, softmax compositing), on the CPU in fp32, at each instantiated shape:
+
+  * ungrouped frames (the reconstruction decode), ragged counts;
+  * grouped frames with only the first `live` steps of every sequence
+    weighted (the rollout decode in training, physics_models.py:129-139):
+    the dead steps' position gradients must come back 0 (the buffer is
+    pre-filled with NaN) and their target frames are never read (NaN there);
+  * a dense dL/dout and no SSE weight (the standalone conv_st_decoder).
+
+Bar: 1e-4 normwise (north star) on dpos and on every source gradient."""
+import types
+
+import pytest
+import torch
+
+from helpers import rel_err
+from oracle import physics_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+SHAPES = [(2, 32), (3, 36), (2, 64)]
+
+
+def L():
+    from paig_reproduction_amd._lib import lib
+    return lib()
+
+
+def _sources(K, H, seed):
+    g = torch.Generator().manual_seed(seed)
+    h = H // 2
+    tmpl = torch.randn(K, 1, h, h, generator=g) * 2.0
+    cont = torch.randn(K, 3, h, h, generator=g)
+    bg = torch.sigmoid(torch.randn(1, 3, H, H, generator=g))
+    return tmpl, cont, bg
+
+
+def _positions(n, K, H, seed):
+    g = torch.Generator().manual_seed(seed)
+    # mostly inside the frame, some partly or fully outside (zero padding)
+    return (torch.rand(n, 2 * K, generator=g) * 1.5 - 0.25) * H
+
+
+def _reference(K, H, tmpl, cont, bg, pos, tgt, w, dout):
+    """Autograd of sum_f w_f ||out_f - tgt_f||^2 + <dout, out> (fp32, CPU)."""
+    cfg = types.SimpleNamespace(n_objs=K, tmpl=H // 2, size=H)
+    t = tmpl.clone().requires_grad_(True)
+    sc = torch.sigmoid(cont).requires_grad_(True)
+    b = bg.clone().requires_grad_(True)
+    p = pos.clone().requires_grad_(True)
+    joint = torch.cat([t.repeat(1, 3, 1, 1) + 5, sc], 1)
+    out = O.st_decoder(cfg, joint, b, p)
+    loss = 0.0
+    if w is not None:
+        loss = loss + (w.view(-1, 1, 1, 1) * (out - tgt) ** 2).sum()
+    if dout is not None:
+        loss = loss + (out * dout).sum()
+    loss.backward()
+    return p.grad, t.grad.reshape(-1), sc.grad.reshape(-1), b.grad.reshape(-1)
+
+
+def _run(K, H, tmpl, cont, bg, pos_t, pos_view, tgt_t, tgt_view, w, dout, F_, live):
+    """paig_decoder_bwd + the slab reduction on the device; returns
+    (dpos [F, 2K], d template, d sigmoid(content), d background)."""
+    h = H // 2
+    lib = L()
+    st = torch.cuda.current_stream().cuda_stream
+    td, cd, bd = tmpl.to(DEV).contiguous(), cont.to(DEV).contiguous(), bg.to(DEV).contiguous()
+    slab_len = int(lib.paig_decoder_slab_len(K, h, H))
+    grp = pos_view[3]
+    nb = lib.paig_decoder_bwd_blocks(F_, grp, live, K, h, H)
+    slab = torch.full((nb * slab_len,), float("nan"), device=DEV)
+    scr_n = lib.paig_decoder_bwd_scratch(F_, K, h, H)
+    scratch = torch.empty(scr_n, device=DEV) if scr_n else None
+    dpos = torch.full((F_, 2 * K), float("nan"), device=DEV)
+    wd = w.to(DEV) if w is not None else None
+    dd = dout.to(DEV).contiguous() if dout is not None else None
+    rc = lib.paig_decoder_bwd(pos_view[0], pos_view[1], pos_view[2], pos_view[3], td.data_ptr(), cd.data_ptr(),
+                              bd.data_ptr(), tgt_view[0], tgt_view[1], tgt_view[2], tgt_view[3],
+                              None if wd is None else wd.data_ptr(), None if dd is None else dd.data_ptr(),
+                              3 * H * H, dpos.data_ptr(), slab.data_ptr(),
+                              None if scratch is None else scratch.data_ptr(), F_, live, K, h, H, st)
+    assert rc == 0, lib.paig_last_error()
+    dsrc = torch.empty(slab_len, device=DEV)
+    assert lib.paig_slab_reduce(slab.data_ptr(), nb, slab_len, slab_len, dsrc.data_ptr(), 0, st) == 0
+    torch.cuda.synchronize()
+    del pos_t, tgt_t
+    ds = dsrc.cpu()
+    return dpos.cpu(), ds[:K * h * h], ds[K * h * h:4 * K * h * h], ds[4 * K * h * h:]
+
+
+def _check(got, ref, what):
+    names = ("dpos", "d_template", "d_content", "d_background")
+    for a, b, n in zip(got, ref, names):
+        e = rel_err(a, b)
+        assert e <= 1e-4, f"{what}: {n} rel err {e:.3g}"
+
+
+@pytest.mark.parametrize("K,H", SHAPES)
+@pytest.mark.parametrize("F_", [1, 7, 37])
+def test_decoder_bwd_ungrouped(K, H, F_):
+    tmpl, cont, bg = _sources(K, H, 10 * K + H)
+    pos = _positions(F_, K, H, F_)
+    g = torch.Generator().manual_seed(99 + F_)
+    tgt = torch.rand(F_, 3, H, H, generator=g)
+    w = torch.rand(F_, generator=g) + 0.1
+    pd, td = pos.to(DEV).contiguous(), tgt.to(DEV).contiguous()
+    got = _run(K, H, tmpl, cont, bg, pd, (pd.data_ptr(), 0, 2 * K, 0), td, (td.data_ptr(), 3 * H * H, 0, 0), w,
+               None, F_, 0)
+    _check(got, _reference(K, H, tmpl, cont, bg, pos, tgt, w, None), f"K={K} H={H} F={F_}")
+
+
+@pytest.mark.parametrize("K,H", SHAPES)
+@pytest.mark.parametrize("B,R,live", [(5, 9, 3), (3, 46, 6), (2, 4, 4), (9, 16, 12)])
+def test_decoder_bwd_live_steps(K, H, B, R, live):
+    """The rollout layout of the engine: positions pvs[B][R+1][2K] from step
+    1, targets input[B][T][3][H][W] from frame ins; only steps < live carry
+    a loss weight.  Dead targets are NaN: any read of them would show."""
+    ins, T = 2, R + 2
+    tmpl, cont, bg = _sources(K, H, 7 * K + H + R)
+    g = torch.Generator().manual_seed(B * 100 + R)
+    pvs = torch.zeros(B, R + 1, 2 * K)
+    pvs[:, 1:] = _positions(B * R, K, H, B + R).view(B, R, 2 * K)
+    x = torch.rand(B, T, 3, H, H, generator=g)
+    if live < R:
+        x[:, ins + live:] = float("nan")
+    w = torch.zeros(B, R)
+    w[:, :live] = torch.rand(B, live, generator=g) + 0.1
+    pd, xd = pvs.to(DEV).contiguous(), x.to(DEV).contiguous()
+    fr = 3 * H * H
+    got = _run(K, H, tmpl, cont, bg, pd, (pd.data_ptr() + 2 * K * 4, (R + 1) * 2 * K, 2 * K, R), xd,
+               (xd.data_ptr() + ins * fr * 4, T * fr, R, fr), w.reshape(-1), None, B * R, live if live < R else 0)
+    assert torch.isfinite(got[0]).all(), "dead-step position gradients not written"
+    if live < R:
+        assert (got[0].view(B, R, 2 * K)[:, live:] == 0).all()
+    pos = pvs[:, 1:].reshape(B * R, 2 * K)
+    tgt = torch.nan_to_num(x[:, ins:].reshape(B * R, 3, H, H), nan=0.0)
+    _check(got, _reference(K, H, tmpl, cont, bg, pos, tgt, w.reshape(-1), None), f"K={K} H={H} B={B} R={R} live={live}")
+
+
+@pytest.mark.parametrize("K,H", SHAPES)
+def test_decoder_bwd_dense(K, H):
+    F_ = 11
+    tmpl, cont, bg = _sources(K, H, 3 * K + H)
+    pos = _positions(F_, K, H, 5)
+    dout = torch.randn(F_, 3, H, H, generator=torch.Generator().manual_seed(4))
+    pd, dd = pos.to(DEV).contiguous(), dout.to(DEV).contiguous()
+    # no SSE weight: the target pointer is never read (the dense grads stand in)
+    got = _run(K, H, tmpl, cont, bg, pd, (pd.data_ptr(), 0, 2 * K, 0), dd, (dd.data_ptr(), 3 * H * H, 0, 0), None,
+               dout, F_, 0)
+    _check(got, _reference(K, H, tmpl, cont, bg, pos, None, None, dout), f"dense K={K} H={H}")
+
+
+def test_decoder_bwd_deterministic():
+    """Two launches give bit-identical results (fixed reduction order)."""
+    K, H, F_ = 2, 32, 600
+    tmpl, cont, bg = _sources(K, H, 1)
+    pos = _positions(F_, K, H, 2)
+    g = torch.Generator().manual_seed(3)
+    tgt, w = torch.rand(F_, 3, H, H, generator=g), torch.rand(F_, generator=g)
+    pd, td = pos.to(DEV).contiguous(), tgt.to(DEV).contiguous()
+    args = (K, H, tmpl, cont, bg, pd, (pd.data_ptr(), 0, 2 * K, 0), td, (td.data_ptr(), 3 * H * H, 0, 0), w, None,
+            F_, 0)
+    a, b = _run(*args), _run(*args)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

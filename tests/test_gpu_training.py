@@ -221,3 +221,76 @@ def test_optimizer_matches_torch(kind):
     for k, p in named.items():
         e = rel_err(p.detach(), ref[k].detach())
         assert e <= 2e-6, (kind, k, e)   # Adam's sqrt / bias correction round differently by an ulp
+
+
+@pytest.mark.parametrize("kind", ["rmsprop", "adam", "momentum"])
+def test_optimizer_skips_params_without_grad(kind):
+    """torch semantics after zero_grad(set_to_none=True): a full
+    step, zero_grad, then a standalone encoder backward (only the encoder's
+    parameters get gradients) and optimizer.step(): exactly the encoder's
+    parameters move, as torch.optim moves them from the same gradients and
+    state; every other parameter (whose flat gradient slot still holds the
+    previous step's values) stays put.  Then a fused step accumulates onto
+    the encoder grads only."""
+    dev = torch.device("cuda:0")
+    from helpers import load_golden
+    z = load_golden("spring_s12")
+    m = _model(z, dev)
+    m.build_optimizer(1e-3, kind, True)
+    x = _x(z["input_u8"], dev)
+    make = {"adam": lambda ps: torch.optim.Adam(ps, lr=1e-3), "rmsprop": lambda ps: torch.optim.RMSprop(ps, lr=1e-3),
+            "momentum": lambda ps: torch.optim.SGD(ps, momentum=0.9, lr=1e-3)}[kind]
+    # step 1: full backward (every live parameter has a gradient)
+    m.output = m(x)
+    tl, _ = m.compute_loss()
+    m.optimizer.zero_grad(set_to_none=True)
+    tl.backward()
+    torch.cuda.synchronize()
+    named = {k: p for k, p in m.named_parameters() if p.grad is not None}
+    ref = {k: torch.nn.Parameter(p.detach().clone()) for k, p in named.items()}
+    for k, p in ref.items():
+        p.grad = named[k].grad.detach().clone()
+    topt = make(list(ref.values()))
+    topt.step()
+    m.optimizer.step()
+    # step 2: standalone encoder call, only encoder.* get gradients
+    m.optimizer.zero_grad(set_to_none=True)
+    topt.zero_grad(set_to_none=True)
+    frames = x[:, :m.input_steps + m.pred_steps].reshape(-1, 3, 32, 32)
+    pos, _, _ = m.encoder(frames)
+    pos.sum().backward()
+    torch.cuda.synchronize()
+    enc = [k for k, p in named.items() if p.grad is not None]
+    assert enc and all(k.startswith("encoder.") for k in enc)
+    assert all(named[k].grad is None for k in named if not k.startswith("encoder."))
+    for k in enc:
+        ref[k].grad = named[k].grad.detach().clone()
+    before = {k: p.detach().clone() for k, p in named.items()}
+    topt.step()
+    m.optimizer.step()
+    torch.cuda.synchronize()
+    for k, p in named.items():
+        if k in enc:
+            assert rel_err(p.detach(), ref[k].detach()) <= 2e-6, (kind, k)
+        else:
+            assert torch.equal(p.detach(), before[k]), f"{kind}: {k} moved without a gradient"
+    # step 3: a fused step onto the encoder's accumulated grads: the others
+    # start from zero, not from their stale slots
+    g_enc = {k: named[k].grad.detach().clone() for k in enc}
+    m.output = m(x)
+    tl, _ = m.compute_loss()
+    tl.backward()
+    torch.cuda.synchronize()
+    m2 = _model(z, dev)
+    with torch.no_grad():
+        for (k, p), (k2, p2) in zip(m.named_parameters(), m2.named_parameters()):
+            p2.copy_(p)
+    m2.build_optimizer(1e-3, kind, True)
+    m2.output = m2(x)
+    tl2, _ = m2.compute_loss()
+    tl2.backward()
+    torch.cuda.synchronize()
+    named2 = dict(m2.named_parameters())
+    for k in named:
+        want = named2[k].grad + (g_enc[k] if k in g_enc else 0)
+        assert rel_err(named[k].grad, want) <= 1e-6, (kind, k)

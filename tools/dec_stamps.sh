@@ -1,0 +1,11 @@
+#!/bin/bash
+# Diagnostic build of the decoder backward with s_memtime phase stamps
+# (-DPAIG_DEC_STAMPS) linked with the other objects into build/libpaig_stamps.so.
+set -e
+cd "$(dirname "$0")/../paig_reproduction_amd/csrc"
+make -s
+mkdir -p build/stamps diag
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DPAIG_DEC_STAMPS -c decoder.hip -o build/stamps/decoder.o
+objs=$(for f in *.hip; do b=${f%.hip}; [ "$b" != decoder ] && echo build/$b.o; done)
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o diag/libpaig_stamps.so $objs build/stamps/decoder.o
+echo built diag/libpaig_stamps.so
