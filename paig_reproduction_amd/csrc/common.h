@@ -99,13 +99,11 @@ __device__ __forceinline__ void f16_range_note(float rmax) {
 int paig_f16_range_conv(int clear);
 int paig_f16_range_gemm(int clear);
 
-// fixed power-of-two scale of the weights in the split-precision convs: f16
-// keeps 22 significant bits for |w| >= 2^-(3 + 8) and overflows at 2^(16 - 8)
-// (range-guarded); per-block weight maxima cost a serial pass per launch
-#define PAIG_W_EXP 8
-// the same for activations (values bounded by construction: ReLU'd conv
-// outputs of [0, 1] frames, masked objects): full f16 precision for
-// |a| >= 2^-11, a range-flagged overflow at 2^8; gradients get dynamic scales
+// fixed power-of-two scale of the fallback paths (a conv weight gradient
+// without the forward's recorded X maximum, GEMM math 4 / 5's fixed operand):
+// full f16 precision for |v| >= 2^-11, a range-flagged overflow at 2^8.  The
+// training step scales every operand dynamically (per tile, per output
+// channel, running per block) instead.
 #define PAIG_A_EXP 8
 
 // power-of-two exponent e with m * 2^e in [2^14, 2^15) (f16's top binade,
@@ -115,6 +113,13 @@ int paig_f16_range_gemm(int clear);
 __device__ __forceinline__ int f16_scale_exp(float m) {
   const int b = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m));
   int e = b > 0 ? 14 - (((b >> 23) & 255) - 127) : 100;
+  return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
+
+// per-lane form of f16_scale_exp (m >= 0 need not be uniform; 0 for m == 0)
+__device__ __forceinline__ int f16_scale_exp_v(float m) {
+  const int b = __builtin_bit_cast(int, m);
+  int e = b > 0 ? 14 - (((b >> 23) & 255) - 127) : 0;
   return e < -100 ? -100 : (e > 100 ? 100 : e);
 }
 

@@ -11,14 +11,15 @@
 // so the three-term product does fp32-accurate convolutions at ~5x the f32
 // matrix rate; these layers (3..128 channels) then run at the HBM/LDS
 // roofline instead of the MFMA one.  Precision modes (PM):
-//   0  f16 hi/lo   (22 significant bits).  Activations and weights go in
-//                  unscaled (|v| < 65504 required: the kernels flag a larger
-//                  value, paig_f16_range_status); gradients are scaled by
-//                  powers of two into f16's top binade: per tile in dgrad
-//                  (the tile's outputs are complete, the epilogue scales
-//                  back), by a running block exponent in wgrad (whose pixel
-//                  sums span tiles: a tile needing a smaller exponent first
-//                  rescales the accumulators, exactly)
+//   0  f16 hi/lo   (22 significant bits).  Every operand is scaled by a
+//                  power of two into f16's top binade: forward activations
+//                  and dgrad gradients per tile (the tile's outputs are
+//                  complete, the epilogue scales back), weights per output
+//                  channel (paig_conv_wprep's header, or the block's own
+//                  staging), wgrad X by the forward's recorded maximum and
+//                  dY by a running block exponent (whose pixel sums span
+//                  tiles: a tile needing a smaller exponent first rescales
+//                  the accumulators, exactly).  No operand has a range limit
 //   1  bf16 hi/lo  (16 significant bits, fp32 range; no longer launched:
 //                  its wgrad errors measured 100x the fp32 envelope)
 //   2  bf16 hi only (one MFMA: the bf16 configuration, BASELINE config #2)
@@ -326,7 +327,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
   constexpr int NRB = H / RT;
   const int co0 = blockIdx.y * NT * 16;   // this block's COUT slice
-  float rmax = 0.f;                       // f16 range guard of the scaled weights
+  float rmax = 0.f;                       // f16 range guard (fixed-scale A/B builds only)
   __shared__ float smax[4];
 
   // ---- weights in fragment order: [s][nt][lane][8]; dgrad: transposed + flipped
@@ -340,10 +341,14 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     }
     return v;
   };
-  // PM 0: the weights are scaled by the fixed 2^PAIG_W_EXP (common.h; the
-  // epilogue takes it back out exactly) and range-guarded
-  int ew = 0;
-  float wsc = 1.f;
+  // PM 0: every output channel's weights are scaled by their own power of
+  // two (max |w| of the channel into [2^14, 2^15): no range limit, 22
+  // significant bits), ewn[nt] for this lane's channel of N-tile nt; the
+  // epilogue takes it back out exactly
+  int ewn[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) ewn[nt] = 0;
+  __shared__ int sew[PM == 0 ? NT * 16 : 1];   // in-kernel staging: the slice's channel exponents
   // ---- zero the halo columns (never written by the staging)
   if (PADL > 0) {
     for (int i = tid; i < FPT * ROWS * 2 * PADL * CC; i += 256) {
@@ -423,13 +428,16 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   // back out exactly.  The block's running max of the tile maxima goes to
   // xm.p[blockIdx.x] (the wgrad of the same input scales X by their max).
   constexpr bool SCL = PM == 0, DYN = PM == 0 && PAIG_SCALE_MODE < 2;
-  float tsc = 1.f, tinv = 1.f, xrun = 0.f;
+  float tsc = 1.f, tinv[NT], xrun = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) tinv[nt] = 1.f;
   auto tile_scale = [&]() {
     const float m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
     xrun = fmaxf(xrun, m);
     const int e = f16_scale_exp(m);
     tsc = __builtin_amdgcn_ldexpf(1.f, e);
-    tinv = __builtin_amdgcn_ldexpf(1.f, -(e + ew));
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) tinv[nt] = __builtin_amdgcn_ldexpf(1.f, -(e + ewn[nt]));
   };
   auto issue = [&](int t) {
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
@@ -535,36 +543,61 @@ if constexpr (W % 4 == 0) {
   int lt = blockIdx.x;
   auto tile_of = [&](int l) { return l < ntiles ? xcd_tile(l, ntiles) : ntiles; };
   issue(tile_of(lt));
-  // PM 0: the slice's weights scaled by 2^ew (max |w| into [2^14, 2^15)), so
-  // small weights keep 22 significant bits instead of an f16-subnormal lo
-  // piece; the epilogue takes the exponent back out exactly
-  if constexpr (PM == 0) {
-    ew = PAIG_W_EXP;
-    wsc = __builtin_amdgcn_ldexpf(1.f, ew);
-  }
   if (PM == 0 && wp != nullptr) {
     // pre-split images of the whole COUT (paig_conv_wprep, once per step):
-    // this slice's NT tiles of every k-step, coalesced 16-byte copies
-    constexpr int NTT = NT * C::NB, WLO = NS * NTT * 64;
+    // the channel exponents (header), then this slice's NT tiles of every
+    // k-step, coalesced 16-byte copies
+    constexpr int NTT = NT * C::NB, WLO = NS * NTT * 64, HDR = NTT * 16 * 4 / 16;
+    const int* hdr = reinterpret_cast<const int*>(wp);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) ewn[nt] = hdr[co0 + nt * 16 + (lane & 15)];
+    const s16x8* img = wp + HDR;
     for (int idx = tid; idx < NS * NT * 64; idx += 256) {
       const int s = idx / (NT * 64), r = idx - s * (NT * 64);
       const int src = (s * NTT + blockIdx.y * NT) * 64 + r;
-      *reinterpret_cast<s16x8*>(Wh + idx * 8) = wp[src];
-      *reinterpret_cast<s16x8*>(Wl + idx * 8) = wp[WLO + src];
+      *reinterpret_cast<s16x8*>(Wh + idx * 8) = img[src];
+      *reinterpret_cast<s16x8*>(Wl + idx * 8) = img[WLO + src];
     }
   } else {
+    if constexpr (PM == 0) {
+      // the slice's channel maxima (bit patterns of non-negative floats
+      // order as integers: an LDS atomic max, order-independent)
+      for (int i = tid; i < NT * 16; i += 256) sew[i] = 0;
+      __syncthreads();
+      float pm[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) pm[nt] = 0.f;
+      for (int idx = tid; idx < NS * NT * 64; idx += 256) {
+        const int nt = (idx >> 6) % NT;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pm[nt] = fmaxf(pm[nt], fabsf(wval(idx, j)));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) atomicMax(&sew[nt * 16 + (tid & 15)], __builtin_bit_cast(int, pm[nt]));
+      __syncthreads();
+      for (int i = tid; i < NT * 16; i += 256) sew[i] = f16_scale_exp_v(__builtin_bit_cast(float, sew[i]));
+      __syncthreads();
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) ewn[nt] = sew[nt * 16 + (lane & 15)];
+    }
     for (int idx = tid; idx < NS * NT * 64; idx += 256) {
+      const int cl = ((idx >> 6) % NT) * 16 + (idx & 15);
+      const int e = PM == 0 ? sew[cl] : 0;
       s16x8 vh, vl;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         short h, l;
-        split<PM>(wval(idx, j) * wsc, h, l, rmax);
+        split<PM>(__builtin_amdgcn_ldexpf(wval(idx, j), e), h, l, rmax);
         vh[j] = h;
         vl[j] = l;
       }
       *reinterpret_cast<s16x8*>(Wh + idx * 8) = vh;
       if (PM != 2) *reinterpret_cast<s16x8*>(Wl + idx * 8) = vl;
     }
+  }
+  if constexpr (!DYN) {   // fixed activation scale (A/B builds): the weight exponents alone
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) tinv[nt] = __builtin_amdgcn_ldexpf(1.f, -ewn[nt]);
   }
   // the bias of this lane's output channels (block constant)
   float bvs[NT];
@@ -623,7 +656,7 @@ if constexpr (W % 4 == 0) {
           if (f >= F) continue;
           float* op = out.frame(f) + co * HW + (long long)y * W + x;
           f32x4 v = acc[mt][nt];
-          if constexpr (SCL) v *= tinv;
+          if constexpr (SCL) v *= tinv[nt];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += bv;
           if (flags & 1) {
@@ -647,7 +680,7 @@ if constexpr (W % 4 == 0) {
             const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
             if (f >= F) continue;
             float* op = out.frame(f) + co * HW + (long long)y * W + x;
-            float v = (SCL ? acc[mt][nt][r] * tinv : acc[mt][nt][r]) + bv;
+            float v = (SCL ? acc[mt][nt][r] * tinv[nt] : acc[mt][nt][r]) + bv;
             if (flags & 1) v = v < 0.f ? 0.f : v;
             if (flags & 4) v += *op;
             if (flags & 2) v = aux.frame(f)[co * HW + (long long)y * W + x] > 0.f ? v : 0.f;
@@ -1443,61 +1476,89 @@ int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks,
 
 // ----------------------------------------------------------- weight prep
 // The forward / dgrad kernels' weight images, built once per step for every
-// conv (the same values and split as the in-kernel staging: scaled by the
-// fixed 2^PAIG_W_EXP, f16 hi / lo, range-guarded), in fragment order over
-// the whole COUT: entry (s, nt, lane) = 8 channels of k-chunk 4s + lane/16
-// for output channel 16 nt + lane%16; the lo image follows the hi one.  A
-// block then stages its slice with coalesced 16-byte copies instead of one
-// scattered 4-byte weight load (and split) per value, which measured
-// 0.4-8 us per launch (the most on the small-frame, wide-channel layers).
+// conv: a header of one int per output channel (its weight exponent: the
+// channel's max |w| scaled into [2^14, 2^15), so no magnitude overflows f16
+// and every weight keeps 22 significant bits relative to its channel's
+// largest), then the scaled weights split into f16 hi / lo, in fragment
+// order over the whole COUT: entry (s, nt, lane) = 8 channels of k-chunk
+// 4s + lane/16 for output channel 16 nt + lane%16; the lo image follows the
+// hi one.  A block then stages its slice with coalesced 16-byte copies
+// instead of one scattered 4-byte weight load (and split) per value, which
+// measured 0.4-8 us per launch (the most on the small-frame, wide-channel
+// layers).  The kernels' in-kernel staging (no image) forms the same
+// exponents and values.
 struct WPrepJob {
   const float* w;
   s16x8* out;
-  int cin, cout, ks, dg, entries;
+  int cin, cout, ks, dg;
 };
 constexpr int WPREP_MAX = 64;
 struct WPrepJobs {
   WPrepJob j[WPREP_MAX];
-  int blk0[WPREP_MAX + 1];   // first block of each job (WPREP_T entries per block)
+  int blk0[WPREP_MAX + 1];   // first block of each job (one block per 16-channel N-tile)
   int n;
 };
 constexpr int WPREP_T = 256;
 
-// one value per thread (entry e = t / 8, channel j = t % 8): one scattered
-// weight load each, the 8 lanes of an entry store its 16 bytes together
+__device__ __forceinline__ int wprep_hdr_entries(int cout) { return (cout + 15) / 16 * 16 * 4 / 16; }
+
+// one block per (job, N-tile of 16 output channels, WPREP_S k-steps): the
+// 16 channel maxima (thread t: channel t % 16; every block of the tile forms
+// them, from L2), their exponents, then its k-steps' entries
+constexpr int WPREP_S = 4;
 __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
-  float rmax = 0.f;
   int q = 0;
   while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.blk0[q + 1]) ++q;
   const WPrepJob jb = jobs.j[q];
-  const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16;
-  const float wsc = __builtin_amdgcn_ldexpf(1.f, PAIG_W_EXP);
-  const int t = ((int)blockIdx.x - jobs.blk0[q]) * WPREP_T + threadIdx.x;
-  const int e = t >> 3, j = t & 7;
-  if (e < jb.entries) {
-    const int s = e / (NTT * 64), rem = e - s * NTT * 64, ln = rem & 63, ntg = rem >> 6;
-    const int kc = 4 * s + (ln >> 4), co = ntg * 16 + (ln & 15);
+  const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16, NS = (KC + 3) / 4;
+  const int NSC = (NS + WPREP_S - 1) / WPREP_S;   // k-step chunks per N-tile
+  const int bl = (int)blockIdx.x - jobs.blk0[q], nt = bl / NSC, s0 = (bl % NSC) * WPREP_S;
+  const int tid = threadIdx.x;
+  auto wv = [&](int kc, int j, int co) {
     float v = 0.f;
     if (kc < KC && co < jb.cout) {
       const int tap = kc / CC, ci = (kc % CC) * 8 + j;
       if (ci < jb.cin) v = jb.dg ? jb.w[(ci * jb.cout + co) * KK + (KK - 1 - tap)] : jb.w[(co * jb.cin + ci) * KK + tap];
     }
-    short h, l;
-    split<0>(v * wsc, h, l, rmax);
-    short* o = reinterpret_cast<short*>(jb.out);
-    o[(long long)e * 8 + j] = h;
-    o[((long long)jb.entries + e) * 8 + j] = l;
+    return v;
+  };
+  __shared__ float red[WPREP_T];
+  __shared__ int ex[16];
+  const int cl = tid & 15, co = nt * 16 + cl;
+  float m = 0.f;
+  for (int i = tid >> 4; i < KC * 8; i += WPREP_T / 16) m = fmaxf(m, fabsf(wv(i >> 3, i & 7, co)));
+  red[tid] = m;
+  __syncthreads();
+  if (tid < 16) {
+    float mm = 0.f;
+    for (int r = 0; r < WPREP_T / 16; ++r) mm = fmaxf(mm, red[r * 16 + tid]);
+    ex[tid] = f16_scale_exp_v(mm);
+    if (s0 == 0) reinterpret_cast<int*>(jb.out)[nt * 16 + tid] = ex[tid];
   }
-  f16_range_note(rmax);
+  __syncthreads();
+  const int HDR = wprep_hdr_entries(jb.cout), ENT = NS * NTT * 64;
+  short* img = reinterpret_cast<short*>(jb.out + HDR);
+  // this block's entries: (s, lane) -> value index t = ((s - s0) * 64 + lane) * 8 + j
+  const int ns = NS - s0 < WPREP_S ? NS - s0 : WPREP_S;
+  for (int t = tid; t < ns * 64 * 8; t += WPREP_T) {
+    const int j = t & 7, ln = (t >> 3) & 63, s = s0 + (t >> 9);
+    const int kc = 4 * s + (ln >> 4), c = nt * 16 + (ln & 15);
+    float rm = 0.f;
+    short h, l;
+    split<0>(__builtin_amdgcn_ldexpf(wv(kc, j, c), ex[ln & 15]), h, l, rm);
+    const long long e = (long long)(s * NTT + nt) * 64 + ln;
+    img[e * 8 + j] = h;
+    img[((long long)ENT + e) * 8 + j] = l;
+  }
 }
 
 extern "C" {
 
-// 16-bit elements of one prepped weight image pair (hi + lo) for a
-// forward / dgrad kernel with cin input and cout output channels
+// 16-bit elements of one prepped weight image (channel-exponent header + hi
+// + lo) for a forward / dgrad kernel with cin input and cout output channels
 long long paig_conv_wprep_size(int cin, int cout, int ks) {
   const int KC = ks * ks * ((cin + 7) / 8), NS = (KC + 3) / 4, NTT = (cout + 15) / 16;
-  return 2ll * NS * NTT * 64 * 8;
+  return 2ll * NS * NTT * 64 * 8 + (long long)NTT * 16 * 2;
 }
 
 int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
@@ -1510,10 +1571,10 @@ int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cou
       const int i = b + q;
       PAIG_REQUIRE(w[i] && out[i] && cin[i] > 0 && cout[i] > 0 && ks[i] > 0, "conv_wprep: job %d", i);
       PAIG_REQUIRE(((uintptr_t)out[i] & 15) == 0, "conv_wprep: job %d output not 16-byte aligned", i);
-      const int e = (int)(paig_conv_wprep_size(cin[i], cout[i], ks[i]) / 16);
-      jobs.j[q] = WPrepJob{w[i], static_cast<s16x8*>(out[i]), cin[i], cout[i], ks[i], dg[i], e};
+      jobs.j[q] = WPrepJob{w[i], static_cast<s16x8*>(out[i]), cin[i], cout[i], ks[i], dg[i]};
       jobs.blk0[q] = blocks;
-      blocks += cdiv(8ll * e, WPREP_T);
+      const int NS = (ks[i] * ks[i] * ((cin[i] + 7) / 8) + 3) / 4;
+      blocks += (cout[i] + 15) / 16 * ((NS + WPREP_S - 1) / WPREP_S);
     }
     jobs.blk0[jobs.n] = blocks;
     hipLaunchKernelGGL(conv_wprep_k, dim3(blocks), dim3(WPREP_T), 0, (hipStream_t)stream, jobs);

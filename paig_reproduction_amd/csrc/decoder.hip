@@ -22,6 +22,8 @@
 //     sum is deterministic; paig_slab_reduce finishes it.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 struct Src {
@@ -610,6 +612,9 @@ struct DecCu {
   // fp64 partials per position gradient: the 4 row sums of every wave, or
   // (K = 3, LDS budget) the 2 half-wave sums
   static constexpr int RPW = K >= 3 ? 2 : 4, NR = NW * RPW;
+  // the two passes in alternating order by wave half (the K = 3 state does
+  // not fit the registers twice)
+  static constexpr bool ALT = K == 2;
   static_assert(NR <= 64, "one wave finishes a position gradient");
 };
 
@@ -645,6 +650,48 @@ __device__ __forceinline__ Ax axis(float ic, int h) {
   a.d0 = v0 ? -1.f : 0.f;
   a.d1 = v1 ? 1.f : 0.f;
   return a;
+}
+
+// bilinear sample of two source planes at once (packed fp32 math: the two
+// planes of a texel's float4 half), from the separable tap weights
+// ax / ay = (w0, w1, dw0, dw1) of the column / row: value and (DRV) d/dix,
+// d/diy
+template <bool DRV>
+__device__ __forceinline__ void samp_pair(pf32x2 A, pf32x2 B, pf32x2 Cc, pf32x2 D, float4 ax, float4 ay, pf32x2& v,
+                                          pf32x2& dx, pf32x2& dy) {
+  const pf32x2 top = ax.x * A + ax.y * B, bot = ax.x * Cc + ax.y * D;
+  v = ay.x * top + ay.y * bot;
+  if constexpr (DRV) {
+    const pf32x2 dtop = ax.z * A + ax.w * B, dbot = ax.z * Cc + ax.w * D;
+    dx = ay.x * dtop + ay.y * dbot;
+    dy = ay.z * top + ay.w * bot;
+  }
+}
+
+// One 8-byte LDS read that the compiler cannot pair with a neighbour into a
+// ds_read2_b64 (8 LDS cycles for 2 x 8 B per lane, half the bandwidth of
+// two single reads).  Its completion is tracked by lds_wait below, not by
+// the compiler.
+template <int OFF>
+__device__ __forceinline__ pf32x2 lds_read_b64(unsigned addr) {
+  pf32x2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+// wait until at most N LDS operations are outstanding, then hand out the
+// NV values read by lds_read_b64 (tied as in/out operands, so no use of them
+// can be scheduled above the wait)
+template <int N, int NV>
+__device__ __forceinline__ void lds_wait(pf32x2* v) {
+  static_assert(NV == 5 || NV == 10, "batch size");
+  if constexpr (NV == 5) {
+    asm volatile("s_waitcnt lgkmcnt(%5)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]) : "i"(N));
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(%10)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+                   "+v"(v[8]), "+v"(v[9])
+                 : "i"(N));
+  }
 }
 
 // Diagnostic build only (-DPAIG_DEC_STAMPS, tools/dec_stamps.sh): s_memtime
@@ -683,14 +730,6 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   const int R = pos.grp;
   const bool grouped = R > 0 && Rl > 0 && Rl < R;
   const int NL = grouped ? (F / R) * Rl : F;
-  // dead frames (steps Rl..R-1 of every sequence): zero position gradients
-  if (grouped) {
-    const long long per = (long long)(R - Rl) * 2 * K, nd = (long long)(F / R) * per;
-    for (long long e = (long long)blockIdx.x * NT + tid; e < nd; e += (long long)gridDim.x * NT) {
-      const long long b = e / per, rem = e % per;
-      dpos[(b * R + Rl + rem / (2 * K)) * 2 * K + rem % (2 * K)] = 0.f;
-    }
-  }
   const int first = blockIdx.x * FPB;
   const int nf = first < NL ? (NL - first < FPB ? NL - first : FPB) : 0;
 
@@ -740,36 +779,9 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
     return tgt.grp > 0 ? tgt.p + (long long)c.tq * tgt.fs + (long long)c.tr * tgt.gs : tgt.p + (long long)c.f * tgt.fs;
   };
 
-  // ---- prologue: sources, background, frame 0's tables / weight / targets
-  for (int t = tid; t < K * hp * hp; t += NT) {
-    const int k = t / (hp * hp), q = t % (hp * hp), y = q / hp - 1, x = q % hp - 1;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)h) {
-      const int o = y * h + x;
-      v.x = S.tmpl[k * hh + o] + 5.f;
-      v.y = 1.f / (1.f + expf(-S.cont[(k * 3 + 0) * hh + o]));
-      v.z = 1.f / (1.f + expf(-S.cont[(k * 3 + 1) * hh + o]));
-      v.w = 1.f / (1.f + expf(-S.cont[(k * 3 + 2) * hh + o]));
-    }
-    SRC[k][q] = v;
-  }
+  // ---- prologue: frame 0's loads first (their latency overlaps the staging below)
   float bgv[PS][3], gbg[PS][3], tn[PS][3];
   float gsrc[NIT][PL];
-#pragma unroll
-  for (int s = 0; s < PS; ++s) {
-    const int p = tid + NT * s;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      bgv[s][c] = p < HW ? S.bg[c * HW + p] : 0.f;
-      gbg[s][c] = 0.f;
-      tn[s][c] = 0.f;
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < NIT; ++u)
-#pragma unroll
-    for (int q = 0; q < PL; ++q) gsrc[u][q] = 0.f;
-  for (int j = tid; j < H; j += NT) BC[j] = base_coord(j, H);
   // this thread's table entry: an axis entry (tid in [TC0, TC0 + NC)) or a
   // gather entry (tid in [TG0, TG0 + NG)); (ck, cax) = the object / axis
   // whose position it reads
@@ -805,14 +817,53 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   DecCursor c2 = nf > 2 ? advance(c1) : c1;
   float w_cur = 0.f, p0 = 0.f, ppos = 0.f;
   bool act_cur = false, act_prev = false;
+#pragma unroll
+  for (int s2 = 0; s2 < PS; ++s2)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) tn[s2][c] = 0.f;
   if (nf > 0) {
+    fetch(ccur);
     p0 = pos_of(ccur)[2 * ck + cax];
     ppos = pos_of(c1)[2 * ck + cax];
     w_cur = dsse != nullptr ? uniform_f(dsse[ccur.f]) : 0.f;
     act_cur = is_active(w_cur);
-    fetch(ccur);
   }
-  __syncthreads();   // BC
+  // sources, background, base coordinates, dead frames' position gradients
+  for (int t = tid; t < K * hp * hp; t += NT) {
+    const int k = t / (hp * hp), q = t % (hp * hp), y = q / hp - 1, x = q % hp - 1;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)h) {
+      const int o = y * h + x;
+      v.x = S.tmpl[k * hh + o] + 5.f;
+      v.y = 1.f / (1.f + expf(-S.cont[(k * 3 + 0) * hh + o]));
+      v.z = 1.f / (1.f + expf(-S.cont[(k * 3 + 1) * hh + o]));
+      v.w = 1.f / (1.f + expf(-S.cont[(k * 3 + 2) * hh + o]));
+    }
+    SRC[k][q] = v;
+  }
+#pragma unroll
+  for (int s = 0; s < PS; ++s) {
+    const int p = tid + NT * s;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      bgv[s][c] = p < HW ? S.bg[c * HW + p] : 0.f;
+      gbg[s][c] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NIT; ++u)
+#pragma unroll
+    for (int q = 0; q < PL; ++q) gsrc[u][q] = 0.f;
+  for (int j = tid; j < H; j += NT) BC[j] = base_coord(j, H);
+  // dead frames (steps Rl..R-1 of every sequence): zero position gradients
+  if (grouped) {
+    const int per = (R - Rl) * 2 * K, nd = (F / R) * per;
+    for (int e = blockIdx.x * NT + tid; e < nd; e += gridDim.x * NT) {
+      const int b = e / per, rem = e - b * per;
+      dpos[((long long)b * R + Rl + rem / (2 * K)) * 2 * K + rem % (2 * K)] = 0.f;
+    }
+  }
+  __syncthreads();   // SRC, BC
   if (nf > 0) tables(p0, 0, 0);
   __syncthreads();
   DEC_STAMP(0, 0);
@@ -826,140 +877,131 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
     ppos = pos_of(c2)[2 * ck + cax];
     const float wnext = dsse != nullptr ? dsse[c1.f] : 0.f;
     DEC_STAMP(it, 1);
+    // The two passes of an iteration, in an order that alternates between the
+    // wave halves (each SIMD holds waves w, w+4, w+8, w+12): half the waves
+    // gather (LDS-read heavy) while the other half sample (VALU heavy).
+    auto pass2 = [&]() {
     // ---- pass 2 of frame it-1: source texels gather from G; its position gradients
-    if (it >= 1 && act_prev) {
-      const int sl = (it - 1) & 1, gs = (it - 1) % 3;
-      if (wv < 2 * K) {   // wave e finishes position gradient e from the NR row partials
-        const double v = lane < NR ? RED[sl][wv][lane] : 0.0;
-        const double tot = wave_sum_dpp_d(v);
-        const float dth = (float)(tot * (double)h * 0.5);
-        if (lane == 0) dpos[(long long)cprev.f * 2 * K + wv] = -dth / (float)h;
-      }
-#pragma unroll
-      for (int u = 0; u < NIT; ++u) {
-        const int t = tid + NT * u;
-        if (NIT == 1 || t < NI) {
-          // item t: texel tx = t % (K hh), plane pair hf (PL = 2) or all 4 planes
-          const int tx = t % (K * hh), hf = PL == 2 ? t / (K * hh) : 0;
-          const int k = tx / hh, q = tx % hh, ys = q / h, xs = q % h;
-          const int i0 = J0[gs][k][1][ys], c0 = J0[gs][k][0][xs];
-          float wy[GW], wx[GW];
-#pragma unroll
-          for (int a2 = 0; a2 < GW; ++a2) {
-            wy[a2] = WT[gs][k][1][ys][a2];
-            wx[a2] = WT[gs][k][0][xs][a2];
-          }
-          // columns c0 + b: the even b share c0's parity (consecutive slots
-          // from gslot(c0)), the odd b the other one: every read below is an
-          // immediate offset from one of two bases
-          const int be = i0 * GPITCH + gslot<H>(c0), bo = i0 * GPITCH + gslot<H>(c0 + 1);
-          const float2* ge[2] = {&G[sl][hf][k][be], &G[sl][1][k][be]};
-          const float2* go[2] = {&G[sl][hf][k][bo], &G[sl][1][k][bo]};
-          float acc[PL];
-#pragma unroll
-          for (int q2 = 0; q2 < PL; ++q2) acc[q2] = 0.f;
-#pragma unroll
-          for (int b = 0; b < GW; ++b) {
-            float r[PL];
-#pragma unroll
-            for (int q2 = 0; q2 < PL; ++q2) r[q2] = 0.f;
-#pragma unroll
-            for (int a2 = 0; a2 < GW; ++a2) {   // rows i0 .. i0+4
-              const int o = a2 * GPITCH + (b >> 1);
-              const float2 v = (b & 1) ? go[0][o] : ge[0][o];
-              r[0] = fmaf(wy[a2], v.x, r[0]);
-              r[1] = fmaf(wy[a2], v.y, r[1]);
-              if constexpr (PL == 4) {
-                const float2 v2 = (b & 1) ? go[1][o] : ge[1][o];
-                r[2] = fmaf(wy[a2], v2.x, r[2]);
-                r[3] = fmaf(wy[a2], v2.y, r[3]);
-              }
-            }
-#pragma unroll
-            for (int q2 = 0; q2 < PL; ++q2) acc[q2] = fmaf(wx[b], r[q2], acc[q2]);
-          }
-#pragma unroll
-          for (int q2 = 0; q2 < PL; ++q2) gsrc[u][q2] += acc[q2];
+  #ifdef PAIG_DEC_SKIP_P2   // diagnostic builds only (tools/dec_stamps.sh): phase cost by elimination
+      if (false) {
+  #else
+      if (it >= 1 && act_prev) {
+  #endif
+        const int sl = (it - 1) & 1, gs = (it - 1) % 3;
+        if (wv < 2 * K) {   // wave e finishes position gradient e from the NR row partials
+          const double v = lane < NR ? RED[sl][wv][lane] : 0.0;
+          const double tot = wave_sum_dpp_d(v);
+          const float dth = (float)(tot * (double)h * 0.5);
+          if (lane == 0) dpos[(long long)cprev.f * 2 * K + wv] = -dth / (float)h;
         }
+  #pragma unroll
+        for (int u = 0; u < NIT; ++u) {
+          const int t = tid + NT * u;
+          if (NIT == 1 || t < NI) {
+            // item t: texel tx = t % (K hh), plane pair hf (PL = 2) or all 4 planes
+            const int tx = t % (K * hh), hf = PL == 2 ? t / (K * hh) : 0;
+            const int k = tx / hh, q = tx % hh, ys = q / h, xs = q % h;
+            const int i0 = J0[gs][k][1][ys], c0 = J0[gs][k][0][xs];
+            float wy[GW], wx[GW];
+  #pragma unroll
+            for (int a2 = 0; a2 < GW; ++a2) {
+              wy[a2] = WT[gs][k][1][ys][a2];
+              wx[a2] = WT[gs][k][0][xs][a2];
+            }
+            // columns c0 + b: the even b share c0's parity (consecutive slots
+            // from gslot(c0)), the odd b the other one: every read below is an
+            // immediate offset from one of two bases.  The reads are issued as
+            // single ds_read_b64 (inline asm: the compiler would pair them into
+            // ds_read2_b64, which moves half the bytes per LDS cycle), one
+            // column (5 rows x the plane pairs) per batch, two batches ahead.
+            const int be = i0 * GPITCH + gslot<H>(c0), bo = i0 * GPITCH + gslot<H>(c0 + 1);
+            unsigned ae[2], ao[2];
+#pragma unroll
+            for (int q2 = 0; q2 < 2; ++q2) {
+              ae[q2] = (unsigned)(uintptr_t)&G[sl][q2 == 0 ? hf : 1][k][be];
+              ao[q2] = (unsigned)(uintptr_t)&G[sl][q2 == 0 ? hf : 1][k][bo];
+            }
+            // packed fp32 accumulators: one plane pair per pf32x2
+            pf32x2 acc[PL / 2];
+#pragma unroll
+            for (int q2 = 0; q2 < PL / 2; ++q2) acc[q2] = pf32x2{0.f, 0.f};
+            pf32x2 vb[3][GW][PL / 2];   // batches in flight (ring of 3 columns)
+            auto issue = [&](auto bc) {
+              constexpr int b = decltype(bc)::value;
+#pragma unroll
+              for (int a2 = 0; a2 < GW; ++a2)
+#pragma unroll
+                for (int q2 = 0; q2 < PL / 2; ++q2)
+                  vb[b % 3][a2][q2] = lds_read_b64<(b >> 1) * 8>((b & 1 ? ao[q2] : ae[q2]) + a2 * GPITCH * 8);
+            };
+            auto consume = [&](auto bc) {
+              constexpr int b = decltype(bc)::value;
+              // the reads issued after this column's: columns b+1 and b+2 (if any)
+              constexpr int younger = ((b + 2 < GW ? 2 : (b + 1 < GW ? 1 : 0))) * GW * (PL / 2);
+              lds_wait<(younger < 15 ? younger : 15), GW * (PL / 2)>(&vb[b % 3][0][0]);
+              pf32x2 r[PL / 2];
+#pragma unroll
+              for (int q2 = 0; q2 < PL / 2; ++q2) r[q2] = pf32x2{0.f, 0.f};
+#pragma unroll
+              for (int a2 = 0; a2 < GW; ++a2)
+#pragma unroll
+                for (int q2 = 0; q2 < PL / 2; ++q2) r[q2] += wy[a2] * vb[b % 3][a2][q2];
+#pragma unroll
+              for (int q2 = 0; q2 < PL / 2; ++q2) acc[q2] += wx[b] * r[q2];
+            };
+            issue(std::integral_constant<int, 0>{});
+            issue(std::integral_constant<int, 1>{});
+            issue(std::integral_constant<int, 2>{});
+            consume(std::integral_constant<int, 0>{});
+            issue(std::integral_constant<int, 3>{});
+            consume(std::integral_constant<int, 1>{});
+            issue(std::integral_constant<int, 4>{});
+            consume(std::integral_constant<int, 2>{});
+            consume(std::integral_constant<int, 3>{});
+            consume(std::integral_constant<int, 4>{});
+  #pragma unroll
+            for (int q2 = 0; q2 < PL / 2; ++q2) {
+              gsrc[u][2 * q2] += acc[q2].x;
+              gsrc[u][2 * q2 + 1] += acc[q2].y;
+            }
+          }
+        }
+      } else if (it >= 1 && tid < 2 * K) {
+        dpos[(long long)cprev.f * 2 * K + tid] = 0.f;
       }
-    } else if (it >= 1 && tid < 2 * K) {
-      dpos[(long long)cprev.f * 2 * K + tid] = 0.f;
-    }
-    DEC_STAMP(it, 2);
+    };
+    auto pass1 = [&]() {
     // ---- pass 1 of frame it
-    if (it < nf && act_cur) {
-      const int sl = it & 1;
-      const float w_f = 2.f * w_cur;
-      const float* dof = dout.p ? dout.p + (long long)ccur.f * dout.fs : nullptr;
-      double sx[K], sy[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) sx[k] = sy[k] = 0.0;
-#pragma unroll
-      for (int s = 0; s < PS; ++s) {
-        const int p = tid + NT * s;
-        if (PS > 1 && p >= HW) break;
-        const int i = p / H, j = p % H;
-        // K >= 3: the derivative planes are re-formed from the texels after
-        // the blend instead of being held across it (register budget)
-        constexpr bool HOLD = K < 3;
-        float sv[K][4], sdx[HOLD ? K : 1][4], sdy[HOLD ? K : 1][4];
-        float4 wxa[K], wya[K];
-        int base[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          wxa[k] = AXW[sl][k][0][j];
-          wya[k] = AXW[sl][k][1][i];
-          base[k] = AXC[sl][k][1][i] * hp + AXC[sl][k][0][j];
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const float4 ax = wxa[k], ay = wya[k];
-          const int bs = base[k];
-          const float4 a = SRC[k][bs], b = SRC[k][bs + 1], c = SRC[k][bs + hp], d = SRC[k][bs + hp + 1];
-          const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-          const float cv[4] = {c.x, c.y, c.z, c.w}, dv[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float top = fmaf(ax.y, bv[q], ax.x * av[q]), bot = fmaf(ax.y, dv[q], ax.x * cv[q]);
-            sv[k][q] = fmaf(ay.y, bot, ay.x * top);
-            if constexpr (HOLD) {
-              const float dtop = fmaf(ax.w, bv[q], ax.z * av[q]), dbot = fmaf(ax.w, dv[q], ax.z * cv[q]);
-              sdx[k][q] = fmaf(ay.y, dbot, ay.x * dtop);
-              sdy[k][q] = fmaf(ay.w, bot, ay.z * top);
-            }
+  #ifdef PAIG_DEC_SKIP_P1
+      if (false) {
+  #else
+      if (it < nf && act_cur) {
+  #endif
+        const int sl = it & 1;
+        const float w_f = 2.f * w_cur;
+        const float* dof = dout.p ? dout.p + (long long)ccur.f * dout.fs : nullptr;
+        double sx[K], sy[K];
+  #pragma unroll
+        for (int k = 0; k < K; ++k) sx[k] = sy[k] = 0.0;
+  #pragma unroll
+        for (int s = 0; s < PS; ++s) {
+          const int p = tid + NT * s;
+          if (PS > 1 && p >= HW) break;
+          const int i = p / H, j = p % H;
+          // K >= 3: the derivative planes are re-formed from the texels after
+          // the blend instead of being held across it (register budget)
+          constexpr bool HOLD = K < 3;
+          float sv[K][4], sdx[HOLD ? K : 1][4], sdy[HOLD ? K : 1][4];
+          float4 wxa[K], wya[K];
+          int base[K];
+  #pragma unroll
+          for (int k = 0; k < K; ++k) {
+            wxa[k] = AXW[sl][k][0][j];
+            wya[k] = AXW[sl][k][1][i];
+            base[k] = AXC[sl][k][1][i] * hp + AXC[sl][k][0][j];
           }
-        }
-        float o[3], m[K + 1];
-        blend<K>(sv, bgv[s], o, m);
-        float g[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          g[c] = w_f * (o[c] - tn[s][c]);
-          if (dof) g[c] += dof[c * HW + p];
-          gbg[s][c] = fmaf(m[K], g[c], gbg[s][c]);
-        }
-        const int gof = i * GPITCH + gslot<H>(j);
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          float dT = 0.f;
-          float dC[3];
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            dC[c] = m[k] * g[c];
-            dT = fmaf(g[c], sv[k][1 + c] - o[c], dT);
-          }
-          dT *= m[k];
-          G[sl][0][k][gof] = make_float2(dT, dC[0]);
-          G[sl][1][k][gof] = make_float2(dC[1], dC[2]);
-          const float gq[4] = {dT, dC[0], dC[1], dC[2]};
-          float gx = 0.f, gy = 0.f;
-          if constexpr (HOLD) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              gx = fmaf(gq[q], sdx[k][q], gx);
-              gy = fmaf(gq[q], sdy[k][q], gy);
-            }
-          } else {
+  #pragma unroll
+          for (int k = 0; k < K; ++k) {
             const float4 ax = wxa[k], ay = wya[k];
             const int bs = base[k];
             const float4 a = SRC[k][bs], b = SRC[k][bs + 1], c = SRC[k][bs + hp], d = SRC[k][bs + hp + 1];
@@ -968,33 +1010,93 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const float top = fmaf(ax.y, bv[q], ax.x * av[q]), bot = fmaf(ax.y, dv[q], ax.x * cv[q]);
-              const float dtop = fmaf(ax.w, bv[q], ax.z * av[q]), dbot = fmaf(ax.w, dv[q], ax.z * cv[q]);
-              gx = fmaf(gq[q], fmaf(ay.y, dbot, ay.x * dtop), gx);
-              gy = fmaf(gq[q], fmaf(ay.w, bot, ay.z * top), gy);
+              sv[k][q] = fmaf(ay.y, bot, ay.x * top);
+              if constexpr (HOLD) {
+                const float dtop = fmaf(ax.w, bv[q], ax.z * av[q]), dbot = fmaf(ax.w, dv[q], ax.z * cv[q]);
+                sdx[k][q] = fmaf(ay.y, dbot, ay.x * dtop);
+                sdy[k][q] = fmaf(ay.w, bot, ay.z * top);
+              }
             }
           }
-          sx[k] += (double)gx;
-          sy[k] += (double)gy;
+          float o[3], m[K + 1];
+          blend<K>(sv, bgv[s], o, m);
+          float g[3];
+  #pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            g[c] = w_f * (o[c] - tn[s][c]);
+            if (dof) g[c] += dof[c * HW + p];
+            gbg[s][c] = fmaf(m[K], g[c], gbg[s][c]);
+          }
+          const int gof = i * GPITCH + gslot<H>(j);
+  #pragma unroll
+          for (int k = 0; k < K; ++k) {
+            float dT = 0.f;
+            float dC[3];
+  #pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              dC[c] = m[k] * g[c];
+              dT = fmaf(g[c], sv[k][1 + c] - o[c], dT);
+            }
+            dT *= m[k];
+            G[sl][0][k][gof] = make_float2(dT, dC[0]);
+            G[sl][1][k][gof] = make_float2(dC[1], dC[2]);
+            const float gq[4] = {dT, dC[0], dC[1], dC[2]};
+            float gx = 0.f, gy = 0.f;
+            if constexpr (HOLD) {
+  #pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                gx = fmaf(gq[q], sdx[k][q], gx);
+                gy = fmaf(gq[q], sdy[k][q], gy);
+              }
+            } else {
+              const int bs = base[k];
+              const float4 a = SRC[k][bs], b = SRC[k][bs + 1], c = SRC[k][bs + hp], d = SRC[k][bs + hp + 1];
+              pf32x2 gxy = {0.f, 0.f}, gyy = {0.f, 0.f};
+  #pragma unroll
+              for (int q = 0; q < 4; q += 2) {
+                pf32x2 v, dx, dy;
+                samp_pair<true>(q ? pf32x2{a.z, a.w} : pf32x2{a.x, a.y}, q ? pf32x2{b.z, b.w} : pf32x2{b.x, b.y},
+                                q ? pf32x2{c.z, c.w} : pf32x2{c.x, c.y}, q ? pf32x2{d.z, d.w} : pf32x2{d.x, d.y}, wxa[k],
+                                wya[k], v, dx, dy);
+                const pf32x2 gp = {gq[q], gq[q + 1]};
+                gxy += gp * dx;
+                gyy += gp * dy;
+              }
+              gx = gxy.x + gxy.y;
+              gy = gyy.x + gyy.y;
+            }
+            sx[k] += (double)gx;
+            sy[k] += (double)gy;
+          }
+        }
+        double sv2[2 * K];
+  #pragma unroll
+        for (int k = 0; k < K; ++k) {
+          sv2[2 * k] = sx[k];
+          sv2[2 * k + 1] = sy[k];
+        }
+        row_sums_dpp_d<2 * K>(sv2);
+        if constexpr (C::RPW == 2) {
+  #pragma unroll
+          for (int e = 0; e < 2 * K; ++e) sv2[e] += __shfl_xor(sv2[e], 16, 64);   // rows 0+1, 2+3
+          if ((lane & 31) == 0)
+  #pragma unroll
+            for (int e = 0; e < 2 * K; ++e) RED[sl][e][wv * 2 + (lane >> 5)] = sv2[e];
+        } else {
+          if ((lane & 15) == 0)
+  #pragma unroll
+            for (int e = 0; e < 2 * K; ++e) RED[sl][e][wv * 4 + (lane >> 4)] = sv2[e];
         }
       }
-      double sv2[2 * K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        sv2[2 * k] = sx[k];
-        sv2[2 * k + 1] = sy[k];
-      }
-      row_sums_dpp_d<2 * K>(sv2);
-      if constexpr (C::RPW == 2) {
-#pragma unroll
-        for (int e = 0; e < 2 * K; ++e) sv2[e] += __shfl_xor(sv2[e], 16, 64);   // rows 0+1, 2+3
-        if ((lane & 31) == 0)
-#pragma unroll
-          for (int e = 0; e < 2 * K; ++e) RED[sl][e][wv * 2 + (lane >> 5)] = sv2[e];
-      } else {
-        if ((lane & 15) == 0)
-#pragma unroll
-          for (int e = 0; e < 2 * K; ++e) RED[sl][e][wv * 4 + (lane >> 4)] = sv2[e];
-      }
+    };
+    if (!C::ALT || wv < C::NW / 2) {
+      pass2();
+      DEC_STAMP(it, 2);
+      pass1();
+    } else {
+      pass1();
+      DEC_STAMP(it, 2);
+      pass2();
     }
     DEC_STAMP(it, 3);
     // ---- frame it+1: targets (in flight across the barrier and pass 2) and loss weight

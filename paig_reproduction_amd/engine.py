@@ -299,10 +299,10 @@ class Engine:
     CONV_MATH = {"split": 128, "fp32": 0, "bf16": 256}
 
     # the same choice for the dense layers (paig_gemm_ex math) per GEMM kind
-    # (forward, wgrad, dgrad): f16 pieces with the activations / gradients
-    # scaled by running powers of two, the weights at the fixed 2^8 (4:
-    # op(A) dynamic, op(B) = W fixed; 6: both dynamic)
-    GEMM_MATH = {"split": (4, 6, 4), "fp32": (0, 0, 0), "bf16": (3, 3, 3)}
+    # (forward, wgrad, dgrad): f16 pieces, both operands (activations /
+    # gradients and the weights) scaled by running powers of two (math 6): no
+    # range limit on any operand
+    GEMM_MATH = {"split": (6, 6, 6), "fp32": (0, 0, 0), "bf16": (3, 3, 3)}
     FWD, WGRAD, DGRAD = 0, 1, 2
 
     def gemm_math(self, kind):
@@ -523,8 +523,10 @@ class Engine:
         S["view"] = view
         S["conv_input"] = conv_input
         # per conv: the split forward's per-block max |input| slots, which
-        # set the X scale of the same input's wgrad (every slot is written)
-        xmax = _empty(len(lay.ops) * XMAX_SLOTS, dev)
+        # set the X scale of the same input's wgrad (every slot is written;
+        # zeroed so that a slot no forward wrote falls back to the guarded
+        # fixed scale instead of a garbage exponent)
+        xmax = torch.zeros(len(lay.ops) * XMAX_SLOTS, device=dev)
         S["xmax"] = lambda i: ptr(xmax) + i * XMAX_SLOTS * 4
         S["xmax_buf"] = xmax
         # split path: every conv's forward and dgrad weight images, pre-split

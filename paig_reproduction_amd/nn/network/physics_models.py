@@ -310,18 +310,19 @@ class PhysicsNet(BaseNetTorch):
 
     def check_numerics(self):
         """Raise if a split-precision kernel flagged an operand outside f16's
-        range since the last check: weights are staged at a fixed 2^8 scale
-        (|w| >= 256 is flagged); activations and gradients are scaled by
-        powers of two from their own maxima and have no limit.
+        range since the last check.  The step's operands (activations,
+        gradients, weights) are all scaled by powers of two from their own
+        maxima and have no range limit; the flag remains for the fixed-scale
+        fallbacks of the C ABI (a conv weight gradient called without the
+        forward's xmax slots, GEMM math 1 / 5), which the step never takes.
         Synchronises the device: BaseNetTorch calls it at log steps only."""
         if self.conv_math != "split":
             return
         rc = lib().paig_f16_range_status(1)
         if rc != 0:
             raise FloatingPointError(
-                "split-precision path: a weight reached |w| >= 256, beyond the f16 staging range of the "
-                "fp32-accurate 16-bit matrix-core kernels; rerun with --conv_math fp32" if rc > 0 else
-                f"paig_f16_range_status failed ({rc})")
+                "split-precision path: an operand beyond the f16 staging range of a fixed-scale fallback "
+                "kernel; rerun with --conv_math fp32" if rc > 0 else f"paig_f16_range_status failed ({rc})")
 
     def _anchor_for_modules(self):
         return torch.zeros((), requires_grad=True)

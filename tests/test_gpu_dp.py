@@ -8,13 +8,17 @@ reference loop being replaced is single-process (nn/network/base.py:141-152);
 the DP contract is that the averaged per-rank gradients of equal halves are
 the full batch's gradient (the losses are batch means).
 
-Bars: 6e-6 normwise on every step's all-reduced flat gradients (test_gpu_
-fullsize's halves bar, ~3x the measured fp32 reassociation error) and, with
-momentum SGD (an update linear in the gradient), on the final parameters.
-RMSprop's first update is lr * sign(g) / sqrt(1 - alpha) for |g| >> eps, so a
-gradient component at rounding-noise level can flip its parameter's update:
-for RMSprop the gradients are checked at every step and the parameters are
-reported, not bounded.
+Every step is compared from the same starting state (the single-process
+run loads the DP run's parameters and optimizer buffers before each step):
+over several steps the two trajectories would part at the first near-tie
+max-pool / ReLU decision that a one-ulp parameter difference flips, as any
+two fp32 runs of the reference do.  Bars: 6e-6 normwise on every step's
+all-reduced flat gradients (test_gpu_fullsize's halves bar, ~3x the
+measured fp32 reassociation error) and, with momentum SGD (an update linear
+in the gradient), on the updated parameters.  RMSprop's first update is
+lr * sign(g) / sqrt(1 - alpha) for |g| >> eps, so a gradient component at
+rounding-noise level can flip its parameter's update: for RMSprop the
+updated parameters are reported, not bounded.
 """
 import os
 import socket
@@ -72,16 +76,13 @@ def test_dp_step_equals_single_process(kind, tmp_path):
     procs = [_run(["--mode", "dp", "--rank", str(r), "--world", "2", "--port", str(port), "--kind", kind,
                    "--out", str(dp)]) for r in range(2)]
     _wait(procs)
-    _wait([_run(["--mode", "single", "--kind", kind, "--out", str(single)])])
+    _wait([_run(["--mode", "single", "--kind", kind, "--out", str(single), "--src", str(dp)])])
     for i in range(3):
         for nm in ("g32", "g64"):
-            a, b = np.load(dp / f"{nm}_{i}.npy"), np.load(single / f"{nm}_{i}.npy")
-            e = _rel(a, b)
-            if kind == "rmsprop" and i > 0:
-                continue   # after RMSprop's sign-sensitive first update the trajectories may part (docstring)
+            e = _rel(np.load(dp / f"post_{nm}_{i}.npy"), np.load(single / f"post_{nm}_{i}.npy"))
             assert e <= 6e-6, f"{kind} step {i}: all-reduced {nm} rel err {e:.3g}"
-    ep = _rel(np.load(dp / "p32.npy"), np.load(single / "p32.npy"))
-    e64 = _rel(np.load(dp / "p64.npy"), np.load(single / "p64.npy"))
-    print(f"{kind}: final parameters rel err fp32 {ep:.3g} fp64 {e64:.3g}")
-    if kind == "momentum":
-        assert ep <= 6e-6 and e64 <= 6e-6, (ep, e64)
+        ep = _rel(np.load(dp / f"post_p32_{i}.npy"), np.load(single / f"post_p32_{i}.npy"))
+        e64 = _rel(np.load(dp / f"post_p64_{i}.npy"), np.load(single / f"post_p64_{i}.npy"))
+        print(f"{kind} step {i}: updated parameters rel err fp32 {ep:.3g} fp64 {e64:.3g}")
+        if kind == "momentum":
+            assert ep <= 6e-6 and e64 <= 6e-6, (i, ep, e64)

@@ -306,11 +306,11 @@ def test_slab_reduce_multi(lens, aligned, accumulate):
             assert float((got - want).abs().max()) <= 1e-4 * max(1.0, float(want.abs().max()))
 
 
-# ---- range: activations and gradients (power-of-two scales from their own
-# maxima) work at any magnitude, including beyond f16's 65504; weights (fixed
-# 2^8 scale) up to 256, and the device range flag is raised beyond, as by a
-# wgrad called without the forward's xmax slots (fixed 2^8 for X) and GEMM
-# math 1 (unscaled) beyond 65504
+# ---- range: activations, gradients and weights (power-of-two scales from
+# their own maxima: per tile, per block, per output channel) work at any
+# magnitude, including beyond f16's 65504; the device range flag is raised
+# only by a wgrad called without the forward's xmax slots (fixed 2^8 for X)
+# and GEMM math 1 (unscaled) beyond 65504
 XMAX_SLOTS = 2048
 
 
@@ -398,20 +398,53 @@ def test_conv_split_xmax_fallback_flag():
     assert _range_status() == 1
 
 
-def test_conv_split_weight_range_flag():
-    """Conv weights are staged at a fixed 2^8 scale: |w| >= 256 cannot be
-    represented, and the kernel flags it (PhysicsNet raises at its next check)."""
-    cin, cout, hw, F_ = 8, 8, 32, 2
+@pytest.mark.parametrize("wscale", [1e3, 3e-4])
+def test_conv_split_weight_any_range(wscale):
+    """Conv weights get a power-of-two exponent per output channel (in-kernel
+    staging and paig_conv_wprep images alike): weights up to 1e3 (and tiny
+    ones), channels of very different magnitude, match fp64 conv2d at the
+    split bars, forward and dgrad, and raise no range flag."""
+    cin, cout, hw, ks, F_ = 16, 16, 16, 3, 3
     _range_status()
-    x = torch.rand(F_, cin, hw, hw, device=DEV)
-    w = torch.randn(cout, cin, 3, 3, device=DEV)
-    w[0, 0, 1, 1] = 300.0
-    b = torch.zeros(cout, device=DEV)
+    torch.manual_seed(11)
+    x = torch.rand(F_, cin, hw, hw)
+    w = torch.randn(cout, cin, ks, ks) * wscale
+    w[3] *= 1e-4          # a channel far below the others
+    w[5, 2, 1, 1] = 3.0 * wscale
+    b = torch.randn(cout)
+    dy = torch.randn(F_, cout, hw, hw)
+    xr, wr = x.clone().double().requires_grad_(True), w.clone().double()
+    y = F.conv2d(xr, wr, b.double(), padding="same")
+    y.backward(dy.double())
+    xg, wg, bg, dyg = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
+    # in-kernel staging
     out = torch.empty(F_, cout, hw, hw, device=DEV)
-    L().paig_conv2d_fwd(p(x), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout, hw, hw,
-                        3, 128, st())
-    assert _range_status() == 1
-    assert _range_status() == 0   # cleared by the read
+    L().paig_conv2d_fwd(p(xg), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout, hw,
+                        hw, ks, 128, st())
+    dx = torch.empty(F_, cin, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(dyg), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, None, 0, p(wg), None, F_, cout, cin, hw,
+                        hw, ks, 8 | 128, st())
+    torch.cuda.synchronize()
+    assert rel_err(out, y.detach()) <= 1e-5
+    assert rel_err(dx, xr.grad) <= 1e-5
+    # prepped images (the training step's path)
+    jobs = [(cin, cout, 0), (cout, cin, 1)]
+    sizes = [int(L().paig_conv_wprep_size(a, c, ks)) for a, c, _ in jobs]
+    buf = torch.zeros(sum(sizes), dtype=torch.int16, device=DEV)
+    outs = [buf.data_ptr(), buf.data_ptr() + 2 * sizes[0]]
+    n = len(jobs)
+    L().paig_conv_wprep(n, (ctypes.c_void_p * n)(*[p(wg)] * n), (ctypes.c_int * n)(*[j[0] for j in jobs]),
+                        (ctypes.c_int * n)(*[j[1] for j in jobs]), (ctypes.c_int * n)(ks, ks),
+                        (ctypes.c_int * n)(*[j[2] for j in jobs]), (ctypes.c_void_p * n)(*outs), st())
+    out2 = torch.empty_like(out)
+    dx2 = torch.empty_like(dx)
+    L().paig_conv2d_fwd_pw(p(xg), cin * hw * hw, 0, 0, p(out2), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout,
+                           hw, hw, ks, 128, None, 0, None, 0, outs[0], st())
+    L().paig_conv2d_fwd_pw(p(dyg), cout * hw * hw, 0, 0, p(dx2), cin * hw * hw, None, 0, p(wg), None, F_, cout, cin,
+                           hw, hw, ks, 8 | 128, None, 0, None, 0, outs[1], st())
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out) and torch.equal(dx2, dx), "prepped images must match in-kernel staging bit for bit"
+    assert _range_status() == 0
 
 
 def test_gemm_math1_range_flag():

@@ -3,15 +3,20 @@ of the data-parallel training step on cuda:0 over gloo, or the
 single-process reference on the concatenated batch.
 
   python tests/workers/dp_step_worker.py --mode dp --rank R --world 2 --port P --kind K --out DIR
-  python tests/workers/dp_step_worker.py --mode single --kind K --out DIR
+  python tests/workers/dp_step_worker.py --mode single --kind K --out DIR --src DPDIR
 
-Both run the same 3 steps (3 fixed global batches of 2B sequences,
-synthetic spring_color, seq 12) through paig_reproduction_amd.graph_step
-(bench.py's step): DP ranks take disjoint halves of every global batch and
-replay the split HIP graph with the early-bucket all-reduce between the two
-replays, then FlatOptimizer.step (late bucket + fp64 scalars, the update).
-Writes the flat gradient buffer after every step and the final parameters
-(rank 0 / single) to DIR as .npy.
+Both run 3 steps (3 fixed global batches of 2B sequences, synthetic
+spring_color, seq 12) through paig_reproduction_amd.graph_step (bench.py's
+step): DP ranks take disjoint halves of every global batch and replay the
+split HIP graph with the early-bucket all-reduce between the two replays,
+then FlatOptimizer.step (late bucket + fp64 scalars, the update).  Rank 0
+writes, per step, the state it started from (parameters, optimizer
+buffers), the all-reduced flat gradients and the parameters after the
+update.  The single-process run loads each of those starting states and
+takes the same step on the whole batch, writing its gradients and updated
+parameters: every step is compared from the same state (a multi-step
+trajectory would part at the first near-tie max-pool / ReLU decision that a
+one-ulp parameter difference flips).
 """
 import argparse
 import os
@@ -35,6 +40,7 @@ def main():
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--kind", default="momentum")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--src", default="", help="single mode: the DP run's output directory")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -50,8 +56,7 @@ def main():
     torch.manual_seed(0)
     m = PhysicsNet("spring_color", 100, 1, "spring_ode_cell", SEQ, 4, 6, 3.0, False, True, 32 * 32,
                    "conv_encoder", "conv_st_decoder", device=dev).to(dev)
-    opt = {"momentum": "momentum", "rmsprop": "rmsprop"}[a.kind]
-    m.build_optimizer(1e-3, opt, True)
+    m.build_optimizer(1e-3, a.kind, True)
     if world > 1:
         for t in m.state_dict().values():
             dist.broadcast(t, 0)
@@ -77,20 +82,37 @@ def main():
     step.eager()
     step.capture()
     with torch.no_grad():
-        m.load_state_dict(init)
-    m.build_optimizer(1e-3, opt, True)   # fresh optimizer state (the graph reads the same flat buffers)
+        m.load_state_dict(init)   # in place: the captured graph reads the same flat buffers
+    opt = m.optimizer
+    opt._ensure_state()
+    for b in opt._bufs:   # fresh optimizer state, in place (a captured RMSprop step reads these buffers)
+        b.zero_()
+    opt.steps = 0
     torch.cuda.synchronize()
     flat = m._flat
+    save = a.mode == "single" or a.rank == 0
+
+    def dump(tag, i, arrs):
+        for nm, t in arrs.items():
+            np.save(os.path.join(a.out, f"{tag}_{nm}_{i}.npy"), t.detach().cpu().numpy())
+
     for i in range(STEPS):
+        if a.mode == "single":
+            # start from the DP run's state before its step i
+            src = a.src
+            with torch.no_grad():
+                flat.p32.copy_(torch.from_numpy(np.load(os.path.join(src, f"pre_p32_{i}.npy"))).to(dev))
+                flat.p64.copy_(torch.from_numpy(np.load(os.path.join(src, f"pre_p64_{i}.npy"))).to(dev))
+                for j, b in enumerate(opt._bufs):
+                    b.copy_(torch.from_numpy(np.load(os.path.join(src, f"pre_buf{j}_{i}.npy"))).to(dev))
+            opt.steps = i
+        elif save:
+            dump("pre", i, {"p32": flat.p32, "p64": flat.p64, **{f"buf{j}": b for j, b in enumerate(opt._bufs)}})
         load(i)
         step()
         torch.cuda.synchronize()
-        if a.mode == "single" or a.rank == 0:
-            np.save(os.path.join(a.out, f"g32_{i}.npy"), flat.g32.cpu().numpy())
-            np.save(os.path.join(a.out, f"g64_{i}.npy"), flat.g64.cpu().numpy())
-    if a.mode == "single" or a.rank == 0:
-        np.save(os.path.join(a.out, "p32.npy"), flat.p32.cpu().numpy())
-        np.save(os.path.join(a.out, "p64.npy"), flat.p64.cpu().numpy())
+        if save:
+            dump("post", i, {"g32": flat.g32, "g64": flat.g64, "p32": flat.p32, "p64": flat.p64})
     if world > 1:
         # every rank holds the same parameters
         t = flat.p32.clone()

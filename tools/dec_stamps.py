@@ -40,6 +40,14 @@ def main():
             arr = w[:, 4]
             print(f"  it {it:2d}: " + "  ".join(f"{n} {np.mean(x):6.0f} (max {np.max(x):6.0f})" for n, x in zip(names, seg))
                   + f"  arrival spread {arr.max() - arr.min():6.0f}  total {np.mean(w[:, 5] - w[:, 1]):6.0f}")
+        # per wave, relative to the earliest loop-top stamp of the iteration
+        for it in valid[2:4]:
+            w = b[blk, :, it]
+            t0 = w[:, 1].min()
+            print(f"  it {it} per wave (cycles from the first wave's loop top): top / pass2 end / pass1 end / "
+                  "tables end / barrier in / out")
+            for wv in range(w.shape[0]):
+                print("    w%2d " % wv + " ".join("%6d" % (w[wv, ph] - t0) for ph in range(1, 6)))
 
 
 if __name__ == "__main__":
