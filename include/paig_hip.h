@@ -258,6 +258,12 @@ int paig_stn_fwd(const float* U, const float* theta, float* out, int N, int C, i
                  void* stream);
 int paig_stn_bwd(const float* U, const float* theta, const float* dout, float* dU, float* dtheta, int N, int C,
                  int Hi, int Wi, int Ho, int Wo, void* stream);
+/* the same for a float64 theta (affine_grid in fp64, the grid cast to fp32
+ * before sampling, dtheta summed in fp64; stn.py:12-14 with a double theta) */
+int paig_stn_fwd_f64(const float* U, const double* theta, float* out, int N, int C, int Hi, int Wi, int Ho, int Wo,
+                     void* stream);
+int paig_stn_bwd_f64(const float* U, const double* theta, const float* dout, float* dU, double* dtheta, int N, int C,
+                     int Hi, int Wi, int Ho, int Wo, void* stream);
 /* d *= (y > 0) in place (n elements) */
 int paig_relu_mask(const float* y, float* d, long long n, void* stream);
 

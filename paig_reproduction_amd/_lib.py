@@ -82,6 +82,8 @@ SIGNATURES = {
     "paig_decoder_parts": (I, [P, LL, P, P, P, P, P, I, I, I, I, P]),
     "paig_stn_fwd": (I, [P, P, P, I, I, I, I, I, I, P]),
     "paig_stn_bwd": (I, [P, P, P, P, P, I, I, I, I, I, I, P]),
+    "paig_stn_fwd_f64": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "paig_stn_bwd_f64": (I, [P, P, P, P, P, I, I, I, I, I, I, P]),
     "paig_relu_mask": (I, [P, P, LL, P]),
     "paig_loss_reduce": (I, [P, P, I, I, I, I, F32, P, P, P, P]),
     "paig_loss_bwd": (I, [P, P, P, F32, P, P, I, I, I, I, P]),

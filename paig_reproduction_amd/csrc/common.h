@@ -205,6 +205,19 @@ __device__ __forceinline__ void row_sums_dpp_d(double* v) {
 #pragma unroll
   for (int i = 0; i < N; ++i) v[i] += dpp_d<0x140>(v[i]);
 }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// fp32 wave sum through DPP row reductions + 4 readlanes (wave-uniform result)
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  const auto rl = [&](int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
+  return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);

@@ -1525,7 +1525,9 @@ __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
   __shared__ float red[WPREP_T];
   __shared__ int ex[16];
   const int cl = tid & 15, co = nt * 16 + cl;
+  // (unrolled: the loads of one thread are independent, keep 8 in flight)
   float m = 0.f;
+#pragma unroll 8
   for (int i = tid >> 4; i < KC * 8; i += WPREP_T / 16) m = fmaxf(m, fabsf(wv(i >> 3, i & 7, co)));
   red[tid] = m;
   __syncthreads();
@@ -1540,6 +1542,7 @@ __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
   short* img = reinterpret_cast<short*>(jb.out + HDR);
   // this block's entries: (s, lane) -> value index t = ((s - s0) * 64 + lane) * 8 + j
   const int ns = NS - s0 < WPREP_S ? NS - s0 : WPREP_S;
+#pragma unroll 8
   for (int t = tid; t < ns * 64 * 8; t += WPREP_T) {
     const int j = t & 7, ln = (t >> 3) & 63, s = s0 + (t >> 9);
     const int kc = 4 * s + (ln >> 4), c = nt * 16 + (ln & 15);

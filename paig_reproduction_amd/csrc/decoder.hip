@@ -630,6 +630,60 @@ __device__ __forceinline__ int gslot(int j) { return (j & 1) * (H / 2) + (j >> 1
 struct DecCursor {
   int f, pq, pr, tq, tr;
 };
+struct DecFrames {
+  PosView pos;
+  FView tgt;
+  int R, Rl;
+  bool grouped;
+  __device__ DecFrames(PosView p, FView t, int rl) : pos(p), tgt(t), R(p.grp), Rl(rl) {
+    grouped = R > 0 && Rl > 0 && Rl < R;
+  }
+  __device__ int live(int F) const { return grouped ? (F / R) * Rl : F; }
+  __device__ DecCursor at(int n) const {
+    DecCursor c;
+    if (grouped) {
+      c.pq = c.tq = n / Rl;
+      c.pr = c.tr = n % Rl;
+      c.f = c.pq * R + c.pr;
+    } else {
+      c.f = n;
+      c.pq = pos.grp > 0 ? n / pos.grp : 0;
+      c.pr = pos.grp > 0 ? n % pos.grp : 0;
+      c.tq = tgt.grp > 0 ? n / tgt.grp : 0;
+      c.tr = tgt.grp > 0 ? n % tgt.grp : 0;
+    }
+    return c;
+  }
+  __device__ DecCursor next(DecCursor c) const {
+    if (grouped) {
+      if (++c.pr == Rl) {
+        c.pr = 0;
+        ++c.pq;
+      }
+      c.tq = c.pq;
+      c.tr = c.pr;
+      c.f = c.pq * R + c.pr;
+    } else {
+      ++c.f;
+      if (pos.grp > 0 && ++c.pr == pos.grp) {
+        c.pr = 0;
+        ++c.pq;
+      }
+      if (tgt.grp > 0 && ++c.tr == tgt.grp) {
+        c.tr = 0;
+        ++c.tq;
+      }
+    }
+    return c;
+  }
+  __device__ const float* pos_of(const DecCursor& c) const {
+    return pos.grp > 0 ? pos.p + (long long)c.pq * pos.outer + (long long)c.pr * pos.inner
+                       : pos.p + (long long)c.f * pos.inner;
+  }
+  __device__ const float* tgt_of(const DecCursor& c) const {
+    return tgt.grp > 0 ? tgt.p + (long long)c.tq * tgt.fs + (long long)c.tr * tgt.gs : tgt.p + (long long)c.f * tgt.fs;
+  }
+};
 
 // separable bilinear setup of one axis: tap index (padded source), masked
 // weights of the two taps and their d/dcoord (0 for out-of-range taps)
@@ -734,50 +788,11 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   const int nf = first < NL ? (NL - first < FPB ? NL - first : FPB) : 0;
 
   // ---- frame cursors (wave-uniform)
-  auto cur_at = [&](int n) {
-    DecCursor c;
-    if (grouped) {
-      c.pq = c.tq = n / Rl;
-      c.pr = c.tr = n % Rl;
-      c.f = c.pq * R + c.pr;
-    } else {
-      c.f = n;
-      c.pq = pos.grp > 0 ? n / pos.grp : 0;
-      c.pr = pos.grp > 0 ? n % pos.grp : 0;
-      c.tq = tgt.grp > 0 ? n / tgt.grp : 0;
-      c.tr = tgt.grp > 0 ? n % tgt.grp : 0;
-    }
-    return c;
-  };
-  auto advance = [&](DecCursor c) {
-    if (grouped) {
-      if (++c.pr == Rl) {
-        c.pr = 0;
-        ++c.pq;
-      }
-      c.tq = c.pq;
-      c.tr = c.pr;
-      c.f = c.pq * R + c.pr;
-    } else {
-      ++c.f;
-      if (pos.grp > 0 && ++c.pr == pos.grp) {
-        c.pr = 0;
-        ++c.pq;
-      }
-      if (tgt.grp > 0 && ++c.tr == tgt.grp) {
-        c.tr = 0;
-        ++c.tq;
-      }
-    }
-    return c;
-  };
-  auto pos_of = [&](const DecCursor& c) {
-    return pos.grp > 0 ? pos.p + (long long)c.pq * pos.outer + (long long)c.pr * pos.inner
-                       : pos.p + (long long)c.f * pos.inner;
-  };
-  auto tgt_of = [&](const DecCursor& c) {
-    return tgt.grp > 0 ? tgt.p + (long long)c.tq * tgt.fs + (long long)c.tr * tgt.gs : tgt.p + (long long)c.f * tgt.fs;
-  };
+  const DecFrames FR(pos, tgt, Rl);
+  auto cur_at = [&](int n) { return FR.at(n); };
+  auto advance = [&](DecCursor c) { return FR.next(c); };
+  auto pos_of = [&](const DecCursor& c) { return FR.pos_of(c); };
+  auto tgt_of = [&](const DecCursor& c) { return FR.tgt_of(c); };
 
   // ---- prologue: frame 0's loads first (their latency overlaps the staging below)
   float bgv[PS][3], gbg[PS][3], tn[PS][3];
@@ -1145,10 +1160,189 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decoder forward for the headline shapes ((K, H) = (2, 32), (3, 36)).
+// HBM-bound: per frame the target is read and the decoded frame written
+// (2 x 3 H W floats); everything else (sources, axis tables) lives in LDS.
+//   * each thread owns 4 consecutive pixels of one row: the row's axis table
+//     entry is shared by the 4, and targets / outputs / background move as one
+//     16-byte access per channel;
+//   * a block walks a contiguous run of frames, software-pipelined over ONE
+//     barrier per frame: iteration it forms the axis tables of frame it+1 (from
+//     positions loaded an iteration earlier), issues frame it+1's target loads
+//     and frame it+2's position loads, samples / composites frame it and writes
+//     it, and sums its SSE per wave (finished by thread 0 next iteration);
+//   * sources are sampled as in the backward (padded float4 texel image,
+//     separable tap weights), two planes per packed fp32 op.
+template <int K, int H>
+struct DecFw {
+  static constexpr int h = H / 2, hp = h + 2, HW = H * H;
+  static constexpr int GPR = H / 4, NGRP = H * GPR;        // 4-pixel groups per row / frame
+  static constexpr int NT = (NGRP + 63) / 64 * 64, NW = NT / 64;
+  static constexpr int NC = K * 2 * H;                      // axis table entries
+  static_assert(H % 4 == 0 && NC <= NT, "decoder forward geometry");
+};
+
+template <int K, int H>
+__global__ void __launch_bounds__((DecFw<K, H>::NT))
+dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse, int F, int FPB) {
+  using C = DecFw<K, H>;
+  constexpr int h = C::h, hp = C::hp, HW = C::HW, GPR = C::GPR, NC = C::NC, NW = C::NW;
+  __shared__ float4 SRC[K][hp * hp];    // (template + 5, sigmoid(content) x 3), zero border
+  __shared__ float4 AX[2][K][2][H];     // w0, w1, padded first-tap index (bits), -
+  __shared__ float RED[2][NW];          // per-wave SSE partials
+  __shared__ double BC[H];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int first = blockIdx.x * FPB;
+  const int nf = first < F ? (F - first < FPB ? F - first : FPB) : 0;
+  if (nf == 0) return;   // block-uniform
+  const DecFrames FR(pos, tgt, 0);
+  const bool px = tid < C::NGRP;
+  const int i = px ? tid / GPR : 0, p = px ? i * H + (tid % GPR) * 4 : 0;
+  const bool is_c = tid < NC;
+  const int ck = is_c ? tid / (2 * H) : 0, cax = is_c ? (tid / H) & 1 : 0, cj = is_c ? tid % H : 0;
+  const bool has_t = sse != nullptr;
+
+  auto ld4 = [&](const float* b) { return *reinterpret_cast<const float4*>(b); };
+  float4 tn[3], bgv[3];
+  auto fetch = [&](const DecCursor& c, float4* t) {
+    if (!has_t || !px) return;
+    const float* tf = FR.tgt_of(c) + p;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) t[ch] = ld4(tf + ch * HW);
+  };
+  DecCursor ccur = FR.at(first);
+  DecCursor c1 = nf > 1 ? FR.next(ccur) : ccur;
+  DecCursor c2 = nf > 2 ? FR.next(c1) : c1;
+  fetch(ccur, tn);
+  float p0 = 0.f, ppos = 0.f;
+  if (is_c) {
+    p0 = FR.pos_of(ccur)[2 * ck + cax];
+    ppos = FR.pos_of(c1)[2 * ck + cax];
+  }
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) bgv[ch] = px ? ld4(S.bg + ch * HW + p) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int t = tid; t < K * hp * hp; t += C::NT) {
+    const int k = t / (hp * hp), q = t % (hp * hp), y = q / hp - 1, x = q % hp - 1;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)h) {
+      const int o = y * h + x, hh = h * h;
+      v.x = S.tmpl[k * hh + o] + 5.f;
+      v.y = 1.f / (1.f + expf(-S.cont[(k * 3 + 0) * hh + o]));
+      v.z = 1.f / (1.f + expf(-S.cont[(k * 3 + 1) * hh + o]));
+      v.w = 1.f / (1.f + expf(-S.cont[(k * 3 + 2) * hh + o]));
+    }
+    SRC[k][q] = v;
+  }
+  for (int j = tid; j < H; j += C::NT) BC[j] = base_coord(j, H);
+  auto tables = [&](float l, int slot) {
+    if (is_c) {
+      const Ax x = axis(src_coord(BC[cj], (double)(((float)H / 2.f - l) / (float)h), h), h);
+      AX[slot][ck][cax][cj] = make_float4(x.w0, x.w1, __int_as_float(x.c), 0.f);
+    }
+  };
+  __syncthreads();   // SRC, BC
+  tables(p0, 0);
+  __syncthreads();
+
+  DecCursor cprev = ccur;
+  for (int it = 0; it < nf; ++it) {
+    if (it + 1 < nf) tables(ppos, (it + 1) & 1);
+    if (is_c) ppos = FR.pos_of(c2)[2 * ck + cax];
+    float4 tq[3];
+    if (it + 1 < nf) fetch(c1, tq);
+    if (has_t && it >= 1 && tid == 0) {   // SSE of frame it-1 (partials before the last barrier)
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) a += RED[(it - 1) & 1][w];
+      sse[cprev.f] = a;
+    }
+    const int sl = it & 1;
+    float acc = 0.f;
+    if (px) {
+      float o[4][3];
+      float4 ay[K];
+      int rb[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        ay[k] = AX[sl][k][1][i];
+        rb[k] = __float_as_int(ay[k].z) * hp;
+      }
+      const float bq[3][4] = {{bgv[0].x, bgv[0].y, bgv[0].z, bgv[0].w},
+                              {bgv[1].x, bgv[1].y, bgv[1].z, bgv[1].w},
+                              {bgv[2].x, bgv[2].y, bgv[2].z, bgv[2].w}};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float sv[K][4];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float4 ax = AX[sl][k][0][(p % H) + q];
+          const int bs = rb[k] + __float_as_int(ax.z);
+          const float4 a = SRC[k][bs], b = SRC[k][bs + 1], c = SRC[k][bs + hp], d = SRC[k][bs + hp + 1];
+          pf32x2 v0, v1, dx, dy;
+          samp_pair<false>(pf32x2{a.x, a.y}, pf32x2{b.x, b.y}, pf32x2{c.x, c.y}, pf32x2{d.x, d.y}, ax, ay[k], v0, dx, dy);
+          samp_pair<false>(pf32x2{a.z, a.w}, pf32x2{b.z, b.w}, pf32x2{c.z, c.w}, pf32x2{d.z, d.w}, ax, ay[k], v1, dx, dy);
+          sv[k][0] = v0.x;
+          sv[k][1] = v0.y;
+          sv[k][2] = v1.x;
+          sv[k][3] = v1.y;
+        }
+        const float bg3[3] = {bq[0][q], bq[1][q], bq[2][q]};
+        float m[K + 1];
+        blend<K>(sv, bg3, o[q], m);
+      }
+      float* of = out.frame(ccur.f) + p;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        *reinterpret_cast<float4*>(of + ch * HW) = make_float4(o[0][ch], o[1][ch], o[2][ch], o[3][ch]);
+        if (has_t) {
+          const float tv[4] = {tn[ch].x, tn[ch].y, tn[ch].z, tn[ch].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float d = tv[q] - o[q][ch];
+            acc = fmaf(d, d, acc);
+          }
+        }
+      }
+    }
+    if (has_t) {
+      acc = wave_sum_dpp(acc);
+      if (lane == 0) RED[sl][wv] = acc;
+    }
+    cprev = ccur;
+    ccur = c1;
+    c1 = c2;
+    if (it + 3 < nf) c2 = FR.next(c2);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) tn[ch] = tq[ch];
+    __syncthreads();
+  }
+  if (has_t && tid == 0) {
+    float a = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) a += RED[(nf - 1) & 1][w];
+    sse[cprev.f] = a;
+  }
+}
+
 template <int K>
 static int dec_launch_fwd(PosView pv, Src S, FViewW out, FView tgt, float* sse, int F, int h, int H, hipStream_t st) {
   const int lds = (K * h * h * 4) * 4;
   int g = (F + 1) / 2 < 1024 ? (F + 1) / 2 : 1024;   // >= 2 frames per block: source staging amortised
+  // the one-barrier-per-frame kernel: 16-byte accesses need 16-byte aligned frames
+  const bool al = ((uintptr_t)out.p | (uintptr_t)S.bg) % 16 == 0 && out.fs % 4 == 0 &&
+                  (sse == nullptr || ((uintptr_t)tgt.p % 16 == 0 && tgt.fs % 4 == 0 && tgt.gs % 4 == 0));
+  if (al && H == 2 * h && ((K == 2 && H == 32) || (K == 3 && H == 36))) {
+    const int fpb = cdiv(F, g);
+    g = cdiv(F, fpb);
+    if constexpr (K == 2)
+      hipLaunchKernelGGL((dec_fwd_cu_k<2, 32>), dim3(g), dim3(DecFw<2, 32>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
+    else
+      hipLaunchKernelGGL((dec_fwd_cu_k<3, 36>), dim3(g), dim3(DecFw<3, 36>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
+    PAIG_CHECK_LAUNCH();
+    return 0;
+  }
   if constexpr (K == 2) {
     if (H == 32) {
       hipLaunchKernelGGL((dec_fwd_reg_k<2, 32>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F);
@@ -1215,22 +1409,27 @@ dec_parts_k(PosView pos, Src S, float* __restrict__ contents, float* __restrict_
 // General affine spatial transformer (stn(), nn/network/stn.py:5-16: aten
 // affine_grid + grid_sample, bilinear, zeros padding, align_corners=False)
 // for any theta [N][2][3]: U [N][C][Hi][Wi] -> O [N][C][Ho][Wo].  The grid is
-// formed in fp32 (the reference casts it with .float() before sampling).
-__device__ __forceinline__ float ag_base(int j, int n) {   // affine_grid linspace * (n-1)/n, fp32
-  const float step = 2.f / (float)(n - 1 > 0 ? n - 1 : 1);
-  const float v = n == 1 ? 0.f : ((j < n / 2) ? -1.f + step * (float)j : 1.f - step * (float)(n - 1 - j));
-  return v * (float)(n - 1) / (float)n;
+// formed in theta's precision T, as affine_grid does (fp64 for the fp64
+// physics-derived thetas, Q9), and cast to fp32 before sampling (the
+// reference's grid.float()); the theta gradient sums in T (affine_grid's
+// backward), from fp32 grid gradients.
+template <typename T>
+__device__ __forceinline__ T ag_base(int j, int n) {   // affine_grid linspace * (n-1)/n
+  const T step = T(2) / (T)(n - 1 > 0 ? n - 1 : 1);
+  const T v = n == 1 ? T(0) : ((j < n / 2) ? T(-1) + step * (T)j : T(1) - step * (T)(n - 1 - j));
+  return v * (T)(n - 1) / (T)n;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-stn_fwd_k(const float* __restrict__ U, const float* __restrict__ th, float* __restrict__ O, int N, int C, int Hi,
-          int Wi, int Ho, int Wo) {
+stn_fwd_k(const float* __restrict__ U, const T* __restrict__ th, float* __restrict__ O, int N, int C, int Hi, int Wi,
+          int Ho, int Wo) {
   const long long total = (long long)N * Ho * Wo;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(t / (Ho * Wo)), p = (int)(t % (Ho * Wo)), i = p / Wo, j = p % Wo;
-    const float* a = th + n * 6;
-    const float xb = ag_base(j, Wo), yb = ag_base(i, Ho);
-    const float gx = a[0] * xb + a[1] * yb + a[2], gy = a[3] * xb + a[4] * yb + a[5];
+    const T* a = th + n * 6;
+    const T xb = ag_base<T>(j, Wo), yb = ag_base<T>(i, Ho);
+    const float gx = (float)(a[0] * xb + a[1] * yb + a[2]), gy = (float)(a[3] * xb + a[4] * yb + a[5]);
     const float ix = ((gx + 1.f) * (float)Wi - 1.f) * 0.5f, iy = ((gy + 1.f) * (float)Hi - 1.f) * 0.5f;
     const float fx0 = floorf(ix), fy0 = floorf(iy);
     const int x0 = (int)fx0, y0 = (int)fy0;
@@ -1251,16 +1450,17 @@ stn_fwd_k(const float* __restrict__ U, const float* __restrict__ th, float* __re
 // backward: dU by atomics (scatter of the bilinear weights; this general
 // helper is off the training path), dtheta per sample by a block reduction
 // (one block per sample, deterministic)
+template <typename T>
 __global__ void __launch_bounds__(256)
-stn_bwd_k(const float* __restrict__ U, const float* __restrict__ th, const float* __restrict__ dO, float* __restrict__ dU,
-          float* __restrict__ dth, int N, int C, int Hi, int Wi, int Ho, int Wo) {
+stn_bwd_k(const float* __restrict__ U, const T* __restrict__ th, const float* __restrict__ dO, float* __restrict__ dU,
+          T* __restrict__ dth, int N, int C, int Hi, int Wi, int Ho, int Wo) {
   const int n = blockIdx.x;
-  const float* a = th + n * 6;
-  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const T* a = th + n * 6;
+  T acc[6] = {T(0), T(0), T(0), T(0), T(0), T(0)};
   for (int p = threadIdx.x; p < Ho * Wo; p += blockDim.x) {
     const int i = p / Wo, j = p % Wo;
-    const float xb = ag_base(j, Wo), yb = ag_base(i, Ho);
-    const float gx = a[0] * xb + a[1] * yb + a[2], gy = a[3] * xb + a[4] * yb + a[5];
+    const T xb = ag_base<T>(j, Wo), yb = ag_base<T>(i, Ho);
+    const float gx = (float)(a[0] * xb + a[1] * yb + a[2]), gy = (float)(a[3] * xb + a[4] * yb + a[5]);
     const float ix = ((gx + 1.f) * (float)Wi - 1.f) * 0.5f, iy = ((gy + 1.f) * (float)Hi - 1.f) * 0.5f;
     const float fx0 = floorf(ix), fy0 = floorf(iy);
     const int x0 = (int)fx0, y0 = (int)fy0;
@@ -1282,8 +1482,9 @@ stn_bwd_k(const float* __restrict__ U, const float* __restrict__ th, const float
           if (xs[q] >= 0 && xs[q] < Wi && ys[q] >= 0 && ys[q] < Hi) atomicAdd(du + ys[q] * Wi + xs[q], g * w[q]);
       }
     }
-    // ix = ((gx + 1) Wi - 1) / 2 -> dgx = dix * Wi / 2 ; gx = a0 xb + a1 yb + a2
-    const float dgx = dix * (float)Wi * 0.5f, dgy = diy * (float)Hi * 0.5f;
+    // ix = ((gx + 1) Wi - 1) / 2 -> dgx = dix * Wi / 2 (fp32, grid_sample's
+    // grid gradient); gx = a0 xb + a1 yb + a2 in T
+    const T dgx = (T)(dix * (float)Wi * 0.5f), dgy = (T)(diy * (float)Hi * 0.5f);
     acc[0] += dgx * xb;
     acc[1] += dgx * yb;
     acc[2] += dgx;
@@ -1291,16 +1492,18 @@ stn_bwd_k(const float* __restrict__ U, const float* __restrict__ th, const float
     acc[4] += dgy * yb;
     acc[5] += dgy;
   }
-  __shared__ float red[4][6];
+  __shared__ T red[4][6];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
-    const float v = wave_sum(acc[q]);
+    T v = acc[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) red[wv][q] = v;
   }
   __syncthreads();
   if (threadIdx.x < 6 && dth) {
-    float v = 0.f;
+    T v = T(0);
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += red[w][threadIdx.x];
     dth[n * 6 + threadIdx.x] = v;
   }
@@ -1416,6 +1619,29 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
 
 }  // extern "C"
 
+template <typename T>
+static int stn_fwd(const float* U, const T* theta, float* out, int N, int C, int Hi, int Wi, int Ho, int Wo,
+                   void* stream) {
+  if (N <= 0) return 0;
+  PAIG_REQUIRE(C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "stn_fwd: bad shape");
+  const long long total = (long long)N * Ho * Wo;
+  const int g = (int)(total / 256 + 1 < 8192 ? total / 256 + 1 : 8192);
+  hipLaunchKernelGGL(stn_fwd_k<T>, dim3(g), dim3(256), 0, (hipStream_t)stream, U, theta, out, N, C, Hi, Wi, Ho, Wo);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename T>
+static int stn_bwd(const float* U, const T* theta, const float* dout, float* dU, T* dtheta, int N, int C, int Hi,
+                   int Wi, int Ho, int Wo, void* stream) {
+  if (N <= 0) return 0;
+  PAIG_REQUIRE(C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "stn_bwd: bad shape");
+  hipLaunchKernelGGL(stn_bwd_k<T>, dim3(N), dim3(256), 0, (hipStream_t)stream, U, theta, dout, dU, dtheta, N, C, Hi,
+                     Wi, Ho, Wo);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" {
 
 int paig_decoder_parts(const float* pos, long long pos_inner, const float* tmpl, const float* cont, const float* bg,
@@ -1439,23 +1665,22 @@ int paig_decoder_parts(const float* pos, long long pos_inner, const float* tmpl,
 
 int paig_stn_fwd(const float* U, const float* theta, float* out, int N, int C, int Hi, int Wi, int Ho, int Wo,
                  void* stream) {
-  if (N <= 0) return 0;
-  PAIG_REQUIRE(C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "stn_fwd: bad shape");
-  const long long total = (long long)N * Ho * Wo;
-  const int g = (int)(total / 256 + 1 < 8192 ? total / 256 + 1 : 8192);
-  hipLaunchKernelGGL(stn_fwd_k, dim3(g), dim3(256), 0, (hipStream_t)stream, U, theta, out, N, C, Hi, Wi, Ho, Wo);
-  PAIG_CHECK_LAUNCH();
-  return 0;
+  return stn_fwd<float>(U, theta, out, N, C, Hi, Wi, Ho, Wo, stream);
 }
 
 int paig_stn_bwd(const float* U, const float* theta, const float* dout, float* dU, float* dtheta, int N, int C,
                  int Hi, int Wi, int Ho, int Wo, void* stream) {
-  if (N <= 0) return 0;
-  PAIG_REQUIRE(C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "stn_bwd: bad shape");
-  hipLaunchKernelGGL(stn_bwd_k, dim3(N), dim3(256), 0, (hipStream_t)stream, U, theta, dout, dU, dtheta, N, C, Hi, Wi,
-                     Ho, Wo);
-  PAIG_CHECK_LAUNCH();
-  return 0;
+  return stn_bwd<float>(U, theta, dout, dU, dtheta, N, C, Hi, Wi, Ho, Wo, stream);
+}
+
+int paig_stn_fwd_f64(const float* U, const double* theta, float* out, int N, int C, int Hi, int Wi, int Ho, int Wo,
+                     void* stream) {
+  return stn_fwd<double>(U, theta, out, N, C, Hi, Wi, Ho, Wo, stream);
+}
+
+int paig_stn_bwd_f64(const float* U, const double* theta, const float* dout, float* dU, double* dtheta, int N, int C,
+                     int Hi, int Wi, int Ho, int Wo, void* stream) {
+  return stn_bwd<double>(U, theta, dout, dU, dtheta, N, C, Hi, Wi, Ho, Wo, stream);
 }
 
 }  // extern "C"

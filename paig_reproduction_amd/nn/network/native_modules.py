@@ -215,12 +215,18 @@ def velocity_forward(mod, inp):
 class _STN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, U, theta, out_size):
-        U, th = _f32(U), _f32(theta.reshape(-1, 6))
+        # a float64 theta keeps its precision for the grid (affine_grid in
+        # theta's dtype, cast to fp32 before sampling: stn.py:12-14)
+        f64 = theta.dtype == torch.float64
+        U = _f32(U)
+        require_device(theta)
+        th = theta.detach().reshape(-1, 6).to(torch.float64 if f64 else torch.float32).contiguous()
         N, C, Hi, Wi = U.shape
         assert th.shape[0] == N, ("stn: U and theta batch differ", N, th.shape[0])
         Ho, Wo = int(out_size[0]), int(out_size[1])
         out = torch.empty(N, C, Ho, Wo, device=U.device)
-        lib().paig_stn_fwd(ptr(U), ptr(th), ptr(out), N, C, Hi, Wi, Ho, Wo, stream_handle(U.device))
+        fwd = lib().paig_stn_fwd_f64 if f64 else lib().paig_stn_fwd
+        fwd(ptr(U), ptr(th), ptr(out), N, C, Hi, Wi, Ho, Wo, stream_handle(U.device))
         ctx.save_for_backward(U, th)
         ctx.tshape = theta.shape
         ctx.dtypes = (theta.dtype,)
@@ -233,8 +239,9 @@ class _STN(torch.autograd.Function):
         Ho, Wo = dout.shape[-2:]
         dU = torch.zeros_like(U) if ctx.needs_input_grad[0] else None
         dth = torch.empty_like(th) if ctx.needs_input_grad[1] else None
-        lib().paig_stn_bwd(ptr(U), ptr(th), ptr(dout.float().contiguous()), ptr(dU), ptr(dth), N, C, Hi, Wi, Ho, Wo,
-                           stream_handle(U.device))
+        bwd = lib().paig_stn_bwd_f64 if th.dtype == torch.float64 else lib().paig_stn_bwd
+        bwd(ptr(U), ptr(th), ptr(dout.float().contiguous()), ptr(dU), ptr(dth), N, C, Hi, Wi, Ho, Wo,
+            stream_handle(U.device))
         if dth is not None:
             dth = dth.view(ctx.tshape).to(ctx.dtypes[0])
         return dU, dth, None

@@ -168,3 +168,79 @@ def test_decoder_bwd_deterministic():
     a, b = _run(*args), _run(*args)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+# ---------------------------------------------------------------- forward
+def _fwd(K, H, tmpl, cont, bg, pos_view, tgt_view, F_, out_off=0):
+    """paig_decoder_fwd: (out [F, 3, H, W], sse [F]); out_off shifts the
+    output by that many floats (a misaligned view takes the generic kernel)."""
+    lib = L()
+    st = torch.cuda.current_stream().cuda_stream
+    td, cd, bd = tmpl.to(DEV).contiguous(), cont.to(DEV).contiguous(), bg.to(DEV).contiguous()
+    fr = 3 * H * H
+    buf = torch.full((F_ * fr + out_off,), float("nan"), device=DEV)
+    sse = torch.full((F_,), float("nan"), device=DEV)
+    rc = lib.paig_decoder_fwd(pos_view[0], pos_view[1], pos_view[2], pos_view[3], td.data_ptr(), cd.data_ptr(),
+                              bd.data_ptr(), buf.data_ptr() + 4 * out_off, fr, tgt_view[0], tgt_view[1], tgt_view[2],
+                              tgt_view[3], sse.data_ptr() if tgt_view[0] else None, F_, K, H // 2, H, st)
+    assert rc == 0, lib.paig_last_error()
+    torch.cuda.synchronize()
+    return buf[out_off:].view(F_, 3, H, H).cpu(), sse.cpu()
+
+
+def _fwd_reference(K, H, tmpl, cont, bg, pos, tgt):
+    cfg = types.SimpleNamespace(n_objs=K, tmpl=H // 2, size=H)
+    joint = torch.cat([tmpl.repeat(1, 3, 1, 1) + 5, torch.sigmoid(cont)], 1)
+    out = O.st_decoder(cfg, joint, bg, pos)
+    return out, ((out - tgt) ** 2).sum((1, 2, 3))
+
+
+@pytest.mark.parametrize("K,H", SHAPES)
+@pytest.mark.parametrize("F_", [1, 2, 7, 37, 2051])
+def test_decoder_fwd_ungrouped(K, H, F_):
+    """Every frame decoded and its SSE vs the target (the reconstruction
+    decode); 2051 frames: several frames per block with a ragged last run."""
+    tmpl, cont, bg = _sources(K, H, 5 * K + H)
+    pos = _positions(F_, K, H, 3 + F_)
+    tgt = torch.rand(F_, 3, H, H, generator=torch.Generator().manual_seed(F_))
+    pd, td = pos.to(DEV).contiguous(), tgt.to(DEV).contiguous()
+    out, sse = _fwd(K, H, tmpl, cont, bg, (pd.data_ptr(), 0, 2 * K, 0), (td.data_ptr(), 3 * H * H, 0, 0), F_)
+    ro, rs = _fwd_reference(K, H, tmpl, cont, bg, pos, tgt)
+    assert (out - ro).abs().max().item() <= 1e-5
+    assert rel_err(sse, rs) <= 1e-5
+
+
+@pytest.mark.parametrize("K,H", SHAPES)
+@pytest.mark.parametrize("B,R", [(5, 9), (3, 46), (23, 16)])
+def test_decoder_fwd_grouped(K, H, B, R):
+    """The rollout layout: positions pvs[B][R+1][2K] from step 1, targets
+    input[B][T][3][H][W] from frame ins."""
+    ins, T = 2, R + 2
+    tmpl, cont, bg = _sources(K, H, 11 * K + R)
+    pvs = torch.zeros(B, R + 1, 2 * K)
+    pvs[:, 1:] = _positions(B * R, K, H, B * R).view(B, R, 2 * K)
+    x = torch.rand(B, T, 3, H, H, generator=torch.Generator().manual_seed(R))
+    pd, xd = pvs.to(DEV).contiguous(), x.to(DEV).contiguous()
+    fr = 3 * H * H
+    out, sse = _fwd(K, H, tmpl, cont, bg, (pd.data_ptr() + 2 * K * 4, (R + 1) * 2 * K, 2 * K, R),
+                    (xd.data_ptr() + ins * fr * 4, T * fr, R, fr), B * R)
+    ro, rs = _fwd_reference(K, H, tmpl, cont, bg, pvs[:, 1:].reshape(B * R, 2 * K),
+                            x[:, ins:].reshape(B * R, 3, H, H))
+    assert (out - ro).abs().max().item() <= 1e-5
+    assert rel_err(sse, rs) <= 1e-5
+
+
+@pytest.mark.parametrize("K,H", SHAPES[:2])
+def test_decoder_fwd_aligned_and_generic_agree(K, H):
+    """A 16-byte-misaligned output view takes the generic kernel: same frames
+    (to fp32 rounding) as the vectorized one; no target: SSE never written."""
+    F_ = 19
+    tmpl, cont, bg = _sources(K, H, 2)
+    pos = _positions(F_, K, H, 8)
+    pd = pos.to(DEV).contiguous()
+    a, sa = _fwd(K, H, tmpl, cont, bg, (pd.data_ptr(), 0, 2 * K, 0), (0, 0, 0, 0), F_)
+    b, _ = _fwd(K, H, tmpl, cont, bg, (pd.data_ptr(), 0, 2 * K, 0), (0, 0, 0, 0), F_, out_off=1)
+    assert torch.isnan(sa).all()
+    assert (a - b).abs().max().item() <= 1e-5
+    ro, _ = _fwd_reference(K, H, tmpl, cont, bg, pos, torch.zeros(F_, 3, H, H))
+    assert (a - ro).abs().max().item() <= 1e-5

@@ -19,23 +19,35 @@ from helpers import rel_err
 
 pytestmark = pytest.mark.gpu
 
-# (task, cell, seq_len, input_steps, pred_steps, frame size, batch): BASELINE.json configs
-FULL = [("spring_color", "spring_ode_cell", 50, 4, 6, 32, 100),
-        ("3bp_color", "gravity_ode_cell", 20, 4, 12, 36, 512),
-        ("mnist_spring_color", "spring_ode_cell", 12, 3, 7, 64, 256),
-        ("bouncing_balls", "bouncing_ode_cell", 100, 4, 6, 32, 1024)]
+# (task, cell, seq_len, input_steps, pred_steps, frame size, batch, conv_math): BASELINE.json configs
+# (#2 is spring_color in bf16 at B = 512)
+FULL = [("spring_color", "spring_ode_cell", 50, 4, 6, 32, 100, "split"),
+        ("spring_color", "spring_ode_cell", 50, 4, 6, 32, 512, "bf16"),
+        ("3bp_color", "gravity_ode_cell", 20, 4, 12, 36, 512, "split"),
+        ("mnist_spring_color", "spring_ode_cell", 12, 3, 7, 64, 256, "split"),
+        ("bouncing_balls", "bouncing_ode_cell", 100, 4, 6, 32, 1024, "split")]
+IDS = [f"{c[0]}_B{c[6]}_{c[7]}" for c in FULL]
 # ~3x the worst measured (round 2: 1.9e-6 mnist c15, <= 9.4e-7 elsewhere, 3bp included)
 GRAD_RTOL = 6e-6
+# bf16 operands are rounded per value (no data-dependent scales), so a half
+# batch rounds exactly as the full one; the sums only reassociate in fp32
+# accumulators, as in the split arithmetic
+GRAD_RTOL_BF16 = 2e-5
 
 
-def _setup(task, cell, seq_len, ins, pred, size, B):
+def _setup(task, cell, seq_len, ins, pred, size, B, conv_math):
     from paig_reproduction_amd.nn.datasets.synth import as_model_input, render_sequences
     from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     m = PhysicsNet(task, 100, 1, cell, seq_len, ins, pred, 3.0, False, True, size * size, "conv_encoder",
                    "conv_st_decoder", device=dev).to(dev)
-    x = torch.from_numpy(as_model_input(render_sequences(task, B, seq_len, seed=3))).to(dev)
+    m.conv_math = conv_math
+    # distinct sequences: 64 rendered (rendering seq 50 is slow on the host), tiled
+    n = min(B, 64)
+    u8 = render_sequences(task, n, seq_len, seed=3)
+    u8 = np.concatenate([u8] * (B // n) + ([u8[:B % n]] if B % n else []), 0)
+    x = torch.from_numpy(as_model_input(u8)).to(dev)
     return m, x
 
 
@@ -49,7 +61,7 @@ def _step(m, x):
     return [float(v.detach()) for v in (loss, extrap, recons)], grads
 
 
-@pytest.mark.parametrize("cfg", FULL, ids=[c[0] for c in FULL])
+@pytest.mark.parametrize("cfg", FULL, ids=IDS)
 def test_full_size_step_is_deterministic(cfg):
     m, x = _setup(*cfg)
     l1, g1 = _step(m, x)
@@ -61,7 +73,7 @@ def test_full_size_step_is_deterministic(cfg):
         assert torch.equal(g1[k], g2[k]), k
 
 
-@pytest.mark.parametrize("cfg", FULL, ids=[c[0] for c in FULL])
+@pytest.mark.parametrize("cfg", FULL, ids=IDS)
 def test_full_size_batch_halves_average(cfg):
     m, x = _setup(*cfg)
     B = x.shape[0]
@@ -69,7 +81,8 @@ def test_full_size_batch_halves_average(cfg):
     la, ga = _step(m, x[:B // 2].contiguous())
     lb, gb = _step(m, x[B // 2:].contiguous())
     chaotic = cfg[0] == "3bp_color"
-    lbar, gbar = (2e-3, GRAD_RTOL) if chaotic else (1e-5, GRAD_RTOL)
+    gbar = GRAD_RTOL_BF16 if cfg[7] == "bf16" else GRAD_RTOL
+    lbar = 2e-3 if chaotic else 1e-5
     for i, what in enumerate(("train", "extrap", "recons")):
         bar = 1e-5 if what == "recons" else lbar   # recons does not go through the rollout
         assert rel_err(np.float64(lf[i]), np.float64((la[i] + lb[i]) / 2)) <= bar, what

@@ -579,3 +579,63 @@ def test_conv_fused_pool(cin, cout, hw, mode):
     assert torch.equal(y0, y1)
     assert torch.equal(pool, ref)
     assert L().paig_conv2d_mfma_supported(0, cin, cout, 36, 36, 3, mode | 64) == 0   # 36-wide rows: no in-lane windows
+
+
+@pytest.mark.parametrize("R", [6, 46, 64, 65, 70])
+def test_rollout_spring_adjoint_scan_and_serial(R):
+    """paig_rollout_bwd for the spring cell: the Hillis-Steele scan adjoint
+    (R <= 64) and the serial one (R > 64) against autograd through a float64
+    restatement of the R-step rollout (oracle spring_cell, nn/network/
+    cells.py:31-51), with a loss on every step's positions and velocities:
+    d pos0, d vel0 and the physics-parameter gradients at 1e-4 normwise."""
+    from oracle import physics_oracle as O
+    B, D = 37, 4
+    g = torch.Generator().manual_seed(R)
+    # columns 0 and 1 are the spring's ends (Q3): keep them near the rest
+    # length 2 exp(equil) = 6 so the oscillation never passes n = 0, where
+    # d = x / (n + 1e-4) has a 1e4 slope and any fp32 trajectory decorrelates
+    # from the float64 one
+    pos0 = 16 + 2 * (torch.rand(B, D, generator=g) - 0.5)
+    sgn = torch.where(torch.rand(B, generator=g) < 0.5, -1.0, 1.0)
+    pos0[:, 0] = pos0[:, 1] + sgn * (6 + 2 * (torch.rand(B, generator=g) - 0.5))
+    vel0 = (torch.rand(B, D, generator=g) - 0.5)
+    dt = torch.tensor(0.3, dtype=torch.float32)
+    k = torch.tensor(np.log(4.0), dtype=torch.float64)
+    eq = torch.tensor(np.log(3.0), dtype=torch.float64)
+    dpos_roll = torch.randn(B, R, D, generator=g)
+    dpvs = torch.randn(B, R + 1, 2 * D, generator=g)
+    # reference (float64)
+    P = {"rollout_cell.dt": dt.double(), "rollout_cell.k": k.clone().requires_grad_(True),
+         "rollout_cell.equil": eq.clone().requires_grad_(True)}
+    p = pos0.double().requires_grad_(True)
+    v = vel0.double().requires_grad_(True)
+    loss = (dpvs[:, 0, :D].double() * p).sum() + (dpvs[:, 0, D:].double() * v).sum()
+    pc, vc = p, v
+    for t in range(R):
+        pc, vc = O.spring_cell(P, pc, vc)
+        loss = loss + (dpos_roll[:, t].double() * pc).sum() + (dpvs[:, t + 1, :D].double() * pc).sum() \
+            + (dpvs[:, t + 1, D:].double() * vc).sum()
+    loss.backward()
+    # HIP
+    dev = DEV
+    pvs = torch.empty(B, R + 1, 2 * D, device=dev)
+    vk = vel0.view(B, D // 2, 2).permute(1, 0, 2).contiguous().to(dev)
+    dtg, kg, eqg = dt.to(dev), k.to(dev), eq.to(dev)
+    pg = pos0.to(dev)
+    assert L().paig_rollout_fwd(0, p_(pg), D, p_(vk), p_(dtg), p_(kg), p_(eqg), p_(pvs), B, D, R, st()) == 0
+    dpos0 = torch.empty(B, D, device=dev)
+    dvel0 = torch.empty(D // 2, B, 2, device=dev)
+    part = torch.empty(2 * L().paig_rollout_bwd_blocks(B), device=dev, dtype=torch.float64)
+    gq = torch.zeros(2, device=dev, dtype=torch.float64)
+    dr, dv = dpos_roll.to(dev).contiguous(), dpvs.to(dev).contiguous()
+    assert L().paig_rollout_bwd(0, p_(pvs), p_(dr), p_(dv), p_(dtg), p_(kg), p_(eqg), p_(dpos0), p_(dvel0), p_(part),
+                                p_(gq), p_(gq) + 8, 0, B, D, R, st()) == 0
+    torch.cuda.synchronize()
+    assert rel_err(dpos0, p.grad) <= 1e-4, ("dpos0", rel_err(dpos0, p.grad))
+    assert rel_err(dvel0.permute(1, 0, 2).reshape(B, D), v.grad) <= 1e-4
+    assert rel_err(gq[0:1], P["rollout_cell.k"].grad.view(1)) <= 1e-4
+    assert rel_err(gq[1:2], P["rollout_cell.equil"].grad.view(1)) <= 1e-4
+
+
+def p_(t):
+    return t.data_ptr()

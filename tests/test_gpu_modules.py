@@ -241,3 +241,28 @@ def test_stn_general_affine():
     torch.cuda.synchronize()
     assert rel_err(Ug.grad, Ur.grad) <= 1e-5
     assert rel_err(tg.grad, tr.grad) <= 1e-4
+
+
+def test_stn_float64_theta():
+    """A float64 theta (the reference's physics-derived thetas are fp64, Q9):
+    the grid is formed in fp64 and cast to fp32 before sampling, as
+    F.affine_grid in theta's dtype followed by grid.float() (stn.py:12-14);
+    checked against those aten ops on the CPU (no fixture covers stn)."""
+    from paig_reproduction_amd.nn.network.stn import stn
+    g = torch.Generator().manual_seed(12)
+    U = torch.rand(4, 3, 16, 16, generator=g)
+    theta = (torch.eye(2, 3, dtype=torch.float64).expand(4, 2, 3)
+             + 0.3 * torch.randn(4, 2, 3, generator=g, dtype=torch.float64)).contiguous()
+    Ug, tg = U.to(DEV).requires_grad_(True), theta.to(DEV).requires_grad_(True)
+    out = stn(Ug, tg, (32, 32))
+    Ur, tr = U.clone().requires_grad_(True), theta.clone().requires_grad_(True)
+    grid = F.affine_grid(tr, (4, 3, 32, 32), align_corners=False)
+    ref = F.grid_sample(Ur, grid.float(), align_corners=False)
+    assert rel_err(out, ref) <= 1e-6
+    R = _R(ref.shape, 13)
+    (out * R.to(DEV)).sum().backward()
+    (ref * R).sum().backward()
+    torch.cuda.synchronize()
+    assert tg.grad.dtype == torch.float64
+    assert rel_err(Ug.grad, Ur.grad) <= 1e-5
+    assert rel_err(tg.grad, tr.grad) <= 1e-5
