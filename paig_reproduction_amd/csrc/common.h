@@ -232,6 +232,22 @@ __device__ __forceinline__ double wave_sum_dpp_d(double v) {
   return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
 }
 
+// GEMM epilogue (gemm.hip, dense.hip): activation of the output, then the
+// derivative of a stored activation (aux) for a backward GEMM
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_SIGMOID = 3 };
+enum { AUX_NONE = 0, AUX_RELU = 1, AUX_TANH = 2 };
+__device__ __forceinline__ float epi(float v, int act, int auxm, const float* aux, long long aoff) {
+  if (act == ACT_RELU) v = v < 0.f ? 0.f : v;
+  else if (act == ACT_TANH) v = tanhf(v);
+  else if (act == ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+  if (auxm == AUX_RELU) v = aux[aoff] > 0.f ? v : 0.f;
+  else if (auxm == AUX_TANH) { float t = aux[aoff]; v = v * (1.f - t * t); }
+  return v;
+}
+void paig_gemm_splitk_finish(int M, int N, int S, const float* part, float* C, long long ldc, float beta,
+                             const float* bias, int act, int auxm, const float* aux, long long ldaux,
+                             const float* rowpart, float* rowsum, hipStream_t st);
+
 // MFMA implicit-GEMM convolutions (conv_mfma.hip): return 1 when the shape is
 // instantiated there (launch status in *rc), 0 to fall back to the VALU path.
 // xmax (nullable): per-block max |input| of a split-precision forward

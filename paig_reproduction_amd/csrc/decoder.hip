@@ -1180,16 +1180,40 @@ struct DecFw {
   static constexpr int GPR = H / 4, NGRP = H * GPR;        // 4-pixel groups per row / frame
   static constexpr int NT = (NGRP + 63) / 64 * 64, NW = NT / 64;
   static constexpr int NC = K * 2 * H;                      // axis table entries
-  static_assert(H % 4 == 0 && NC <= NT, "decoder forward geometry");
+  // texel image rows: even padded columns first, then odd ones (the 4 pixels
+  // of a quad span 2 source columns, so neighbouring quads read texels 2
+  // apart: split by parity they are consecutive); row pitch in texels chosen
+  // by a bank model of the ds_read_b128 lane groups (1.04 / 1.10 LDS cycles
+  // per group against 1.41 / 1.36 for the plain image)
+  static constexpr int P = H == 32 ? 24 : 25;
+  static_assert(H % 4 == 0 && NC <= NT && hp % 2 == 0 && P >= hp, "decoder forward geometry");
 };
+__device__ __forceinline__ int texel_slot(int hp, int x) { return (x & 1) * (hp / 2) + (x >> 1); }
+
+// Rank of lane l in the order of ds_read_b128's four 16-lane bank groups
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, the same + 32): the pixel quads of
+// one group are then 16 consecutive quads (two output rows at H = 32), whose
+// texels are consecutive in the split image.
+__device__ __forceinline__ int b128_rank(int l) {
+  const int m = l & 31;
+  int g, r;
+  if (m < 4) g = 0, r = m;
+  else if (m < 12) g = 1, r = m - 4;
+  else if (m < 16) g = 0, r = m - 8;
+  else if (m < 20) g = 1, r = m - 8;
+  else if (m < 28) g = 0, r = m - 12;
+  else g = 1, r = m - 16;
+  return (l & 32) + g * 16 + r;
+}
 
 template <int K, int H>
 __global__ void __launch_bounds__((DecFw<K, H>::NT))
 dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse, int F, int FPB) {
   using C = DecFw<K, H>;
-  constexpr int h = C::h, hp = C::hp, HW = C::HW, GPR = C::GPR, NC = C::NC, NW = C::NW;
-  __shared__ float4 SRC[K][hp * hp];    // (template + 5, sigmoid(content) x 3), zero border
-  __shared__ float4 AX[2][K][2][H];     // w0, w1, padded first-tap index (bits), -
+  constexpr int h = C::h, hp = C::hp, HW = C::HW, GPR = C::GPR, NC = C::NC, NW = C::NW, P = C::P;
+  __shared__ float4 SRC[K][hp * P];     // (template + 5, sigmoid(content) x 3), zero border, split rows
+  __shared__ float4 AXC[2][K][4][GPR];  // column 4g+q: w0, w1, texel slots of the two taps (bits)
+  __shared__ float4 AXR[2][K][H];       // row: w0, w1, texel-row offset (bits), -
   __shared__ float RED[2][NW];          // per-wave SSE partials
   __shared__ double BC[H];
 
@@ -1198,8 +1222,9 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
   const int nf = first < F ? (F - first < FPB ? F - first : FPB) : 0;
   if (nf == 0) return;   // block-uniform
   const DecFrames FR(pos, tgt, 0);
-  const bool px = tid < C::NGRP;
-  const int i = px ? tid / GPR : 0, p = px ? i * H + (tid % GPR) * 4 : 0;
+  const int n = wv * 64 + b128_rank(lane);   // this thread's pixel quad
+  const bool px = n < C::NGRP;
+  const int i = px ? n / GPR : 0, g = px ? n % GPR : 0, p = i * H + 4 * g;
   const bool is_c = tid < NC;
   const int ck = is_c ? tid / (2 * H) : 0, cax = is_c ? (tid / H) & 1 : 0, cj = is_c ? tid % H : 0;
   const bool has_t = sse != nullptr;
@@ -1224,7 +1249,7 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) bgv[ch] = px ? ld4(S.bg + ch * HW + p) : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int t = tid; t < K * hp * hp; t += C::NT) {
-    const int k = t / (hp * hp), q = t % (hp * hp), y = q / hp - 1, x = q % hp - 1;
+    const int k = t / (hp * hp), q = t % (hp * hp), yp = q / hp, xp = q % hp, y = yp - 1, x = xp - 1;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)h) {
       const int o = y * h + x, hh = h * h;
@@ -1233,13 +1258,17 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
       v.z = 1.f / (1.f + expf(-S.cont[(k * 3 + 1) * hh + o]));
       v.w = 1.f / (1.f + expf(-S.cont[(k * 3 + 2) * hh + o]));
     }
-    SRC[k][q] = v;
+    SRC[k][yp * P + texel_slot(hp, xp)] = v;
   }
   for (int j = tid; j < H; j += C::NT) BC[j] = base_coord(j, H);
   auto tables = [&](float l, int slot) {
     if (is_c) {
       const Ax x = axis(src_coord(BC[cj], (double)(((float)H / 2.f - l) / (float)h), h), h);
-      AX[slot][ck][cax][cj] = make_float4(x.w0, x.w1, __int_as_float(x.c), 0.f);
+      if (cax == 0)
+        AXC[slot][ck][cj & 3][cj >> 2] =
+            make_float4(x.w0, x.w1, __int_as_float(texel_slot(hp, x.c)), __int_as_float(texel_slot(hp, x.c + 1)));
+      else
+        AXR[slot][ck][cj] = make_float4(x.w0, x.w1, __int_as_float(x.c * P), 0.f);
     }
   };
   __syncthreads();   // SRC, BC
@@ -1266,8 +1295,8 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
       int rb[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        ay[k] = AX[sl][k][1][i];
-        rb[k] = __float_as_int(ay[k].z) * hp;
+        ay[k] = AXR[sl][k][i];
+        rb[k] = __float_as_int(ay[k].z);
       }
       const float bq[3][4] = {{bgv[0].x, bgv[0].y, bgv[0].z, bgv[0].w},
                               {bgv[1].x, bgv[1].y, bgv[1].z, bgv[1].w},
@@ -1277,9 +1306,9 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
         float sv[K][4];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const float4 ax = AX[sl][k][0][(p % H) + q];
-          const int bs = rb[k] + __float_as_int(ax.z);
-          const float4 a = SRC[k][bs], b = SRC[k][bs + 1], c = SRC[k][bs + hp], d = SRC[k][bs + hp + 1];
+          const float4 ax = AXC[sl][k][q][g];
+          const int sa = rb[k] + __float_as_int(ax.z), sb = rb[k] + __float_as_int(ax.w);
+          const float4 a = SRC[k][sa], b = SRC[k][sb], c = SRC[k][sa + P], d = SRC[k][sb + P];
           pf32x2 v0, v1, dx, dy;
           samp_pair<false>(pf32x2{a.x, a.y}, pf32x2{b.x, b.y}, pf32x2{c.x, c.y}, pf32x2{d.x, d.y}, ax, ay[k], v0, dx, dy);
           samp_pair<false>(pf32x2{a.z, a.w}, pf32x2{b.z, b.w}, pf32x2{c.z, c.w}, pf32x2{d.z, d.w}, ax, ay[k], v1, dx, dy);

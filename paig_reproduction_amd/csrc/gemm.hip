@@ -32,19 +32,7 @@ constexpr int LDRK = BK + 2;    // [row][k] image pitch
 constexpr int LDKR = 64 + 16;   // [k][row] image pitch
 constexpr int IMG = (BK * LDKR > 64 * LDRK ? BK * LDKR : 64 * LDRK);
 
-enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_SIGMOID = 3 };
-enum { AUX_NONE = 0, AUX_RELU = 1, AUX_TANH = 2 };
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ float epi(float v, int act, int auxm, const float* aux, long long aoff) {
-  if (act == ACT_RELU) v = v < 0.f ? 0.f : v;
-  else if (act == ACT_TANH) v = tanhf(v);
-  else if (act == ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
-  if (auxm == AUX_RELU) v = aux[aoff] > 0.f ? v : 0.f;
-  else if (auxm == AUX_TANH) { float t = aux[aoff]; v = v * (1.f - t * t); }
-  return v;
-}
 
 // the source of out-of-range operand elements (Tile::load_bf)
 __device__ __attribute__((aligned(16))) float zero16[4];   // zero-initialised, never written
@@ -954,6 +942,27 @@ static void launch_gemm(int math, int tile, dim3 grid, hipStream_t st, int M, in
 
 }  // namespace
 
+// split-K epilogue: C = sum_s part[s] (+ beta C) (+ bias) -> act -> * aux'
+// (and rowsum = sum_s rowpart[s]); the vector form where the shapes allow
+void paig_gemm_splitk_finish(int M, int N, int S, const float* part, float* C, long long ldc, float beta,
+                             const float* bias, int act, int auxm, const float* aux, long long ldaux,
+                             const float* rowpart, float* rowsum, hipStream_t st) {
+  const bool v4 = N % 4 == 0 && vec_ok(C, ldc) && (!bias || (uintptr_t)bias % 16 == 0) &&
+                  (!aux || auxm == AUX_NONE || vec_ok(aux, ldaux)) && (uintptr_t)part % 16 == 0 &&
+                  (long long)S * M * N < (1ll << 31) && (long long)M * ldc < (1ll << 31) &&
+                  (long long)M * ldaux < (1ll << 31) &&
+                  (long long)M * N >= (1 << 19);   // smaller outputs keep the scalar form (4x the threads)
+  long long n_el = (v4 ? (long long)M * N / 4 : (long long)M * N) + (rowsum ? M : 0);
+  int g = cdiv(n_el, 256);
+  if (g > 4096) g = 4096;
+  if (v4)
+    hipLaunchKernelGGL(gemm_splitk_epilogue_v_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, (int)ldc, beta, bias,
+                       act, auxm, aux, (int)ldaux, rowpart, rowsum);
+  else
+    hipLaunchKernelGGL(gemm_splitk_epilogue_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, ldc, beta, bias, act,
+                       auxm, aux, ldaux, rowpart, rowsum);
+}
+
 extern "C" {
 
 int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
@@ -1014,19 +1023,7 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
 #undef PAIG_G
   PAIG_CHECK_LAUNCH();
   if (S > 1) {
-    const bool v4 = N % 4 == 0 && vec_ok(C, ldc) && (!bias || (uintptr_t)bias % 16 == 0) && (!aux || auxm == AUX_NONE ||
-                    vec_ok(aux, ldaux)) && (uintptr_t)part % 16 == 0 && (long long)S * M * N < (1ll << 31) &&
-                    (long long)M * ldc < (1ll << 31) && (long long)M * ldaux < (1ll << 31) &&
-                    (long long)M * N >= (1 << 19);   // smaller outputs keep the scalar form (4x the threads)
-    long long n_el = (v4 ? (long long)M * N / 4 : (long long)M * N) + (rowsum ? M : 0);
-    int g = cdiv(n_el, 256);
-    if (g > 4096) g = 4096;
-    if (v4)
-      hipLaunchKernelGGL(gemm_splitk_epilogue_v_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, (int)ldc, beta, bias,
-                         act, auxm, aux, (int)ldaux, rowpart, rowsum);
-    else
-      hipLaunchKernelGGL(gemm_splitk_epilogue_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, ldc, beta, bias, act,
-                         auxm, aux, ldaux, rowpart, rowsum);
+    paig_gemm_splitk_finish(M, N, S, part, C, ldc, beta, bias, act, auxm, aux, ldaux, rowpart, rowsum, st);
     PAIG_CHECK_LAUNCH();
   }
   return 0;

@@ -245,6 +245,51 @@ def test_gemm_ex(ta, tb, M, N, K, math):
         assert rel_err(rs, A.t().sum(1)) <= 2e-5
 
 
+# The encoder projection's three products as the engine issues them (math 6):
+# forward (bias + ReLU, split-K), wgrad (plain sums + fused bias gradient),
+# dgrad (no split) -- the LDS-free fragment-image kernels of dense.hip.
+# Operand rows spread over 10^-2..10^2 (the per-row exponents / running
+# exponents): normwise and per-row bars vs float64.
+@pytest.mark.parametrize("form", ["fwd", "fwd_tb0", "wgrad", "dgrad", "dgrad_tb1"])
+def test_gemm_dense_forms(form):
+    g = torch.Generator().manual_seed(len(form))
+    ta, tb, M, N, K, act = {"fwd": (0, 1, 2000, 200, 3072, 1), "fwd_tb0": (0, 0, 1000, 200, 3072, 1),
+                            "wgrad": (1, 0, 200, 3072, 2000, 0), "dgrad": (0, 0, 2000, 3072, 200, 0),
+                            "dgrad_tb1": (0, 1, 1500, 3072, 200, 0)}[form]
+
+    def spread(*shape):
+        return torch.randn(*shape, generator=g) * 10.0 ** (4 * torch.rand(shape[0], 1, generator=g) - 2)
+    A = spread(K, M) if ta else spread(M, K)
+    Bm = spread(N, K) if tb else spread(K, N)
+    bias = torch.randn(N, generator=g) if act else None
+    opA, opB = (A.t() if ta else A).double(), (Bm.t() if tb else Bm).double()
+    ref = opA @ opB + (bias.double() if act else 0.0)
+    if act:
+        ref = torch.relu(ref)
+    Ag, Bg = A.to(DEV), Bm.to(DEV)
+    bg = bias.to(DEV) if act else None
+    ws = torch.empty(max(1, L().paig_gemm_workspace(M, N, K)), device=DEV)
+    rs = torch.full((M,), float("nan"), device=DEV)
+    outs = []
+    for _ in range(2):
+        C = torch.full((M, N), float("nan"), device=DEV)
+        rc = L().paig_gemm_ex(ta, tb, M, N, K, 1.0, p(Ag), A.shape[1], p(Bg), Bm.shape[1], 0.0, p(C), N,
+                              p(bg) if act else None, act, 0, None, 0, p(rs) if ta else None, p(ws), ws.numel(), 6,
+                              st())
+        torch.cuda.synchronize()
+        assert rc == 0, L().paig_last_error()
+        outs.append(C.cpu())
+    assert torch.equal(outs[0], outs[1]), "not deterministic"
+    C = outs[0].double()
+    assert rel_err(C, ref) <= 2e-5
+    # per output row, against that row's own magnitude (rows whose reference is all ReLU-zero skipped)
+    rn = ref.abs().amax(1)
+    ok = rn > 0
+    assert float(((C - ref).abs().amax(1)[ok] / rn[ok]).max()) <= 1e-4
+    if ta:
+        assert rel_err(rs.cpu().double(), opA.sum(1)) <= 2e-5
+
+
 def test_pool_upsample():
     x = torch.relu(torch.randn(5, 6, 16, 16))
     xg = x.to(DEV)
