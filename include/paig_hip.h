@@ -164,6 +164,27 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
                  long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
                  const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,
                  void* stream);
+/* Dense layers on pre-split operands (psgemm.hip).  A "PS image" holds a
+ * logical matrix X[R][K] (reduction dim K) split once into f16 hi + lo planes
+ * ([ceil(K/32)][R rounded up to 64][32] each), one power-of-two exponent per
+ * row (max_k |X[r][k]| 2^e in [2^14, 2^15)).
+ * paig_ps_split fills up to 8 images in one launch; job i reads
+ * op(X)[r][k] = src[i][r * sr[i] + k * sk[i]] (sk == 1 or sr == 1), R[i] x K[i],
+ * into dst[i] (paig_ps_bytes(R, K) bytes, 256-byte aligned) and, when rowsum
+ * and rowsum[i] are not NULL, its fp32 row sums into rowsum[i] (R floats: for
+ * an image of dY^T, the bias gradient of dW = dY^T X).
+ * paig_psgemm: C[M][N] = alpha sum_k A[m][k] B[n][k] (+beta C) (+bias[n]) -> act
+ * -> * aux' (the paig_gemm_ex epilogue) from the images of A (M x K) and B
+ * (N x K); 3 f16 MFMAs per product, fp32-accurate like paig_gemm_ex math 6.
+ * Replaces the per-tile operand conversion of the split GEMMs for
+ * nn/network/blocks.py:71-75,98-100 (l1, l2: forward, dgrad, wgrad). */
+long long paig_ps_bytes(int R, int K);
+int paig_ps_split(int n, const float* const* src, const long long* sr, const long long* sk, const int* R,
+                  const int* K, void* const* dst, float* const* rowsum, void* stream);
+size_t paig_psgemm_workspace(int M, int N, int K);
+int paig_psgemm(int M, int N, int K, const void* A_img, const void* B_img, float alpha, float* C, long long ldc,
+                float beta, const float* bias, int act, int auxm, const float* aux, long long ldaux, float* ws,
+                size_t ws_floats, void* stream);
 size_t paig_colsum_workspace(int M, int N);
 int paig_colsum(const float* X, int M, int N, long long ld, float* out, int accumulate, float* ws, void* stream);
 int paig_slab_reduce(const float* slab, int nblk, long long ld, int len, float* out, int accumulate, void* stream);
