@@ -188,9 +188,8 @@ int paig_psgemm(int M, int N, int K, const void* A_img, const void* B_img, float
 size_t paig_colsum_workspace(int M, int N);
 int paig_colsum(const float* X, int M, int N, long long ld, float* out, int accumulate, float* ws, void* stream);
 int paig_slab_reduce(const float* slab, int nblk, long long ld, int len, float* out, int accumulate, void* stream);
-/* up to 32 independent deterministic slab reductions (host arrays of ntask entries), two launches;
-   each src slab is scratch: its rows are overwritten by partial sums */
-int paig_slab_reduce_multi(int ntask, float* const* src, const int* nblk, const int* len, float* const* dst,
+/* up to 32 independent deterministic slab reductions in one launch (host arrays of ntask entries) */
+int paig_slab_reduce_multi(int ntask, const float* const* src, const int* nblk, const int* len, float* const* dst,
                            int accumulate, void* stream);
 int paig_axpby(const float* x, float* y, long long n, float a, float b, void* stream);
 

@@ -7,8 +7,6 @@
 //   deterministic slab / column reductions for weight and bias gradients.
 #include "common.h"
 
-#include <type_traits>
-
 #define PAIG_MAX_SLAB_TASKS 32
 
 namespace {
@@ -734,113 +732,109 @@ __global__ void __launch_bounds__(256) slab_reduce_k(const float* __restrict__ s
   }
 }
 
-// Many reductions, two launches: task t sums nblk[t] rows of len[t] floats
-// (row stride len[t]) into dst[t], in a fixed order (deterministic).
-//   stage 1: a block owns (task, 64-lane column chunk, SLAB_RC-row chunk);
-//     its 4 waves each load 8 rows at once (independent loads, whole 1 KB
-//     rows per wave instruction on the float4 path), sum them in row order
-//     and combine in a fixed tree; the chunk sum overwrites the chunk's first
-//     row in place (every row of the chunk was read before the barrier), or
-//     goes straight to dst[t] when the task has a single chunk;
-//   stage 2: one thread per column sums the chunk rows in order into dst[t].
-// The float4 path needs len % 4 == 0 and 16-byte aligned src / dst.
-constexpr int SLAB_RC = 32;
+// Many reductions in one launch: task t sums nblk[t] rows of len[t] floats
+// (row stride len[t]) into dst[t]; blocks [start[t], start[t+1]) serve task t.
 struct SlabTasks {
-  float* src[PAIG_MAX_SLAB_TASKS];
+  const float* src[PAIG_MAX_SLAB_TASKS];
   float* dst[PAIG_MAX_SLAB_TASKS];
   int nblk[PAIG_MAX_SLAB_TASKS];
   int len[PAIG_MAX_SLAB_TASKS];
-  int vec[PAIG_MAX_SLAB_TASKS];
-  int start[PAIG_MAX_SLAB_TASKS + 1];    // stage-1 blocks of task t: [start[t], start[t+1])
-  int start2[PAIG_MAX_SLAB_TASKS + 1];   // stage-2 blocks
+  int vec[PAIG_MAX_SLAB_TASKS];  // 1: len % 4 == 0 and src/dst 16-B aligned -> float4 path
+  int start[PAIG_MAX_SLAB_TASKS + 1];
   int ntask;
   int accumulate;
 };
 
-template <int V>
-__device__ __forceinline__ void slab_chunk(float* __restrict__ src, float* __restrict__ dst, int len, int nblk, int blk,
-                                           int accumulate, float (*red)[64 * 4]) {
-  using VT = typename std::conditional<V == 4, float4, float>::type;
-  const int ncc = (len + 64 * V - 1) / (64 * V);
-  const int cc = blk % ncc, rc = blk / ncc;
+// Scalar path (64 columns per block): 16 waves, each lane owns one column,
+// the waves stride the rows (4 independent accumulators each), then a
+// fixed-order combine.
+__device__ __forceinline__ void slab_cols_scalar(const float* __restrict__ src, float* dst, int len, int nblk,
+                                                 int blk, int accumulate, float (*red)[64]) {
+  constexpr int NW = 16;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int col = cc * 64 * V + lane * V;
-  const int r0 = rc * SLAB_RC;
-  const bool ok = col < len;
-  float acc[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) acc[e] = 0.f;
-  if (ok) {
-    VT v[SLAB_RC / 4];
-#pragma unroll
-    for (int u = 0; u < SLAB_RC / 4; ++u) {
-      const int r = r0 + wv * (SLAB_RC / 4) + u;
-      v[u] = r < nblk ? *reinterpret_cast<const VT*>(src + (long long)r * len + col) : VT{};
+  const int i = blk * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < len) {
+    int b = wv;
+    for (; b + 3 * NW < nblk; b += 4 * NW) {
+      s0 += src[(long long)b * len + i];
+      s1 += src[(long long)(b + NW) * len + i];
+      s2 += src[(long long)(b + 2 * NW) * len + i];
+      s3 += src[(long long)(b + 3 * NW) * len + i];
     }
-#pragma unroll
-    for (int u = 0; u < SLAB_RC / 4; ++u) {
-      const float* f = reinterpret_cast<const float*>(&v[u]);
-#pragma unroll
-      for (int e = 0; e < V; ++e) acc[e] += f[e];
-    }
+    for (; b < nblk; b += NW) s0 += src[(long long)b * len + i];
   }
-#pragma unroll
-  for (int e = 0; e < V; ++e) red[wv][lane * V + e] = acc[e];
+  red[wv][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (wv == 0 && ok) {
-    float out[V];
+  if (wv == 0 && i < len) {
+    float v = 0.f;
 #pragma unroll
-    for (int e = 0; e < V; ++e)
-      out[e] = (red[0][lane * V + e] + red[1][lane * V + e]) + (red[2][lane * V + e] + red[3][lane * V + e]);
-    const bool single = nblk <= SLAB_RC;
-    float* o = single ? dst + col : src + (long long)r0 * len + col;
-    if (single && accumulate)
-#pragma unroll
-      for (int e = 0; e < V; ++e) out[e] += o[e];
-    *reinterpret_cast<VT*>(o) = *reinterpret_cast<const VT*>(out);
+    for (int w = 0; w < NW; ++w) v += red[w][lane];
+    dst[i] = accumulate ? dst[i] + v : v;
   }
 }
 
-__global__ void __launch_bounds__(256) slab_stage1_k(SlabTasks T) {
-  __shared__ float red[4][64 * 4];
+// Vector path (32 columns per block): 8 lanes x float4 cover one 128-B row
+// segment, so a wave reads 8 rows per instruction and a task gets twice the
+// blocks of the scalar path (the decoder's 5 K-column source reduction:
+// 80 -> 160 CUs busy, 11 -> 7.5 us).  Rows r, r+128, ... go to row lane r; a
+// fixed-shape LDS tree combines the 128 row lanes, so the order is the same
+// every run.
+__device__ __forceinline__ void slab_cols_vec(const float* __restrict__ src0, float* dst, int len, int nblk, int blk,
+                                              int accumulate, float4 (*red)[8]) {
+  constexpr int NR = 128;
+  const int c4 = threadIdx.x & 7, r = threadIdx.x >> 3;
+  const int col = blk * 32 + c4 * 4;
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+  if (col < len) {
+    const float* src = src0 + col;
+    int b = r;
+    for (; b + NR < nblk; b += 2 * NR) {
+      const float4 a = *reinterpret_cast<const float4*>(src + (long long)b * len);
+      const float4 c = *reinterpret_cast<const float4*>(src + (long long)(b + NR) * len);
+      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+      s1.x += c.x; s1.y += c.y; s1.z += c.z; s1.w += c.w;
+    }
+    if (b < nblk) {
+      const float4 a = *reinterpret_cast<const float4*>(src + (long long)b * len);
+      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+    }
+  }
+  red[r][c4] = make_float4(s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w);
+  __syncthreads();
+#pragma unroll
+  for (int h = NR / 2; h >= 1; h >>= 1) {
+    if (r < h) {
+      const float4 a = red[r][c4], c = red[r + h][c4];
+      red[r][c4] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w);
+    }
+    __syncthreads();
+  }
+  if (r == 0 && col < len) {
+    const float4 v = red[0][c4];
+    float4* d = reinterpret_cast<float4*>(dst + col);
+    if (accumulate) {
+      const float4 o = *d;
+      *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    } else {
+      *d = v;
+    }
+  }
+}
+
+// Many reductions in one launch: task t sums nblk[t] rows of len[t] floats
+// (row stride len[t]) into dst[t]; blocks [start[t], start[t+1]) serve task t
+// (the path is uniform per block).
+__global__ void __launch_bounds__(1024) slab_reduce_multi_k(SlabTasks T) {
+  __shared__ float4 red_v[128][8];
+  __shared__ float red_s[16][64];
   int t = 0;
   while (t + 1 < T.ntask && (int)blockIdx.x >= T.start[t + 1]) ++t;
   const int blk = (int)blockIdx.x - T.start[t];
-  if (T.vec[t]) slab_chunk<4>(T.src[t], T.dst[t], T.len[t], T.nblk[t], blk, T.accumulate, red);
-  else slab_chunk<1>(T.src[t], T.dst[t], T.len[t], T.nblk[t], blk, T.accumulate, red);
-}
-
-__global__ void __launch_bounds__(256) slab_stage2_k(SlabTasks T) {
-  int t = 0;
-  while (t + 1 < T.ntask && (int)blockIdx.x >= T.start2[t + 1]) ++t;
-  const int blk = (int)blockIdx.x - T.start2[t];
-  const int len = T.len[t], nch = (T.nblk[t] + SLAB_RC - 1) / SLAB_RC;
-  const float* src = T.src[t];
-  float* dst = T.dst[t];
-  if (T.vec[t]) {
-    const int col = (blk * 256 + threadIdx.x) * 4;
-    if (col >= len) return;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int c = 0; c < nch; ++c) {
-      const float4 v = *reinterpret_cast<const float4*>(src + (long long)c * SLAB_RC * len + col);
-      a.x += v.x;
-      a.y += v.y;
-      a.z += v.z;
-      a.w += v.w;
-    }
-    float4* d = reinterpret_cast<float4*>(dst + col);
-    if (T.accumulate) {
-      const float4 o = *d;
-      a = make_float4(o.x + a.x, o.y + a.y, o.z + a.z, o.w + a.w);
-    }
-    *d = a;
-  } else {
-    const int col = blk * 256 + threadIdx.x;
-    if (col >= len) return;
-    float a = 0.f;
-    for (int c = 0; c < nch; ++c) a += src[(long long)c * SLAB_RC * len + col];
-    dst[col] = T.accumulate ? dst[col] + a : a;
-  }
+  if (T.vec[t])
+    slab_cols_vec(T.src[t], T.dst[t], T.len[t], T.nblk[t], blk, T.accumulate, red_v);
+  else
+    slab_cols_scalar(T.src[t], T.dst[t], T.len[t], T.nblk[t], blk, T.accumulate, red_s);
 }
 
 // part[s][n] = sum over rows r in stripe s of X[r][n]
@@ -1064,12 +1058,12 @@ int paig_vel_unpack_add(const float* dX, const float* dpos0, float* dpos, int B,
   return 0;
 }
 
-int paig_slab_reduce_multi(int ntask, float* const* src, const int* nblk, const int* len, float* const* dst,
+int paig_slab_reduce_multi(int ntask, const float* const* src, const int* nblk, const int* len, float* const* dst,
                            int accumulate, void* stream) {
   PAIG_REQUIRE(ntask >= 0 && ntask <= PAIG_MAX_SLAB_TASKS, "slab_reduce_multi: %d tasks", ntask);
   if (ntask == 0) return 0;
   SlabTasks T;
-  int b1 = 0, b2 = 0;
+  int blocks = 0;
   for (int t = 0; t < ntask; ++t) {
     PAIG_REQUIRE(len[t] >= 0 && nblk[t] >= 0, "slab_reduce_multi: task %d len %d nblk %d", t, len[t], nblk[t]);
     T.src[t] = src[t];
@@ -1077,28 +1071,15 @@ int paig_slab_reduce_multi(int ntask, float* const* src, const int* nblk, const 
     T.nblk[t] = nblk[t];
     T.len[t] = len[t];
     T.vec[t] = len[t] % 4 == 0 && ((uintptr_t)src[t] & 15) == 0 && ((uintptr_t)dst[t] & 15) == 0;
-    T.start[t] = b1;
-    T.start2[t] = b2;
-    const int V = T.vec[t] ? 4 : 1, nch = cdiv(nblk[t], SLAB_RC);
-    // an empty task (no rows) still zeroes dst: one stage-1 chunk of zeros
-    if (len[t] > 0) {
-      b1 += cdiv(len[t], 64 * V) * (nch > 0 ? nch : 1);
-      if (nch > 1) b2 += cdiv(len[t], 256 * V);
-    }
+    T.start[t] = blocks;
+    blocks += cdiv(len[t], T.vec[t] ? 32 : 64);
   }
-  T.start[ntask] = b1;
-  T.start2[ntask] = b2;
+  T.start[ntask] = blocks;
   T.ntask = ntask;
   T.accumulate = accumulate;
-  hipStream_t st = (hipStream_t)stream;
-  if (b1 > 0) {
-    hipLaunchKernelGGL(slab_stage1_k, dim3(b1), dim3(256), 0, st, T);
-    PAIG_CHECK_LAUNCH();
-  }
-  if (b2 > 0) {
-    hipLaunchKernelGGL(slab_stage2_k, dim3(b2), dim3(256), 0, st, T);
-    PAIG_CHECK_LAUNCH();
-  }
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(slab_reduce_multi_k, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, T);
+  PAIG_CHECK_LAUNCH();
   return 0;
 }
 

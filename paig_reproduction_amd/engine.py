@@ -362,7 +362,8 @@ class Engine:
             self.L.paig_gemm_ex(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
                                 ptr(gb), ptr(ws), n_ws, self.gemm_math(self.WGRAD), st)
         if need_dx:
-            with self._p("gemm_dgrad:" + name, 2 * rows * O * I, 4 * (rows * O + O * I + 2 * rows * I)):
+            # dY and W read, dX written (+ the activation read for its derivative)
+            with self._p("gemm_dgrad:" + name, 2 * rows * O * I, 4 * (rows * O + O * I + (2 if auxm else 1) * rows * I)):
                 self.L.paig_gemm_ex(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm,
                                     ptr(aux), I, None, ptr(ws), n_ws, self.gemm_math(self.DGRAD), st)
 
