@@ -289,6 +289,7 @@ class Engine:
         self.probe = None
         self.last_masked_objs = None
         self._side = None   # second stream (see _fork)
+        self._xmax = {}     # per-layout xmax slots (see _unet_forward)
         # called once per backward when the early gradient bucket is final
         # (FlatParams.allreduce_early by default; bench.py splits its HIP graph here)
         self.bucket_hook = model._flat.allreduce_early
@@ -556,8 +557,13 @@ class Engine:
         # per conv: the split forward's per-block max |input| slots, which
         # set the X scale of the same input's wgrad (every slot is written;
         # zeroed so that a slot no forward wrote falls back to the guarded
-        # fixed scale instead of a garbage exponent)
-        xmax = torch.zeros(len(lay.ops) * XMAX_SLOTS, device=dev)
+        # fixed scale instead of a garbage exponent).  Kept per (device,
+        # layout): a step of the same shape rewrites exactly the same slots,
+        # so the zero fill (an extra launch per step) happens once.
+        key = (str(dev), len(lay.ops), lay.F, lay.H)
+        xmax = self._xmax.get(key)
+        if xmax is None:
+            xmax = self._xmax[key] = torch.zeros(len(lay.ops) * XMAX_SLOTS, device=dev)
         S["xmax"] = lambda i: ptr(xmax) + i * XMAX_SLOTS * 4
         S["xmax_buf"] = xmax
         # split path: every conv's forward and dgrad weight images, pre-split
