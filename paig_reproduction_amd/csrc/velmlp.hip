@@ -36,6 +36,20 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
   __shared__ float W2s[HID * W2P];
   const int rows = K * B, r0 = blockIdx.x * FRB, tid = threadIdx.x;
   const int nr = rows - r0 < FRB ? rows - r0 : FRB;
+  const int lane = tid & 63, wv = tid >> 6;
+  // every parameter this thread needs is loaded up front, beside W2, so the
+  // block pays ONE memory round trip (the layers used to load W0 / b0, b2
+  // and W4 / b4 after their barriers: three dependent trips)
+  float w[MAXIN], bb0 = 0.f, bb2 = 0.f;
+  if (tid < HID) {
+    for (int i = 0; i < IN; ++i) w[i] = W0[tid * IN + i];
+    bb0 = b0[tid];
+    bb2 = b2[tid];
+  }
+  // output layer: wave wv owns output wv (FRB * OUT == 2 outputs, 2 waves)
+  static_assert(FRB * OUT <= 2, "one output per wave");
+  const int jo = wv % OUT;
+  const float w4a = W4[jo * HID + lane], w4b = lane + 64 < HID ? W4[jo * HID + lane + 64] : 0.f, bb4 = b4[jo];
   if (((uintptr_t)W2 & 15) == 0) {   // all of W2 in flight at once: 20 float4 per thread
 #pragma unroll 5
     for (int e = tid; e < HID * HID / 4; e += 128) {
@@ -58,13 +72,11 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
   }
   __syncthreads();
   if (tid < HID) {
-    float w[MAXIN];
-    for (int i = 0; i < IN; ++i) w[i] = W0[tid * IN + i];
 #pragma unroll
     for (int r = 0; r < FRB; ++r) {
       float a = 0.f;
       if (r < nr) {
-        a = b0[tid];
+        a = bb0;
         for (int i = 0; i < IN; ++i) a = fmaf(Xs[r][i], w[i], a);
         a = tanhf(a);
         h1[(long long)(r0 + r) * HID + tid] = a;
@@ -76,7 +88,7 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
   if (tid < HID) {
     float a[FRB];
 #pragma unroll
-    for (int r = 0; r < FRB; ++r) a[r] = b2[tid];
+    for (int r = 0; r < FRB; ++r) a[r] = bb2;
     const float* wr = W2s + tid * W2P;
 #pragma unroll 10
     for (int u = 0; u < HID; ++u) {
@@ -91,14 +103,14 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
     }
   }
   __syncthreads();
-  // vel[r][j]: one wave per output, lanes split the hidden units
-  const int lane = tid & 63, wv = tid >> 6;
-  for (int o = wv; o < nr * OUT; o += blockDim.x >> 6) {
-    const int r = o / OUT, j = o % OUT;
-    float a = 0.f;
-    for (int t = lane; t < HID; t += 64) a = fmaf(H2[r][t], W4[j * HID + t], a);
+  // vel[r][j]: one wave per output, lanes split the hidden units (the same
+  // two-term order per lane as a stride-64 loop)
+  if (wv < nr * OUT) {
+    const int r = wv / OUT;
+    float a = fmaf(H2[r][lane], w4a, 0.f);
+    if (lane + 64 < HID) a = fmaf(H2[r][lane + 64], w4b, a);
     a = wave_sum(a);
-    if (lane == 0) vel[(long long)(r0 + r) * OUT + j] = a + b4[j];
+    if (lane == 0) vel[(long long)(r0 + r) * OUT + jo] = a + bb4;
   }
 }
 
@@ -143,16 +155,19 @@ velmlp_bwd_k(const float* __restrict__ dvel, const float* __restrict__ X, const 
     H1[r][u] = r < nr ? h1[(long long)(r0 + r) * HID + u] : 0.f;
   }
   if (tid < RB * OUT) DV[tid / OUT][tid % OUT] = tid / OUT < nr ? dvel[(long long)(r0 + tid / OUT) * OUT + tid % OUT] : 0.f;
-  __syncthreads();
-  // ---- layer 4 (linear): dz2 = (dvel W4) * tanh'(h2);  gW4 = dvel^T h2, gb4 = sum dvel
+  // layer 4's operands loaded before the barrier too: the whole block pays
+  // one memory round trip
+  float w4[OUT], hvr[RB];
   if (tid < HID) {
-    float g4[OUT] = {0.f, 0.f};
-    // all loads of this phase in flight together (one latency, not RB)
-    float w4[OUT], hvr[RB];
 #pragma unroll
     for (int j = 0; j < OUT; ++j) w4[j] = W4[j * HID + tid];
 #pragma unroll
     for (int r = 0; r < RB; ++r) hvr[r] = r < nr ? h2[(long long)(r0 + r) * HID + tid] : 0.f;
+  }
+  __syncthreads();
+  // ---- layer 4 (linear): dz2 = (dvel W4) * tanh'(h2);  gW4 = dvel^T h2, gb4 = sum dvel
+  if (tid < HID) {
+    float g4[OUT] = {0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
       const float hv = hvr[r];

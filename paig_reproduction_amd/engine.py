@@ -439,11 +439,12 @@ class Engine:
         self._encoder_forward(S, lay, x_view, ws, st)
         masks, objs, enc_pos = S["masks"], S["objs"], S["enc_pos"]
 
-        # Two independent chains follow the position head; they run concurrently:
-        #   side stream: velocity MLP -> physics rollout (one thread per
-        #                sequence: latency-bound, a few blocks)
-        #   main stream: reconstruction decode of all B*Te frames
-        # Everything the side chain touches is allocated before the fork.
+        # Two independent chains follow the position head: velocity MLP ->
+        # physics rollout (one thread per sequence: latency-bound, a few
+        # blocks) and VFN sources -> reconstruction decode of all B*Te frames.
+        # They run on one stream (see _one_stream); PAIG_SCHED=0 puts the first
+        # on a side stream.  Everything a side chain touches is allocated
+        # before the fork.
         recons = _empty(F * lay.frame, dev)
         sse_rec = _empty(F, dev)
         vel0 = None
@@ -464,30 +465,41 @@ class Engine:
         prm = self.cell_params(lay)
         S["pvs"] = pvs
 
-        sst = self._fork(dev)
-        # ---- (side) velocity encoder
-        if vel0 is not None:
-            if lay.alt_vel:
-                L.paig_vel_pack(ptr(enc_pos), ptr(S["Xv"]), B, lay.Te, K, lay.ins, 1, sst)
-                self.linear(S["Xv"], K * B, "velocity_encoder.init_vel_linear", vel0, 0, sst, ws)
-            else:   # the whole MLP (packing fused) in one launch
-                pm = "velocity_encoder.init_vel_mlp."
-                L.paig_velmlp_fwd(ptr(enc_pos), B, lay.Te, K, lay.ins, *[ptr(self.p(pm + n)) for n in (
-                    "0.weight", "0.bias", "2.weight", "2.bias", "4.weight", "4.bias")], ptr(S["Xv"]), ptr(S["v1"]),
-                    ptr(S["v2"]), ptr(vel0), sst)
-        # ---- (side) physics rollout (all R steps in one launch)
-        L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0), ptr(prm[0]),
-                           ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, sst)
-        # ---- (main) VariableFromNetwork sources, then the reconstruction decode
-        # (all B*Te frames, SSE vs input fused)
-        L.paig_vfn_fwd_multi(3, *[_parr([ptr(self.p(nm + suf)) for nm, _, _ in vf])
-                                  for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
-                             _parr([ptr(src[nm][0]) for nm, _, _ in vf]), _parr([ptr(src[nm][1]) for nm, _, _ in vf]),
-                             _parr([ptr(src[nm][2]) for nm, _, _ in vf]), _iarr([P for _, P, _ in vf]), st)
-        with self._p("dec_fwd:recon", 0, self._dec_bytes(F, lay)):
-            L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons), lay.frame,
-                               x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, st)
-        self._join(dev)
+        def velocity(q):   # velocity encoder, then the physics rollout (all R steps in one launch)
+            if vel0 is not None:
+                if lay.alt_vel:
+                    L.paig_vel_pack(ptr(enc_pos), ptr(S["Xv"]), B, lay.Te, K, lay.ins, 1, q)
+                    self.linear(S["Xv"], K * B, "velocity_encoder.init_vel_linear", vel0, 0, q, ws)
+                else:   # the whole MLP (packing fused) in one launch
+                    pm = "velocity_encoder.init_vel_mlp."
+                    L.paig_velmlp_fwd(ptr(enc_pos), B, lay.Te, K, lay.ins, *[ptr(self.p(pm + n)) for n in (
+                        "0.weight", "0.bias", "2.weight", "2.bias", "4.weight", "4.bias")], ptr(S["Xv"]),
+                        ptr(S["v1"]), ptr(S["v2"]), ptr(vel0), q)
+            L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0), ptr(prm[0]),
+                               ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, q)
+
+        def vfn_src(q):    # VariableFromNetwork sources
+            L.paig_vfn_fwd_multi(3, *[_parr([ptr(self.p(nm + suf)) for nm, _, _ in vf])
+                                      for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                                 _parr([ptr(src[nm][0]) for nm, _, _ in vf]),
+                                 _parr([ptr(src[nm][1]) for nm, _, _ in vf]),
+                                 _parr([ptr(src[nm][2]) for nm, _, _ in vf]), _iarr([P for _, P, _ in vf]), q)
+
+        def dec_rec(q):    # reconstruction decode (all B*Te frames, SSE vs input fused)
+            with self._p("dec_fwd:recon", 0, self._dec_bytes(F, lay)):
+                L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons),
+                                   lay.frame, x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, q)
+
+        if self._one_stream():
+            velocity(st)
+            vfn_src(st)
+            dec_rec(st)
+        else:
+            sst = self._fork(dev)
+            velocity(sst)                  # (side) velocity encoder + rollout
+            vfn_src(st)                    # (main) VFN sources, reconstruction decode
+            dec_rec(st)
+            self._join(dev)
 
         # ---- rollout decode (all B*R frames in one launch, SSE vs input[:, ins:])
         out = _empty(B * lay.R * lay.frame, dev)
@@ -677,7 +689,7 @@ class Engine:
                         ptr(enc_pos), F, K, 200, float(H / 2), st)
         S.update(masks=masks, objs=objs, l1_x=l1_x, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
 
-    # -- a second stream for the latency-bound per-sequence chains ---------
+    # -- a second stream for the per-sequence chains (PAIG_SCHED=0 only) ----
     def _fork(self, dev):
         """Side stream ordered after everything issued so far on the current
         stream; graph capture records the fork as a branch."""
@@ -687,6 +699,16 @@ class Engine:
         ev.record(torch.cuda.current_stream(dev))
         self._side.wait_event(ev)
         return self._side.cuda_stream
+
+    def _one_stream(self):
+        """The per-sequence chains (velocity encoder, rollout and their
+        backward) and the decoder / VFN work run on ONE stream: inside a
+        replayed HIP graph every cross-stream edge costs 5-10 us of idle
+        queue even when it is long satisfied (tools/timeline.py), more than
+        the concurrent kernels overlapped (they slow each other down), so the
+        serial order measured 0.6% faster than the round-2 two-stream order
+        (PAIG_SCHED=0).  Probed runs keep one stream too."""
+        return os.environ.get("PAIG_SCHED", "2") != "0"
 
     def _join(self, dev):
         ev = torch.cuda.Event()
@@ -754,61 +776,78 @@ class Engine:
                ("var_net_background", 3 * HW, 1, S["src"]["var_net_background"][1]))
         vparts = [_empty(L.paig_vfn_bwd_blocks(P) * 200, dev) for _, P, _, _ in vfn]
 
-        # ---- (main) rollout-frame decoder backward: d rollout positions + partial source grads
-        live_frames = B * roll_live if roll_live else B * R
-        with self._p("dec_bwd:rollout", 0, self._dec_bwd_bytes(live_frames, B * R, lay, d_out is not None)):
-            L.paig_decoder_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
-                               *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
-                               ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, roll_live, K, h, H, st)
-
-        # the side chain's inputs exist before the fork (a temporary made after
-        # it could be recycled by a main-stream allocation while the side
-        # kernel still reads it)
-        d_pvs_c = d_pvs.contiguous() if d_pvs is not None else None
-        sst = self._fork(dev)
-        # ---- (side) rollout adjoint -> d pos0, d vel0, physics params
         prm = self.cell_params(lay)
         gk = gq = None
         if lay.cell == 0:
             gk, gq = self.g("rollout_cell.k"), self.g("rollout_cell.equil")
         elif lay.cell == 2:
             gk = self.g("rollout_cell.g")
-        L.paig_rollout_bwd(lay.cell, ptr(pvs), ptr(dpos_roll), ptr(d_pvs_c),
-                           ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(dpos0), ptr(dvel0), ptr(rpart), ptr(gk), ptr(gq),
-                           0, B, D, R, sst)
-        # ---- (side) velocity encoder backward -> d packed inputs
-        if S["vel0"] is not None:
-            if lay.alt_vel:
-                self.linear_bwd(S["Xv"], dvel0, K * B, "velocity_encoder.init_vel_linear", dXv, None, 0, sst, ws)
-            else:   # one launch; its partial weight grads join the U-Net's batched slab reduction
-                pm = "velocity_encoder.init_vel_mlp."
-                L.paig_velmlp_bwd(ptr(dvel0), ptr(S["Xv"]), ptr(S["v1"]), ptr(S["v2"]), ptr(self.p(pm + "0.weight")),
-                                  ptr(self.p(pm + "2.weight")), ptr(self.p(pm + "4.weight")), ptr(dXv), ptr(vslab),
-                                  K * B, lay.ins, sst)
-                g0 = self.g(pm + "0.weight")
-                assert self.g(pm + "4.bias").data_ptr() == g0.data_ptr() + (vlen - 2) * 4, "velocity MLP grads not contiguous"
-                S["extra_slabs"].append((vslab, vblk, vlen, g0))
+        # the chains' inputs exist before any fork (a temporary made after it
+        # could be recycled by a main-stream allocation while a side kernel
+        # still reads it)
+        d_pvs_c = d_pvs.contiguous() if d_pvs is not None else None
+        d_enc_c = d_enc_pos.contiguous() if d_enc_pos is not None else None
+        live_frames = B * roll_live if roll_live else B * R
 
-        # ---- (main) reconstruction decoder backward, source-grad reduction, VFN backward
-        with self._p("dec_bwd:recon", 0, self._dec_bwd_bytes(F, F, lay, d_recons is not None)):
-            L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
-                               ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, 0, K,
-                               h, H, st)
-        L.paig_slab_reduce_multi(1, (ctypes.c_void_p * 1)(ptr(slab)), (ctypes.c_int * 1)(nb_rec + nb_roll),
-                                 (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, st)
-        if d_enc_pos is not None:
-            L.paig_axpby(ptr(d_enc_pos.contiguous()), ptr(denc), F * D, 1.0, 1.0, st)
-        offs = [0, vfn[0][1], vfn[0][1] + vfn[1][1]]
-        L.paig_vfn_bwd_multi(3, _parr([ptr(dsrc) + o * 4 for o in offs]), _parr([ptr(r) for _, _, _, r in vfn]),
-                             _iarr([sg for _, _, sg, _ in vfn]), _parr([ptr(S["src"][nm][0]) for nm, _, _, _ in vfn]),
-                             _parr([ptr(self.p(nm + ".l2.weight")) for nm, _, _, _ in vfn]),
-                             *[_parr([ptr(self.g(nm + suf)) for nm, _, _, _ in vfn])
-                               for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
-                             _parr([ptr(pt) for pt in vparts]), _iarr([P for _, P, _, _ in vfn]), st)
-        self._join(dev)
-        del d_pvs_c   # (kept alive across the side chain)
+        def dec_roll(q):   # rollout-frame decoder backward: d rollout positions + partial source grads
+            with self._p("dec_bwd:rollout", 0, self._dec_bwd_bytes(live_frames, B * R, lay, d_out is not None)):
+                L.paig_decoder_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
+                                   *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
+                                   ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, roll_live, K, h, H, q)
 
-        L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
+        def dec_rec(q):    # reconstruction decoder backward: d enc_pos + partial source grads
+            with self._p("dec_bwd:recon", 0, self._dec_bwd_bytes(F, F, lay, d_recons is not None)):
+                L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
+                                   ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, 0,
+                                   K, h, H, q)
+
+        def physics(q):    # rollout adjoint -> d pos0, d vel0, physics params; velocity encoder backward
+            L.paig_rollout_bwd(lay.cell, ptr(pvs), ptr(dpos_roll), ptr(d_pvs_c), ptr(prm[0]), ptr(prm[1]),
+                               ptr(prm[2]), ptr(dpos0), ptr(dvel0), ptr(rpart), ptr(gk), ptr(gq), 0, B, D, R, q)
+            if S["vel0"] is not None:
+                if lay.alt_vel:
+                    self.linear_bwd(S["Xv"], dvel0, K * B, "velocity_encoder.init_vel_linear", dXv, None, 0, q, ws)
+                else:   # one launch; its partial weight grads join the U-Net's batched slab reduction
+                    pm = "velocity_encoder.init_vel_mlp."
+                    L.paig_velmlp_bwd(ptr(dvel0), ptr(S["Xv"]), ptr(S["v1"]), ptr(S["v2"]),
+                                      ptr(self.p(pm + "0.weight")), ptr(self.p(pm + "2.weight")),
+                                      ptr(self.p(pm + "4.weight")), ptr(dXv), ptr(vslab), K * B, lay.ins, q)
+                    g0 = self.g(pm + "0.weight")
+                    assert self.g(pm + "4.bias").data_ptr() == g0.data_ptr() + (vlen - 2) * 4, \
+                        "velocity MLP grads not contiguous"
+                    S["extra_slabs"].append((vslab, vblk, vlen, g0))
+
+        def sources(q):    # source-gradient reduction (both decoders' slab rows), VFN backward
+            L.paig_slab_reduce_multi(1, (ctypes.c_void_p * 1)(ptr(slab)), (ctypes.c_int * 1)(nb_rec + nb_roll),
+                                     (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, q)
+            offs = [0, vfn[0][1], vfn[0][1] + vfn[1][1]]
+            L.paig_vfn_bwd_multi(3, _parr([ptr(dsrc) + o * 4 for o in offs]), _parr([ptr(r) for _, _, _, r in vfn]),
+                                 _iarr([sg for _, _, sg, _ in vfn]),
+                                 _parr([ptr(S["src"][nm][0]) for nm, _, _, _ in vfn]),
+                                 _parr([ptr(self.p(nm + ".l2.weight")) for nm, _, _, _ in vfn]),
+                                 *[_parr([ptr(self.g(nm + suf)) for nm, _, _, _ in vfn])
+                                   for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                                 _parr([ptr(pt) for pt in vparts]), _iarr([P for _, P, _, _ in vfn]), q)
+
+        if self._one_stream():
+            dec_roll(st)
+            physics(st)
+            dec_rec(st)
+            sources(st)
+            if d_enc_c is not None:
+                L.paig_axpby(ptr(d_enc_c), ptr(denc), F * D, 1.0, 1.0, st)
+            L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
+        else:
+            dec_roll(st)
+            sst = self._fork(dev)
+            physics(sst)   # (side) rollout adjoint + velocity encoder backward
+            dec_rec(st)    # (main) reconstruction decoder backward, source reduction, VFN backward
+            sources(st)
+            if d_enc_c is not None:
+                L.paig_axpby(ptr(d_enc_c), ptr(denc), F * D, 1.0, 1.0, st)
+            self._join(dev)
+            L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
+        del d_pvs_c, d_enc_c   # (kept alive across the side chain)
 
         self._encoder_backward(S, denc, st)
 
