@@ -229,6 +229,13 @@ int paig_head_fwd(const float* h2, const float* W3, const float* b3, float* h3, 
 int paig_head_bwd_blocks(int rows);
 int paig_head_bwd(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab, int F,
                   int K, int IN, float half, void* stream);
+/* paig_head_bwd with the velocity encoder's input gradient (dX of the packed
+ * rows, dpos0 of step S-1, as paig_vel_unpack_add takes them) added to dpos on
+ * the fly: the train step's unpack-add + head backward in one launch
+ * (blocks.py:43-48,101-103); F = B * Te frames */
+int paig_head_bwd_vel(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab,
+                      int F, int K, int IN, float half, const float* dX, const float* dpos0, int B, int Te, int S,
+                      int alt, void* stream);
 
 /* ---- velocity encoder input packing (blocks.py:33-45) */
 int paig_vel_pack(const float* pos, float* X, int B, int Te, int K, int S, int alt, void* stream);

@@ -45,6 +45,7 @@ SIGNATURES = {
     "paig_head_fwd": (I, [P, P, P, P, P, I, I, I, F32, P]),
     "paig_head_bwd_blocks": (I, [I]),
     "paig_head_bwd": (I, [P, P, P, P, P, P, I, I, I, F32, P]),
+    "paig_head_bwd_vel": (I, [P, P, P, P, P, P, I, I, I, F32, P, P, I, I, I, I, P]),
     "paig_maxpool2_fwd": (I, [P, LL, P, LL, I, I, I, I, P]),
     "paig_maxpool2_bwd_relu": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
     "paig_upsample2_fwd": (I, [P, LL, P, LL, I, I, I, I, I, I, P]),

@@ -300,11 +300,38 @@ head_fwd_k(const float* __restrict__ h2, const float* __restrict__ W3, const flo
   }
 }
 
+// the velocity encoder's input gradient folded into d enc_pos (what
+// paig_vel_unpack_add adds, in the same order): dX [K*B][cols] of the packed
+// rows, dpos0 [B][2K] of step S-1 (nullable)
+struct VelGrad {
+  const float* dX;
+  const float* dpos0;
+  int B, Te, S, alt;
+};
+__device__ __forceinline__ float vel_grad(const VelGrad& v, int K, int f, int k, int j) {
+  const int b = f / v.Te, t = f % v.Te;
+  if (v.dX == nullptr && v.dpos0 == nullptr) return 0.f;
+  if (t >= v.S) return 0.f;
+  const int cols = (v.alt ? v.S - 1 : v.S) * 2;
+  float g = 0.f;
+  if (v.dX) {
+    const float* xr = v.dX + (long long)(k * v.B + b) * cols;
+    if (v.alt) {
+      if (t >= 1) g += xr[(t - 1) * 2 + j];
+      if (t <= v.S - 2) g -= xr[t * 2 + j];
+    } else {
+      g += xr[t * 2 + j];
+    }
+  }
+  if (v.dpos0 && t == v.S - 1) g += v.dpos0[(long long)b * 2 * K + 2 * k + j];
+  return g;
+}
+
 // slab row per block: [W3 (2*IN) | b3 (2)]
 __global__ void __launch_bounds__(256)
 head_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const float* __restrict__ dpos,
            const float* __restrict__ W3, float* __restrict__ dh2, float* __restrict__ slab, int F, int K, int IN,
-           float half) {
+           float half, VelGrad vg) {
   __shared__ float D3[HEAD_RB][2];
   const int n0 = blockIdx.x * HEAD_RB, rows = K * F, tid = threadIdx.x;
   const int nr = rows - n0 < HEAD_RB ? rows - n0 : HEAD_RB;
@@ -314,7 +341,8 @@ head_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const flo
     if (r < nr) {
       const int n = n0 + r, k = n / F, f = n % F;
       const float t = tanhf(h3[(long long)n * 2 + j]);
-      d = dpos[(long long)f * 2 * K + 2 * k + j] * half * (1.f - t * t);
+      const float dp = dpos[(long long)f * 2 * K + 2 * k + j] + vel_grad(vg, K, f, k, j);
+      d = dp * half * (1.f - t * t);
     }
     D3[r][j] = d;
   }
@@ -362,7 +390,20 @@ int paig_head_bwd(const float* h2, const float* h3, const float* dpos, const flo
   const int rows = K * F;
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(head_bwd_k, dim3(cdiv(rows, HEAD_RB)), dim3(256), 0, (hipStream_t)stream, h2, h3, dpos, W3, dh2,
-                     slab, F, K, IN, half);
+                     slab, F, K, IN, half, VelGrad{nullptr, nullptr, 1, 1, 0, 0});
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_head_bwd_vel(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab,
+                      int F, int K, int IN, float half, const float* dX, const float* dpos0, int B, int Te, int S,
+                      int alt, void* stream) {
+  const int rows = K * F;
+  if (rows <= 0) return 0;
+  PAIG_REQUIRE(B > 0 && Te > 0 && F == B * Te && S <= Te, "head_bwd_vel: F=%d != B=%d x Te=%d or S=%d > Te", F, B,
+               Te, S);
+  hipLaunchKernelGGL(head_bwd_k, dim3(cdiv(rows, HEAD_RB)), dim3(256), 0, (hipStream_t)stream, h2, h3, dpos, W3, dh2,
+                     slab, F, K, IN, half, VelGrad{dX, dpos0, B, Te, S, alt});
   PAIG_CHECK_LAUNCH();
   return 0;
 }

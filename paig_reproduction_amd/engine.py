@@ -836,7 +836,12 @@ class Engine:
             sources(st)
             if d_enc_c is not None:
                 L.paig_axpby(ptr(d_enc_c), ptr(denc), F * D, 1.0, 1.0, st)
-            L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
+            # the velocity encoder's input gradient is added inside the head
+            # backward (PAIG_FUSE_VEL=0: the separate unpack-add launch)
+            vel = (dXv, dpos0, B, lay.Te, lay.ins, int(lay.alt_vel))
+            if os.environ.get("PAIG_FUSE_VEL", "1") == "0":
+                L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
+                vel = None
         else:
             dec_roll(st)
             sst = self._fork(dev)
@@ -847,11 +852,12 @@ class Engine:
                 L.paig_axpby(ptr(d_enc_c), ptr(denc), F * D, 1.0, 1.0, st)
             self._join(dev)
             L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
+            vel = None
         del d_pvs_c, d_enc_c   # (kept alive across the side chain)
 
-        self._encoder_backward(S, denc, st)
+        self._encoder_backward(S, denc, st, vel=vel)
 
-    def _encoder_backward(self, S, denc, st, hook=True):
+    def _encoder_backward(self, S, denc, st, hook=True, vel=None):
         """ConvolutionalEncoder backward from d enc_pos (denc [F][2K]): position
         head, l2/l1, mask softmax, U-Net; all its weight gradients."""
         lay = S["lay"]
@@ -865,8 +871,13 @@ class Engine:
         dh2 = _empty(K * F * 200, dev)
         hblk = L.paig_head_bwd_blocks(K * F)
         hslab = _empty(hblk * (2 * 200 + 2), dev)
-        L.paig_head_bwd(ptr(S["h2"]), ptr(S["h3"]), ptr(denc), ptr(self.p("encoder.l3.weight")), ptr(dh2), ptr(hslab),
-                        F, K, 200, float(H / 2), st)
+        if vel is not None:   # + the velocity encoder's input gradient (dXv, dpos0, B, Te, S, alt)
+            dXv, dpos0, Bv, Tev, Sv, altv = vel
+            L.paig_head_bwd_vel(ptr(S["h2"]), ptr(S["h3"]), ptr(denc), ptr(self.p("encoder.l3.weight")), ptr(dh2),
+                                ptr(hslab), F, K, 200, float(H / 2), ptr(dXv), ptr(dpos0), Bv, Tev, Sv, altv, st)
+        else:
+            L.paig_head_bwd(ptr(S["h2"]), ptr(S["h3"]), ptr(denc), ptr(self.p("encoder.l3.weight")), ptr(dh2),
+                            ptr(hslab), F, K, 200, float(H / 2), st)
         g3 = self.g("encoder.l3.weight")
         assert self.g("encoder.l3.bias").data_ptr() == g3.data_ptr() + 400 * 4, "l3 grads not contiguous"
         S["extra_slabs"].append((hslab, hblk, 402, g3))
