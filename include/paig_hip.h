@@ -216,6 +216,13 @@ int paig_vfn_bwd_multi(int n, const float* const* d, const float* const* y, cons
 int paig_velmlp_fwd(const float* pos, int B, int Te, int K, int S, const float* W0, const float* b0, const float* W2,
                     const float* b2, const float* W4, const float* b4, float* X, float* h1, float* h2, float* vel,
                     void* stream);
+/* paig_velmlp_fwd and paig_vfn_fwd_multi (n instances) in ONE launch (the two
+ * are independent; the train step's stream runs them back to back) */
+int paig_velmlp_vfn_fwd(const float* pos, int B, int Te, int K, int S, const float* W0, const float* b0,
+                        const float* W2, const float* b2, const float* W4, const float* b4, float* X, float* h1,
+                        float* h2, float* vel, int n, const float* const* vW1, const float* const* vb1,
+                        const float* const* vW2, const float* const* vb2, float* const* hout, float* const* y,
+                        float* const* ypost, const int* P, void* stream);
 int paig_velmlp_bwd_blocks(int rows);
 int paig_velmlp_slab_len(int S);
 int paig_velmlp_bwd(const float* dvel, const float* X, const float* h1, const float* h2, const float* W0,

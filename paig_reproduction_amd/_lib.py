@@ -39,6 +39,7 @@ SIGNATURES = {
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
     "paig_gather_u8_f32": (I, [P, P, P, I, LL, P]),
     "paig_velmlp_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
+    "paig_velmlp_vfn_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P]),
     "paig_velmlp_bwd_blocks": (I, [I]),
     "paig_velmlp_slab_len": (I, [I]),
     "paig_velmlp_bwd": (I, [P, P, P, P, P, P, P, P, P, I, I, P]),

@@ -12,6 +12,7 @@
 #include <stdio.h>
 
 #include "common.h"
+#include "vfn.h"
 
 static thread_local char g_err[512];
 
@@ -24,78 +25,9 @@ void paig_set_error(const char* fmt, ...) {
 
 namespace {
 
-constexpr int VH = 200;  // VariableFromNetwork hidden width (blocks.py:314)
-constexpr int VIN = 10;  // ones[1, 10]
+using namespace paig_vfn;
 
-// The three VariableFromNetwork instances (template, content, background) of a
-// step run as ONE launch per phase: a block finds its instance in a small
-// task table (block ranges), so the three latency-bound GEMVs overlap.
-constexpr int VMAX = 4;
-struct VfnFwdTasks {
-  const float* W1[VMAX];
-  const float* b1[VMAX];
-  const float* W2[VMAX];
-  const float* b2[VMAX];
-  float* hout[VMAX];
-  float* y[VMAX];
-  float* ypost[VMAX];
-  int P[VMAX];
-  int blk0[VMAX + 1];
-  int n;
-};
-struct VfnBwdTasks {
-  const float* d[VMAX];
-  const float* y[VMAX];
-  const float* h[VMAX];
-  const float* W2[VMAX];
-  float* dW1[VMAX];
-  float* db1[VMAX];
-  float* dW2[VMAX];
-  float* db2[VMAX];
-  float* part[VMAX];
-  int sig[VMAX];
-  int P[VMAX];
-  int blk0[VMAX + 1];   // bwd1 block ranges (rows per block = VROWS)
-  int n;
-};
-constexpr int VROWS = 8;
-
-__device__ __forceinline__ int task_of(const int* blk0, int n, int b) {
-  int k = 0;
-  while (k + 1 < n && b >= blk0[k + 1]) ++k;
-  return k;
-}
-
-// h = tanh(W1 @ ones + b1) in LDS; one wave per output row afterwards.
-__global__ void __launch_bounds__(256) vfn_fwd_k(VfnFwdTasks T) {
-  const int k = task_of(T.blk0, T.n, blockIdx.x);
-  const int bid = blockIdx.x - T.blk0[k], nb = T.blk0[k + 1] - T.blk0[k];
-  const float* __restrict__ W1 = T.W1[k];
-  const float* __restrict__ W2 = T.W2[k];
-  const int P = T.P[k];
-  __shared__ float h[VH];
-  for (int j = threadIdx.x; j < VH; j += blockDim.x) {
-    float s = 0.f;
-    for (int i = 0; i < VIN; ++i) s += W1[j * VIN + i];  // x = ones
-    const float v = tanhf(s + T.b1[k][j]);
-    h[j] = v;
-    if (bid == 0) T.hout[k][j] = v;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wg = (bid * blockDim.x + threadIdx.x) >> 6;
-  const int nw = (nb * blockDim.x) >> 6;
-  for (int p = wg; p < P; p += nw) {
-    float s = 0.f;
-    for (int j = lane; j < VH; j += 64) s = fmaf(W2[(long long)p * VH + j], h[j], s);
-    s = wave_sum(s);
-    if (lane == 0) {
-      const float v = s + T.b2[k][p];
-      T.y[k][p] = v;
-      if (T.ypost[k]) T.ypost[k][p] = 1.f / (1.f + expf(-v));
-    }
-  }
-}
+__global__ void __launch_bounds__(256) vfn_fwd_k(VfnFwdTasks T) { vfn_fwd_block(T, blockIdx.x); }
 
 // dy = d (raw) or d * s (1 - s), s = sigmoid(y) ; dW2 = dy h^T ; db2 = dy ;
 // part[blk][j] = sum_{p in blk} W2[p][j] dy[p]
@@ -340,23 +272,8 @@ int paig_vfn_fwd_multi(int n, const float* const* W1, const float* const* b1, co
                        const float* const* b2, float* const* hout, float* const* y, float* const* ypost, const int* P,
                        void* stream) {
   PAIG_REQUIRE(n >= 1 && n <= VMAX, "paig_vfn_fwd_multi: n=%d (1..%d)", n, VMAX);
-  VfnFwdTasks T{};
-  T.n = n;
-  T.blk0[0] = 0;
-  for (int k = 0; k < n; ++k) {
-    T.W1[k] = W1[k];
-    T.b1[k] = b1[k];
-    T.W2[k] = W2[k];
-    T.b2[k] = b2[k];
-    T.hout[k] = hout[k];
-    T.y[k] = y[k];
-    T.ypost[k] = ypost ? ypost[k] : nullptr;
-    T.P[k] = P[k];
-    int g = (P[k] + 3) / 4;
-    if (g > 1024) g = 1024;
-    if (g < 1) g = 1;
-    T.blk0[k + 1] = T.blk0[k] + g;
-  }
+  VfnFwdTasks T;
+  vfn_fwd_tasks(T, n, W1, b1, W2, b2, hout, y, ypost, P);
   hipLaunchKernelGGL(vfn_fwd_k, dim3(T.blk0[n]), dim3(256), 0, (hipStream_t)stream, T);
   PAIG_CHECK_LAUNCH();
   return 0;

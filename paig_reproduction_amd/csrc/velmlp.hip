@@ -9,6 +9,7 @@
 // gradients (the parameters' flat-buffer order) for the step's batched
 // deterministic slab reduction.
 #include "common.h"
+#include "vfn.h"
 
 namespace {
 
@@ -26,15 +27,32 @@ __device__ __forceinline__ float packed_in(const float* pos, int B, int Te, int 
 // LDS with an odd row pitch (lanes walk different rows: conflict-free)
 constexpr int FRB = 1, W2P = HID + 1;
 
-__global__ void __launch_bounds__(128)
-velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const float* __restrict__ W0,
-             const float* __restrict__ b0, const float* __restrict__ W2, const float* __restrict__ b2,
-             const float* __restrict__ W4, const float* __restrict__ b4, float* __restrict__ X,
-             float* __restrict__ h1, float* __restrict__ h2, float* __restrict__ vel) {
+struct VelFwd {
+  const float* pos;
+  int B, Te, K, IN;
+  const float *W0, *b0, *W2, *b2, *W4, *b4;
+  float *X, *h1, *h2, *vel;
+};
+
+// one row block of NTHR (>= 128) threads
+template <int NTHR>
+__device__ __forceinline__ void velmlp_fwd_block(const VelFwd& a, int blk) {
+  const float* __restrict__ pos = a.pos;
+  const int B = a.B, Te = a.Te, K = a.K, IN = a.IN;
+  const float* __restrict__ W0 = a.W0;
+  const float* __restrict__ b0 = a.b0;
+  const float* __restrict__ W2 = a.W2;
+  const float* __restrict__ b2 = a.b2;
+  const float* __restrict__ W4 = a.W4;
+  const float* __restrict__ b4 = a.b4;
+  float* __restrict__ X = a.X;
+  float* __restrict__ h1 = a.h1;
+  float* __restrict__ h2 = a.h2;
+  float* __restrict__ vel = a.vel;
   __shared__ float Xs[FRB][MAXIN];
   __shared__ float H1[HID][FRB], H2[FRB][HID + 1];   // H1 [u][r]: one broadcast read per u
   __shared__ float W2s[HID * W2P];
-  const int rows = K * B, r0 = blockIdx.x * FRB, tid = threadIdx.x;
+  const int rows = K * B, r0 = blk * FRB, tid = threadIdx.x;
   const int nr = rows - r0 < FRB ? rows - r0 : FRB;
   const int lane = tid & 63, wv = tid >> 6;
   // every parameter this thread needs is loaded up front, beside W2, so the
@@ -52,7 +70,7 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
   const float w4a = W4[jo * HID + lane], w4b = lane + 64 < HID ? W4[jo * HID + lane + 64] : 0.f, bb4 = b4[jo];
   if (((uintptr_t)W2 & 15) == 0) {   // all of W2 in flight at once: 20 float4 per thread
 #pragma unroll 5
-    for (int e = tid; e < HID * HID / 4; e += 128) {
+    for (int e = tid; e < HID * HID / 4; e += NTHR) {
       const f32x4v v = reinterpret_cast<const f32x4v*>(W2)[e];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -62,7 +80,7 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
     }
   } else {
 #pragma unroll 8
-    for (int q = tid; q < HID * HID; q += 128) W2s[(q / HID) * W2P + q % HID] = W2[q];
+    for (int q = tid; q < HID * HID; q += NTHR) W2s[(q / HID) * W2P + q % HID] = W2[q];
   }
   for (int e = tid; e < nr * IN; e += blockDim.x) {
     const int r = e / IN, c = e % IN;
@@ -112,6 +130,16 @@ velmlp_fwd_k(const float* __restrict__ pos, int B, int Te, int K, int IN, const 
     a = wave_sum(a);
     if (lane == 0) vel[(long long)(r0 + r) * OUT + jo] = a + bb4;
   }
+}
+
+__global__ void __launch_bounds__(128) velmlp_fwd_k(VelFwd a) { velmlp_fwd_block<128>(a, blockIdx.x); }
+
+// the velocity MLP's row blocks and the VariableFromNetwork forward's blocks
+// (independent computations) in ONE launch of 256-thread blocks: on the
+// step's single stream every launch saved is time saved
+__global__ void __launch_bounds__(256) velmlp_vfn_fwd_k(VelFwd a, int nvel, paig_vfn::VfnFwdTasks T) {
+  if ((int)blockIdx.x < nvel) velmlp_fwd_block<256>(a, blockIdx.x);
+  else paig_vfn::vfn_fwd_block(T, blockIdx.x - nvel);
 }
 
 // slab row (per block): [W0 (HID*IN) | b0 (HID) | W2 (HID*HID) | b2 (HID) | W4 (OUT*HID) | b4 (OUT)]
@@ -244,8 +272,26 @@ int paig_velmlp_fwd(const float* pos, int B, int Te, int K, int S, const float* 
   const int IN = 2 * S, rows = K * B;
   if (rows <= 0) return 0;
   PAIG_REQUIRE(IN <= MAXIN && S <= Te, "velmlp: input_steps %d unsupported (max %d)", S, MAXIN / 2);
-  hipLaunchKernelGGL(velmlp_fwd_k, dim3(cdiv(rows, FRB)), dim3(128), 0, (hipStream_t)stream, pos, B, Te, K, IN, W0, b0,
-                     W2, b2, W4, b4, X, h1, h2, vel);
+  const VelFwd a{pos, B, Te, K, IN, W0, b0, W2, b2, W4, b4, X, h1, h2, vel};
+  hipLaunchKernelGGL(velmlp_fwd_k, dim3(cdiv(rows, FRB)), dim3(128), 0, (hipStream_t)stream, a);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_velmlp_vfn_fwd(const float* pos, int B, int Te, int K, int S, const float* W0, const float* b0,
+                        const float* W2, const float* b2, const float* W4, const float* b4, float* X, float* h1,
+                        float* h2, float* vel, int n, const float* const* vW1, const float* const* vb1,
+                        const float* const* vW2, const float* const* vb2, float* const* hout, float* const* y,
+                        float* const* ypost, const int* P, void* stream) {
+  const int IN = 2 * S, rows = K * B;
+  PAIG_REQUIRE(rows > 0 && IN <= MAXIN && S <= Te, "velmlp_vfn: rows=%d, input_steps %d (max %d)", rows, S,
+               MAXIN / 2);
+  PAIG_REQUIRE(n >= 1 && n <= paig_vfn::VMAX, "velmlp_vfn: n=%d (1..%d)", n, paig_vfn::VMAX);
+  paig_vfn::VfnFwdTasks T;
+  const int nv = paig_vfn::vfn_fwd_tasks(T, n, vW1, vb1, vW2, vb2, hout, y, ypost, P);
+  const VelFwd a{pos, B, Te, K, IN, W0, b0, W2, b2, W4, b4, X, h1, h2, vel};
+  const int nvel = cdiv(rows, FRB);
+  hipLaunchKernelGGL(velmlp_vfn_fwd_k, dim3(nvel + nv), dim3(256), 0, (hipStream_t)stream, a, nvel, T);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

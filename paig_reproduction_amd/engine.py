@@ -491,8 +491,20 @@ class Engine:
                                    lay.frame, x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, q)
 
         if self._one_stream():
-            velocity(st)
-            vfn_src(st)
+            if vel0 is not None and not lay.alt_vel and os.environ.get("PAIG_FUSE_VFN", "0") != "0":
+                # velocity MLP + VFN sources in one launch (independent), then the rollout
+                pm = "velocity_encoder.init_vel_mlp."
+                L.paig_velmlp_vfn_fwd(ptr(enc_pos), B, lay.Te, K, lay.ins, *[ptr(self.p(pm + n)) for n in (
+                    "0.weight", "0.bias", "2.weight", "2.bias", "4.weight", "4.bias")], ptr(S["Xv"]), ptr(S["v1"]),
+                    ptr(S["v2"]), ptr(vel0), 3, *[_parr([ptr(self.p(nm + suf)) for nm, _, _ in vf])
+                                                  for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                    _parr([ptr(src[nm][0]) for nm, _, _ in vf]), _parr([ptr(src[nm][1]) for nm, _, _ in vf]),
+                    _parr([ptr(src[nm][2]) for nm, _, _ in vf]), _iarr([P for _, P, _ in vf]), st)
+                L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0),
+                                   ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, st)
+            else:
+                velocity(st)
+                vfn_src(st)
             dec_rec(st)
         else:
             sst = self._fork(dev)
