@@ -491,7 +491,7 @@ class Engine:
                                    lay.frame, x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, q)
 
         if self._one_stream():
-            if vel0 is not None and not lay.alt_vel and os.environ.get("PAIG_FUSE_VFN", "0") != "0":
+            if vel0 is not None and not lay.alt_vel and os.environ.get("PAIG_FUSE_VFN", "1") != "0":
                 # velocity MLP + VFN sources in one launch (independent), then the rollout
                 pm = "velocity_encoder.init_vel_mlp."
                 L.paig_velmlp_vfn_fwd(ptr(enc_pos), B, lay.Te, K, lay.ins, *[ptr(self.p(pm + n)) for n in (
