@@ -207,6 +207,10 @@ int paig_vfn_fwd_multi(int n, const float* const* W1, const float* const* b1, co
 int paig_vfn_bwd_multi(int n, const float* const* d, const float* const* y, const int* sig, const float* const* h,
                        const float* const* W2, float* const* dW1, float* const* db1, float* const* dW2,
                        float* const* db2, float* const* part, const int* P, void* stream);
+/* paig_vfn_bwd_multi's first phase only (dW2, db2, the block partials of dh) */
+int paig_vfn_bwd1_multi(int n, const float* const* d, const float* const* y, const int* sig, const float* const* h,
+                        const float* const* W2, float* const* dW1, float* const* db1, float* const* dW2,
+                        float* const* db2, float* const* part, const int* P, void* stream);
 
 /* ---- velocity encoder MLP fused (blocks.py:22-29, forward :43-48): rows
  * K*B of [2S] packed from pos [B][Te][2K] -> 100 tanh -> 100 tanh -> 2.
@@ -243,6 +247,15 @@ int paig_head_bwd(const float* h2, const float* h3, const float* dpos, const flo
 int paig_head_bwd_vel(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab,
                       int F, int K, int IN, float half, const float* dX, const float* dpos0, int B, int Te, int S,
                       int alt, void* stream);
+/* paig_head_bwd_vel and the second phase of paig_vfn_bwd_multi (n instances,
+ * the same arguments; its first phase ran before, paig_vfn_bwd1_multi) in
+ * one launch */
+int paig_head_bwd_vel_vfn2(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2,
+                           float* slab, int F, int K, int IN, float half, const float* dX, const float* dpos0, int B,
+                           int Te, int S, int alt, int n, const float* const* d, const float* const* y,
+                           const int* sig, const float* const* h, const float* const* W2, float* const* dW1,
+                           float* const* db1, float* const* dW2, float* const* db2, float* const* part, const int* P,
+                           void* stream);
 
 /* ---- velocity encoder input packing (blocks.py:33-45) */
 int paig_vel_pack(const float* pos, float* X, int B, int Te, int K, int S, int alt, void* stream);

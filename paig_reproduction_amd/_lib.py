@@ -47,6 +47,8 @@ SIGNATURES = {
     "paig_head_bwd_blocks": (I, [I]),
     "paig_head_bwd": (I, [P, P, P, P, P, P, I, I, I, F32, P]),
     "paig_head_bwd_vel": (I, [P, P, P, P, P, P, I, I, I, F32, P, P, I, I, I, I, P]),
+    "paig_head_bwd_vel_vfn2": (I, [P, P, P, P, P, P, I, I, I, F32, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P,
+                                   P]),
     "paig_maxpool2_fwd": (I, [P, LL, P, LL, I, I, I, I, P]),
     "paig_maxpool2_bwd_relu": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
     "paig_upsample2_fwd": (I, [P, LL, P, LL, I, I, I, I, I, I, P]),
@@ -75,6 +77,7 @@ SIGNATURES = {
     "paig_vfn_bwd": (I, [P, P, I, P, P, P, P, P, P, P, I, P]),
     "paig_vfn_fwd_multi": (I, [I, P, P, P, P, P, P, P, P, P]),
     "paig_vfn_bwd_multi": (I, [I, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "paig_vfn_bwd1_multi": (I, [I, P, P, P, P, P, P, P, P, P, P, P, P]),
     "paig_vel_pack": (I, [P, P, I, I, I, I, I, P]),
     "paig_vel_unpack_add": (I, [P, P, P, I, I, I, I, I, P]),
     "paig_rollout_fwd": (I, [I, P, LL, P, P, P, P, P, I, I, I, P]),

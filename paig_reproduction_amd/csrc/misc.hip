@@ -75,18 +75,7 @@ __global__ void __launch_bounds__(256) vfn_bwd1_k(VfnBwdTasks T) {
 
 // one 64-lane block per (instance, hidden unit j): dh[j] = sum of the
 // partials, then the tanh' and the first layer's grads (input = ones)
-__global__ void vfn_bwd2_k(VfnBwdTasks T) {
-  const int k = blockIdx.x / VH, j = blockIdx.x % VH;
-  const int nblk = T.blk0[k + 1] - T.blk0[k];
-  const float* __restrict__ part = T.part[k];
-  float s = 0.f;
-  for (int b = threadIdx.x; b < nblk; b += 64) s += part[b * VH + j];
-  s = wave_sum(s);
-  const float hj = T.h[k][j];
-  const float g = s * (1.f - hj * hj);
-  if (threadIdx.x < VIN) T.dW1[k][j * VIN + threadIdx.x] = g;
-  if (threadIdx.x == 0) T.db1[k][j] = g;
-}
+__global__ void vfn_bwd2_k(VfnBwdTasks T) { vfn_bwd2_item(T, blockIdx.x, threadIdx.x); }
 
 // losses: pred, extrap, recons (means of per-frame SSE)
 __global__ void loss_reduce_k(const float* __restrict__ sse_rec, const float* __restrict__ sse_roll, int B, int Te,
@@ -287,32 +276,32 @@ int paig_vfn_fwd(const float* W1, const float* b1, const float* W2, const float*
 int paig_vfn_bwd_blocks(int P) { return cdiv(P, VROWS); }
 
 // d: adjoint of y (sig = 0) or of sigmoid(y) (sig = 1). part[k]: >= blocks(P[k])*200 floats.
-int paig_vfn_bwd_multi(int n, const float* const* d, const float* const* y, const int* sig, const float* const* h,
-                       const float* const* W2, float* const* dW1, float* const* db1, float* const* dW2,
-                       float* const* db2, float* const* part, const int* P, void* stream) {
+static int vfn_bwd_launch(int n, const float* const* d, const float* const* y, const int* sig, const float* const* h,
+                          const float* const* W2, float* const* dW1, float* const* db1, float* const* dW2,
+                          float* const* db2, float* const* part, const int* P, void* stream, bool phase1_only) {
   PAIG_REQUIRE(n >= 1 && n <= VMAX, "paig_vfn_bwd_multi: n=%d (1..%d)", n, VMAX);
-  VfnBwdTasks T{};
-  T.n = n;
-  T.blk0[0] = 0;
-  for (int k = 0; k < n; ++k) {
-    T.d[k] = d[k];
-    T.y[k] = y[k];
-    T.sig[k] = sig[k];
-    T.h[k] = h[k];
-    T.W2[k] = W2[k];
-    T.dW1[k] = dW1[k];
-    T.db1[k] = db1[k];
-    T.dW2[k] = dW2[k];
-    T.db2[k] = db2[k];
-    T.part[k] = part[k];
-    T.P[k] = P[k];
-    T.blk0[k + 1] = T.blk0[k] + cdiv(P[k], VROWS);
-  }
+  VfnBwdTasks T;
+  vfn_bwd_tasks(T, n, d, y, sig, h, W2, dW1, db1, dW2, db2, part, P);
   hipLaunchKernelGGL(vfn_bwd1_k, dim3(T.blk0[n]), dim3(256), 0, (hipStream_t)stream, T);
   PAIG_CHECK_LAUNCH();
+  if (phase1_only) return 0;
   hipLaunchKernelGGL(vfn_bwd2_k, dim3(VH * n), dim3(64), 0, (hipStream_t)stream, T);
   PAIG_CHECK_LAUNCH();
   return 0;
+}
+
+int paig_vfn_bwd_multi(int n, const float* const* d, const float* const* y, const int* sig, const float* const* h,
+                       const float* const* W2, float* const* dW1, float* const* db1, float* const* dW2,
+                       float* const* db2, float* const* part, const int* P, void* stream) {
+  return vfn_bwd_launch(n, d, y, sig, h, W2, dW1, db1, dW2, db2, part, P, stream, false);
+}
+
+// phase 1 only (dW2, db2 and the per-block partials of dh): phase 2 then runs
+// inside paig_head_bwd_vel_vfn2's launch
+int paig_vfn_bwd1_multi(int n, const float* const* d, const float* const* y, const int* sig, const float* const* h,
+                        const float* const* W2, float* const* dW1, float* const* db1, float* const* dW2,
+                        float* const* db2, float* const* part, const int* P, void* stream) {
+  return vfn_bwd_launch(n, d, y, sig, h, W2, dW1, db1, dW2, db2, part, P, stream, true);
 }
 
 int paig_vfn_bwd(const float* d, const float* y, int sig, const float* h, const float* W2, float* dW1, float* db1,

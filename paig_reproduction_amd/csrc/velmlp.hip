@@ -373,13 +373,13 @@ __device__ __forceinline__ float vel_grad(const VelGrad& v, int K, int f, int k,
   return g;
 }
 
-// slab row per block: [W3 (2*IN) | b3 (2)]
-__global__ void __launch_bounds__(256)
-head_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const float* __restrict__ dpos,
-           const float* __restrict__ W3, float* __restrict__ dh2, float* __restrict__ slab, int F, int K, int IN,
-           float half, VelGrad vg) {
+// slab row per block: [W3 (2*IN) | b3 (2)]; blk = the block's row block
+__device__ __forceinline__ void head_bwd_block(const float* __restrict__ h2, const float* __restrict__ h3,
+                                               const float* __restrict__ dpos, const float* __restrict__ W3,
+                                               float* __restrict__ dh2, float* __restrict__ slab, int F, int K,
+                                               int IN, float half, const VelGrad& vg, int blk) {
   __shared__ float D3[HEAD_RB][2];
-  const int n0 = blockIdx.x * HEAD_RB, rows = K * F, tid = threadIdx.x;
+  const int n0 = blk * HEAD_RB, rows = K * F, tid = threadIdx.x;
   const int nr = rows - n0 < HEAD_RB ? rows - n0 : HEAD_RB;
   if (tid < HEAD_RB * 2) {
     const int r = tid >> 1, j = tid & 1;
@@ -393,7 +393,7 @@ head_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const flo
     D3[r][j] = d;
   }
   __syncthreads();
-  float* s = slab + (long long)blockIdx.x * (2 * IN + 2);
+  float* s = slab + (long long)blk * (2 * IN + 2);
   for (int u = tid; u < IN; u += blockDim.x) {
     const float w0 = W3[u], w1 = W3[IN + u];
     float g0 = 0.f, g1 = 0.f;
@@ -412,6 +412,28 @@ head_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const flo
     float a = 0.f;
     for (int r = 0; r < nr; ++r) a += D3[r][tid];
     s[2 * IN + tid] = a;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+head_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const float* __restrict__ dpos,
+           const float* __restrict__ W3, float* __restrict__ dh2, float* __restrict__ slab, int F, int K, int IN,
+           float half, VelGrad vg) {
+  head_bwd_block(h2, h3, dpos, W3, dh2, slab, F, K, IN, half, vg, blockIdx.x);
+}
+
+// the head backward's row blocks and the VariableFromNetwork backward's phase
+// 2 (independent: its phase 1 ran earlier on the stream) in one launch; a
+// phase-2 block takes 4 items, one per wave
+__global__ void __launch_bounds__(256)
+head_bwd_vfn2_k(const float* __restrict__ h2, const float* __restrict__ h3, const float* __restrict__ dpos,
+                const float* __restrict__ W3, float* __restrict__ dh2, float* __restrict__ slab, int F, int K, int IN,
+                float half, VelGrad vg, int nhead, paig_vfn::VfnBwdTasks T, int nitems) {
+  if ((int)blockIdx.x < nhead) {
+    head_bwd_block(h2, h3, dpos, W3, dh2, slab, F, K, IN, half, vg, blockIdx.x);
+  } else {
+    const int item = ((int)blockIdx.x - nhead) * 4 + (threadIdx.x >> 6);
+    if (item < nitems) paig_vfn::vfn_bwd2_item(T, item, threadIdx.x & 63);
   }
 }
 
@@ -437,6 +459,25 @@ int paig_head_bwd(const float* h2, const float* h3, const float* dpos, const flo
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(head_bwd_k, dim3(cdiv(rows, HEAD_RB)), dim3(256), 0, (hipStream_t)stream, h2, h3, dpos, W3, dh2,
                      slab, F, K, IN, half, VelGrad{nullptr, nullptr, 1, 1, 0, 0});
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_head_bwd_vel_vfn2(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2,
+                           float* slab, int F, int K, int IN, float half, const float* dX, const float* dpos0, int B,
+                           int Te, int S, int alt, int n, const float* const* d, const float* const* y,
+                           const int* sig, const float* const* h, const float* const* W2, float* const* dW1,
+                           float* const* db1, float* const* dW2, float* const* db2, float* const* part, const int* P,
+                           void* stream) {
+  const int rows = K * F;
+  PAIG_REQUIRE(rows > 0 && B > 0 && Te > 0 && F == B * Te && S <= Te,
+               "head_bwd_vel_vfn2: F=%d != B=%d x Te=%d or S=%d > Te", F, B, Te, S);
+  PAIG_REQUIRE(n >= 1 && n <= paig_vfn::VMAX, "head_bwd_vel_vfn2: n=%d (1..%d)", n, paig_vfn::VMAX);
+  paig_vfn::VfnBwdTasks T;
+  paig_vfn::vfn_bwd_tasks(T, n, d, y, sig, h, W2, dW1, db1, dW2, db2, part, P);
+  const int nhead = cdiv(rows, HEAD_RB), nitems = paig_vfn::VH * n;
+  hipLaunchKernelGGL(head_bwd_vfn2_k, dim3(nhead + cdiv(nitems, 4)), dim3(256), 0, (hipStream_t)stream, h2, h3, dpos,
+                     W3, dh2, slab, F, K, IN, half, VelGrad{dX, dpos0, B, Te, S, alt}, nhead, T, nitems);
   PAIG_CHECK_LAUNCH();
   return 0;
 }

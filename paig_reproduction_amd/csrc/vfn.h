@@ -106,4 +106,44 @@ inline int vfn_fwd_tasks(VfnFwdTasks& T, int n, const float* const* W1, const fl
   return T.blk0[n];
 }
 
+// backward phase 2, one item = (instance k, hidden unit j) on one 64-lane
+// wave: dh[j] = the phase-1 block partials summed, the tanh', and the first
+// layer's grads (input = ones)
+__device__ __forceinline__ void vfn_bwd2_item(const VfnBwdTasks& T, int item, int lane) {
+  const int k = item / VH, j = item % VH;
+  const int nblk = T.blk0[k + 1] - T.blk0[k];
+  const float* __restrict__ part = T.part[k];
+  float s = 0.f;
+  for (int b = lane; b < nblk; b += 64) s += part[b * VH + j];
+  s = wave_sum(s);
+  const float hj = T.h[k][j];
+  const float g = s * (1.f - hj * hj);
+  if (lane < VIN) T.dW1[k][j * VIN + lane] = g;
+  if (lane == 0) T.db1[k][j] = g;
+}
+
+// the backward task table of n <= VMAX instances; returns phase 1's block count
+inline int vfn_bwd_tasks(VfnBwdTasks& T, int n, const float* const* d, const float* const* y, const int* sig,
+                         const float* const* h, const float* const* W2, float* const* dW1, float* const* db1,
+                         float* const* dW2, float* const* db2, float* const* part, const int* P) {
+  T = VfnBwdTasks{};
+  T.n = n;
+  T.blk0[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    T.d[k] = d[k];
+    T.y[k] = y[k];
+    T.sig[k] = sig[k];
+    T.h[k] = h[k];
+    T.W2[k] = W2[k];
+    T.dW1[k] = dW1[k];
+    T.db1[k] = db1[k];
+    T.dW2[k] = dW2[k];
+    T.db2[k] = db2[k];
+    T.part[k] = part[k];
+    T.P[k] = P[k];
+    T.blk0[k + 1] = T.blk0[k] + (P[k] + VROWS - 1) / VROWS;
+  }
+  return T.blk0[n];
+}
+
 }  // namespace paig_vfn

@@ -829,29 +829,36 @@ class Engine:
                         "velocity MLP grads not contiguous"
                     S["extra_slabs"].append((vslab, vblk, vlen, g0))
 
-        def sources(q):    # source-gradient reduction (both decoders' slab rows), VFN backward
+        def sources(q, split=False):   # source-gradient reduction (both decoders' slab rows), VFN backward
             L.paig_slab_reduce_multi(1, (ctypes.c_void_p * 1)(ptr(slab)), (ctypes.c_int * 1)(nb_rec + nb_roll),
                                      (ctypes.c_int * 1)(slab_len), (ctypes.c_void_p * 1)(ptr(dsrc)), 0, q)
             offs = [0, vfn[0][1], vfn[0][1] + vfn[1][1]]
-            L.paig_vfn_bwd_multi(3, _parr([ptr(dsrc) + o * 4 for o in offs]), _parr([ptr(r) for _, _, _, r in vfn]),
-                                 _iarr([sg for _, _, sg, _ in vfn]),
-                                 _parr([ptr(S["src"][nm][0]) for nm, _, _, _ in vfn]),
-                                 _parr([ptr(self.p(nm + ".l2.weight")) for nm, _, _, _ in vfn]),
-                                 *[_parr([ptr(self.g(nm + suf)) for nm, _, _, _ in vfn])
-                                   for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
-                                 _parr([ptr(pt) for pt in vparts]), _iarr([P for _, P, _, _ in vfn]), q)
+            args = (3, _parr([ptr(dsrc) + o * 4 for o in offs]), _parr([ptr(r) for _, _, _, r in vfn]),
+                    _iarr([sg for _, _, sg, _ in vfn]),
+                    _parr([ptr(S["src"][nm][0]) for nm, _, _, _ in vfn]),
+                    _parr([ptr(self.p(nm + ".l2.weight")) for nm, _, _, _ in vfn]),
+                    *[_parr([ptr(self.g(nm + suf)) for nm, _, _, _ in vfn])
+                      for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
+                    _parr([ptr(pt) for pt in vparts]), _iarr([P for _, P, _, _ in vfn]))
+            if split:      # phase 1 here, phase 2 inside the head backward's launch
+                L.paig_vfn_bwd1_multi(*args, q)
+                return args
+            L.paig_vfn_bwd_multi(*args, q)
+            return None
 
         if self._one_stream():
             dec_roll(st)
             physics(st)
             dec_rec(st)
-            sources(st)
+            fuse_vel = os.environ.get("PAIG_FUSE_VEL", "1") != "0"
+            # VFN backward phase 2 inside the head backward's launch
+            vfn2 = sources(st, split=fuse_vel and os.environ.get("PAIG_FUSE_VFN2", "1") != "0")
             if d_enc_c is not None:
                 L.paig_axpby(ptr(d_enc_c), ptr(denc), F * D, 1.0, 1.0, st)
             # the velocity encoder's input gradient is added inside the head
             # backward (PAIG_FUSE_VEL=0: the separate unpack-add launch)
-            vel = (dXv, dpos0, B, lay.Te, lay.ins, int(lay.alt_vel))
-            if os.environ.get("PAIG_FUSE_VEL", "1") == "0":
+            vel = (dXv, dpos0, B, lay.Te, lay.ins, int(lay.alt_vel), vfn2)
+            if not fuse_vel:
                 L.paig_vel_unpack_add(ptr(dXv), ptr(dpos0), ptr(denc), B, lay.Te, K, lay.ins, int(lay.alt_vel), st)
                 vel = None
         else:
@@ -883,8 +890,13 @@ class Engine:
         dh2 = _empty(K * F * 200, dev)
         hblk = L.paig_head_bwd_blocks(K * F)
         hslab = _empty(hblk * (2 * 200 + 2), dev)
-        if vel is not None:   # + the velocity encoder's input gradient (dXv, dpos0, B, Te, S, alt)
-            dXv, dpos0, Bv, Tev, Sv, altv = vel
+        if vel is not None and vel[6] is not None:   # + the VFN backward's phase 2
+            dXv, dpos0, Bv, Tev, Sv, altv, vfn2 = vel
+            L.paig_head_bwd_vel_vfn2(ptr(S["h2"]), ptr(S["h3"]), ptr(denc), ptr(self.p("encoder.l3.weight")),
+                                     ptr(dh2), ptr(hslab), F, K, 200, float(H / 2), ptr(dXv), ptr(dpos0), Bv, Tev,
+                                     Sv, altv, *vfn2, st)
+        elif vel is not None:   # + the velocity encoder's input gradient (dXv, dpos0, B, Te, S, alt)
+            dXv, dpos0, Bv, Tev, Sv, altv, _ = vel
             L.paig_head_bwd_vel(ptr(S["h2"]), ptr(S["h3"]), ptr(denc), ptr(self.p("encoder.l3.weight")), ptr(dh2),
                                 ptr(hslab), F, K, 200, float(H / 2), ptr(dXv), ptr(dpos0), Bv, Tev, Sv, altv, st)
         else:
