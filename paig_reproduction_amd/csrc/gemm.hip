@@ -350,8 +350,13 @@ __device__ __forceinline__ s16x8 frag16(const short* img, int r0, int lane) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// Occupancy over ring depth: the l1 dgrad's 1536 blocks fit the 256 CUs in
+// one round at 6 blocks per CU (LDS allows 6), i.e. <= 80 VGPRs; a 3-deep
+// register ring needs 124 (4 per CU: two rounds), and 2-deep spills at 80.
+// Measured (tools/gemm_bench.py): depth 1 at 6 waves/SIMD 27.6 us vs 31.7 us
+// for that GEMM, the others unchanged; the step 1.168 vs 1.177 ms
 template <bool TA, bool TB, int PM, bool VEC>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6)))
 gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
              const float* __restrict__ B, long long ldb, int vecb, float* __restrict__ C, long long ldc, float beta,
              const float* __restrict__ bias, int act, int auxm, const float* __restrict__ aux, long long ldaux,
@@ -392,9 +397,9 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
   __shared__ float smx[8];
 
   // register ring of NS K-tiles: the loads of tile k + NS are issued right
-  // after tile k is parked in LDS, so NS-1 tiles stay in flight behind the
-  // MFMAs (these GEMMs are short per block: latency, not bandwidth, bound)
-  constexpr int NS = 3;
+  // after tile k is parked in LDS, so they fly behind tile k's MFMAs (and
+  // the other 5 blocks of the CU hide the rest; see the occupancy note above)
+  constexpr int NS = 1;
   Tile<!TA> ta[NS];
   Tile<TB> tb[NS];
 #pragma unroll
@@ -406,7 +411,12 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
 #pragma unroll
     for (int st = 0; st < NS; ++st) {
       const int kk = k0 + st * BK;
-      if (kk >= kend) break;
+      // a stage past kend skips its work (uniform branch) but still issues
+      // its (zero) ring loads: every path then issues the same loads in the
+      // same order, so the compiler's wait before a stage's use counts the
+      // NS-1 tiles behind it (a `break` here made it drain the whole ring at
+      // the top of every NS-tile group)
+      if (kk < kend) {
       // this K-tile's max |op(A)| / |op(B)| (dynamic operands), published
       // before the barrier (the previous tile's smx reads finished before the
       // last one)
@@ -450,8 +460,10 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
       store16<TB, PM>(tb[st], Bh, Bl, tid, bsc, DB ? dmx : rmax);
       if (do_rs) rs4 += ta[st].v[0] + ta[st].v[1];
       __syncthreads();
+      }
       ta[st].template load_bf<VEC>(A, lda, m0, kk + NS * BK, M, kend, tid);
       tb[st].template load_bf<VEC>(B, ldb, n0, kk + NS * BK, N, kend, tid);
+      if (kk < kend) {
       s16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -473,6 +485,7 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
           }
           acc[i][j] = gmma<PM>(ah[i], bh[j], acc[i][j]);
         }
+      }
     }
   }
   if (do_rs) {
@@ -657,7 +670,7 @@ gemm_split_w_k(int M, int N, int K, int kchunk, float alpha, const float* __rest
 #pragma unroll
     for (int st = 0; st < NS; ++st) {
       const int kk = k0 + st * BK;
-      if (kk >= kend) break;
+      if (kk < kend) {   // (no break: see gemm_split_k)
       if constexpr (DA) {
         const float ma = wave_max_u(ta[st].amax());
         if (lane == 0) smx[wv] = ma;
@@ -703,8 +716,10 @@ gemm_split_w_k(int M, int N, int K, int kchunk, float alpha, const float* __rest
         for (int e = 0; e < TTA::E; ++e) rs4 += ta[st].v[e];
       }
       __syncthreads();
+      }
       ta[st].template load_bf<VEC>(A, lda, m0, kk + NS * BK, M, kend, tid);
       tb[st].template load_bf<VEC>(B, ldb, n0, kk + NS * BK, N, kend, tid);
+      if (kk < kend) {
       s16x8 ah[MI], al[MI], bh[NJ], bl[NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
@@ -726,6 +741,7 @@ gemm_split_w_k(int M, int N, int K, int kchunk, float alpha, const float* __rest
           }
           acc[i][j] = gmma<PM>(ah[i], bh[j], acc[i][j]);
         }
+      }
     }
   }
   if (do_rs) {
