@@ -251,9 +251,14 @@ def run_workload(a, world, rank, dev, task, batch, seq_len, conv_math, steps, wa
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # an event after every step (stream-ordered, no sync): per-step device
+    # intervals for the median; `value` stays the whole-loop mean
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
+    evs[0].record()
     for i in range(steps):
         loss = step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -263,6 +268,8 @@ def run_workload(a, world, rank, dev, task, batch, seq_len, conv_math, steps, wa
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     gstep.finish()
+    per = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+    med_ms = per[len(per) // 2] if len(per) % 2 else 0.5 * (per[len(per) // 2 - 1] + per[len(per) // 2])
     lossv = float(loss.item())
     # roofline probes: every tagged main-stream launch timed with HIP events
     # on its stream, over eager steps of the same workload after the timed region
@@ -272,7 +279,7 @@ def run_workload(a, world, rank, dev, task, batch, seq_len, conv_math, steps, wa
         eager_step()
     eng.probe = None
     kds = probe.summaries()
-    res = {"value": world * batch * steps / el, "el": el, "loss": lossv, "kds": kds, "split": gstep.split,
+    res = {"value": world * batch * steps / el, "el": el, "med_ms": med_ms, "loss": lossv, "kds": kds, "split": gstep.split,
            "opt_in_graph": gstep.opt_in_graph, "dataset_seqs": int(u8.shape[0]), "ins": ins, "pred": pred, "size": size,
            "u8_head": u8[:100]}
     del gstep, m, eng, it, xbuf
@@ -281,23 +288,65 @@ def run_workload(a, world, rank, dev, task, batch, seq_len, conv_math, steps, wa
     return res
 
 
+PEAK_F16_TFLOPS = 2500.0   # dense 16-bit MFMA (f16 / bf16), MI355X_MICROARCH.md
+MFMA_FAMILIES = ("conv_fwd", "conv_dgrad", "conv_wgrad", "conv_bwd", "gemm_fwd", "gemm_wgrad", "gemm_dgrad")
+
+
+def mfma_roof(conv_math):
+    """(matrix-core FLOPs issued per algorithmic FLOP, peak TFLOP/s) of the
+    MFMA kernels: split = 3 f16 MFMAs per product (hi*hi + hi*lo + lo*hi),
+    bf16 = 1, fp32 = the f32-input MFMA at the fp32 rate."""
+    return {"split": (3, PEAK_F16_TFLOPS), "bf16": (1, PEAK_F16_TFLOPS), "fp32": (1, PEAK_FP32_TFLOPS)}[conv_math]
+
+
 def roof_of(kd, conv_math):
+    """Both roofs of one probed launch: HBM (algorithmic bytes / launch time
+    vs 8 TB/s) and, for the matrix-core kernels, MFMA (the FLOPs the matrix
+    cores issue / launch time vs their dense peak); `bound` / `frac` are the
+    binding one (the larger fraction)."""
     sec = kd["avg_ms"] * 1e-3
     tflops = kd["flops"] / sec / 1e12
-    if conv_math == "fp32" and kd["tag"].split(":")[0] in ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm_fwd",
-                                                           "gemm_wgrad", "gemm_dgrad"):
-        # f32-input MFMA: bounded by the fp32 matrix rate
-        return {"bound": "mfma", "kernel": kd["tag"], "achieved": round(tflops, 3), "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4), "avg_us": round(kd["avg_ms"] * 1e3, 2),
-                "launches": kd["n"], "algorithmic_flops": kd["flops"], "algorithmic_bytes": kd["bytes"]}
-    # 16-bit matrix cores / VALU kernels: HBM-bound; achieved = algorithmic
-    # bytes per launch / launch time
     gbs = kd["bytes"] / sec / 1e9
-    return {"bound": "hbm", "kernel": kd["tag"], "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_tflops": round(tflops, 2),
-            "avg_us": round(kd["avg_ms"] * 1e3, 2), "avg_us_events_raw": round(kd["avg_ms_raw"] * 1e3, 2),
-            "event_overhead_us": round(kd["overhead_ms"] * 1e3, 2), "launches": kd["n"],
-            "algorithmic_flops": kd["flops"], "algorithmic_bytes": kd["bytes"]}
+    fam = kd["tag"].split(":")[0]
+    hbm_frac = gbs / PEAK_HBM_GBS
+    mfma = None
+    if fam in MFMA_FAMILIES and kd["flops"]:
+        mult, peak = mfma_roof(conv_math)
+        mfma = {"achieved": round(mult * tflops, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(mult * tflops / peak, 4), "mfma_flops_per_flop": mult}
+    out = {"kernel": kd["tag"], "avg_us": round(kd["avg_ms"] * 1e3, 2),
+           "avg_us_events_raw": round(kd["avg_ms_raw"] * 1e3, 2), "event_overhead_us": round(kd["overhead_ms"] * 1e3, 2),
+           "launches": kd["n"], "algorithmic_flops": kd["flops"], "algorithmic_bytes": kd["bytes"],
+           "algorithmic_tflops": round(tflops, 2),
+           "hbm": {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(hbm_frac, 4)},
+           "mfma": mfma}
+    if mfma is not None and mfma["frac"] > hbm_frac:
+        out.update({"bound": "mfma", "achieved": mfma["achieved"], "peak": mfma["peak"], "unit": "TFLOP/s",
+                    "frac": mfma["frac"]})
+    else:
+        out.update({"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(hbm_frac, 4)})
+    return out
+
+
+# the fixed headline probe, comparable across rounds: the backward of the
+# ShallowUNet's c11 (24 -> 8 channels at 32 x 32; wgrad + dgrad, or the fused
+# backward kernel when the layer runs one)
+HEADLINE_LAYER = "c11"
+
+
+def headline_roof(kds, conv_math):
+    parts = [t for t in ("conv_bwd:" + HEADLINE_LAYER, "conv_wgrad:" + HEADLINE_LAYER,
+                         "conv_dgrad:" + HEADLINE_LAYER) if t in kds]
+    if not parts:
+        return None
+    agg = {"tag": "conv_bwd:" + HEADLINE_LAYER, "n": min(kds[t]["n"] for t in parts),
+           "avg_ms": sum(kds[t]["avg_ms"] for t in parts), "avg_ms_raw": sum(kds[t]["avg_ms_raw"] for t in parts),
+           "overhead_ms": kds[parts[0]]["overhead_ms"],
+           "flops": sum(kds[t]["flops"] for t in parts), "bytes": sum(kds[t]["bytes"] for t in parts)}
+    r = roof_of(agg, conv_math)
+    r["launch_tags"] = parts
+    return r
 
 
 def main():
@@ -342,10 +391,12 @@ def main():
     # the other large kernel families, for the record
     others = {}
     for want in ("dec_bwd:rollout", "dec_bwd:recon", "dec_fwd:rollout", "gemm_fwd:encoder.l1", "gemm_dgrad:encoder.l2",
-                 "conv_wgrad:c11", "conv_fwd:c11", "conv_dgrad:c2"):
+                 "conv_wgrad:c11", "conv_fwd:c11", "conv_dgrad:c2", "conv_bwd:c11", "conv_bwd:c2"):
         if want in kds and want != tag:
             rr = roof_of(kds[want], a.conv_math)
             others[want] = {k: rr[k] for k in ("bound", "achieved", "unit", "frac", "avg_us")}
+            others[want]["hbm_frac"] = rr["hbm"]["frac"]
+            others[want]["mfma_frac"] = rr["mfma"]["frac"] if rr["mfma"] else None
     # BASELINE configs #2-#5 as extra legs (per-rank B, the same DP path)
     legs = {}
     if a.legs:
@@ -373,7 +424,9 @@ def main():
             "metric": METRIC if (a.task, a.batch) == ("spring_color", 100) else
             f"video-seqs/sec (train step) {a.task} B={a.batch}",
             "value": round(value, 2), "unit": "video-seqs/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(el / a.steps * 1e3, 3), "ms_per_step_median": round(r["med_ms"], 4),
+            "value_median": round(world * a.batch / (r["med_ms"] * 1e-3), 2),
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16" if a.conv_math == "bf16" else "fp32",
             "data": "synthetic",
             "config": {"workload": f"{a.task} PhysicsNet train step (get_batch gather+fwd+loss+bwd+allreduce+RMSprop), "
@@ -382,7 +435,7 @@ def main():
                        "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}",
                        "conv_math": a.conv_math, "split_graph": r["split"],
                        "optimizer_in_graph": r["opt_in_graph"], "dataset_seqs": r["dataset_seqs"]},
-            "roofline": roof, "roofline_others": others, "cpu_baseline": cpu, "final_loss": round(r["loss"], 4),
+            "roofline": roof, "roofline_headline": headline_roof(kds, a.conv_math), "roofline_others": others, "cpu_baseline": cpu, "final_loss": round(r["loss"], 4),
             # whole-step memory-side traffic (committed PMC profile) at this run's step time
             "hbm_step": None if step_bytes is None else {
                 "bytes_per_step": round(step_bytes), "achieved_GBs": round(step_bytes / (el / a.steps) / 1e9, 1),

@@ -28,6 +28,10 @@
 extern "C" {
 #endif
 
+/* Version of this interface: bumped whenever an entry point's argument list
+ * or a data layout it exchanges changes (the Python binding refuses a library
+ * of another version). */
+#define PAIG_ABI_VERSION 2
 const char* paig_last_error(void);
 int paig_abi_version(void);
 /* f16 range guard of the split-precision path.  Activations and gradients

@@ -16,6 +16,8 @@ LIB_PATH = os.path.join(_HERE, "libpaig_hip.so")
 XMAX_SLOTS = 2048
 
 AB_PATH = os.environ.get("PAIG_AB_LIB")
+# include/paig_hip.h PAIG_ABI_VERSION: the SIGNATURES below are this version's
+ABI_VERSION = 2
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -125,6 +127,13 @@ class _Lib:
                             "(or __graft_entry__.build()); there is no CPU fallback")
         self.path = path
         self.dll = ctypes.CDLL(path)
+        self.dll.paig_abi_version.restype = I
+        self.dll.paig_abi_version.argtypes = []
+        ver = self.dll.paig_abi_version()
+        if ver != ABI_VERSION:
+            # an A/B build of another interface version would take this
+            # version's argument lists (shifted arguments, misread layouts)
+            raise PaigError(f"{path}: C ABI version {ver}, this binding is version {ABI_VERSION}")
         self.fns = {}
         for name, (rt, args) in SIGNATURES.items():
             if path != LIB_PATH and not hasattr(self.dll, name):

@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// the declarations every entry point must match (and PAIG_ABI_VERSION)
+#include "../../include/paig_hip.h"
+
 #define PAIG_E_SHAPE 1001
 #define PAIG_E_UNSUPPORTED 1002
 

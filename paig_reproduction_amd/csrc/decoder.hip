@@ -1611,6 +1611,11 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
   PAIG_REQUIRE(pos_grp <= 0 || F % pos_grp == 0, "decoder_bwd: F=%d is not a multiple of the group %d", F, pos_grp);
   PAIG_REQUIRE(pos_grp <= 0 || tgt_grp == pos_grp || live == 0,
                "decoder_bwd: target group %d must equal the position group %d", tgt_grp, pos_grp);
+  // live > 0 promises that the frames past `live` in every group carry a zero
+  // SSE weight and no dense gradient: the one-CU kernels skip them, the
+  // generic ones walk them (zero contribution), so both give the same result
+  PAIG_REQUIRE(live == 0 || dout == nullptr, "decoder_bwd: live=%d with a dense dL/dout (dead frames would be skipped)",
+               live);
   PosView pv{pos, pos_outer, pos_inner, pos_grp};
   Src S{tmpl, cont, bg};
   FView t{tgt, tgt_fs, tgt_gs, tgt_grp};

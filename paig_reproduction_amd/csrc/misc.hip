@@ -237,7 +237,9 @@ extern "C" {
 
 const char* paig_last_error(void) { return g_err; }
 
-int paig_abi_version(void) { return 1; }
+// 2: paig_decoder_bwd(_blocks) take `live`; the paig_conv_wprep image starts
+// with the channel-exponent header (round 3)
+int paig_abi_version(void) { return PAIG_ABI_VERSION; }
 
 // f16 range guard (common.h): waits for the device, then reads (and with
 // clear != 0 resets) the flags the split-precision kernels set when an

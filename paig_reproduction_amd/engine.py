@@ -536,7 +536,17 @@ class Engine:
             "contents": cont.view(K, 3, h, h),
             "background_content": bgp.view(1, 3, H, H),
         }
+        if not need_saved:
+            self._release_xmax(S)
         return res, (S if need_saved else None)
+
+    def _release_xmax(self, S):
+        """Return a forward's xmax slots to the free list (its backward has
+        been queued, or there is none); stream order keeps the next user
+        behind every kernel that reads them."""
+        buf = S.pop("xmax_buf", None)
+        if buf is not None:
+            self._xmax.setdefault(S["xmax_key"], []).append(buf)
 
     def _unet_forward(self, S, lay, x_view, st, fuse_head=False):
         """The U-Net plan over F frames addressed by x_view (frame view
@@ -581,15 +591,18 @@ class Engine:
         # per conv: the split forward's per-block max |input| slots, which
         # set the X scale of the same input's wgrad (every slot is written;
         # zeroed so that a slot no forward wrote falls back to the guarded
-        # fixed scale instead of a garbage exponent).  Kept per (device,
-        # layout): a step of the same shape rewrites exactly the same slots,
-        # so the zero fill (an extra launch per step) happens once.
+        # fixed scale instead of a garbage exponent).  Each forward owns its
+        # buffer until its backward has consumed it (a second forward before
+        # the first one's backward takes another); buffers return to a
+        # per-(device, layout) free list, so steady-state steps reuse one
+        # buffer (a step of the same shape rewrites exactly the same slots)
+        # and the zero fill (an extra launch) happens once.
         key = (str(dev), len(lay.ops), lay.F, lay.H)
-        xmax = self._xmax.get(key)
-        if xmax is None:
-            xmax = self._xmax[key] = torch.zeros(len(lay.ops) * XMAX_SLOTS, device=dev)
+        free = self._xmax.setdefault(key, [])
+        xmax = free.pop() if free else torch.zeros(len(lay.ops) * XMAX_SLOTS, device=dev)
         S["xmax"] = lambda i: ptr(xmax) + i * XMAX_SLOTS * 4
         S["xmax_buf"] = xmax
+        S["xmax_key"] = key
         # split path: every conv's forward and dgrad weight images, pre-split
         # in one launch per step (paig_conv_wprep) and copied by the kernels
         wp = {}
@@ -1076,3 +1089,4 @@ class Engine:
         dsts = (ctypes.c_void_p * n)(*[ptr(s[3]) for s in slabs])
         L.paig_slab_reduce_multi(n, srcs, nbs, lens, dsts, 0, st)
         S["_slabs"] = slabs
+        self._release_xmax(S)

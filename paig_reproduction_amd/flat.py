@@ -23,6 +23,19 @@ from ._lib import lib, ptr, stream_handle
 _OWNER = weakref.WeakValueDictionary()
 
 
+class _DeferredMean:
+    """An asynchronous gloo SUM all-reduce whose divide by the world size
+    runs at wait(): the same start / overlap / wait() contract as RCCL's AVG
+    work handle (FlatParams.allreduce_early / allreduce_grads)."""
+
+    def __init__(self, work, t, n):
+        self.work, self.t, self.n = work, t, n
+
+    def wait(self):
+        self.work.wait()
+        self.t.div_(self.n)
+
+
 def deposit_grad(p, g):
     """Add gradient g to parameter p with torch semantics (p.grad None ->
     set, else accumulate).  A parameter that lives in a FlatParams buffer gets
@@ -206,11 +219,16 @@ class FlatParams:
     @staticmethod
     def _mean(t, group, async_op=False):
         """In-place mean over the group: RCCL AVG over xGMI; gloo (the CPU
-        harness of the DP path) has no AVG, so SUM then scale."""
+        harness of the DP path) has no AVG, so SUM then scale -- asynchronous
+        too when asked (the divide deferred to wait()), so the early-bucket
+        start / overlap / wait ordering runs the same way on both backends."""
         if dist.get_backend(group) == "nccl":
             return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group, async_op=async_op)
-        w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        t.div_(dist.get_world_size(group))
+        n = dist.get_world_size(group)
+        if async_op:
+            return _DeferredMean(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True), t, n)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.div_(n)
         return None
 
     def allreduce_early(self, group=None):
@@ -221,8 +239,6 @@ class FlatParams:
         if not self._dp(group) or self._redirect is not None or self.n32_early == 0 or self._early_work is not None:
             return
         self._early_work = (self._mean(self.g32[:self.n32_early], group, async_op=True), group)
-        if self._early_work[0] is None:   # gloo: completed synchronously
-            self._early_work = (True, group)
 
     def allreduce_grads(self, group=None):
         """Mean of the gradients over the data-parallel group (RCCL over xGMI):
@@ -238,9 +254,7 @@ class FlatParams:
         if self.n64:
             self._mean(self.g64, group)
         if started:
-            w = self._early_work[0]
-            if w is not True:
-                w.wait()
+            self._early_work[0].wait()
             self._early_work = None
 
 

@@ -66,7 +66,12 @@ class _PhysicsStep(torch.autograd.Function):
             raise RuntimeError("PhysicsNet step was run without saving activations")
         flat = ctx.engine.model._flat
         acc = flat.begin_backward()
-        live = getattr(d_sse_roll, "_paig_live_steps", 0) if d_out is None else 0
+        # the live-steps mark of _LossReduce.backward holds only while the
+        # gradient tensor is unmodified: autograd may accumulate a second
+        # gradient path into it in place (InputBuffer's add_), which keeps the
+        # tensor (and the attribute) but bumps its version counter
+        mark = getattr(d_sse_roll, "_paig_live_steps", None) if d_out is None else None
+        live = mark[0] if mark is not None and d_sse_roll._version == mark[1] else 0
         ctx.engine.backward(ctx.S, d_sse_rec, d_sse_roll, d_out, d_rec, d_enc, d_pvs, roll_live=live)
         # nothing reached the rollout branch (quirk Q1: the loss read a stale
         # output): the velocity encoder and physics parameters are not in the
@@ -103,10 +108,11 @@ class _LossReduce(torch.autograd.Function):
         if de is None:
             # no extrapolation loss in the graph: only the first pred steps of
             # every sequence carry a weight (physics_models.py:129-139), so the
-            # rollout decoder backward walks those frames only.  A gradient
-            # that autograd accumulates with another one loses the mark and
-            # falls back to every frame.
-            wroll._paig_live_steps = pred
+            # rollout decoder backward walks those frames only.  The mark
+            # carries the tensor's version: a gradient that autograd
+            # accumulates with another one (in place or not) no longer
+            # matches it and falls back to every frame.
+            wroll._paig_live_steps = (pred, wroll._version)
         return wrec, wroll, None, None, None, None, None
 
 

@@ -47,7 +47,7 @@ def test_library_loads_and_exports_every_symbol():
     for name in header_protos():
         assert hasattr(dll, name), name
     L = _lib.lib()
-    assert L.paig_abi_version() == 1
+    assert L.paig_abi_version() == _lib.ABI_VERSION
     # size queries are host-only and safe without a GPU
     assert L.paig_decoder_slab_len(2, 16, 32) == 2 * 16 * 16 * 4 + 3 * 32 * 32
     assert L.paig_decoder_bwd_blocks(1600, 0, 0, 2, 16, 32) >= 1

@@ -1,0 +1,141 @@
+"""The 1e-4 parity bar at BASELINE.json's benched sizes:
+the CPU oracle (tests' checker, oracle/physics_oracle.py, pinned to the
+reference's golden vectors) runs on the GPU box's host cores -- as bench.py's
+cpu_baseline already does -- on the workload the bench line is quoted on.
+
+* config #1, spring_color B=100, seq_len 50 (4 in / 6 pred / 40 extrap), the
+  headline workload, whole batch: the HIP step's outputs (latent positions,
+  masks, reconstructions, the 46 rollout frames, positions/velocities) and
+  losses within 1e-4 normwise of the fp32 oracle (north_star); EVERY
+  parameter gradient element-wise against the float64 oracle within
+  ENVELOPE_K x the spread of honest fp32 runs (the oracle on one-ulp-perturbed
+  weights), as tests/test_gpu_envelope.py does on the fixtures.
+* config #3 (3bp B=512, seq 20) and config #5 (bouncing B=1024, 96 rollout
+  steps): the HIP step runs the whole batch; its per-sequence outputs and
+  per-frame squared errors for a deterministic subset of SUBSET sequences
+  (spread over the batch) are compared with the oracle's forward of those
+  sequences (sequences are independent: the forward of a subset is the
+  subset of the forward).  Batch-level gradients at these sizes are covered by
+  test_gpu_fullsize (batch-halves additivity) on top of the fixture parity.
+
+Reference workload: runners/torch_run_physics.py:49-75 (presets),
+nn/network/physics_models.py:119-142 (losses), :204-245 (forward).
+"""
+import numpy as np
+import pytest
+import torch
+
+from envelope import ENVELOPE_FLOOR, ENVELOPE_K, _ulp_perturbed
+from helpers import RTOL, rel_err
+from oracle import physics_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+OUT_KEYS = ("enc_pos", "enc_masks", "recons_out", "output_seq", "pos_vel_seq")
+ENSEMBLE_FULL = 4
+ROLLOUT_RTOL_3BP = 2e-3   # chaotic 3-body rollout (test_gpu_parity)
+SUBSET = 32
+
+
+def _threads():
+    import os
+    n = len(os.sched_getaffinity(0))
+    torch.set_num_threads(max(1, min(n, 16)))
+
+
+def _model(task, cell, seq_len, ins, pred, size, B, seed=3):
+    from paig_reproduction_amd.nn.datasets.synth import as_model_input, render_sequences
+    from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = PhysicsNet(task, 100, 1, cell, seq_len, ins, pred, 3.0, False, True, size * size, "conv_encoder",
+                   "conv_st_decoder", device=dev).to(dev)
+    m.conv_math = "split"
+    n = min(B, 128)
+    u8 = render_sequences(task, n, seq_len, seed=seed)
+    u8 = np.concatenate([u8] * (B // n) + ([u8[:B % n]] if B % n else []), 0)
+    x = torch.from_numpy(as_model_input(u8))
+    state = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    cfg = O.Cfg(task, cell, seq_len, ins, pred, size, 3.0)
+    return m, x, state, cfg
+
+
+def _hip_step(m, x):
+    dev = torch.device("cuda:0")
+    xd = x.to(dev)
+    m.output = m(xd)
+    loss, (pred, extrap, recons) = m.compute_loss()
+    m.zero_grad(set_to_none=True)
+    loss.backward()
+    torch.cuda.synchronize()
+    out = {"enc_pos": m.enc_pos, "enc_masks": m.enc_masks, "recons_out": m.recons_out, "output_seq": m.output,
+           "pos_vel_seq": m.pos_vel_seq}
+    out = {k: v.detach().double().cpu().numpy() for k, v in out.items()}
+    L = {"train": float(loss.detach()), "extrap": float(extrap.detach()), "recons": float(recons.detach())}
+    g = {k: p.grad.detach().double().cpu().numpy() for k, p in m.named_parameters() if p.grad is not None}
+    sse = (m._sse_rec.detach().double().cpu().numpy(), m._sse_roll.detach().double().cpu().numpy())
+    return out, L, g, sse
+
+
+def test_config1_spring_b100_seq50_matches_oracle():
+    _threads()
+    m, x, state, cfg = _model("spring_color", "spring_ode_cell", 50, 4, 6, 32, 100)
+    out, L, g, _ = _hip_step(m, x)
+    o32, L32, g32 = O.train_step(state, cfg, x)
+    errs = {}
+    for k in OUT_KEYS:
+        errs[k] = rel_err(out[k].reshape(-1), o32[k].detach().double().numpy().reshape(-1))
+    for k in ("train", "extrap", "recons"):
+        errs["loss_" + k] = rel_err(np.float64(L[k]), np.float64(float(L32[k])))
+    print("config #1 outputs/losses vs fp32 oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
+    over = {k: v for k, v in errs.items() if v > RTOL}
+    assert not over, over
+    # gradients, every element, against the float64 oracle with the fp32 envelope
+    _, _, g64 = O.train_step_f64(state, cfg, x)
+    ens = [g32] + [O.train_step(_ulp_perturbed(state, s), cfg, x)[2] for s in range(ENSEMBLE_FULL)]
+    assert sorted(g) == sorted(g64), set(g) ^ set(g64)
+    rows = {}
+    for k in g64:
+        ref = g64[k].detach().double().numpy()
+        e_hip = rel_err(g[k], ref)
+        e_32 = max(rel_err(r[k].detach().double().numpy(), ref) for r in ens)
+        rows[k] = (e_hip, e_32, max(ENVELOPE_K * e_32, ENVELOPE_FLOOR))
+    worst = max(rows.items(), key=lambda kv: kv[1][0] / kv[1][2])
+    print("config #1 worst gradient (hip, fp32 spread, bar):", worst)
+    bad = {k: v for k, v in rows.items() if v[0] > v[2]}
+    assert not bad, bad
+
+
+def _subset_check(task, cell, seq_len, ins, pred, size, B, rollout_rtol):
+    _threads()
+    m, x, state, cfg = _model(task, cell, seq_len, ins, pred, size, B, seed=5)
+    out, _, _, (sse_rec, sse_roll) = _hip_step(m, x)
+    idx = np.linspace(0, B - 1, SUBSET).round().astype(np.int64)
+    P = {k: v.detach() for k, v in state.items()}
+    xs = x[torch.from_numpy(idx)]
+    with torch.no_grad():
+        o = O.forward(P, cfg, xs)
+    Te, R = cfg.Te, cfg.R
+    errs = {}
+    for k in ("enc_pos", "recons_out", "output_seq", "pos_vel_seq"):
+        errs[k] = rel_err(out[k][idx].reshape(-1), o[k].double().numpy().reshape(-1))
+    masks = out["enc_masks"].reshape(B, Te, -1)[idx]
+    errs["enc_masks"] = rel_err(masks.reshape(-1), o["enc_masks"].double().numpy().reshape(-1))
+    # per-frame squared errors (the loss terms before the batch means)
+    ref_rec = torch.sum(torch.square(xs[:, :Te] - o["recons_out"]), dim=[2, 3, 4]).double().numpy()
+    ref_roll = torch.sum(torch.square(xs[:, ins:] - o["output_seq"]), dim=[2, 3, 4]).double().numpy()
+    errs["sse_rec"] = rel_err(sse_rec.reshape(B, Te)[idx], ref_rec)
+    errs["sse_roll"] = rel_err(sse_roll.reshape(B, R)[idx], ref_roll)
+    print(task, "subset outputs vs fp32 oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
+    rollout = ("output_seq", "pos_vel_seq", "sse_roll")
+    over = {k: v for k, v in errs.items() if v > (rollout_rtol if k in rollout else RTOL)}
+    assert not over, over
+    return errs
+
+
+def test_config3_3bp_b512_subset_matches_oracle():
+    _subset_check("3bp_color", "gravity_ode_cell", 20, 4, 12, 36, 512, ROLLOUT_RTOL_3BP)
+
+
+def test_config5_bouncing_b1024_r96_subset_matches_oracle():
+    _subset_check("bouncing_balls", "bouncing_ode_cell", 100, 4, 6, 32, 1024, RTOL)

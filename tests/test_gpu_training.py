@@ -294,3 +294,62 @@ def test_optimizer_skips_params_without_grad(kind):
     for k in named:
         want = named2[k].grad + (g_enc[k] if k in g_enc else 0)
         assert rel_err(named[k].grad, want) <= 1e-6, (kind, k)
+
+
+def test_rollout_sse_second_gradient_path():
+    """the live-steps hint that lets the rollout decoder backward
+    skip the frames without a loss weight (physics_models.py:129-139 weights
+    loss[:, :pred_steps] only) must not survive when the per-frame SSE gets a
+    second gradient path that autograd accumulates into the same tensor:
+    every rollout frame then carries a weight.  Gradients of
+    train_loss + 0.5 * sum(sse_roll) must equal the sum of the two losses'
+    separate gradients."""
+    dev = torch.device("cuda:0")
+    z = _load("traj_spring_s12")
+    x = _x(z["input_u8_0"], dev)
+
+    def grads(which):
+        m = _model(z, dev)
+        m.output = m(x)
+        loss, _ = m.compute_loss()
+        extra = 0.5 * m._sse_roll.sum()
+        total = {"train": loss, "sse": extra, "both": loss + extra}[which]
+        total.backward()
+        return {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+
+    ga, gb, gc = grads("train"), grads("sse"), grads("both")
+    assert set(gc) == set(ga) | set(gb)
+    worst = 0.0
+    for k in gc:
+        want = ga.get(k, 0) + gb.get(k, 0)
+        worst = max(worst, rel_err(gc[k], want))
+    # the extrapolation frames' decoder gradient reaches the VFN sources: a
+    # surviving mark would drop it entirely (an O(1) error)
+    assert worst <= 1e-5, worst
+
+
+def test_two_forwards_before_backward():
+    """each grad-enabled forward owns the per-launch activation
+    maxima its conv weight gradients are scaled by (the split arithmetic's
+    X exponent).  Two forwards of the same shape -- the second on inputs 64x
+    larger -- then ONE backward of the summed losses must give the sum of the
+    two steps' separate gradients (a shared buffer would scale the first
+    step's activations by the second's maxima)."""
+    dev = torch.device("cuda:0")
+    z = _load("traj_spring_s12")
+    x1 = _x(z["input_u8_0"], dev)
+    x2 = _x(z["input_u8_1"], dev) * 64.0
+
+    def grads(xs):
+        m = _model(z, dev)
+        total = 0
+        for x in xs:
+            m.output = m(x)
+            loss, _ = m.compute_loss()
+            total = total + loss
+        total.backward()
+        return {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+
+    ga, gb, gc = grads([x1]), grads([x2]), grads([x1, x2])
+    worst = max(rel_err(gc[k], ga[k] + gb[k]) for k in gc)
+    assert worst <= 1e-5, worst
