@@ -105,6 +105,23 @@ int paig_conv2d_wgrad(const float* x, long long x_fs, int x_grp, long long x_gs,
 int paig_conv2d_wgrad_ex(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
                          float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
                          int flags, const float* xmax, int xmax_n, void* stream);
+/* Fused backward of one 3x3 "same" conv layer (aten convolution_backward of
+ * blocks.py:246-276 / :113-170), split path only (flags & 128 f16 hi/lo,
+ * flags & 256 bf16): ONE launch computes what paig_conv2d_fwd_pw (flags & 8,
+ * the data gradient) and paig_conv2d_wgrad_ex compute, from one staging of
+ * each tile's dY and X:
+ *   dx [F][Cin][H][W] = conv_transpose(dy, w), times (aux > 0) with flags & 2,
+ *                       added to dx's contents with flags & 4;
+ *   slab rows [nblk][Cout*Cin*9 | Cout] of per-block weight + bias gradient
+ *                       partials (paig_conv2d_wgrad's layout; *nblk_out rows).
+ * xmax: the forward's per-block max |x| slots (the X scale, as
+ * paig_conv2d_wgrad_ex); wprep: the layer's data-gradient weight image
+ * (paig_conv_wprep dg = 1; nullable).  Shapes: paig_conv2d_bwd_supported. */
+int paig_conv2d_bwd_supported(int Cin, int Cout, int H, int W, int ks, int flags);
+int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
+                    float* dx, long long dx_fs, const float* aux, long long aux_fs, const float* w, float* slab,
+                    int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks, int flags,
+                    const float* xmax, int xmax_n, const void* wprep, void* stream);
 
 /* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,

@@ -39,6 +39,8 @@ SIGNATURES = {
     "paig_conv_wprep": (I, [I, P, P, P, P, P, P, P]),
     "paig_conv2d_wgrad_ex": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
+    "paig_conv2d_bwd_supported": (I, [I, I, I, I, I, I]),
+    "paig_conv2d_bwd": (I, [P, LL, I, LL, P, LL, P, LL, P, LL, P, P, I, P, I, I, I, I, I, I, I, P, I, P, P]),
     "paig_gather_u8_f32": (I, [P, P, P, I, LL, P]),
     "paig_velmlp_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "paig_velmlp_vfn_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P]),
@@ -109,7 +111,8 @@ SIGNATURES = {
     "paig_sgd_f64": (I, [P, P, P, LL, F64, F64, I, P]),
 }
 
-_QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported", "paig_velmlp_bwd_blocks",
+_QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported",
+          "paig_conv2d_bwd_supported", "paig_velmlp_bwd_blocks",
           "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_mask_blocks", "paig_conv_wprep_size", "paig_gemm_workspace", "paig_colsum_workspace",
           "paig_ps_bytes", "paig_psgemm_workspace",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",

@@ -101,6 +101,7 @@ __device__ __forceinline__ void f16_range_note(float rmax) {
   }
 int paig_f16_range_conv(int clear);
 int paig_f16_range_gemm(int clear);
+int paig_f16_range_bwd(int clear);
 
 // fixed power-of-two scale of the fallback paths (a conv weight gradient
 // without the forward's recorded X maximum, GEMM math 4 / 5's fixed operand):

@@ -1,0 +1,724 @@
+// Fused backward of one U-Net convolution layer on the gfx950 16-bit matrix
+// cores (split-precision operands, conv_split.hip's arithmetic).  Reference:
+// aten convolution_backward behind nn/network/blocks.py:246-276 (ShallowUNet)
+// and :113-170 (UNet); one launch replaces the layer's data-gradient and
+// weight-gradient kernels (paig_conv2d_fwd_pw flags & 8, paig_conv2d_wgrad_ex).
+//
+// Per persistent tile (whole rows of one frame, or whole frames; <= 256
+// pixels) the block stages ONCE
+//   * dY with a one-pixel halo as an NHWC 16-bit image (8 channels = one
+//     16-byte slot per pixel, odd pixel pitch): the data gradient's A operand
+//     (one ds_read_b128 per fragment, as the dgrad kernel reads it) AND, read
+//     with ds_read_b64_tr_b16 (4 pixels x 16 channels -> 4 pixels of one
+//     channel per lane), the weight gradient's A operand dY[co][pixel];
+//   * X with a one-pixel halo as 4-channel quad planes (the weight gradient's
+//     B operand, transposed reads whose per-lane row address absorbs the tap
+//     shift, as conv_wgrad_split_k);
+// and computes
+//   * dX[pixel][ci] = sum_(tap, co) dY[pixel + tap][co] * W[co][ci][flip(tap)]
+//     for the tile's pixels (ReLU' of the layer input and accumulation into
+//     the existing gradient in the epilogue, as the dgrad kernel);
+//   * dW[co][ci][tap] += sum_pixel dY[co][pixel] * X[pixel + tap][ci] and
+//     db[co] += sum_pixel dY[co][pixel] (exact fp32, from the staging
+//     registers), one slab row per block (the same slab layout as the wgrad
+//     kernel: one batched deterministic reduction afterwards).
+// What the two separate kernels did twice is done once: dY read from HBM and
+// converted to 16-bit pieces once (the dgrad and the wgrad each did), X read
+// once (the wgrad's staging and the dgrad's ReLU' mask read it separately).
+//
+// Scales (PM 0, f16 hi/lo): X by one power of two per launch (the forward's
+// recorded maximum, xmax); dY by one power of two per tile (its own max; the
+// weight-gradient accumulators follow each tile's exponent by exact power-of-
+// two rescaling); weights per output channel (paig_conv_wprep's header).  The
+// data gradient of a tile is complete in the tile, so its epilogue takes the
+// exponents back out exactly.  PM 2: bf16 hi only, unscaled (BASELINE config
+// #2).
+#include "split_common.h"
+
+namespace {
+
+// LDS bytes of a block at tiles of <= tpx pixels (both images, the weights,
+// the fused-upsample window)
+constexpr int sbwd_lds(int CIN, int COUT, int H, int W, bool UPS, int PM, int tpx) {
+  const int FPT = H * W <= tpx ? tpx / (H * W) : 1, RT = H * W <= tpx ? H : rows_fit(H, W, tpx);
+  const int ROWS = RT + 2, CCD = rup(COUT, 8) / 8, PSD = CCD % 2 == 0 ? CCD + 1 : CCD;
+  const int RPD = W == 8 ? to_mod16((W + 2) * PSD, 8) : (W + 2) * PSD;
+  const int IMGD = (FPT * ROWS * RPD + 2) * 8, WIMG = ceil_div(9 * CCD, 4) * ceil_div(CIN, 16) * 64 * 8;
+  const int XIMG = rup(CIN, 4) / 4 * rup(FPT * ROWS * (W + 4) * 4 + 80, 128);
+  return (IMGD + WIMG + XIMG) * 2 * (PM == 2 ? 1 : 2) + (UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0);
+}
+// pixels per tile: the largest of 256 / 128 / 64 whose staging lets two
+// blocks share a CU (the 8 x 8 / 9 x 9 levels' multi-frame tiles and the
+// 32-channel weight images would not)
+constexpr int sbwd_tpx(int CIN, int COUT, int H, int W, bool UPS, int PM) {
+  for (int t = 256; t >= 64; t /= 2)
+    if (sbwd_lds(CIN, COUT, H, W, UPS, PM, t) <= LDS_MAX / 2) return t;
+  return 64;
+}
+
+// 4 waves split the weight-gradient N-tiles (each wave owns every 4th one
+// over all pixels: no cross-wave reduction); the data gradient's M-tiles of
+// 16 pixels are split over the waves as in the dgrad kernel
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
+struct SBwdCfg {
+  static constexpr int KK = KS * KS, PADL = KS / 2;
+  static constexpr int NIMG = PM == 2 ? 1 : 2;
+  static constexpr int TPX = sbwd_tpx(CIN, COUT, H, W, UPS, PM);
+  static constexpr int FPT = H * W <= TPX ? TPX / (H * W) : 1;
+  static constexpr int RT = H * W <= TPX ? H : rows_fit(H, W, TPX);
+  static constexpr int TPXV = FPT * RT * W;                   // valid pixels per tile
+  static constexpr int ROWS = RT + KS - 1;
+  // ---- dY image: NHWC, 8-channel slots, halo PADL
+  static constexpr int CCD = rup(COUT, 8) / 8;
+  static constexpr int PSD = CCD % 2 == 0 ? CCD + 1 : CCD;    // odd pitch: 16 pixels -> 16 bank groups
+  static constexpr int TWPX = W + 2 * PADL;
+  static constexpr int RPD = W == 8 ? to_mod16(TWPX * PSD, 8) : TWPX * PSD;
+  static constexpr int ZSLOT = FPT * ROWS * RPD;              // a zero slot after the image
+  static constexpr int IMGD = (ZSLOT + 2) * 8;                // (+1 spare slot: wgrad reads of 8-channel dY)
+  // ---- data gradient: k = (tap, 8-channel chunk of dY), 4 chunks per MFMA k-step
+  static constexpr int KC = KK * CCD, NS = ceil_div(KC, 4);
+  static constexpr int NTD = ceil_div(CIN, 16);               // 16-channel tiles of dX
+  static constexpr int NMT = ceil_div(TPXV, 16), MW = ceil_div(NMT, 4);
+  static constexpr int WIMG = NS * NTD * 64 * 8;
+  // ---- X image (weight gradient B operand): 4-channel quad planes
+  static constexpr int CQ = rup(CIN, 4) / 4, NQ = KK * CQ, NTX = ceil_div(NQ, 4);
+  static constexpr int OFFX = PADL > 0 ? 2 : 0, TWX = W + 2 * OFFX;
+  static constexpr int XPL = rup(FPT * ROWS * TWX * 4 + 80, 128);
+  static constexpr int XIMG = CQ * XPL;
+  // ---- weight gradient: D[co][(tap, ci)], K = pixels in k-blocks of 32
+  static constexpr int MT = ceil_div(COUT, 16), NTW = ceil_div(NTX, 4);
+  static constexpr int KB = ceil_div(TPXV, 32);
+  static constexpr int NCOL = CIN * KK, SLAB = COUT * NCOL + COUT;
+  // ---- staging units: UPX pixels x (8 dY | 4 X) channels, pixel fastest
+  static constexpr int UPX = W % 2 == 0 ? 2 : 1, W2 = W / UPX;
+  static constexpr int NID = FPT * ROWS * W2 * CCD, NLD = ceil_div(NID, 256);
+  static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = ceil_div(NIX, 256);
+  static constexpr int UPW = FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2);   // fused-upsample window (floats)
+  static constexpr int LDS = (IMGD + WIMG + XIMG) * 2 * NIMG + (UPS ? UPW * 4 : 0);
+  static constexpr bool VEC4 = W % 4 == 0;
+  // X prefetched a tile ahead where its registers are cheap (else loaded
+  // when staged)
+  static constexpr bool XPIPE = !UPS && NLX * 8 <= 32;
+  static_assert(H % RT == 0, "RT divides H");
+  static_assert(KS == 3, "3x3 layers (the 1x1 heads are fused elsewhere)");
+};
+
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
+__global__ void __launch_bounds__(256, 2)
+conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restrict__ w, int flags,
+                 float* __restrict__ slab, int F, int ntiles, XMax xm, const s16x8* __restrict__ wp) {
+  using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
+  constexpr int KK = C::KK, PADL = C::PADL, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, TPXV = C::TPXV;
+  constexpr int CCD = C::CCD, PSD = C::PSD, RPD = C::RPD, KC = C::KC, NS = C::NS, NTD = C::NTD, MW = C::MW;
+  constexpr int CQ = C::CQ, NQ = C::NQ, NTX = C::NTX, OFFX = C::OFFX, TWX = C::TWX, XPL = C::XPL;
+  constexpr int MT = C::MT, NTW = C::NTW, KB = C::KB, NCOL = C::NCOL, UPX = C::UPX, W2 = C::W2;
+  constexpr int NID = C::NID, NLD = C::NLD, NIX = C::NIX, NLX = C::NLX;
+  constexpr long long HW = (long long)H * W;
+  constexpr long long XPLANE = UPS ? (long long)(H / 2) * (W / 2) : HW;
+  constexpr int NRB = H / RT;
+  extern __shared__ __attribute__((aligned(16))) short lds16[];
+  short* Dh = lds16;
+  short* Dl = Dh + (C::NIMG == 2 ? C::IMGD : 0);
+  short* Wh = lds16 + C::NIMG * C::IMGD;
+  short* Wl = Wh + (C::NIMG == 2 ? C::WIMG : 0);
+  short* Xh = lds16 + C::NIMG * (C::IMGD + C::WIMG);
+  short* Xl = Xh + (C::NIMG == 2 ? C::XIMG : 0);
+  float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::IMGD + C::WIMG + C::XIMG));   // UPS window
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
+  __shared__ float smax[4];
+
+  auto xplane = [](int cq) { return cq * XPL + ((cq & 1) ? 16 : 0) + ((cq & 2) ? 64 : 0); };
+  // ---- zero what the staging never writes: the dY image's halo columns,
+  // its zero / spare slots, the X image's halo columns
+  for (int i = tid; i < FPT * ROWS * 2 * PADL * CCD; i += 256) {
+    const int cc = i % CCD, hc = (i / CCD) % (2 * PADL), r = i / (CCD * 2 * PADL);
+    const int xc = hc < PADL ? hc : W + hc;
+    const int o = (r * RPD + xc * PSD + cc) * 8;
+    *reinterpret_cast<s16x8*>(Dh + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (PM != 2) *reinterpret_cast<s16x8*>(Dl + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  if (tid < 2) {
+    *reinterpret_cast<s16x8*>(Dh + (C::ZSLOT + tid) * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (PM != 2) *reinterpret_cast<s16x8*>(Dl + (C::ZSLOT + tid) * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  for (int i = tid; i < FPT * ROWS * 2 * OFFX; i += 256) {
+    const int hc = i % (2 * OFFX), r = i / (2 * OFFX);
+    const int xc = hc < OFFX ? hc : W + hc;
+    for (int cq = 0; cq < CQ; ++cq) {
+      *reinterpret_cast<s16x4*>(Xh + xplane(cq) + (r * TWX + xc) * 4) = s16x4{0, 0, 0, 0};
+      if (PM != 2) *reinterpret_cast<s16x4*>(Xl + xplane(cq) + (r * TWX + xc) * 4) = s16x4{0, 0, 0, 0};
+    }
+  }
+
+  // ---- scales (PM 0): X per launch (ecx), dY per tile (ecd), the
+  // data-gradient weights per output channel (ewn)
+  int ecx = PAIG_A_EXP, ecd = PM == 0 && PAIG_SCALE_MODE < 2 ? 100 : 0;
+  float xsc = 1.f, dsc = __builtin_amdgcn_ldexpf(1.f, ecd);
+  float rmax = 0.f;   // range guard (fixed X scale without xmax slots)
+  int ewn[NTD];
+#pragma unroll
+  for (int nt = 0; nt < NTD; ++nt) ewn[nt] = 0;
+
+  // ---- data-gradient weights in fragment order ([s][nt][lane][8]): the
+  // layer's transposed + flipped weights (dgrad image of paig_conv_wprep, or
+  // staged here from w)
+  auto wval = [&](int idx, int j) {
+    const int ln = idx & 63, snt = idx >> 6, nt = snt % NTD, s = snt / NTD;
+    const int kc = 4 * s + (ln >> 4), ci = nt * 16 + (ln & 15);
+    float v = 0.f;
+    if (kc < KC && ci < CIN) {
+      const int tap = kc / CCD, co = (kc % CCD) * 8 + j;
+      if (co < COUT) v = w[(co * CIN + ci) * KK + (KK - 1 - tap)];
+    }
+    return v;
+  };
+  __shared__ int sew[PM == 0 ? NTD * 16 : 1];
+  if (PM == 0 && wp != nullptr) {
+    const int* hdr = reinterpret_cast<const int*>(wp);
+    constexpr int HDR = NTD * 16 * 4 / 16;
+#pragma unroll
+    for (int nt = 0; nt < NTD; ++nt) ewn[nt] = hdr[nt * 16 + (lane & 15)];
+    const s16x8* img = wp + HDR;
+    constexpr int WLO = NS * NTD * 64;
+    for (int idx = tid; idx < NS * NTD * 64; idx += 256) {
+      *reinterpret_cast<s16x8*>(Wh + idx * 8) = img[idx];
+      *reinterpret_cast<s16x8*>(Wl + idx * 8) = img[WLO + idx];
+    }
+  } else {
+    if constexpr (PM == 0) {
+      for (int i = tid; i < NTD * 16; i += 256) sew[i] = 0;
+      __syncthreads();
+      float pm[NTD];
+#pragma unroll
+      for (int nt = 0; nt < NTD; ++nt) pm[nt] = 0.f;
+      for (int idx = tid; idx < NS * NTD * 64; idx += 256) {
+        const int nt = (idx >> 6) % NTD;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pm[nt] = fmaxf(pm[nt], fabsf(wval(idx, j)));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NTD; ++nt) atomicMax(&sew[nt * 16 + (tid & 15)], __builtin_bit_cast(int, pm[nt]));
+      __syncthreads();
+      for (int i = tid; i < NTD * 16; i += 256) sew[i] = f16_scale_exp_v(__builtin_bit_cast(float, sew[i]));
+      __syncthreads();
+#pragma unroll
+      for (int nt = 0; nt < NTD; ++nt) ewn[nt] = sew[nt * 16 + (lane & 15)];
+    }
+    for (int idx = tid; idx < NS * NTD * 64; idx += 256) {
+      const int cl = ((idx >> 6) % NTD) * 16 + (idx & 15);
+      const int e = PM == 0 ? sew[cl] : 0;
+      s16x8 vh, vl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        short h, l;
+        float rm = 0.f;
+        split<PM>(__builtin_amdgcn_ldexpf(wval(idx, j), e), h, l, rm);
+        vh[j] = h;
+        vl[j] = l;
+      }
+      *reinterpret_cast<s16x8*>(Wh + idx * 8) = vh;
+      if (PM != 2) *reinterpret_cast<s16x8*>(Wl + idx * 8) = vl;
+    }
+  }
+
+  // ---- data-gradient fragment offsets (slots): pixel base per M-tile,
+  // (tap, chunk) per k-step
+  int pbase[MW];
+#pragma unroll
+  for (int mt = 0; mt < MW; ++mt) {
+    int pix = (wv * MW + mt) * 16 + (lane & 15);
+    if (pix >= TPXV) pix = 0;   // padding rows of the last M-tile: finite data, never stored
+    const int fi = pix / (RT * W), rem = pix % (RT * W);
+    pbase[mt] = (fi * ROWS + rem / W) * RPD + (rem % W) * PSD;
+  }
+  int soff[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int kc = 4 * s + g;
+    if (kc >= KC) kc = 0;   // zero weights there
+    const int tap = kc / CCD, cc = kc % CCD;
+    soff[s] = (tap / KS) * RPD + (tap % KS) * PSD + cc;
+  }
+  // ---- weight-gradient transposed-read addressing: lane 4q + pl of its
+  // 16-lane group supplies row q (pixel 8g + 4h + q of the k-block) of
+  // column quad pl
+  const int qq = (lane >> 2) & 3, pl = lane & 3;
+  int colt[NTW];
+#pragma unroll
+  for (int jn = 0; jn < NTW; ++jn) {
+    int cq = (wv + jn * 4) * 4 + pl;
+    if (cq >= NQ) cq = 0;   // padded columns: finite data, never stored
+    const int tap = cq / CQ, ciq = cq % CQ;
+    colt[jn] = xplane(ciq) + ((tap / KS) * TWX + tap % KS) * 4;
+  }
+  // dY slot of tile pixel j (its centre position in the halo'd image); the
+  // zero slot past the valid pixels
+  auto dslot = [&](int j) {
+    if (TPXV % 32 != 0 && j >= TPXV) return C::ZSLOT;
+    const int fi = j / (RT * W), rem = j % (RT * W);
+    return (fi * ROWS + rem / W + PADL) * RPD + (rem % W + PADL) * PSD;
+  };
+  auto xpos = [&](int j) {   // X image position of tile pixel j at tap (0, 0)
+    if (TPXV % 32 != 0 && j >= TPXV) j = 0;   // its dY is zero
+    const int fi = j / (RT * W), rem = j % (RT * W);
+    return ((fi * ROWS + rem / W) * TWX + rem % W + (OFFX - PADL)) * 4;
+  };
+
+  f32x4 accw[MT][NTW];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) accw[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[NLD][8];   // bias partials of this thread's dY units (centre rows), unscaled fp32
+#pragma unroll
+  for (int l = 0; l < NLD; ++l)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bacc[l][c] = 0.f;
+
+  // ---- staging.  dY unit i = (frame fi, image row r, chunk cc, pixel xp),
+  // prefetched a tile ahead; X unit i = (fi, r, quad cq, xp)
+  float2 pd[NLD][8];
+  float2 px[C::XPIPE ? NLX : 1][4];
+  using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
+  UP up;
+  auto load_d = [&](int t) {
+    const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+    const float* fb = dy.frame(f0 < F ? f0 : 0);
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int i = tid + l * 256;
+      const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CCD, fi = i / (W2 * ROWS * CCD);
+      const int gy = y0 + r - PADL;
+      const bool ok = i < NID && f0 + fi < F && gy >= 0 && gy < H;
+      const int off = fi * (int)dy.fs + cc * 8 * (int)HW + gy * W + xp;
+      static_assert(8 * HW <= 8 * 4096, "paig_zero_planes covers the unit");
+      const float* base = ok ? fb + off : paig_zero_planes;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float* q = COUT % 8 == 0 || cc * 8 + c < COUT ? base + c * (int)HW : paig_zeros;
+        pd[l][c] = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
+      }
+    }
+  };
+  auto load_x = [&](int t, int i, float2* v) {
+    const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
+    const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+    const int gy = y0 + r - PADL;
+    const bool ok = i < NIX && f0 + fi < F && gy >= 0 && gy < H;
+    const float* fb = x.frame(f0 < F ? f0 : 0);
+    const int off = fi * (int)x.fs + cq * 4 * (int)XPLANE + gy * W + xp;
+    const float* base = ok ? fb + off : paig_zero_planes;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float* q = CIN % 4 == 0 || cq * 4 + c < CIN ? base + c * (int)XPLANE : paig_zeros;
+      v[c] = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
+    }
+  };
+  auto issue = [&](int t) {
+    load_d(t);
+    if constexpr (UPS) {
+      up.issue(x, F, (t / NRB) * FPT, (t % NRB) * RT, tid);
+    } else if constexpr (C::XPIPE) {
+#pragma unroll
+      for (int l = 0; l < NLX; ++l) load_x(t, tid + l * 256, px[l]);
+    }
+  };
+  auto put_d = [&](int i, const float2* v) {
+    const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CCD, fi = i / (W2 * ROWS * CCD);
+    const int o = ((fi * ROWS + r) * RPD + (xp + PADL) * PSD + cc) * 8;
+    s16x8 h0, l0, h1, l1;
+    if constexpr (PM == 0) {
+      pf32x2 sv[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) sv[c] = pf32x2{v[c].x, v[c].y} * dsc;
+      u32x4 a0, b0, a1, b1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        { const HiLo q_ = split_pk(sv[2 * k].x, sv[2 * k + 1].x); a0[k] = q_.h; b0[k] = q_.l; }
+        { const HiLo q_ = split_pk(sv[2 * k].y, sv[2 * k + 1].y); a1[k] = q_.h; b1[k] = q_.l; }
+      }
+      h0 = __builtin_bit_cast(s16x8, a0);
+      l0 = __builtin_bit_cast(s16x8, b0);
+      h1 = __builtin_bit_cast(s16x8, a1);
+      l1 = __builtin_bit_cast(s16x8, b1);
+    } else {
+      float rm = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        short h, lo;
+        split<PM>(v[c].x, h, lo, rm);
+        h0[c] = h;
+        l0[c] = lo;
+        split<PM>(v[c].y, h, lo, rm);
+        h1[c] = h;
+        l1[c] = lo;
+      }
+    }
+    *reinterpret_cast<s16x8*>(Dh + o) = h0;
+    if (PM != 2) *reinterpret_cast<s16x8*>(Dl + o) = l0;
+    if constexpr (UPX == 2) {
+      *reinterpret_cast<s16x8*>(Dh + o + PSD * 8) = h1;
+      if (PM != 2) *reinterpret_cast<s16x8*>(Dl + o + PSD * 8) = l1;
+    }
+  };
+  auto put_x = [&](int i, const float2* v) {
+    const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+    const int o = xplane(cq) + ((fi * ROWS + r) * TWX + xp + OFFX) * 4;
+    s16x8 hv, lv;
+    if constexpr (PM == 0) {
+      pf32x2 sv[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sv[c] = pf32x2{v[c].x, v[c].y} * xsc;
+        rmax = amax2(rmax, sv[c].x, sv[c].y);
+      }
+      u32x4 a, b;
+      { const HiLo q_ = split_pk(sv[0].x, sv[1].x); a[0] = q_.h; b[0] = q_.l; }
+      { const HiLo q_ = split_pk(sv[2].x, sv[3].x); a[1] = q_.h; b[1] = q_.l; }
+      { const HiLo q_ = split_pk(sv[0].y, sv[1].y); a[2] = q_.h; b[2] = q_.l; }
+      { const HiLo q_ = split_pk(sv[2].y, sv[3].y); a[3] = q_.h; b[3] = q_.l; }
+      hv = __builtin_bit_cast(s16x8, a);
+      lv = __builtin_bit_cast(s16x8, b);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        short h, lo;
+        split<PM>(v[c].x, h, lo, rmax);
+        hv[c] = h;
+        lv[c] = lo;
+        split<PM>(v[c].y, h, lo, rmax);
+        hv[4 + c] = h;
+        lv[4 + c] = lo;
+      }
+    }
+    if constexpr (UPX == 2) {
+      *reinterpret_cast<s16x8*>(Xh + o) = hv;
+      if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = lv;
+    } else {
+      *reinterpret_cast<s16x4*>(Xh + o) = s16x4{hv[0], hv[1], hv[2], hv[3]};
+      if (PM != 2) *reinterpret_cast<s16x4*>(Xl + o) = s16x4{lv[0], lv[1], lv[2], lv[3]};
+    }
+  };
+  // this wave's max |dY| of the prefetched tile into smax[wv] (before the
+  // loop-top barrier; the commit after it reads the block max)
+  auto tile_max = [&]() {
+    float m = 0.f;
+#pragma unroll
+    for (int l = 0; l < NLD; ++l)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) m = amax2(m, pd[l][c].x, pd[l][c].y);
+    m = wave_max_u(m);
+    if (lane == 0) smax[wv] = m;
+  };
+  auto commit = [&](int t) {
+    if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) {
+      // every tile is staged at its own exponent (its max into [2^14, 2^15):
+      // the data gradient of a small-gradient tile keeps full precision);
+      // the weight-gradient accumulators, held at scale 2^(ecx + ecd), follow
+      // exactly (powers of two).  An exponent rise is capped at 2^64 per tile
+      // so that rescaled accumulators cannot overflow (tiles 2^64 smaller
+      // than the ones before are staged at a lower scale instead)
+      const int te = f16_scale_exp(fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3])));
+      const int td = te < ecd + 64 ? te : ecd + 64;
+      if (td != ecd) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) accw[m][j][r] = __builtin_amdgcn_ldexpf(accw[m][j][r], td - ecd);
+        ecd = td;
+        dsc = __builtin_amdgcn_ldexpf(1.f, ecd);
+      }
+    }
+    const int f0 = (t / NRB) * FPT;
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int i = tid + l * 256;
+      if (NID % 256 != 0 && i >= NID) break;
+      put_d(i, pd[l]);
+      // bias partials: the tile's own rows (not the halo), frames < F
+      const int r = (i / W2) % ROWS, fi = i / (W2 * ROWS * CCD);
+      if (r >= PADL && r < PADL + RT && f0 + fi < F) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) bacc[l][c] += pd[l][c].x + pd[l][c].y;
+      }
+    }
+    if constexpr (UPS) {
+      const int y0 = (t % NRB) * RT;
+      up.commit(Sl, tid);
+      __syncthreads();
+#pragma unroll 1
+      for (int i = tid; i < NIX; i += 256) {
+        const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+        const int gy = y0 + r - PADL;
+        const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+        float2 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          v[c] = (ok && cq * 4 + c < CIN)
+                     ? make_float2(UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp),
+                                   UPX == 2 ? UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp + 1) : 0.f)
+                     : make_float2(0.f, 0.f);
+        put_x(i, v);
+      }
+    } else if constexpr (C::XPIPE) {
+#pragma unroll
+      for (int l = 0; l < NLX; ++l) {
+        const int i = tid + l * 256;
+        if (NIX % 256 != 0 && i >= NIX) break;
+        put_x(i, px[l]);
+      }
+    } else {
+#pragma unroll 1
+      for (int i = tid; i < NIX; i += 256) {
+        float2 v[4];
+        load_x(t, i, v);
+        put_x(i, v);
+      }
+    }
+  };
+
+  int lt = blockIdx.x;
+  auto tile_of = [&](int l) { return l < ntiles ? xcd_tile(l, ntiles) : ntiles; };
+  issue(tile_of(lt));
+  if (PM == 0 && xm.p) {
+    // the launch's X exponent: max over the forward's per-block slots
+    float m = 0.f;
+    for (int i = tid * 4; i < xm.n; i += 1024) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xm.p + i);
+      m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    }
+    m = wave_max_u(m);
+    if (lane == 0) smax[wv] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    if (m > 0.f) ecx = f16_scale_exp(m);   // all-zero slots (never written): the fixed scale, guarded
+    __syncthreads();
+  }
+  if constexpr (PM == 0) xsc = __builtin_amdgcn_ldexpf(1.f, ecx);
+  else ecx = 0;
+
+  for (; lt < ntiles; lt += gridDim.x) {
+    const int tile = xcd_tile(lt, ntiles);
+    const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
+    if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) tile_max();
+    __syncthreads();   // the previous tile's fragment reads are done
+    commit(tile);
+    __syncthreads();
+    issue(tile_of(lt + gridDim.x));
+
+    // ---- weight gradient: all 4 waves over all k-blocks, each its N-tiles
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int p0 = kb * 32;
+      s16x8 ah[MT], al[MT];
+      const int d0 = dslot(p0 + 8 * g + qq), d1 = dslot(p0 + 8 * g + 4 + qq);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        // channels 16m + 4pl .. +3: chunk 2m + pl/2, half pl%2 (rows co >=
+        // COUT read finite neighbouring data and are discarded)
+        const int co = 2 * m + (pl >> 1), hoff = (pl & 1) * 4;
+        const int a0 = (d0 + co) * 8 + hoff, a1 = (d1 + co) * 8 + hoff;
+        ah[m] = __builtin_shufflevector(tr_read(Dh + a0), tr_read(Dh + a1), 0, 1, 2, 3, 4, 5, 6, 7);
+        al[m] = PM != 2 ? __builtin_shufflevector(tr_read(Dl + a0), tr_read(Dl + a1), 0, 1, 2, 3, 4, 5, 6, 7) : ah[m];
+      }
+      const int r0 = xpos(p0 + 8 * g + qq), r1 = xpos(p0 + 8 * g + 4 + qq);
+#pragma unroll
+      for (int jn = 0; jn < NTW; ++jn) {
+        if (wv + jn * 4 < NTX) {   // wave-uniform: EXEC stays full for the transposed reads
+          const s16x8 bh = __builtin_shufflevector(tr_read(Xh + r0 + colt[jn]), tr_read(Xh + r1 + colt[jn]), 0, 1,
+                                                   2, 3, 4, 5, 6, 7);
+          const s16x8 bl = PM != 2 ? __builtin_shufflevector(tr_read(Xl + r0 + colt[jn]),
+                                                             tr_read(Xl + r1 + colt[jn]), 0, 1, 2, 3, 4, 5, 6, 7)
+                                   : bh;
+#pragma unroll
+          for (int m = 0; m < MT; ++m) accw[m][jn] = mma3<PM>(ah[m], al[m], bh, bl, accw[m][jn]);
+        }
+      }
+    }
+
+    // ---- data gradient of the tile's pixels
+    f32x4 accd[MW][NTD];
+#pragma unroll
+    for (int mt = 0; mt < MW; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTD; ++nt) accd[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      s16x8 bh[NTD], bl[NTD];
+#pragma unroll
+      for (int nt = 0; nt < NTD; ++nt) {
+        const int o = ((s * NTD + nt) * 64 + lane) * 8;
+        bh[nt] = *reinterpret_cast<const s16x8*>(Wh + o);
+        bl[nt] = PM != 2 ? *reinterpret_cast<const s16x8*>(Wl + o) : bh[nt];
+      }
+#pragma unroll
+      for (int mt = 0; mt < MW; ++mt) {
+        const int o = (pbase[mt] + soff[s]) * 8;
+        const s16x8 ah = *reinterpret_cast<const s16x8*>(Dh + o);
+        const s16x8 al = PM != 2 ? *reinterpret_cast<const s16x8*>(Dl + o) : ah;
+#pragma unroll
+        for (int nt = 0; nt < NTD; ++nt) accd[mt][nt] = mma3<PM>(ah, al, bh[nt], bl[nt], accd[mt][nt]);
+      }
+    }
+    // epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for input
+    // channel ci = nt*16 + (lane&15); flags 2: * (aux > 0), 4: accumulate
+#pragma unroll
+    for (int nt = 0; nt < NTD; ++nt) {
+      const int ci = nt * 16 + (lane & 15);
+      if (ci >= CIN) continue;
+      const float tinv = PM == 0 ? __builtin_amdgcn_ldexpf(1.f, -(ecd + ewn[nt])) : 1.f;
+#pragma unroll
+      for (int mt = 0; mt < MW; ++mt) {
+        const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+        if constexpr (C::VEC4) {
+          if (pix >= TPXV) continue;
+          const int fi = pix / (RT * W), rem = pix % (RT * W);
+          const int y = y0 + rem / W, xx = rem % W, f = f0 + fi;
+          if (f >= F) continue;
+          float* op = dx.frame(f) + ci * HW + (long long)y * W + xx;
+          f32x4 v = accd[mt][nt] * tinv;
+          if (flags & 4) v += *reinterpret_cast<const f32x4*>(op);
+          if (flags & 2) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(aux.frame(f) + ci * HW + (long long)y * W + xx);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
+          }
+          *reinterpret_cast<f32x4*>(op) = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int pr = pix + r;
+            if (pr >= TPXV) break;
+            const int fi = pr / (RT * W), rem = pr % (RT * W);
+            const int y = y0 + rem / W, xx = rem % W, f = f0 + fi;
+            if (f >= F) continue;
+            float* op = dx.frame(f) + ci * HW + (long long)y * W + xx;
+            float v = accd[mt][nt][r] * tinv;
+            if (flags & 4) v += *op;
+            if (flags & 2) v = aux.frame(f)[ci * HW + (long long)y * W + xx] > 0.f ? v : 0.f;
+            *op = v;
+          }
+        }
+      }
+    }
+  }
+
+  // ---- this block's slab row: weight gradients (each wave its N-tiles,
+  // scaled back exactly), then the bias
+  float* s = slab + (long long)blockIdx.x * C::SLAB;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int nt = wv + j * 4;
+      if (nt >= NTX) continue;
+      const int col = nt * 16 + (lane & 15), cq = col >> 2;
+      const int tap = cq / CQ, ci = (cq % CQ) * 4 + (col & 3);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = m * 16 + (lane >> 4) * 4 + r;
+        float v = accw[m][j][r];
+        if constexpr (PM == 0) v = __builtin_amdgcn_ldexpf(v, -(ecx + ecd));
+        if (co < COUT && cq < NQ && ci < CIN) s[co * NCOL + ci * KK + tap] = v;
+      }
+    }
+  // bias: unit i of thread i % 256 (slot i / 256) kept the partials of its 8
+  // channels; one thread per channel sums the units of its chunk in unit
+  // order (deterministic)
+  __syncthreads();
+  float* Rb = reinterpret_cast<float*>(lds16);   // [NLD][256][8]
+#pragma unroll
+  for (int l = 0; l < NLD; ++l)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) Rb[(l * 256 + tid) * 8 + c] = bacc[l][c];
+  __syncthreads();
+  if (tid < COUT) {
+    const int cc = tid / 8, c = tid % 8;
+    float v = 0.f;
+    for (int i = 0; i < NID; ++i)
+      if ((i / (W2 * ROWS)) % CCD == cc) v += Rb[i * 8 + c];
+    s[COUT * NCOL + tid] = v;
+  }
+  if constexpr (PM == 0) f16_range_note(rmax);
+}
+
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
+static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, int flags, float* slab, int nblk_max,
+                       int* nblk_out, int F, hipStream_t st, XMax xm, const void* wp) {
+  using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
+  constexpr int LDS = C::LDS > C::NLD * 256 * 8 * 4 ? C::LDS : C::NLD * 256 * 8 * 4;
+  static_assert(LDS <= LDS_MAX, "fused backward: staging exceeds the LDS");
+  const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
+  auto k = conv_bwd_split_k<CIN, COUT, H, W, KS, UPS, PM>;
+  static int resident = 0;
+  if (!resident) {
+    if (LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    resident = persistent_grid((const void*)k, LDS);
+  }
+  int nb = ntiles < nblk_max ? ntiles : nblk_max;
+  if (nb > resident) nb = resident;
+  if (nb < 1) nb = 1;
+  *nblk_out = nb;
+  PAIG_REQUIRE(!xm.p || (xm.n % 4 == 0 && (reinterpret_cast<uintptr_t>(xm.p) & 15) == 0),
+               "conv split bwd: xmax needs 16-byte alignment and a multiple of 4 slots (%d)", xm.n);
+  PAIG_REQUIRE(!(flags & 2) || aux.p, "conv split bwd: ReLU' mask (flags & 2) without aux");
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), LDS, st, x, dy, dx, aux, w, flags, slab, F, ntiles, xm,
+                     PM == 0 ? static_cast<const s16x8*>(wp) : nullptr);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+// (CIN, COUT, H) of the fused layers: the 3x3 convs with a data gradient
+// (every layer but the first) of the ShallowUNet at 32 x 32 (spring,
+// bouncing) and 36 x 36 (3bp); *_UP: the convs whose input is the fused 2x
+// upsample
+#define PAIG_BWD_SHAPES(X)                                                                  \
+  X(8, 8, 32) X(8, 16, 16) X(16, 16, 16) X(16, 32, 8) X(32, 32, 8) X(32, 16, 16) X(24, 8, 32) \
+  X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(16, 32, 9) X(32, 32, 9) X(32, 16, 18) X(24, 8, 36)
+
+}  // namespace
+
+extern "C" {
+
+int paig_conv2d_bwd_supported(int Cin, int Cout, int H, int W, int ks, int flags) {
+  if (H != W || ks != 3 || !(flags & (128 | 256)) || (flags & 32)) return 0;
+#define PAIG_CASE(CI, CO, HH) \
+  if (Cin == CI && Cout == CO && H == HH) return 1;
+  PAIG_BWD_SHAPES(PAIG_CASE)
+#undef PAIG_CASE
+  return 0;
+}
+
+int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
+                    float* dx, long long dx_fs, const float* aux, long long aux_fs, const float* w, float* slab,
+                    int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks, int flags,
+                    const float* xmax, int xmax_n, const void* wprep, void* stream) {
+  *nblk_out = 0;
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(paig_conv2d_bwd_supported(Cin, Cout, H, W, ks, flags),
+               "paig_conv2d_bwd: no fused kernel for Cin=%d Cout=%d H=%d W=%d ks=%d flags=%d", Cin, Cout, H, W, ks,
+               flags);
+  PAIG_REQUIRE(x_grp == 0 || H * W >= 256, "paig_conv2d_bwd: multi-frame tiles need a plain frame stride");
+  PAIG_REQUIRE(nblk_max > 0 && slab && dx && dy && x && w, "paig_conv2d_bwd: null operand or no slab rows");
+  hipStream_t st = (hipStream_t)stream;
+  FView vx{x, x_fs, x_gs, x_grp}, vd{dy, dy_fs, 0, 0}, va{aux, aux_fs, 0, 0};
+  FViewW vdx{dx, dx_fs};
+  XMax xm{const_cast<float*>(xmax), xmax_n};
+  const bool b16 = (flags & 256) != 0;
+  const int fl = flags & 6;
+#define PAIG_CASE(CI, CO, HH)                                                                                      \
+  if (Cin == CI && Cout == CO && H == HH)                                                                          \
+    return b16 ? sbwd_launch<CI, CO, HH, HH, 3, false, 2>(vx, vd, vdx, va, w, fl, slab, nblk_max, nblk_out, F, st, \
+                                                            xm, wprep)                                             \
+               : sbwd_launch<CI, CO, HH, HH, 3, false, 0>(vx, vd, vdx, va, w, fl, slab, nblk_max, nblk_out, F, st, \
+                                                            xm, wprep);
+  PAIG_BWD_SHAPES(PAIG_CASE)
+#undef PAIG_CASE
+  return PAIG_E_UNSUPPORTED;
+}
+
+}  // extern "C"
+
+PAIG_F16_RANGE_ACCESSOR(paig_f16_range_bwd)

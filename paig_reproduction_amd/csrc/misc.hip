@@ -250,12 +250,12 @@ int paig_f16_range_status(int clear) {
     paig_set_error("paig_f16_range_status: %s", hipGetErrorString(e));
     return -(int)e;
   }
-  const int a = paig_f16_range_conv(clear), b = paig_f16_range_gemm(clear);
-  if (a < 0 || b < 0) {
+  const int a = paig_f16_range_conv(clear), b = paig_f16_range_gemm(clear), c = paig_f16_range_bwd(clear);
+  if (a < 0 || b < 0 || c < 0) {
     paig_set_error("paig_f16_range_status: flag read failed");
     return -1;
   }
-  return (a | b) ? 1 : 0;
+  return (a | b | c) ? 1 : 0;
 }
 
 // y[P] = W2 tanh(W1 1 + b1) + b2 ; hout[200] ; ypost = sigmoid(y) if non-null

@@ -981,6 +981,14 @@ class Engine:
         self._psgemm("gemm_wgrad:encoder.l1", 200, n1, KF, i_dh1t, i_xt, self.g("encoder.l1.weight"), n1, ws, st)
         self._psgemm("gemm_dgrad:encoder.l1", KF, n1, 200, i_dh1, ps["w1t"], dobjs, n1, ws, st)
 
+    def _fused_bwd(self, cin, cout, Hl, ks, cm):
+        """The layer backward runs as one fused launch (paig_conv2d_bwd)
+        where the library has the shape; PAIG_FUSED_BWD=0 keeps the separate
+        data- and weight-gradient kernels (A/B)."""
+        if os.environ.get("PAIG_FUSED_BWD", "1") == "0" or not cm:
+            return False
+        return bool(self.L.paig_conv2d_bwd_supported(cin, cout, Hl, Hl, ks, cm))
+
     def _unet_backward(self, S, dacts, st):
         lay = S["lay"]
         L = self.L
@@ -1032,14 +1040,36 @@ class Engine:
                 slab = _empty(nblk_max * (cout * cin * ks * ks + cout), dev)
                 nb = ctypes.c_int(0)
                 fl = 2 * F * cin * cout * ks * ks * Hl * Hl
+                gw = self.g(lay.prefix + op["name"] + ".weight")
+                n_w = cout * cin * ks * ks
+                if src[0] != "X0" and not xfl and self._fused_bwd(cin, cout, Hl, ks, cm):
+                    # the layer's data and weight gradients in ONE launch from
+                    # one staging of dY and X (csrc/conv_bwd.hip)
+                    dxv, _ = dview(src)
+                    mode = state(src)
+                    flags = cm | (4 if mode == "accum" else 0)
+                    aux = (None, 0)
+                    if relu_fin:
+                        assert len(fin) == 1 and fin[0][0] == src, f"{op['name']}: mixed ReLU finalization"
+                        a = view(src)[0]
+                        aux = (a[0], a[1])
+                        flags |= 2
+                    # algorithmic bytes: X and dY read, dX written (+ read when accumulating)
+                    nbytes = 4 * F * Hl * Hl * (cin + cout + cin * (2 if mode == "accum" else 1))
+                    with self._p("conv_bwd:" + op["name"], 2 * fl, nbytes):
+                        L.paig_conv2d_bwd(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], dxv[0], dxv[1], aux[0], aux[1],
+                                          ptr(self.p(lay.prefix + op["name"] + ".weight")), ptr(slab), nblk_max,
+                                          ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, cm | (flags & 6),
+                                          S["xmax"](i), XMAX_SLOTS, S["wprep"].get((i, 1)), st)
+                    slabs.append((slab, nb.value, n_w + cout, gw))
+                    mark(src)
+                    continue
                 nbytes = 4 * F * (cin * (Hl // (2 if xfl else 1)) ** 2 + cout * Hl * Hl)
                 with self._p("conv_wgrad:" + op["name"], fl, nbytes):
                     L.paig_conv2d_wgrad_ex(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], ptr(slab), nblk_max,
                                            ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, xfl | cm, S["xmax"](i),
                                            XMAX_SLOTS, st)
-                gw = self.g(lay.prefix + op["name"] + ".weight")
                 gb = self.g(lay.prefix + op["name"] + ".bias")
-                n_w = cout * cin * ks * ks
                 assert gb.data_ptr() == gw.data_ptr() + n_w * 4, "flat grads: weight and bias must be adjacent"
                 slabs.append((slab, nb.value, n_w + cout, gw))
                 if src[0] == "X0":

@@ -72,6 +72,10 @@ class _PhysicsStep(torch.autograd.Function):
         # tensor (and the attribute) but bumps its version counter
         mark = getattr(d_sse_roll, "_paig_live_steps", None) if d_out is None else None
         live = mark[0] if mark is not None and d_sse_roll._version == mark[1] else 0
+        # incoming gradients may be broadcast views (d sum(sse)/d sse is an
+        # expanded scalar, stride 0): the kernels read dense vectors
+        d_sse_rec = d_sse_rec.contiguous() if d_sse_rec is not None else None
+        d_sse_roll = d_sse_roll.contiguous() if d_sse_roll is not None else None
         ctx.engine.backward(ctx.S, d_sse_rec, d_sse_roll, d_out, d_rec, d_enc, d_pvs, roll_live=live)
         # nothing reached the rollout branch (quirk Q1: the loss read a stale
         # output): the velocity encoder and physics parameters are not in the
