@@ -35,6 +35,10 @@
 // #2).
 #include "split_common.h"
 
+#ifndef PAIG_BWD_MINW
+#define PAIG_BWD_MINW 0   // A/B builds: force the blocks per CU the kernels are compiled for
+#endif
+
 namespace {
 
 // LDS bytes of a block at tiles of <= tpx pixels (both images, the weights,
@@ -54,6 +58,18 @@ constexpr int sbwd_tpx(int CIN, int COUT, int H, int W, bool UPS, int PM) {
   for (int t = 256; t >= 64; t /= 2)
     if (sbwd_lds(CIN, COUT, H, W, UPS, PM, t) <= LDS_MAX / 2) return t;
   return 64;
+}
+
+// waves per SIMD (= blocks per CU) each shape compiles for without spilling
+// (measured: -Rpass-analysis=kernel-resource-usage at 2 / 3 / 4)
+constexpr int sbwd_minw(int CIN, int COUT, int H, int PM) {
+  if (CIN == 8 && COUT == 8 && H == 32) return 4;
+  if (PM == 2 && CIN == 8 && COUT == 16 && H == 16) return 3;
+  if (PM == 2 && CIN == 24 && COUT == 8 && H == 32) return 3;
+  if (CIN == 8 && COUT == 8 && H == 36) return 3;
+  if (CIN == 8 && COUT == 16 && H == 18) return PM == 2 ? 4 : 3;
+  if (CIN == 16 && COUT == 16 && H == 18) return 3;
+  return 2;
 }
 
 // 4 waves split the weight-gradient N-tiles (each wave owns every 4th one
@@ -99,12 +115,17 @@ struct SBwdCfg {
   // X prefetched a tile ahead where its registers are cheap (else loaded
   // when staged)
   static constexpr bool XPIPE = !UPS && NLX * 8 <= 32;
+  // blocks per CU the kernel is compiled for (__launch_bounds__): the most
+  // that compile without register spills (sbwd_minw), within the LDS
+  static constexpr int LDSB = LDS_MAX / (LDS > (NLD * 256 * 8 + 256) * 4 ? LDS : (NLD * 256 * 8 + 256) * 4);
+  static constexpr int MW0 = PAIG_BWD_MINW > 0 ? PAIG_BWD_MINW : sbwd_minw(CIN, COUT, H, PM);
+  static constexpr int MINW = MW0 < LDSB ? MW0 : LDSB;
   static_assert(H % RT == 0, "RT divides H");
   static_assert(KS == 3, "3x3 layers (the 1x1 heads are fused elsewhere)");
 };
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, (SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>::MINW))
 conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restrict__ w, int flags,
                  float* __restrict__ slab, int F, int ntiles, XMax xm, const s16x8* __restrict__ wp) {
   using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
@@ -625,20 +646,30 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       }
     }
   // bias: unit i of thread i % 256 (slot i / 256) kept the partials of its 8
-  // channels; one thread per channel sums the units of its chunk in unit
-  // order (deterministic)
+  // channels.  Two fixed-order stages: thread (channel co, part q) sums the
+  // units q, q + NP, ... of co's chunk; thread co then sums its NP parts
   __syncthreads();
-  float* Rb = reinterpret_cast<float*>(lds16);   // [NLD][256][8]
+  float* Rb = reinterpret_cast<float*>(lds16);   // [NLD][256][8], then [COUT][NP]
+  constexpr int NP = 256 / COUT, NU = FPT * ROWS * W2;   // parts per channel, units per chunk
+  float* Rp = Rb + NLD * 256 * 8;
 #pragma unroll
   for (int l = 0; l < NLD; ++l)
 #pragma unroll
     for (int c = 0; c < 8; ++c) Rb[(l * 256 + tid) * 8 + c] = bacc[l][c];
   __syncthreads();
-  if (tid < COUT) {
-    const int cc = tid / 8, c = tid % 8;
+  if (tid < NP * COUT) {
+    const int co = tid % COUT, q = tid / COUT, cc = co / 8, c = co % 8;
     float v = 0.f;
-    for (int i = 0; i < NID; ++i)
-      if ((i / (W2 * ROWS)) % CCD == cc) v += Rb[i * 8 + c];
+    for (int j = q; j < NU; j += NP) {
+      const int xpi = j % W2, r = (j / W2) % ROWS, fi = j / (W2 * ROWS);
+      v += Rb[((((fi * CCD + cc) * ROWS) + r) * W2 + xpi) * 8 + c];
+    }
+    Rp[co * NP + q] = v;
+  }
+  __syncthreads();
+  if (tid < COUT) {
+    float v = 0.f;
+    for (int q = 0; q < NP; ++q) v += Rp[tid * NP + q];
     s[COUT * NCOL + tid] = v;
   }
   if constexpr (PM == 0) f16_range_note(rmax);
@@ -648,7 +679,8 @@ template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
 static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, int flags, float* slab, int nblk_max,
                        int* nblk_out, int F, hipStream_t st, XMax xm, const void* wp) {
   using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
-  constexpr int LDS = C::LDS > C::NLD * 256 * 8 * 4 ? C::LDS : C::NLD * 256 * 8 * 4;
+  constexpr int RED = (C::NLD * 256 * 8 + 256) * 4;   // the bias reduction's LDS
+  constexpr int LDS = C::LDS > RED ? C::LDS : RED;
   static_assert(LDS <= LDS_MAX, "fused backward: staging exceeds the LDS");
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   auto k = conv_bwd_split_k<CIN, COUT, H, W, KS, UPS, PM>;
