@@ -45,11 +45,12 @@ namespace {
 // the fused-upsample window)
 constexpr int sbwd_lds(int CIN, int COUT, int H, int W, bool UPS, int PM, int tpx) {
   const int FPT = H * W <= tpx ? tpx / (H * W) : 1, RT = H * W <= tpx ? H : rows_fit(H, W, tpx);
-  const int ROWS = RT + 2, CCD = rup(COUT, 8) / 8, PSD = CCD % 2 == 0 ? CCD + 1 : CCD;
+  const int ROWS = RT + 2, ROWSD = ROWS + (UPS ? 2 : 0), CCD = rup(COUT, 8) / 8, PSD = CCD % 2 == 0 ? CCD + 1 : CCD;
   const int RPD = W == 8 ? to_mod16((W + 2) * PSD, 8) : (W + 2) * PSD;
-  const int IMGD = (FPT * ROWS * RPD + 2) * 8, WIMG = ceil_div(9 * CCD, 4) * ceil_div(CIN, 16) * 64 * 8;
-  const int XIMG = rup(CIN, 4) / 4 * rup(FPT * ROWS * (W + 4) * 4 + 80, 128);
-  return (IMGD + WIMG + XIMG) * 2 * (PM == 2 ? 1 : 2) + (UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0);
+  const int IMGD = (FPT * ROWSD * RPD + 2) * 8, WIMG = ceil_div(9 * CCD, 4) * ceil_div(CIN, 16) * 64 * 8;
+  const int XIMG = rup(CIN, 4) / 4 * rup(FPT * ROWS * (W + 4) * 4 + 80, 128) * 2 * (PM == 2 ? 1 : 2);
+  const int XREG = XIMG > (UPS ? CIN * (RT + 2) * W * 4 : 0) ? XIMG : CIN * (RT + 2) * W * 4;
+  return (IMGD + WIMG) * 2 * (PM == 2 ? 1 : 2) + XREG + (UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0);
 }
 // pixels per tile: the largest of 256 / 128 / 64 whose staging lets two
 // blocks share a CU (the 8 x 8 / 9 x 9 levels' multi-frame tiles and the
@@ -83,18 +84,25 @@ struct SBwdCfg {
   static constexpr int FPT = H * W <= TPX ? TPX / (H * W) : 1;
   static constexpr int RT = H * W <= TPX ? H : rows_fit(H, W, TPX);
   static constexpr int TPXV = FPT * RT * W;                   // valid pixels per tile
-  static constexpr int ROWS = RT + KS - 1;
+  static constexpr int ROWS = RT + KS - 1;                    // X image rows (halo PADL)
+  // fused upsample input (c7 / c10): the data gradient is formed for one
+  // more row above and below the tile (EXT), so that the 2x upsample's
+  // transpose of the tile's rows (low-resolution rows y0/2 .. (y0+RT)/2 - 1,
+  // each fed by 4 full-resolution rows) completes inside the tile
+  static constexpr int EXT = UPS ? 1 : 0;
+  static constexpr int RTD = RT + 2 * EXT, ROWSD = ROWS + 2 * EXT;   // dX rows, dY image rows
+  static constexpr int TPXD = FPT * RTD * W;                  // data-gradient pixels per tile
   // ---- dY image: NHWC, 8-channel slots, halo PADL
   static constexpr int CCD = rup(COUT, 8) / 8;
   static constexpr int PSD = CCD % 2 == 0 ? CCD + 1 : CCD;    // odd pitch: 16 pixels -> 16 bank groups
   static constexpr int TWPX = W + 2 * PADL;
   static constexpr int RPD = W == 8 ? to_mod16(TWPX * PSD, 8) : TWPX * PSD;
-  static constexpr int ZSLOT = FPT * ROWS * RPD;              // a zero slot after the image
+  static constexpr int ZSLOT = FPT * ROWSD * RPD;             // a zero slot after the image
   static constexpr int IMGD = (ZSLOT + 2) * 8;                // (+1 spare slot: wgrad reads of 8-channel dY)
   // ---- data gradient: k = (tap, 8-channel chunk of dY), 4 chunks per MFMA k-step
   static constexpr int KC = KK * CCD, NS = ceil_div(KC, 4);
   static constexpr int NTD = ceil_div(CIN, 16);               // 16-channel tiles of dX
-  static constexpr int NMT = ceil_div(TPXV, 16), MW = ceil_div(NMT, 4);
+  static constexpr int NMT = ceil_div(TPXD, 16), MW = ceil_div(NMT, 4);
   static constexpr int WIMG = NS * NTD * 64 * 8;
   // ---- X image (weight gradient B operand): 4-channel quad planes
   static constexpr int CQ = rup(CIN, 4) / 4, NQ = KK * CQ, NTX = ceil_div(NQ, 4);
@@ -107,10 +115,13 @@ struct SBwdCfg {
   static constexpr int NCOL = CIN * KK, SLAB = COUT * NCOL + COUT;
   // ---- staging units: UPX pixels x (8 dY | 4 X) channels, pixel fastest
   static constexpr int UPX = W % 2 == 0 ? 2 : 1, W2 = W / UPX;
-  static constexpr int NID = FPT * ROWS * W2 * CCD, NLD = ceil_div(NID, 256);
+  static constexpr int NID = FPT * ROWSD * W2 * CCD, NLD = ceil_div(NID, 256);
   static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = ceil_div(NIX, 256);
   static constexpr int UPW = FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2);   // fused-upsample window (floats)
-  static constexpr int LDS = (IMGD + WIMG + XIMG) * 2 * NIMG + (UPS ? UPW * 4 : 0);
+  // the X image's region (UPS: it later holds the tile's full-resolution dX)
+  static constexpr int XREG = XIMG * 2 * NIMG > (UPS ? CIN * (RT + 2) * W * 4 : 0) ? XIMG * 2 * NIMG
+                                                                                    : CIN * (RT + 2) * W * 4;
+  static constexpr int LDS = (IMGD + WIMG) * 2 * NIMG + XREG + (UPS ? UPW * 4 : 0);
   static constexpr bool VEC4 = W % 4 == 0;
   // X prefetched a tile ahead where its registers are cheap (else loaded
   // when staged)
@@ -122,6 +133,10 @@ struct SBwdCfg {
   static constexpr int MINW = MW0 < LDSB ? MW0 : LDSB;
   static_assert(H % RT == 0, "RT divides H");
   static_assert(KS == 3, "3x3 layers (the 1x1 heads are fused elsewhere)");
+  static_assert(!UPS || (FPT == 1 && RT % 2 == 0 && W % 4 == 0), "fused upsample: whole even row blocks of one frame");
+  // UPS: the tile's full-resolution dX rows [RTD][W] per channel (fp32) are
+  // parked in the X image's region (free once the weight-gradient MFMAs ran)
+  static_assert(!UPS || CIN * RTD * W * 4 <= XREG, "fused upsample: dX tile does not fit the X region");
 };
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
@@ -130,6 +145,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
                  float* __restrict__ slab, int F, int ntiles, XMax xm, const s16x8* __restrict__ wp) {
   using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int KK = C::KK, PADL = C::PADL, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, TPXV = C::TPXV;
+  constexpr int EXT = C::EXT, RTD = C::RTD, ROWSD = C::ROWSD, TPXD = C::TPXD;
   constexpr int CCD = C::CCD, PSD = C::PSD, RPD = C::RPD, KC = C::KC, NS = C::NS, NTD = C::NTD, MW = C::MW;
   constexpr int CQ = C::CQ, NQ = C::NQ, NTX = C::NTX, OFFX = C::OFFX, TWX = C::TWX, XPL = C::XPL;
   constexpr int MT = C::MT, NTW = C::NTW, KB = C::KB, NCOL = C::NCOL, UPX = C::UPX, W2 = C::W2;
@@ -144,14 +160,14 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   short* Wl = Wh + (C::NIMG == 2 ? C::WIMG : 0);
   short* Xh = lds16 + C::NIMG * (C::IMGD + C::WIMG);
   short* Xl = Xh + (C::NIMG == 2 ? C::XIMG : 0);
-  float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::IMGD + C::WIMG + C::XIMG));   // UPS window
+  float* Sl = reinterpret_cast<float*>(reinterpret_cast<char*>(Xh) + C::XREG);   // UPS window
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
   __shared__ float smax[4];
 
   auto xplane = [](int cq) { return cq * XPL + ((cq & 1) ? 16 : 0) + ((cq & 2) ? 64 : 0); };
   // ---- zero what the staging never writes: the dY image's halo columns,
   // its zero / spare slots, the X image's halo columns
-  for (int i = tid; i < FPT * ROWS * 2 * PADL * CCD; i += 256) {
+  for (int i = tid; i < FPT * ROWSD * 2 * PADL * CCD; i += 256) {
     const int cc = i % CCD, hc = (i / CCD) % (2 * PADL), r = i / (CCD * 2 * PADL);
     const int xc = hc < PADL ? hc : W + hc;
     const int o = (r * RPD + xc * PSD + cc) * 8;
@@ -248,9 +264,9 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
 #pragma unroll
   for (int mt = 0; mt < MW; ++mt) {
     int pix = (wv * MW + mt) * 16 + (lane & 15);
-    if (pix >= TPXV) pix = 0;   // padding rows of the last M-tile: finite data, never stored
-    const int fi = pix / (RT * W), rem = pix % (RT * W);
-    pbase[mt] = (fi * ROWS + rem / W) * RPD + (rem % W) * PSD;
+    if (pix >= TPXD) pix = 0;   // padding rows of the last M-tile: finite data, never stored
+    const int fi = pix / (RTD * W), rem = pix % (RTD * W);
+    pbase[mt] = (fi * ROWSD + rem / W) * RPD + (rem % W) * PSD;
   }
   int soff[NS];
 #pragma unroll
@@ -277,7 +293,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   auto dslot = [&](int j) {
     if (TPXV % 32 != 0 && j >= TPXV) return C::ZSLOT;
     const int fi = j / (RT * W), rem = j % (RT * W);
-    return (fi * ROWS + rem / W + PADL) * RPD + (rem % W + PADL) * PSD;
+    return (fi * ROWSD + rem / W + PADL + EXT) * RPD + (rem % W + PADL) * PSD;
   };
   auto xpos = [&](int j) {   // X image position of tile pixel j at tap (0, 0)
     if (TPXV % 32 != 0 && j >= TPXV) j = 0;   // its dY is zero
@@ -308,8 +324,8 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
 #pragma unroll
     for (int l = 0; l < NLD; ++l) {
       const int i = tid + l * 256;
-      const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CCD, fi = i / (W2 * ROWS * CCD);
-      const int gy = y0 + r - PADL;
+      const int xp = UPX * (i % W2), r = (i / W2) % ROWSD, cc = (i / (W2 * ROWSD)) % CCD, fi = i / (W2 * ROWSD * CCD);
+      const int gy = y0 + r - PADL - EXT;
       const bool ok = i < NID && f0 + fi < F && gy >= 0 && gy < H;
       const int off = fi * (int)dy.fs + cc * 8 * (int)HW + gy * W + xp;
       static_assert(8 * HW <= 8 * 4096, "paig_zero_planes covers the unit");
@@ -345,8 +361,8 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
     }
   };
   auto put_d = [&](int i, const float2* v) {
-    const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CCD, fi = i / (W2 * ROWS * CCD);
-    const int o = ((fi * ROWS + r) * RPD + (xp + PADL) * PSD + cc) * 8;
+    const int xp = UPX * (i % W2), r = (i / W2) % ROWSD, cc = (i / (W2 * ROWSD)) % CCD, fi = i / (W2 * ROWSD * CCD);
+    const int o = ((fi * ROWSD + r) * RPD + (xp + PADL) * PSD + cc) * 8;
     s16x8 h0, l0, h1, l1;
     if constexpr (PM == 0) {
       pf32x2 sv[8];
@@ -459,29 +475,37 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       if (NID % 256 != 0 && i >= NID) break;
       put_d(i, pd[l]);
       // bias partials: the tile's own rows (not the halo), frames < F
-      const int r = (i / W2) % ROWS, fi = i / (W2 * ROWS * CCD);
-      if (r >= PADL && r < PADL + RT && f0 + fi < F) {
+      const int r = (i / W2) % ROWSD, fi = i / (W2 * ROWSD * CCD);
+      if (r >= PADL + EXT && r < PADL + EXT + RT && f0 + fi < F) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) bacc[l][c] += pd[l][c].x + pd[l][c].y;
       }
     }
     if constexpr (UPS) {
+      // the half-resolution window (prefetched) -> LDS, then the upsampled
+      // rows: units of 4 pixels x 4 channels (one row4 per channel: shared
+      // taps and source reads), stored as two 2-pixel staging units
       const int y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
       __syncthreads();
+      constexpr int W4 = W / 4;
 #pragma unroll 1
-      for (int i = tid; i < NIX; i += 256) {
-        const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
+      for (int i = tid; i < NIX / 2; i += 256) {
+        const int q = i % W4, r = (i / W4) % ROWS, cq = (i / (W4 * ROWS)) % CQ;
         const int gy = y0 + r - PADL;
-        const bool ok = f0 + fi < F && gy >= 0 && gy < H;
-        float2 v[4];
+        const bool ok = f0 < F && gy >= 0 && gy < H;
+        f32x4 o[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          v[c] = (ok && cq * 4 + c < CIN)
-                     ? make_float2(UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp),
-                                   UPX == 2 ? UP::px1(Sl, fi, cq * 4 + c, gy, y0, xp + 1) : 0.f)
-                     : make_float2(0.f, 0.f);
-        put_x(i, v);
+          o[c] = (ok && cq * 4 + c < CIN) ? UP::row4(Sl, 0, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const int ia = (cq * ROWS + r) * W2 + 2 * q;
+        float2 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][0], o[c][1]);
+        put_x(ia, v);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][2], o[c][3]);
+        put_x(ia + 1, v);
       }
     } else if constexpr (C::XPIPE) {
 #pragma unroll
@@ -583,6 +607,62 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
         for (int nt = 0; nt < NTD; ++nt) accd[mt][nt] = mma3<PM>(ah, al, bh[nt], bl[nt], accd[mt][nt]);
       }
     }
+    if constexpr (UPS) {
+      // full-resolution dX rows y0-1 .. y0+RT of the tile -> LDS [ci][RTD][W]
+      // (the X image is free once every wave's weight-gradient reads are done)
+      float* U = reinterpret_cast<float*>(Xh);
+      __syncthreads();
+#pragma unroll
+      for (int nt = 0; nt < NTD; ++nt) {
+        const int ci = nt * 16 + (lane & 15);
+        if (ci >= CIN) continue;
+        const float tinv = PM == 0 ? __builtin_amdgcn_ldexpf(1.f, -(ecd + ewn[nt])) : 1.f;
+#pragma unroll
+        for (int mt = 0; mt < MW; ++mt) {
+          const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+          if (pix < TPXD) *reinterpret_cast<f32x4*>(U + ci * TPXD + pix) = accd[mt][nt] * tinv;
+        }
+      }
+      __syncthreads();
+      // the 2x bilinear upsample's transpose (aten upsample_bilinear2d
+      // backward, align_corners=False: source s gets outputs 2s-1 .. 2s+2
+      // with weights 1/4, 3/4, 3/4, 1/4; 1 at the clamped edges), gather form
+      // in upsample_bwd_k's order; then ReLU' of the source, accumulate
+      constexpr int HS = H / 2, WS = W / 2, NO = CIN * (RT / 2) * WS;
+      for (int o = tid; o < NO; o += 256) {
+        const int sx = o % WS, sr = (o / WS) % (RT / 2), ci = o / (WS * (RT / 2));
+        const int sy = y0 / 2 + sr;
+        float wy[4], wx[4];
+        wy[0] = sy >= 1 ? 0.25f : 0.f;
+        wy[1] = sy == 0 ? 1.f : 0.75f;
+        wy[2] = sy == HS - 1 ? 1.f : 0.75f;
+        wy[3] = sy <= HS - 2 ? 0.25f : 0.f;
+        wx[0] = sx >= 1 ? 0.25f : 0.f;
+        wx[1] = sx == 0 ? 1.f : 0.75f;
+        wx[2] = sx == WS - 1 ? 1.f : 0.75f;
+        wx[3] = sx <= WS - 2 ? 0.25f : 0.f;
+        float acc = 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          // full row 2sy - 1 + a = tile dX row 2sr + a (row 0 = y0 - 1)
+          if (wy[a] == 0.f) continue;
+          const float* rp = U + ci * TPXD + (2 * sr + a) * W;
+          float row = 0.f;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int xx = 2 * sx - 1 + b;
+            if (wx[b] != 0.f) row = fmaf(wx[b], rp[xx], row);
+          }
+          acc = fmaf(wy[a], row, acc);
+        }
+        if (f0 < F) {
+          float* op = dx.frame(f0) + ((long long)ci * HS + sy) * WS + sx;
+          if (flags & 4) acc += *op;
+          if (flags & 2) acc = aux.frame(f0)[((long long)ci * HS + sy) * WS + sx] > 0.f ? acc : 0.f;
+          *op = acc;
+        }
+      }
+    } else {
     // epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for input
     // channel ci = nt*16 + (lane&15); flags 2: * (aux > 0), 4: accumulate
 #pragma unroll
@@ -624,6 +704,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
         }
       }
     }
+    }   // !UPS
   }
 
   // ---- this block's slab row: weight gradients (each wave its N-tiles,
@@ -650,7 +731,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   // units q, q + NP, ... of co's chunk; thread co then sums its NP parts
   __syncthreads();
   float* Rb = reinterpret_cast<float*>(lds16);   // [NLD][256][8], then [COUT][NP]
-  constexpr int NP = 256 / COUT, NU = FPT * ROWS * W2;   // parts per channel, units per chunk
+  constexpr int NP = 256 / COUT, NU = FPT * ROWSD * W2;   // parts per channel, units per chunk
   float* Rp = Rb + NLD * 256 * 8;
 #pragma unroll
   for (int l = 0; l < NLD; ++l)
@@ -661,8 +742,8 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
     const int co = tid % COUT, q = tid / COUT, cc = co / 8, c = co % 8;
     float v = 0.f;
     for (int j = q; j < NU; j += NP) {
-      const int xpi = j % W2, r = (j / W2) % ROWS, fi = j / (W2 * ROWS);
-      v += Rb[((((fi * CCD + cc) * ROWS) + r) * W2 + xpi) * 8 + c];
+      const int xpi = j % W2, r = (j / W2) % ROWSD, fi = j / (W2 * ROWSD);
+      v += Rb[((((fi * CCD + cc) * ROWSD) + r) * W2 + xpi) * 8 + c];
     }
     Rp[co * NP + q] = v;
   }
@@ -706,6 +787,9 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // (every layer but the first) of the ShallowUNet at 32 x 32 (spring,
 // bouncing) and 36 x 36 (3bp; its 9 x 9 level keeps the separate kernels:
 // odd rows and 32-channel tiles spill registers in the fused form)
+// the fused-upsample layers (input = the 2x bilinear upsample of a half-
+// resolution source; the upsample's transpose folded into the data gradient)
+#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32) X(16, 16, 36)
 #define PAIG_BWD_SHAPES(X)                                                                  \
   X(8, 8, 32) X(8, 16, 16) X(16, 16, 16) X(16, 32, 8) X(32, 32, 8) X(32, 16, 16) X(24, 8, 32) \
   X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(32, 16, 18) X(24, 8, 36)
@@ -715,9 +799,13 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 extern "C" {
 
 int paig_conv2d_bwd_supported(int Cin, int Cout, int H, int W, int ks, int flags) {
-  if (H != W || ks != 3 || !(flags & (128 | 256)) || (flags & 32)) return 0;
+  if (H != W || ks != 3 || !(flags & (128 | 256))) return 0;
 #define PAIG_CASE(CI, CO, HH) \
   if (Cin == CI && Cout == CO && H == HH) return 1;
+  if (flags & 32) {
+    PAIG_BWD_UP_SHAPES(PAIG_CASE)
+    return 0;
+  }
   PAIG_BWD_SHAPES(PAIG_CASE)
 #undef PAIG_CASE
   return 0;
@@ -740,6 +828,17 @@ int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, c
   XMax xm{const_cast<float*>(xmax), xmax_n};
   const bool b16 = (flags & 256) != 0;
   const int fl = flags & 6;
+  if (flags & 32) {
+#define PAIG_CASE(CI, CO, HH)                                                                                     \
+  if (Cin == CI && Cout == CO && H == HH)                                                                         \
+    return b16 ? sbwd_launch<CI, CO, HH, HH, 3, true, 2>(vx, vd, vdx, va, w, fl, slab, nblk_max, nblk_out, F, st, \
+                                                           xm, wprep)                                             \
+               : sbwd_launch<CI, CO, HH, HH, 3, true, 0>(vx, vd, vdx, va, w, fl, slab, nblk_max, nblk_out, F, st, \
+                                                           xm, wprep);
+    PAIG_BWD_UP_SHAPES(PAIG_CASE)
+#undef PAIG_CASE
+    return PAIG_E_UNSUPPORTED;
+  }
 #define PAIG_CASE(CI, CO, HH)                                                                                      \
   if (Cin == CI && Cout == CO && H == HH)                                                                          \
     return b16 ? sbwd_launch<CI, CO, HH, HH, 3, false, 2>(vx, vd, vdx, va, w, fl, slab, nblk_max, nblk_out, F, st, \

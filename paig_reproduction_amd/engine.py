@@ -1025,7 +1025,10 @@ class Engine:
             written.setdefault(region[0], []).append((region[1], region[2]))
 
         slabs = []
+        folded_ups = set()   # upsample ops whose backward a fused conv backward did
         for i in range(nops - 1, -1, -1):
+            if i in folded_ups:
+                continue
             op = lay.ops[i]
             fin = lay.fin[i]
             relu_fin = [r for r, relu in fin if relu]
@@ -1042,6 +1045,33 @@ class Engine:
                 fl = 2 * F * cin * cout * ks * ks * Hl * Hl
                 gw = self.g(lay.prefix + op["name"] + ".weight")
                 n_w = cout * cin * ks * ks
+                if xfl and self._fused_bwd(cin, cout, Hl, ks, cm | 32):
+                    # fused-upsample input (c7 / c10): the layer backward AND the
+                    # upsample's backward in one launch -- the data gradient of
+                    # the upsampled tensor never reaches memory; the launch
+                    # writes the half-resolution source's gradient
+                    up = lay.fused_up[i]
+                    ui = lay.ops.index(up)
+                    usrc = up["src"]
+                    dxv, _ = dview(usrc)
+                    mode = state(usrc)
+                    assert mode == "write", f"{op['name']}: upsample source gradient already written"
+                    flags = cm | 32
+                    aux = (None, 0)
+                    if any(relu for r, relu in lay.fin[ui] if r == usrc):
+                        a = view(usrc)[0]
+                        aux = (a[0], a[1])
+                        flags |= 2
+                    nbytes = 4 * F * (cin * (Hl // 2) ** 2 * (2 if flags & 2 else 1) + cout * Hl * Hl)
+                    with self._p("conv_bwd:" + op["name"], 2 * fl, nbytes):
+                        L.paig_conv2d_bwd(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], dxv[0], dxv[1], aux[0], aux[1],
+                                          ptr(self.p(lay.prefix + op["name"] + ".weight")), ptr(slab), nblk_max,
+                                          ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, flags, S["xmax"](i), XMAX_SLOTS,
+                                          S["wprep"].get((i, 1)), st)
+                    slabs.append((slab, nb.value, n_w + cout, gw))
+                    mark(usrc)
+                    folded_ups.add(ui)
+                    continue
                 if src[0] != "X0" and not xfl and self._fused_bwd(cin, cout, Hl, ks, cm):
                     # the layer's data and weight gradients in ONE launch from
                     # one staging of dY and X (csrc/conv_bwd.hip)

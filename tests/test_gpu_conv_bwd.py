@@ -175,3 +175,48 @@ def test_fused_backward_matches_separate_kernels(cin, cout, hw):
     assert rel_err(dx, dx2) <= 2e-6
     assert rel_err(gw, g[:n].view_as(w)) <= 2e-6
     assert rel_err(gb, g[n:]) <= 2e-6
+
+
+@pytest.mark.parametrize("mode", [128, 256])
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (16, 16, 36)])
+def test_fused_backward_upsample_input(cin, cout, hw, mode):
+    """c7 / c10 (blocks.py:289-290,298-299): the conv input is the 2x bilinear
+    upsample (torchvision Resize) of a ReLU'd half-resolution source.  One
+    launch gives the weight / bias gradients and the SOURCE's gradient (the
+    upsample's backward folded in, ReLU' of the source applied); float64
+    autograd through F.interpolate + conv2d is the reference."""
+    assert L().paig_conv2d_bwd_supported(cin, cout, hw, hw, 3, mode | 32) == 1
+    tol = TOL[mode]
+    for F_ in (3, 1):
+        torch.manual_seed(cin + cout + hw + F_)
+        xs = torch.relu(torch.randn(F_, cin, hw // 2, hw // 2, device=DEV))
+        w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.2
+        b = torch.randn(cout, device=DEV)
+        dy = torch.randn(F_, cout, hw, hw, device=DEV)
+        xr = xs.double().cpu().requires_grad_(True)
+        wr = w.double().cpu().requires_grad_(True)
+        xu = F.interpolate(xr, size=(hw, hw), mode="bilinear", align_corners=False, antialias=True)
+        F.conv2d(xu, wr, padding="same").backward(dy.double().cpu())
+        rdx = xr.grad * (xs.cpu() > 0)
+        hs = hw // 2
+        xmax = None
+        if mode == 128:
+            xmax = torch.zeros(XMAX_SLOTS, device=DEV)
+            out = torch.empty(F_, cout, hw, hw, device=DEV)
+            L().paig_conv2d_fwd_ex(p(xs), cin * hs * hs, 0, 0, p(out), cout * hw * hw, None, 0, p(w), p(b), F_, cin,
+                                   cout, hw, hw, 3, 32 | mode, p(xmax), XMAX_SLOTS, st())
+        dx = torch.full((F_, cin, hs, hs), float("nan"), device=DEV)   # write mode: every element written
+        nmax = 512
+        slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+        nb = ctypes.c_int(0)
+        L().paig_conv2d_bwd(p(xs), cin * hs * hs, 0, 0, p(dy), cout * hw * hw, p(dx), cin * hs * hs, p(xs),
+                            cin * hs * hs, p(w), p(slab), nmax, ctypes.byref(nb), F_, cin, cout, hw, hw, 3,
+                            mode | 32 | 2, p(xmax), XMAX_SLOTS if xmax is not None else 0, None, st())
+        g = torch.empty(cout * cin * 9 + cout, device=DEV)
+        L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
+        torch.cuda.synchronize()
+        n = cout * cin * 9
+        assert torch.isfinite(dx).all()
+        assert rel_err(dx, rdx) <= tol, ("dx", F_)
+        assert rel_err(g[:n].view_as(w), wr.grad) <= tol, ("dw", F_)
+        assert rel_err(g[n:], dy.double().cpu().sum((0, 2, 3))) <= 1e-5, ("db", F_)
