@@ -49,7 +49,8 @@ constexpr int sbwd_lds(int CIN, int COUT, int H, int W, bool UPS, int PM, int tp
   const int RPD = W == 8 ? to_mod16((W + 2) * PSD, 8) : (W + 2) * PSD;
   const int IMGD = (FPT * ROWSD * RPD + 2) * 8, WIMG = ceil_div(9 * CCD, 4) * ceil_div(CIN, 16) * 64 * 8;
   const int XIMG = rup(CIN, 4) / 4 * rup(FPT * ROWS * (W + 4) * 4 + 80, 128) * 2 * (PM == 2 ? 1 : 2);
-  const int XREG = XIMG > (UPS ? CIN * (RT + 2) * W * 4 : 0) ? XIMG : CIN * (RT + 2) * W * 4;
+  const int UPB = UPS ? CIN * (rup(FPT * (RT + 2) * W, 64) + 4) * 4 : 0;
+  const int XREG = XIMG > UPB ? XIMG : UPB;
   return (IMGD + WIMG) * 2 * (PM == 2 ? 1 : 2) + XREG + (UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0);
 }
 // pixels per tile: the largest of 256 / 128 / 64 whose staging lets two
@@ -119,8 +120,8 @@ struct SBwdCfg {
   static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = ceil_div(NIX, 256);
   static constexpr int UPW = FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2);   // fused-upsample window (floats)
   // the X image's region (UPS: it later holds the tile's full-resolution dX)
-  static constexpr int XREG = XIMG * 2 * NIMG > (UPS ? CIN * (RT + 2) * W * 4 : 0) ? XIMG * 2 * NIMG
-                                                                                    : CIN * (RT + 2) * W * 4;
+  static constexpr int UPB = UPS ? CIN * (rup(FPT * (RT + 2) * W, 64) + 4) * 4 : 0;   // the dX tile's bytes
+  static constexpr int XREG = XIMG * 2 * NIMG > UPB ? XIMG * 2 * NIMG : UPB;
   static constexpr int LDS = (IMGD + WIMG) * 2 * NIMG + XREG + (UPS ? UPW * 4 : 0);
   static constexpr bool VEC4 = W % 4 == 0;
   // X prefetched a tile ahead where its registers are cheap (else loaded
@@ -136,7 +137,10 @@ struct SBwdCfg {
   static_assert(!UPS || (FPT == 1 && RT % 2 == 0 && W % 4 == 0), "fused upsample: whole even row blocks of one frame");
   // UPS: the tile's full-resolution dX rows [RTD][W] per channel (fp32) are
   // parked in the X image's region (free once the weight-gradient MFMAs ran)
-  static_assert(!UPS || CIN * RTD * W * 4 <= XREG, "fused upsample: dX tile does not fit the X region");
+  // channel pitch of that image: 4 floats past a multiple of 64 floats, so
+  // the 16 channels of one epilogue store land on distinct bank groups
+  static constexpr int UPP = rup(TPXD, 64) + 4;
+  static_assert(!UPS || CIN * UPP * 4 <= XREG, "fused upsample: dX tile does not fit the X region");
 };
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
@@ -620,46 +624,64 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
 #pragma unroll
         for (int mt = 0; mt < MW; ++mt) {
           const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
-          if (pix < TPXD) *reinterpret_cast<f32x4*>(U + ci * TPXD + pix) = accd[mt][nt] * tinv;
+          if (pix < TPXD) *reinterpret_cast<f32x4*>(U + ci * C::UPP + pix) = accd[mt][nt] * tinv;
         }
       }
       __syncthreads();
       // the 2x bilinear upsample's transpose (aten upsample_bilinear2d
       // backward, align_corners=False: source s gets outputs 2s-1 .. 2s+2
-      // with weights 1/4, 3/4, 3/4, 1/4; 1 at the clamped edges), gather form
-      // in upsample_bwd_k's order; then ReLU' of the source, accumulate
-      constexpr int HS = H / 2, WS = W / 2, NO = CIN * (RT / 2) * WS;
+      // with weights 1/4, 3/4, 3/4, 1/4; 1 at the clamped edges), in
+      // upsample_bwd_k's per-pixel order; then ReLU' of the source and the
+      // store.  Item = 4 consecutive source pixels of one row: full-resolution
+      // columns 8q-1 .. 8q+8 of 4 rows (two float4 + 2 edge values per row)
+      constexpr int HS = H / 2, WS = W / 2, WQ = WS / 4, NO = CIN * (RT / 2) * WQ;
+      static_assert(WS % 4 == 0, "4-pixel source items");
       for (int o = tid; o < NO; o += 256) {
-        const int sx = o % WS, sr = (o / WS) % (RT / 2), ci = o / (WS * (RT / 2));
+        const int q = o % WQ, sr = (o / WQ) % (RT / 2), ci = o / (WQ * (RT / 2));
         const int sy = y0 / 2 + sr;
-        float wy[4], wx[4];
+        float wy[4];
         wy[0] = sy >= 1 ? 0.25f : 0.f;
         wy[1] = sy == 0 ? 1.f : 0.75f;
         wy[2] = sy == HS - 1 ? 1.f : 0.75f;
         wy[3] = sy <= HS - 2 ? 0.25f : 0.f;
-        wx[0] = sx >= 1 ? 0.25f : 0.f;
-        wx[1] = sx == 0 ? 1.f : 0.75f;
-        wx[2] = sx == WS - 1 ? 1.f : 0.75f;
-        wx[3] = sx <= WS - 2 ? 0.25f : 0.f;
-        float acc = 0.f;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           // full row 2sy - 1 + a = tile dX row 2sr + a (row 0 = y0 - 1)
           if (wy[a] == 0.f) continue;
-          const float* rp = U + ci * TPXD + (2 * sr + a) * W;
-          float row = 0.f;
+          const float* rp = U + ci * C::UPP + (2 * sr + a) * W + 8 * q;
+          const f32x4 m0 = *reinterpret_cast<const f32x4*>(rp), m1 = *reinterpret_cast<const f32x4*>(rp + 4);
+          const float l = q > 0 ? rp[-1] : 0.f, r = q < WQ - 1 ? rp[8] : 0.f;
+          // source pixels 4q + k read columns 8q + 2k - 1 .. 8q + 2k + 2
+          const float c[10] = {l, m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3], r};
+          f32x4 row;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const int xx = 2 * sx - 1 + b;
-            if (wx[b] != 0.f) row = fmaf(wx[b], rp[xx], row);
+          for (int k = 0; k < 4; ++k) {
+            const int sx = 4 * q + k;
+            float wx[4];
+            wx[0] = sx >= 1 ? 0.25f : 0.f;
+            wx[1] = sx == 0 ? 1.f : 0.75f;
+            wx[2] = sx == WS - 1 ? 1.f : 0.75f;
+            wx[3] = sx <= WS - 2 ? 0.25f : 0.f;
+            float v = 0.f;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+              if (wx[b] != 0.f) v = fmaf(wx[b], c[2 * k + b], v);
+            row[k] = v;
           }
-          acc = fmaf(wy[a], row, acc);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[k] = fmaf(wy[a], row[k], acc[k]);
         }
         if (f0 < F) {
-          float* op = dx.frame(f0) + ((long long)ci * HS + sy) * WS + sx;
-          if (flags & 4) acc += *op;
-          if (flags & 2) acc = aux.frame(f0)[((long long)ci * HS + sy) * WS + sx] > 0.f ? acc : 0.f;
-          *op = acc;
+          const long long off = ((long long)ci * HS + sy) * WS + 4 * q;
+          float* op = dx.frame(f0) + off;
+          if (flags & 4) acc += *reinterpret_cast<const f32x4*>(op);
+          if (flags & 2) {
+            const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f0) + off);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] = m[k] > 0.f ? acc[k] : 0.f;
+          }
+          *reinterpret_cast<f32x4*>(op) = acc;
         }
       }
     } else {
@@ -789,7 +811,7 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // odd rows and 32-channel tiles spill registers in the fused form)
 // the fused-upsample layers (input = the 2x bilinear upsample of a half-
 // resolution source; the upsample's transpose folded into the data gradient)
-#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32) X(16, 16, 36)
+#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32)
 #define PAIG_BWD_SHAPES(X)                                                                  \
   X(8, 8, 32) X(8, 16, 16) X(16, 16, 16) X(16, 32, 8) X(32, 32, 8) X(32, 16, 16) X(24, 8, 32) \
   X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(32, 16, 18) X(24, 8, 36)
