@@ -86,7 +86,7 @@ def test_config1_spring_b100_seq50_matches_oracle():
     for k in OUT_KEYS:
         errs[k] = rel_err(out[k].reshape(-1), o32[k].detach().double().numpy().reshape(-1))
     for k in ("train", "extrap", "recons"):
-        errs["loss_" + k] = rel_err(np.float64(L[k]), np.float64(float(L32[k])))
+        errs["loss_" + k] = rel_err(np.float64(L[k]), np.float64(float(L32[k].detach())))
     print("config #1 outputs/losses vs fp32 oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
     over = {k: v for k, v in errs.items() if v > RTOL}
     assert not over, over
