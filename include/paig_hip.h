@@ -83,6 +83,18 @@ int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long i
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, float* pool_out,
                        long long pool_fs, const void* wprep, void* stream);
+/* paig_conv2d_fwd_pw that also writes, with the fused pool (flags & 64), one
+ * window code byte per (channel, pooled pixel) to pool_code (nullable; frame
+ * stride pool_code_fs bytes >= ceil(Cout/8)*8*(H/2)*(W/2)): bits 0-3 the
+ * ReLU' mask (> 0) of the window's pixels (y,x), (y,x+1), (y+1,x), (y+1,x+1),
+ * bits 4-5 max_pool2d's argmax among them; layout [Cout/8][H/2][W/2][Cout%8].
+ * The fused layer backward (paig_conv2d_bwd flags & 64) reads them: the max
+ * pool's backward (blocks.py:250,254) folded into the consumer's staging. */
+int paig_conv2d_fwd_pwc(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
+                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, float* pool_out,
+                        long long pool_fs, unsigned char* pool_code, long long pool_code_fs, const void* wprep,
+                        void* stream);
 /* Weight images of the split forward / dgrad kernels, once per step for n
  * convs in one launch: job i reads the layer weight w[i] and writes the
  * images for a kernel with cin[i] input / cout[i] output channels (dgrad,
@@ -116,12 +128,21 @@ int paig_conv2d_wgrad_ex(const float* x, long long x_fs, int x_grp, long long x_
  *                       partials (paig_conv2d_wgrad's layout; *nblk_out rows).
  * xmax: the forward's per-block max |x| slots (the X scale, as
  * paig_conv2d_wgrad_ex); wprep: the layer's data-gradient weight image
- * (paig_conv_wprep dg = 1; nullable).  Shapes: paig_conv2d_bwd_supported. */
+ * (paig_conv_wprep dg = 1; nullable).
+ * flags & 32 (c7 / c10, fused-upsample input): x is the half-resolution
+ *   source of the upsample, dx / aux its gradient / values: the upsample's
+ *   backward (blocks.py:260,269 Resize) is folded in.
+ * flags & 64 (c2 / c4, output max-pooled): dy receives the max pool's
+ *   backward before use -- dy * ReLU'(y) + scatter of dpool [F][Cout][H/2][W/2]
+ *   to the argmax -- from the window codes pcode (paig_conv2d_fwd_pwc) of the
+ *   forward's fused pool (replaces paig_maxpool2_bwd_relu).
+ * Shapes: paig_conv2d_bwd_supported. */
 int paig_conv2d_bwd_supported(int Cin, int Cout, int H, int W, int ks, int flags);
 int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
                     float* dx, long long dx_fs, const float* aux, long long aux_fs, const float* w, float* slab,
                     int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks, int flags,
-                    const float* xmax, int xmax_n, const void* wprep, void* stream);
+                    const float* xmax, int xmax_n, const float* dpool, long long dpool_fs,
+                    const unsigned char* pcode, long long pcode_fs, const void* wprep, void* stream);
 
 /* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,

@@ -40,7 +40,9 @@ SIGNATURES = {
     "paig_conv2d_wgrad_ex": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
     "paig_conv2d_bwd_supported": (I, [I, I, I, I, I, I]),
-    "paig_conv2d_bwd": (I, [P, LL, I, LL, P, LL, P, LL, P, LL, P, P, I, P, I, I, I, I, I, I, I, P, I, P, P]),
+    "paig_conv2d_bwd": (I, [P, LL, I, LL, P, LL, P, LL, P, LL, P, P, I, P, I, I, I, I, I, I, I, P, I, P, LL, P, LL,
+                            P, P]),
+    "paig_conv2d_fwd_pwc": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P, LL, P, LL, P, P]),
     "paig_gather_u8_f32": (I, [P, P, P, I, LL, P]),
     "paig_velmlp_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "paig_velmlp_vfn_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P]),

@@ -57,6 +57,21 @@ struct FViewW {
   __device__ __forceinline__ float* frame(int f) const { return p + (long long)f * fs; }
 };
 
+// The fused 2x2 max pool's outputs of a forward conv (flags & 64): the pooled
+// frames and, optionally, one window code byte per (channel, pooled pixel):
+// bits 0-3 the ReLU' mask (value > 0) of the window's pixels (y, x),
+// (y, x+1), (y+1, x), (y+1, x+1); bits 4-5 the argmax among them in aten's
+// max_pool2d scan order.  Code layout per frame (code_fs bytes):
+// [channel / 8][H/2][W/2][channel % 8] -- a consumer staging 8 channels of one
+// window reads one 8-byte word.
+struct PoolOut {
+  float* p;
+  long long fs;
+  unsigned char* code;
+  long long code_fs;
+  __device__ __forceinline__ float* frame(int f) const { return p + (long long)f * fs; }
+};
+
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -261,13 +276,15 @@ struct XMax {
   int n;
 };
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr, FViewW pout = FViewW{nullptr, 0});
+                       int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr,
+                       PoolOut pout = PoolOut{nullptr, 0, nullptr, 0});
 int paig_conv_mfma_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H,
                          int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
 // Split-precision 16-bit MFMA convolutions (conv_split.hip), selected by
 // flags & 128 (f16x3 forward / bf16x3 dgrad and wgrad) or flags & 256 (bf16).
 int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
-                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr, FViewW pout = FViewW{nullptr, 0});
+                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr,
+                        PoolOut pout = PoolOut{nullptr, 0, nullptr, 0});
 int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout,
                           int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
 int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags);

@@ -380,7 +380,20 @@ int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long i
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, float* pool_out,
                        long long pool_fs, const void* wprep, void* stream) {
+  return paig_conv2d_fwd_pwc(in, in_fs, in_grp, in_gs, out, out_fs, aux, aux_fs, w, bias, F, Cin, Cout, H, W, ks, flags,
+                             xmax, xmax_n, pool_out, pool_fs, nullptr, 0, wprep, stream);
+}
+
+int paig_conv2d_fwd_pwc(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
+                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
+                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, float* pool_out,
+                        long long pool_fs, unsigned char* pool_code, long long pool_code_fs, const void* wprep,
+                        void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (pool_code && !(flags & 64)) {
+    paig_set_error("paig_conv2d_fwd_pwc: window codes need the fused pool (flags & 64)");
+    return PAIG_E_SHAPE;
+  }
   FView vin{in, in_fs, in_gs, in_grp};
   FViewW vout{out, out_fs};
   FView vaux{aux, aux_fs, 0, 0};
@@ -394,7 +407,7 @@ int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long i
   }
   if (!(flags & 16) &&
       paig_conv_mfma_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc, XMax{xmax, xmax_n}, wprep,
-                         FViewW{pool_out, pool_fs}))
+                         PoolOut{pool_out, pool_fs, pool_code, pool_code_fs}))
     return rc;
   if (flags & 32) {
     paig_set_error("paig_conv2d_fwd: fused-upsample input has no instantiation for Cin=%d Cout=%d H=%d", Cin, Cout, H);

@@ -64,8 +64,8 @@ constexpr int sbwd_tpx(int CIN, int COUT, int H, int W, bool UPS, int PM) {
 
 // waves per SIMD (= blocks per CU) each shape compiles for without spilling
 // (measured: -Rpass-analysis=kernel-resource-usage at 2 / 3 / 4)
-constexpr int sbwd_minw(int CIN, int COUT, int H, int PM) {
-  if (CIN == 8 && COUT == 8 && H == 32) return 4;
+constexpr int sbwd_minw(int CIN, int COUT, int H, int PM, bool PF) {
+  if (CIN == 8 && COUT == 8 && H == 32) return PF ? 3 : 4;
   if (PM == 2 && CIN == 8 && COUT == 16 && H == 16) return 3;
   if (PM == 2 && CIN == 24 && COUT == 8 && H == 32) return 3;
   if (CIN == 8 && COUT == 8 && H == 36) return 3;
@@ -77,7 +77,7 @@ constexpr int sbwd_minw(int CIN, int COUT, int H, int PM) {
 // 4 waves split the weight-gradient N-tiles (each wave owns every 4th one
 // over all pixels: no cross-wave reduction); the data gradient's M-tiles of
 // 16 pixels are split over the waves as in the dgrad kernel
-template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM, bool PF = false>
 struct SBwdCfg {
   static constexpr int KK = KS * KS, PADL = KS / 2;
   static constexpr int NIMG = PM == 2 ? 1 : 2;
@@ -130,11 +130,14 @@ struct SBwdCfg {
   // blocks per CU the kernel is compiled for (__launch_bounds__): the most
   // that compile without register spills (sbwd_minw), within the LDS
   static constexpr int LDSB = LDS_MAX / (LDS > (NLD * 256 * 8 + 256) * 4 ? LDS : (NLD * 256 * 8 + 256) * 4);
-  static constexpr int MW0 = PAIG_BWD_MINW > 0 ? PAIG_BWD_MINW : sbwd_minw(CIN, COUT, H, PM);
+  static constexpr int MW0 = PAIG_BWD_MINW > 0 ? PAIG_BWD_MINW : sbwd_minw(CIN, COUT, H, PM, PF);
   static constexpr int MINW = MW0 < LDSB ? MW0 : LDSB;
   static_assert(H % RT == 0, "RT divides H");
   static_assert(KS == 3, "3x3 layers (the 1x1 heads are fused elsewhere)");
   static_assert(!UPS || (FPT == 1 && RT % 2 == 0 && W % 4 == 0), "fused upsample: whole even row blocks of one frame");
+  // PF: the 2x2 max pool of this layer's output folded into the dY staging
+  // (a staging unit's pixel pair is one pooling window's columns)
+  static_assert(!PF || (!UPS && UPX == 2 && COUT % 8 == 0 && H % 2 == 0), "pool fold: even widths, 8-channel chunks");
   // UPS: the tile's full-resolution dX rows [RTD][W] per channel (fp32) are
   // parked in the X image's region (free once the weight-gradient MFMAs ran)
   // channel pitch of that image: 4 floats past a multiple of 64 floats, so
@@ -143,11 +146,12 @@ struct SBwdCfg {
   static_assert(!UPS || CIN * UPP * 4 <= XREG, "fused upsample: dX tile does not fit the X region");
 };
 
-template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
-__global__ void __launch_bounds__(256, (SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>::MINW))
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM, bool PF>
+__global__ void __launch_bounds__(256, (SBwdCfg<CIN, COUT, H, W, KS, UPS, PM, PF>::MINW))
 conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restrict__ w, int flags,
-                 float* __restrict__ slab, int F, int ntiles, XMax xm, const s16x8* __restrict__ wp) {
-  using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
+                 float* __restrict__ slab, int F, int ntiles, XMax xm, const s16x8* __restrict__ wp, FView dpool,
+                 const unsigned char* __restrict__ pcode, long long pcode_fs) {
+  using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM, PF>;
   constexpr int KK = C::KK, PADL = C::PADL, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, TPXV = C::TPXV;
   constexpr int EXT = C::EXT, RTD = C::RTD, ROWSD = C::ROWSD, TPXD = C::TPXD;
   constexpr int CCD = C::CCD, PSD = C::PSD, RPD = C::RPD, KC = C::KC, NS = C::NS, NTD = C::NTD, MW = C::MW;
@@ -320,6 +324,11 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   // prefetched a tile ahead; X unit i = (fi, r, quad cq, xp)
   float2 pd[NLD][8];
   float2 px[C::XPIPE ? NLX : 1][4];
+  // PF: the pooled gradient of each unit's window (8 channels) and the 8
+  // window codes (ReLU' bits + argmax, written by the forward's fused pool)
+  float dpv[PF ? NLD : 1][8];
+  uint2 pcv[PF ? NLD : 1];
+  constexpr int HP = H / 2, WP = W / 2;
   using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
   UP up;
   auto load_d = [&](int t) {
@@ -338,6 +347,37 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       for (int c = 0; c < 8; ++c) {
         const float* q = COUT % 8 == 0 || cc * 8 + c < COUT ? base + c * (int)HW : paig_zeros;
         pd[l][c] = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
+      }
+      if constexpr (PF) {
+        const int pw = (gy >> 1) * WP + (xp >> 1);
+        const float* pb = ok ? dpool.frame(f0) + fi * (int)dpool.fs + cc * 8 * (HP * WP) + pw : paig_zero_planes;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) dpv[l][c] = pb[c * (HP * WP)];
+        const unsigned char* cb = ok ? pcode + (long long)(f0 + fi) * pcode_fs + ((long long)cc * HP * WP + pw) * 8
+                                     : reinterpret_cast<const unsigned char*>(paig_zeros);
+        pcv[l] = *reinterpret_cast<const uint2*>(cb);
+      }
+    }
+  };
+  // PF: the max pool's backward on the prefetched dY of tile t (before its
+  // max and staging): dY = ReLU'(y) * (dY + [pixel is the window's argmax] *
+  // d pooled) -- aten max_pool2d backward + the ReLU' of this layer's output,
+  // in maxpool_bwd_relu's arithmetic order
+  auto fold = [&](int t) {
+    const int y0 = (t % NRB) * RT;
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int i = tid + l * 256;
+      const int r = (i / W2) % ROWSD;
+      const int pr = ((y0 + r - PADL - EXT) & 1) * 2;   // window row of this unit: bits pr, pr + 1
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const unsigned b = ((c < 4 ? pcv[l].x : pcv[l].y) >> (8 * (c & 3))) & 255u;
+        const int am = (int)(b >> 4) & 3;
+        const float vx = pd[l][c].x + (am == pr ? dpv[l][c] : 0.f);
+        const float vy = pd[l][c].y + (am == pr + 1 ? dpv[l][c] : 0.f);
+        pd[l][c].x = (b >> pr) & 1u ? vx : 0.f;
+        pd[l][c].y = (b >> (pr + 1)) & 1u ? vy : 0.f;
       }
     }
   };
@@ -551,6 +591,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   for (; lt < ntiles; lt += gridDim.x) {
     const int tile = xcd_tile(lt, ntiles);
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
+    if constexpr (PF) fold(tile);
     if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) tile_max();
     __syncthreads();   // the previous tile's fragment reads are done
     commit(tile);
@@ -778,15 +819,17 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   if constexpr (PM == 0) f16_range_note(rmax);
 }
 
-template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM, bool PF = false>
 static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, int flags, float* slab, int nblk_max,
-                       int* nblk_out, int F, hipStream_t st, XMax xm, const void* wp) {
-  using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
+                       int* nblk_out, int F, hipStream_t st, XMax xm, const void* wp,
+                       FView dpool = FView{nullptr, 0, 0, 0}, const unsigned char* pcode = nullptr,
+                       long long pcode_fs = 0) {
+  using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM, PF>;
   constexpr int RED = (C::NLD * 256 * 8 + 256) * 4;   // the bias reduction's LDS
   constexpr int LDS = C::LDS > RED ? C::LDS : RED;
   static_assert(LDS <= LDS_MAX, "fused backward: staging exceeds the LDS");
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
-  auto k = conv_bwd_split_k<CIN, COUT, H, W, KS, UPS, PM>;
+  auto k = conv_bwd_split_k<CIN, COUT, H, W, KS, UPS, PM, PF>;
   static int resident = 0;
   if (!resident) {
     if (LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -799,8 +842,10 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
   PAIG_REQUIRE(!xm.p || (xm.n % 4 == 0 && (reinterpret_cast<uintptr_t>(xm.p) & 15) == 0),
                "conv split bwd: xmax needs 16-byte alignment and a multiple of 4 slots (%d)", xm.n);
   PAIG_REQUIRE(!(flags & 2) || aux.p, "conv split bwd: ReLU' mask (flags & 2) without aux");
+  PAIG_REQUIRE(!PF || (dpool.p && pcode && (reinterpret_cast<uintptr_t>(pcode) & 7) == 0 && pcode_fs % 8 == 0),
+               "conv split bwd: pool fold needs the pooled gradient and 8-byte aligned window codes");
   hipLaunchKernelGGL(k, dim3(nb), dim3(256), LDS, st, x, dy, dx, aux, w, flags, slab, F, ntiles, xm,
-                     PM == 0 ? static_cast<const s16x8*>(wp) : nullptr);
+                     PM == 0 ? static_cast<const s16x8*>(wp) : nullptr, dpool, pcode, pcode_fs);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -812,6 +857,9 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // the fused-upsample layers (input = the 2x bilinear upsample of a half-
 // resolution source; the upsample's transpose folded into the data gradient)
 #define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32)
+// the layers whose output feeds a 2x2 max pool fused into their forward
+// (c2, c4): the pool's backward folded into the dY staging (flags & 64)
+#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16)
 #define PAIG_BWD_SHAPES(X)                                                                  \
   X(8, 8, 32) X(8, 16, 16) X(16, 16, 16) X(16, 32, 8) X(32, 32, 8) X(32, 16, 16) X(24, 8, 32) \
   X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(32, 16, 18) X(24, 8, 36)
@@ -824,6 +872,11 @@ int paig_conv2d_bwd_supported(int Cin, int Cout, int H, int W, int ks, int flags
   if (H != W || ks != 3 || !(flags & (128 | 256))) return 0;
 #define PAIG_CASE(CI, CO, HH) \
   if (Cin == CI && Cout == CO && H == HH) return 1;
+  if (flags & 64) {
+    if (flags & 32) return 0;
+    PAIG_BWD_POOL_SHAPES(PAIG_CASE)
+    return 0;
+  }
   if (flags & 32) {
     PAIG_BWD_UP_SHAPES(PAIG_CASE)
     return 0;
@@ -836,7 +889,8 @@ int paig_conv2d_bwd_supported(int Cin, int Cout, int H, int W, int ks, int flags
 int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
                     float* dx, long long dx_fs, const float* aux, long long aux_fs, const float* w, float* slab,
                     int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks, int flags,
-                    const float* xmax, int xmax_n, const void* wprep, void* stream) {
+                    const float* xmax, int xmax_n, const float* dpool, long long dpool_fs,
+                    const unsigned char* pcode, long long pcode_fs, const void* wprep, void* stream) {
   *nblk_out = 0;
   if (F <= 0) return 0;
   PAIG_REQUIRE(paig_conv2d_bwd_supported(Cin, Cout, H, W, ks, flags),
@@ -850,6 +904,18 @@ int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, c
   XMax xm{const_cast<float*>(xmax), xmax_n};
   const bool b16 = (flags & 256) != 0;
   const int fl = flags & 6;
+  if (flags & 64) {
+    const FView vp{dpool, dpool_fs, 0, 0};
+#define PAIG_CASE(CI, CO, HH)                                                                                     \
+  if (Cin == CI && Cout == CO && H == HH)                                                                         \
+    return b16 ? sbwd_launch<CI, CO, HH, HH, 3, false, 2, true>(vx, vd, vdx, va, w, fl, slab, nblk_max, nblk_out,  \
+                                                                 F, st, xm, wprep, vp, pcode, pcode_fs)            \
+               : sbwd_launch<CI, CO, HH, HH, 3, false, 0, true>(vx, vd, vdx, va, w, fl, slab, nblk_max, nblk_out,  \
+                                                                 F, st, xm, wprep, vp, pcode, pcode_fs);
+    PAIG_BWD_POOL_SHAPES(PAIG_CASE)
+#undef PAIG_CASE
+    return PAIG_E_UNSUPPORTED;
+  }
   if (flags & 32) {
 #define PAIG_CASE(CI, CO, HH)                                                                                     \
   if (Cin == CI && Cout == CO && H == HH)                                                                         \

@@ -685,7 +685,7 @@ static int wgrad_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_
 // flags: 1 relu, 2 mask(aux>0), 4 accumulate, 8 dgrad, 32 input = 2x upsample of (H/2 x W/2)
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp,
-                       FViewW pout) {
+                       PoolOut pout) {
   if ((flags & (128 | 256)) &&
       paig_conv_split_fwd(in, out, aux, w, b, F, Cin, Cout, H, W, ks, flags, st, rc, xm, wp, pout))
     return 1;

@@ -148,10 +148,21 @@ __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
   return m;
 }
 
+// the window code byte of PoolOut: ReLU' bits of (a, b, c, d) = (y, x),
+// (y, x+1), (y+1, x), (y+1, x+1) and the argmax in pool4's scan order
+__device__ __forceinline__ unsigned char pool_code(float a, float b, float c, float d) {
+  float m = a;
+  int k = 0;
+  if (b > m || b != b) { m = b; k = 1; }
+  if (c > m || c != c) { m = c; k = 2; }
+  if (d > m || d != d) { m = d; k = 3; }
+  return (unsigned char)((a > 0.f ? 1 : 0) | (b > 0.f ? 2 : 0) | (c > 0.f ? 4 : 0) | (d > 0.f ? 8 : 0) | (k << 4));
+}
+
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false>
 __global__ void __launch_bounds__(256, 2)
 conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
-                 int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp, FViewW pout) {
+                 int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp, PoolOut pout) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
   constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP;
@@ -541,6 +552,12 @@ if constexpr (W % 4 == 0) {
             const f32x4 a = vv[mt], b = vv[mt + C::PO];
             const float2 o = make_float2(pool4(a[0], a[1], b[0], b[1]), pool4(a[2], a[3], b[2], b[3]));
             *reinterpret_cast<float2*>(pout.frame(f) + (long long)co * (HW / 4) + (y / 2) * (W / 2) + x / 2) = o;
+            if (pout.code) {   // the two windows' codes (PoolOut): ReLU' bits + argmax
+              unsigned char* cp = pout.code + (long long)f * pout.code_fs +
+                                  (((long long)(co >> 3) * (H / 2) + y / 2) * (W / 2) + x / 2) * 8 + (co & 7);
+              cp[0] = pool_code(a[0], a[1], b[0], b[1]);
+              cp[8] = pool_code(a[2], a[3], b[2], b[3]);
+            }
           }
         }
       }
@@ -1131,7 +1148,7 @@ if constexpr (W % 4 == 0) {
 
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
-                       hipStream_t st, XMax xm, const void* wp, FViewW pout) {
+                       hipStream_t st, XMax xm, const void* wp, PoolOut pout) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int LDS = C::LDS + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
@@ -1224,7 +1241,7 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
 // bf16 hi only.  Returns 1 if the shape is instantiated here (rc in *rc).
 int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
                         int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp,
-                        FViewW pout) {
+                        PoolOut pout) {
   const bool dg = (flags & 8) != 0, up = (flags & 32) != 0, b16 = (flags & 256) != 0;
   const int fl = flags & (7 | 64);
   if (H != W || !(flags & (128 | 256))) return 0;

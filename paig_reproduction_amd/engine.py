@@ -644,20 +644,29 @@ class Engine:
                 # fused into the conv's epilogue where the split kernel has it
                 pool_v = (None, 0)
                 nxt = ops[i + 1] if i + 1 < len(ops) else None
+                pcode = (None, 0)
                 if (nxt is not None and nxt["op"] == "pool" and nxt["src"] == op["dst"] and not xfl and cm
                         and L.paig_conv2d_mfma_supported(0, op["src"][2], op["dst"][2], Hl, Hl, op["ks"], cm | 64)):
                     pv, _ = view(nxt["dst"])
                     pool_v = (pv[0], pv[1])
                     pooled.add(i + 1)
+                    if self._fused_bwd(op["src"][2], op["dst"][2], Hl, op["ks"], cm | 64):
+                        # the pool windows' codes (ReLU' bits + argmax): the
+                        # backward folds the pool into this layer's dY staging
+                        cfs = -(-op["dst"][2] // 8) * 8 * (Hl // 2) ** 2
+                        cb = torch.empty(F * cfs, dtype=torch.uint8, device=dev)
+                        S.setdefault("pcode", {})[i + 1] = (cb, cfs)
+                        pcode = (cb.data_ptr(), cfs)
                 W_ = self.p(lay.prefix + op["name"] + ".weight")
                 b_ = self.p(lay.prefix + op["name"] + ".bias")
                 fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
                 nbytes = 4 * F * (op["src"][2] * (Hl // (2 if xfl else 1)) ** 2 + op["dst"][2] * Hl * Hl)
                 with self._p("conv_fwd:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_fwd_pw(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
-                                         op["src"][2], op["dst"][2], Hl, Hl, op["ks"],
-                                         (1 if op["relu"] else 0) | xfl | cm | (64 if pool_v[0] else 0),
-                                         S["xmax"](i), XMAX_SLOTS, pool_v[0], pool_v[1], wp.get((i, 0)), st)
+                    L.paig_conv2d_fwd_pwc(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
+                                          op["src"][2], op["dst"][2], Hl, Hl, op["ks"],
+                                          (1 if op["relu"] else 0) | xfl | cm | (64 if pool_v[0] else 0),
+                                          S["xmax"](i), XMAX_SLOTS, pool_v[0], pool_v[1], pcode[0], pcode[1],
+                                          wp.get((i, 0)), st)
             elif op["op"] == "pool":
                 sv, slvl = view(op["src"])
                 Hl = H // slvl
@@ -1030,6 +1039,8 @@ class Engine:
             if i in folded_ups:
                 continue
             op = lay.ops[i]
+            if op["op"] == "pool" and i in S.get("pcode", {}):
+                continue   # folded into the pooled conv's backward (its dY staging), below
             fin = lay.fin[i]
             relu_fin = [r for r, relu in fin if relu]
             src, dst = op["src"], op["dst"]
@@ -1067,7 +1078,7 @@ class Engine:
                         L.paig_conv2d_bwd(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], dxv[0], dxv[1], aux[0], aux[1],
                                           ptr(self.p(lay.prefix + op["name"] + ".weight")), ptr(slab), nblk_max,
                                           ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, flags, S["xmax"](i), XMAX_SLOTS,
-                                          S["wprep"].get((i, 1)), st)
+                                          None, 0, None, 0, S["wprep"].get((i, 1)), st)
                     slabs.append((slab, nb.value, n_w + cout, gw))
                     mark(usrc)
                     folded_ups.add(ui)
@@ -1086,11 +1097,21 @@ class Engine:
                         flags |= 2
                     # algorithmic bytes: X and dY read, dX written (+ read when accumulating)
                     nbytes = 4 * F * Hl * Hl * (cin + cout + cin * (2 if mode == "accum" else 1))
+                    # the max pool of this output (next op), folded: its
+                    # gradient and window codes join the dY staging
+                    fold = (None, 0, None, 0)
+                    pj = i + 1
+                    if pj in S.get("pcode", {}):
+                        pdv, _ = dview(lay.ops[pj]["dst"])
+                        cb, cfs = S["pcode"][pj]
+                        fold = (pdv[0], pdv[1], cb.data_ptr(), cfs)
+                        flags |= 64
+                        nbytes += F * (4 * cout + cout) * (Hl // 2) ** 2   # pooled gradient + codes
                     with self._p("conv_bwd:" + op["name"], 2 * fl, nbytes):
                         L.paig_conv2d_bwd(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], dxv[0], dxv[1], aux[0], aux[1],
                                           ptr(self.p(lay.prefix + op["name"] + ".weight")), ptr(slab), nblk_max,
-                                          ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, cm | (flags & 6),
-                                          S["xmax"](i), XMAX_SLOTS, S["wprep"].get((i, 1)), st)
+                                          ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, cm | (flags & 70),
+                                          S["xmax"](i), XMAX_SLOTS, *fold, S["wprep"].get((i, 1)), st)
                     slabs.append((slab, nb.value, n_w + cout, gw))
                     mark(src)
                     continue

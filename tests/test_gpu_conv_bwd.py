@@ -56,7 +56,7 @@ def _fused(x, w, dy, dx0, aux, mode, xmax, wprep=None):
     nb = ctypes.c_int(0)
     L().paig_conv2d_bwd(p(x), cin * hw * hw, 0, 0, p(dy), cout * hw * hw, p(dx), cin * hw * hw, p(aux),
                         cin * hw * hw, p(w), p(slab), nmax, ctypes.byref(nb), F_, cin, cout, hw, hw, 3, flags,
-                        p(xmax), XMAX_SLOTS if xmax is not None else 0, p(wprep), st())
+                        p(xmax), XMAX_SLOTS if xmax is not None else 0, None, 0, None, 0, p(wprep), st())
     g = torch.empty(cout * cin * 9 + cout, device=DEV)
     L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
     torch.cuda.synchronize()
@@ -211,7 +211,8 @@ def test_fused_backward_upsample_input(cin, cout, hw, mode):
         nb = ctypes.c_int(0)
         L().paig_conv2d_bwd(p(xs), cin * hs * hs, 0, 0, p(dy), cout * hw * hw, p(dx), cin * hs * hs, p(xs),
                             cin * hs * hs, p(w), p(slab), nmax, ctypes.byref(nb), F_, cin, cout, hw, hw, 3,
-                            mode | 32 | 2, p(xmax), XMAX_SLOTS if xmax is not None else 0, None, st())
+                            mode | 32 | 2, p(xmax), XMAX_SLOTS if xmax is not None else 0, None, 0, None, 0, None,
+                            st())
         g = torch.empty(cout * cin * 9 + cout, device=DEV)
         L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
         torch.cuda.synchronize()
@@ -220,3 +221,57 @@ def test_fused_backward_upsample_input(cin, cout, hw, mode):
         assert rel_err(dx, rdx) <= tol, ("dx", F_)
         assert rel_err(g[:n].view_as(w), wr.grad) <= tol, ("dw", F_)
         assert rel_err(g[n:], dy.double().cpu().sum((0, 2, 3))) <= 1e-5, ("db", F_)
+
+
+@pytest.mark.parametrize("mode", [128, 256])
+@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16)])
+def test_fused_backward_pool_fold(cin, cout, hw, mode):
+    """c2 / c4 (blocks.py:249-250, 253-254): the layer's ReLU'd output feeds
+    the skip concat AND a 2x2 max pool.  The forward's fused pool writes one
+    code byte per window (ReLU' bits + argmax, paig_conv2d_fwd_pwc); the
+    layer backward folds the pool's backward into its dY staging
+    (dY = ReLU'(y) (dY_skip + scatter_argmax(d pooled))).  Reference: float64
+    autograd through conv2d + relu + max_pool2d."""
+    assert L().paig_conv2d_bwd_supported(cin, cout, hw, hw, 3, mode | 64) == 1
+    tol = TOL[mode]
+    hp = hw // 2
+    for F_ in (4, 1):
+        torch.manual_seed(cin + cout + hw + F_ + mode)
+        x = torch.relu(torch.randn(F_, cin, hw, hw, device=DEV))
+        w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.2
+        b = torch.randn(cout, device=DEV) * 0.1
+        gy = torch.randn(F_, cout, hw, hw, device=DEV)     # the skip path's gradient (c11's dgrad)
+        gp = torch.randn(F_, cout, hp, hp, device=DEV)     # the pooled output's gradient (c3's dgrad)
+        xr = x.double().cpu().requires_grad_(True)
+        wr = w.double().cpu().requires_grad_(True)
+        br = b.double().cpu().requires_grad_(True)
+        yr = torch.relu(F.conv2d(xr, wr, br, padding="same"))
+        pr = F.max_pool2d(yr, 2)
+        ((yr * gy.double().cpu()).sum() + (pr * gp.double().cpu()).sum()).backward()
+        # GPU forward: conv + ReLU + fused pool with window codes (+ the X maxima)
+        y = torch.empty(F_, cout, hw, hw, device=DEV)
+        pool = torch.empty(F_, cout, hp, hp, device=DEV)
+        cfs = -(-cout // 8) * 8 * hp * hp
+        code = torch.empty(F_ * cfs, dtype=torch.uint8, device=DEV)
+        xmax = torch.zeros(XMAX_SLOTS, device=DEV)
+        L().paig_conv2d_fwd_pwc(p(x), cin * hw * hw, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout,
+                                hw, hw, 3, 1 | 64 | mode, p(xmax) if mode == 128 else None,
+                                XMAX_SLOTS if mode == 128 else 0, p(pool), cout * hp * hp, p(code), cfs, None, st())
+        torch.cuda.synchronize()
+        assert rel_err(pool, pr.detach()) <= TOL[mode]
+        dx = torch.full((F_, cin, hw, hw), float("nan"), device=DEV)
+        nmax = 512
+        slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+        nb = ctypes.c_int(0)
+        L().paig_conv2d_bwd(p(x), cin * hw * hw, 0, 0, p(gy), cout * hw * hw, p(dx), cin * hw * hw, p(x),
+                            cin * hw * hw, p(w), p(slab), nmax, ctypes.byref(nb), F_, cin, cout, hw, hw, 3,
+                            mode | 64 | 2, p(xmax) if mode == 128 else None, XMAX_SLOTS if mode == 128 else 0,
+                            p(gp), cout * hp * hp, p(code), cfs, None, st())
+        g = torch.empty(cout * cin * 9 + cout, device=DEV)
+        L().paig_slab_reduce(p(slab), nb.value, g.numel(), g.numel(), p(g), 0, st())
+        torch.cuda.synchronize()
+        n = cout * cin * 9
+        assert torch.isfinite(dx).all()
+        assert rel_err(dx, xr.grad * (x.cpu() > 0)) <= tol, ("dx", F_)
+        assert rel_err(g[:n].view_as(w), wr.grad) <= tol, ("dw", F_)
+        assert rel_err(g[n:], br.grad) <= (1e-5 if mode == 128 else tol), ("db", F_)
