@@ -57,8 +57,12 @@ constexpr int sbwd_lds(int CIN, int COUT, int H, int W, bool UPS, int PM, int tp
 // blocks share a CU (the 8 x 8 / 9 x 9 levels' multi-frame tiles and the
 // 32-channel weight images would not)
 constexpr int sbwd_tpx(int CIN, int COUT, int H, int W, bool UPS, int PM) {
-  for (int t = 256; t >= 64; t /= 2)
-    if (sbwd_lds(CIN, COUT, H, W, UPS, PM, t) <= LDS_MAX / 2) return t;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int t = 256; t >= 64; t /= 2) {
+      const int rt = H * W <= t ? H : rows_fit(H, W, t);
+      if (UPS && (rt % 2 != 0 || H * W < t)) continue;   // the upsample fold: whole even row blocks of one frame
+      if (sbwd_lds(CIN, COUT, H, W, UPS, PM, t) <= (pass == 0 ? LDS_MAX / 2 : LDS_MAX)) return t;
+    }
   return 64;
 }
 
@@ -856,13 +860,14 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // odd rows and 32-channel tiles spill registers in the fused form)
 // the fused-upsample layers (input = the 2x bilinear upsample of a half-
 // resolution source; the upsample's transpose folded into the data gradient)
-#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32)
+#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32) X(32, 16, 64)
 // the layers whose output feeds a 2x2 max pool fused into their forward
 // (c2, c4): the pool's backward folded into the dY staging (flags & 64)
-#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16)
+#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16) X(16, 16, 64) X(32, 32, 32)
 #define PAIG_BWD_SHAPES(X)                                                                  \
   X(8, 8, 32) X(8, 16, 16) X(16, 16, 16) X(16, 32, 8) X(32, 32, 8) X(32, 16, 16) X(24, 8, 32) \
-  X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(32, 16, 18) X(24, 8, 36)
+  X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(32, 16, 18) X(24, 8, 36)                            \
+  X(16, 16, 64) X(16, 32, 32) X(32, 32, 32) X(48, 16, 64)
 
 }  // namespace
 

@@ -22,6 +22,7 @@ DEV = "cuda:0"
 XMAX_SLOTS = 2048
 TOL = {128: 1e-5, 256: 8e-3}
 SHAPES = [(8, 8, 32), (8, 16, 16), (16, 16, 16), (16, 32, 8), (32, 32, 8), (32, 16, 16), (24, 8, 32),
+          (16, 16, 64), (16, 32, 32), (32, 32, 32), (48, 16, 64),
           (8, 8, 36), (8, 16, 18), (16, 16, 18), (32, 16, 18), (24, 8, 36)]
 
 
@@ -178,7 +179,7 @@ def test_fused_backward_matches_separate_kernels(cin, cout, hw):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32)])
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (32, 16, 64)])
 def test_fused_backward_upsample_input(cin, cout, hw, mode):
     """c7 / c10 (blocks.py:289-290,298-299): the conv input is the 2x bilinear
     upsample (torchvision Resize) of a ReLU'd half-resolution source.  One
@@ -224,7 +225,7 @@ def test_fused_backward_upsample_input(cin, cout, hw, mode):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16)])
+@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16), (16, 16, 64), (32, 32, 32)])
 def test_fused_backward_pool_fold(cin, cout, hw, mode):
     """c2 / c4 (blocks.py:249-250, 253-254): the layer's ReLU'd output feeds
     the skip concat AND a 2x2 max pool.  The forward's fused pool writes one
