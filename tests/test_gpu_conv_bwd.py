@@ -22,7 +22,7 @@ DEV = "cuda:0"
 XMAX_SLOTS = 2048
 TOL = {128: 1e-5, 256: 8e-3}
 SHAPES = [(8, 8, 32), (8, 16, 16), (16, 16, 16), (16, 32, 8), (32, 32, 8), (32, 16, 16), (24, 8, 32),
-          (16, 16, 64), (16, 32, 32), (32, 32, 32), (48, 16, 64),
+          (16, 16, 64), (16, 32, 32),
           (8, 8, 36), (8, 16, 18), (16, 16, 18), (32, 16, 18), (24, 8, 36)]
 
 
@@ -179,7 +179,7 @@ def test_fused_backward_matches_separate_kernels(cin, cout, hw):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (32, 16, 64)])
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (32, 32, 64)])
 def test_fused_backward_upsample_input(cin, cout, hw, mode):
     """c7 / c10 (blocks.py:289-290,298-299): the conv input is the 2x bilinear
     upsample (torchvision Resize) of a ReLU'd half-resolution source.  One
