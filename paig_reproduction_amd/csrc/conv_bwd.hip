@@ -860,12 +860,15 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // odd rows and 32-channel tiles spill registers in the fused form)
 // the fused-upsample layers (input = the 2x bilinear upsample of a half-
 // resolution source; the upsample's transpose folded into the data gradient)
-#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32) X(32, 32, 64)
+#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32)
 // the layers whose output feeds a 2x2 max pool fused into their forward
-// (c2, c4 of both U-Nets): the pool's backward folded into the dY staging
-// (flags & 64).  The UNet's (mnist) 32 x 32 x 32 layer is fused only with
-// its pool (c4; measured: alone (c14) the fused form is 14% slower)
-#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16) X(16, 16, 64) X(32, 32, 32)
+// (c2, c4 of the ShallowUNet): the pool's backward folded into the dY
+// staging (flags & 64).  The UNet (mnist) keeps its standalone pools (its
+// forward convs have no fused pool at 64 / 32 wide), and of its layers only
+// those that measured faster fused are listed (c2, c17: 16 -> 16 at 64 x 64;
+// c3: 16 -> 32 at 32 x 32); its wider or 1-block-per-CU shapes (c4 / c14,
+// c15's upsample, c16) measured 14-40% slower than the separate kernels
+#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16)
 #define PAIG_BWD_SHAPES(X)                                                                  \
   X(8, 8, 32) X(8, 16, 16) X(16, 16, 16) X(16, 32, 8) X(32, 32, 8) X(32, 16, 16) X(24, 8, 32) \
   X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(32, 16, 18) X(24, 8, 36)                            \

@@ -179,7 +179,7 @@ def test_fused_backward_matches_separate_kernels(cin, cout, hw):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (32, 32, 64)])
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32)])
 def test_fused_backward_upsample_input(cin, cout, hw, mode):
     """c7 / c10 (blocks.py:289-290,298-299): the conv input is the 2x bilinear
     upsample (torchvision Resize) of a ReLU'd half-resolution source.  One
@@ -225,7 +225,7 @@ def test_fused_backward_upsample_input(cin, cout, hw, mode):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16), (16, 16, 64), (32, 32, 32)])
+@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16)])
 def test_fused_backward_pool_fold(cin, cout, hw, mode):
     """c2 / c4 (blocks.py:249-250, 253-254): the layer's ReLU'd output feeds
     the skip concat AND a 2x2 max pool.  The forward's fused pool writes one
