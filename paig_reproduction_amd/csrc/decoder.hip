@@ -22,6 +22,8 @@
 //     sum is deterministic; paig_slab_reduce finishes it.
 #include "common.h"
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 namespace {
@@ -584,7 +586,7 @@ __device__ __forceinline__ void gather_entry(float l, const double* bc, int H, i
 // sums per wave, finished by one wave each in the next iteration.  Every global load of frame it+1 (its
 // positions, its loss weight, its targets) is issued one iteration ahead,
 // so no wave waits on memory inside the loop.
-constexpr int DEC_FPB_MIN = 4, DEC_CU_MAX_BLOCKS = 256;
+constexpr int DEC_FPB_MIN = 3, DEC_CU_MAX_BLOCKS = 256;   // 3: 200 blocks for the 600 live rollout frames (16.5 -> 13.4 us; 4: 150)
 
 template <int K, int H>
 struct DecCu {
@@ -1553,8 +1555,14 @@ static int dec_live(int F, int grp, int live) {
 // frames per block of the one-CU kernel: >= DEC_FPB_MIN (the slab row of a
 // block is ~1.7 frames of targets), at most DEC_CU_MAX_BLOCKS blocks
 static int dec_cu_fpb(int NL) {
+  static int fmin = -1;
+  if (fmin < 0) {   // A/B: PAIG_DEC_FPB_MIN
+    const char* e = getenv("PAIG_DEC_FPB_MIN");
+    fmin = e ? atoi(e) : DEC_FPB_MIN;
+    if (fmin < 1) fmin = 1;
+  }
   int fpb = cdiv(NL, DEC_CU_MAX_BLOCKS);
-  return fpb < DEC_FPB_MIN ? DEC_FPB_MIN : fpb;
+  return fpb < fmin ? fmin : fpb;
 }
 
 // Slab rows (= blocks) of paig_decoder_bwd over F frames grouped by grp
