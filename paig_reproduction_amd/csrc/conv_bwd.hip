@@ -35,6 +35,8 @@
 // #2).
 #include "split_common.h"
 
+#include <stdlib.h>
+
 #ifndef PAIG_BWD_MINW
 #define PAIG_BWD_MINW 0   // A/B builds: force the blocks per CU the kernels are compiled for
 #endif
@@ -841,6 +843,16 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
   }
   int nb = ntiles < nblk_max ? ntiles : nblk_max;
   if (nb > resident) nb = resident;
+  {
+    // A/B: PAIG_BWD_MIN_TPB = minimum tiles per block (fewer slab rows on
+    // the layers with few tiles)
+    static int mt = -1;
+    if (mt < 0) {
+      const char* e = getenv("PAIG_BWD_MIN_TPB");
+      mt = e ? atoi(e) : 0;
+    }
+    if (mt > 1 && nb > cdiv(ntiles, mt)) nb = cdiv(ntiles, mt);
+  }
   if (nb < 1) nb = 1;
   *nblk_out = nb;
   PAIG_REQUIRE(!xm.p || (xm.n % 4 == 0 && (reinterpret_cast<uintptr_t>(xm.p) & 15) == 0),

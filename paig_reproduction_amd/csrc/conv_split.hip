@@ -1361,7 +1361,10 @@ __device__ __forceinline__ int wprep_hdr_entries(int cout) { return (cout + 15) 
 // one block per (job, N-tile of 16 output channels, WPREP_S k-steps): the
 // 16 channel maxima (thread t: channel t % 16; every block of the tile forms
 // them, from L2), their exponents, then its k-steps' entries
-constexpr int WPREP_S = 4;
+#ifndef PAIG_WPREP_S
+#define PAIG_WPREP_S 4
+#endif
+constexpr int WPREP_S = PAIG_WPREP_S;
 __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
   int q = 0;
   while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.blk0[q + 1]) ++q;

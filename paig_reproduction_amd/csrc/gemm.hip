@@ -875,7 +875,17 @@ __global__ void __launch_bounds__(256) gemm_splitk_epilogue_v_k(int M, int N, in
 static int choose_split(int M, int N, int K) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
   int s = 1;
-  if (K < 512) return 1;   // a short K loop costs less than the split-K epilogue launch
+  if (K < 512) {
+    // a short K loop usually costs less than the split-K epilogue launch;
+    // A/B (PAIG_GEMM_SMALLK=1): halve K when the grid fills < 256 CUs.  The
+    // split then depends on K and the tile count, never on the row order.
+    static int sk = -1;
+    if (sk < 0) {
+      const char* e = getenv("PAIG_GEMM_SMALLK");
+      sk = e ? atoi(e) : 0;
+    }
+    return (sk && tiles < 256 && K >= 4 * BK) ? 2 : 1;
+  }
   while (tiles * s < 512 && cdiv(K, 2 * s) >= BK && (long long)(2 * s) * M * N <= (4ll << 20)) s *= 2;
   return s;
 }

@@ -397,8 +397,8 @@ class Engine:
     def workspace_floats(self, lay):
         K, F, B = lay.K, lay.F, lay.B
         n1 = lay.l1_in
-        need = [self.L.paig_gemm_workspace(K * F, 200, n1), self.L.paig_gemm_workspace(200, n1, K * F),
-                self.L.paig_gemm_workspace(K * F, n1, 200), self.L.paig_gemm_workspace(200, 200, K * F),
+        need = [self.L.paig_gemm_workspace(K * F, 200, n1), self.L.paig_gemm_workspace(K * F, 200, 200),
+                self.L.paig_gemm_workspace(200, n1, K * F), self.L.paig_gemm_workspace(K * F, n1, 200), self.L.paig_gemm_workspace(200, 200, K * F),
                 self.L.paig_gemm_workspace(2, 200, K * F), self.L.paig_gemm_workspace(100, 100, K * B),
                 self.L.paig_gemm_workspace(K * B, 100, 100), 1 << 16,
                 self.L.paig_psgemm_workspace(K * F, 200, n1), self.L.paig_psgemm_workspace(200, n1, K * F),
