@@ -616,7 +616,11 @@ struct DecCu {
   static constexpr int RPW = K >= 3 ? 2 : 4, NR = NW * RPW;
   // the two passes in alternating order by wave half (the K = 3 state does
   // not fit the registers twice)
-  static constexpr bool ALT = K == 2;
+  static constexpr bool ALT = K == 2 && H <= 36;
+  // G buffers: two (frame parity: pass 1 of frame it beside pass 2 of frame
+  // it-1, one barrier per frame), or one for 64 x 64 frames, whose image
+  // fills half the LDS (a second barrier per frame orders the passes)
+  static constexpr int NGB = H <= 36 ? 2 : 1;
   static_assert(NR <= 64, "one wave finishes a position gradient");
 };
 
@@ -774,7 +778,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   constexpr int h = C::h, hp = C::hp, hh = C::hh, HW = C::HW, PS = C::PS, NIT = C::NIT, GPITCH = C::GPITCH;
   constexpr int NT = C::NT, PL = C::PL, NI = C::NI, NC = C::NC, NG = C::NG, TC0 = C::TC0, TG0 = C::TG0, NR = C::NR;
   __shared__ float4 SRC[K][hp * hp];              // (template + 5, sigmoid(content) x 3), zero border
-  __shared__ float2 G[2][2][K][H * GPITCH];       // [frame parity][plane pair][object][row][slot]
+  __shared__ float2 G[C::NGB][2][K][H * GPITCH];  // [frame parity][plane pair][object][row][slot]
   __shared__ float4 AXW[2][K][2][H];              // per output column (0) / row (1): tap weights w0, w1 and
   __shared__ int AXC[2][K][2][H];                 //   their d/dcoord d0, d1; padded index of the first tap
   __shared__ int J0[3][K][2][h];                  // gather tables (3 frames in flight): first index
@@ -904,7 +908,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   #else
       if (it >= 1 && act_prev) {
   #endif
-        const int sl = (it - 1) & 1, gs = (it - 1) % 3;
+        const int sl = (it - 1) & 1, gs = (it - 1) % 3, gb = C::NGB == 1 ? 0 : sl;
         if (wv < 2 * K) {   // wave e finishes position gradient e from the NR row partials
           const double v = lane < NR ? RED[sl][wv][lane] : 0.0;
           const double tot = wave_sum_dpp_d(v);
@@ -935,8 +939,8 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
             unsigned ae[2], ao[2];
 #pragma unroll
             for (int q2 = 0; q2 < 2; ++q2) {
-              ae[q2] = (unsigned)(uintptr_t)&G[sl][q2 == 0 ? hf : 1][k][be];
-              ao[q2] = (unsigned)(uintptr_t)&G[sl][q2 == 0 ? hf : 1][k][bo];
+              ae[q2] = (unsigned)(uintptr_t)&G[gb][q2 == 0 ? hf : 1][k][be];
+              ao[q2] = (unsigned)(uintptr_t)&G[gb][q2 == 0 ? hf : 1][k][bo];
             }
             // packed fp32 accumulators: one plane pair per pf32x2
             pf32x2 acc[PL / 2];
@@ -994,7 +998,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   #else
       if (it < nf && act_cur) {
   #endif
-        const int sl = it & 1;
+        const int sl = it & 1, gb = C::NGB == 1 ? 0 : sl;
         const float w_f = 2.f * w_cur;
         const float* dof = dout.p ? dout.p + (long long)ccur.f * dout.fs : nullptr;
         double sx[K], sy[K];
@@ -1055,8 +1059,8 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
               dT = fmaf(g[c], sv[k][1 + c] - o[c], dT);
             }
             dT *= m[k];
-            G[sl][0][k][gof] = make_float2(dT, dC[0]);
-            G[sl][1][k][gof] = make_float2(dC[1], dC[2]);
+            G[gb][0][k][gof] = make_float2(dT, dC[0]);
+            G[gb][1][k][gof] = make_float2(dC[1], dC[2]);
             const float gq[4] = {dT, dC[0], dC[1], dC[2]};
             float gx = 0.f, gy = 0.f;
             if constexpr (HOLD) {
@@ -1109,6 +1113,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
     if (!C::ALT || wv < C::NW / 2) {
       pass2();
       DEC_STAMP(it, 2);
+      if constexpr (C::NGB == 1) __syncthreads();   // pass 2 of frame it-1 has read G
       pass1();
     } else {
       pass1();
@@ -1187,7 +1192,7 @@ struct DecFw {
   // apart: split by parity they are consecutive); row pitch in texels chosen
   // by a bank model of the ds_read_b128 lane groups (1.04 / 1.10 LDS cycles
   // per group against 1.41 / 1.36 for the plain image)
-  static constexpr int P = H == 32 ? 24 : 25;
+  static constexpr int P = H == 32 ? 24 : (H == 36 ? 25 : hp + 1);
   static_assert(H % 4 == 0 && NC <= NT && hp % 2 == 0 && P >= hp, "decoder forward geometry");
 };
 __device__ __forceinline__ int texel_slot(int hp, int x) { return (x & 1) * (hp / 2) + (x >> 1); }
@@ -1364,12 +1369,15 @@ static int dec_launch_fwd(PosView pv, Src S, FViewW out, FView tgt, float* sse, 
   // the one-barrier-per-frame kernel: 16-byte accesses need 16-byte aligned frames
   const bool al = ((uintptr_t)out.p | (uintptr_t)S.bg) % 16 == 0 && out.fs % 4 == 0 &&
                   (sse == nullptr || ((uintptr_t)tgt.p % 16 == 0 && tgt.fs % 4 == 0 && tgt.gs % 4 == 0));
-  if (al && H == 2 * h && ((K == 2 && H == 32) || (K == 3 && H == 36))) {
+  if (al && H == 2 * h && ((K == 2 && (H == 32 || H == 64)) || (K == 3 && H == 36))) {
     const int fpb = cdiv(F, g);
     g = cdiv(F, fpb);
-    if constexpr (K == 2)
-      hipLaunchKernelGGL((dec_fwd_cu_k<2, 32>), dim3(g), dim3(DecFw<2, 32>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
-    else
+    if constexpr (K == 2) {
+      if (H == 64)
+        hipLaunchKernelGGL((dec_fwd_cu_k<2, 64>), dim3(g), dim3(DecFw<2, 64>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
+      else
+        hipLaunchKernelGGL((dec_fwd_cu_k<2, 32>), dim3(g), dim3(DecFw<2, 32>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
+    } else
       hipLaunchKernelGGL((dec_fwd_cu_k<3, 36>), dim3(g), dim3(DecFw<3, 36>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
     PAIG_CHECK_LAUNCH();
     return 0;
@@ -1546,6 +1554,8 @@ extern "C" {
 
 // Launch geometry of paig_decoder_bwd: the one-CU-per-block kernel for the
 // headline shapes, the generic kernels otherwise.
+// the one-CU backward's shapes (64 x 64 frames: the per-frame pixel-gradient
+// image alone would fill the LDS; they take the generic kernels)
 static bool dec_cu_shape(int K, int h, int H) { return H == 2 * h && ((K == 2 && H == 32) || (K == 3 && H == 36)); }
 
 static int dec_live(int F, int grp, int live) {
