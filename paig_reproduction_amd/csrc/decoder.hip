@@ -616,11 +616,7 @@ struct DecCu {
   static constexpr int RPW = K >= 3 ? 2 : 4, NR = NW * RPW;
   // the two passes in alternating order by wave half (the K = 3 state does
   // not fit the registers twice)
-  static constexpr bool ALT = K == 2 && H <= 36;
-  // G buffers: two (frame parity: pass 1 of frame it beside pass 2 of frame
-  // it-1, one barrier per frame), or one for 64 x 64 frames, whose image
-  // fills half the LDS (a second barrier per frame orders the passes)
-  static constexpr int NGB = H <= 36 ? 2 : 1;
+  static constexpr bool ALT = K == 2;
   static_assert(NR <= 64, "one wave finishes a position gradient");
 };
 
@@ -778,7 +774,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   constexpr int h = C::h, hp = C::hp, hh = C::hh, HW = C::HW, PS = C::PS, NIT = C::NIT, GPITCH = C::GPITCH;
   constexpr int NT = C::NT, PL = C::PL, NI = C::NI, NC = C::NC, NG = C::NG, TC0 = C::TC0, TG0 = C::TG0, NR = C::NR;
   __shared__ float4 SRC[K][hp * hp];              // (template + 5, sigmoid(content) x 3), zero border
-  __shared__ float2 G[C::NGB][2][K][H * GPITCH];  // [frame parity][plane pair][object][row][slot]
+  __shared__ float2 G[2][2][K][H * GPITCH];       // [frame parity][plane pair][object][row][slot]
   __shared__ float4 AXW[2][K][2][H];              // per output column (0) / row (1): tap weights w0, w1 and
   __shared__ int AXC[2][K][2][H];                 //   their d/dcoord d0, d1; padded index of the first tap
   __shared__ int J0[3][K][2][h];                  // gather tables (3 frames in flight): first index
@@ -908,7 +904,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   #else
       if (it >= 1 && act_prev) {
   #endif
-        const int sl = (it - 1) & 1, gs = (it - 1) % 3, gb = C::NGB == 1 ? 0 : sl;
+        const int sl = (it - 1) & 1, gs = (it - 1) % 3;
         if (wv < 2 * K) {   // wave e finishes position gradient e from the NR row partials
           const double v = lane < NR ? RED[sl][wv][lane] : 0.0;
           const double tot = wave_sum_dpp_d(v);
@@ -939,8 +935,8 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
             unsigned ae[2], ao[2];
 #pragma unroll
             for (int q2 = 0; q2 < 2; ++q2) {
-              ae[q2] = (unsigned)(uintptr_t)&G[gb][q2 == 0 ? hf : 1][k][be];
-              ao[q2] = (unsigned)(uintptr_t)&G[gb][q2 == 0 ? hf : 1][k][bo];
+              ae[q2] = (unsigned)(uintptr_t)&G[sl][q2 == 0 ? hf : 1][k][be];
+              ao[q2] = (unsigned)(uintptr_t)&G[sl][q2 == 0 ? hf : 1][k][bo];
             }
             // packed fp32 accumulators: one plane pair per pf32x2
             pf32x2 acc[PL / 2];
@@ -998,7 +994,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   #else
       if (it < nf && act_cur) {
   #endif
-        const int sl = it & 1, gb = C::NGB == 1 ? 0 : sl;
+        const int sl = it & 1;
         const float w_f = 2.f * w_cur;
         const float* dof = dout.p ? dout.p + (long long)ccur.f * dout.fs : nullptr;
         double sx[K], sy[K];
@@ -1059,8 +1055,8 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
               dT = fmaf(g[c], sv[k][1 + c] - o[c], dT);
             }
             dT *= m[k];
-            G[gb][0][k][gof] = make_float2(dT, dC[0]);
-            G[gb][1][k][gof] = make_float2(dC[1], dC[2]);
+            G[sl][0][k][gof] = make_float2(dT, dC[0]);
+            G[sl][1][k][gof] = make_float2(dC[1], dC[2]);
             const float gq[4] = {dT, dC[0], dC[1], dC[2]};
             float gx = 0.f, gy = 0.f;
             if constexpr (HOLD) {
@@ -1113,7 +1109,6 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
     if (!C::ALT || wv < C::NW / 2) {
       pass2();
       DEC_STAMP(it, 2);
-      if constexpr (C::NGB == 1) __syncthreads();   // pass 2 of frame it-1 has read G
       pass1();
     } else {
       pass1();
@@ -1165,6 +1160,310 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
 #pragma unroll
       for (int c = 0; c < 3; ++c) s_bg[c * HW + p] = gbg[s][c];
   }
+}
+
+// ---------------------------------------------------------------------------
+// Decoder backward for 64 x 64 frames (mnist: (K, H) = (2, 64)), one CU per
+// block.  One frame's pixel-gradient image G (K objects x 4 planes x 4096
+// pixels = 128 KB) does not fit the LDS beside the sources, so a frame is
+// processed in two bands of H/2 output rows:
+//   pass 1 (band b): sample / composite / dL/dout for the band's rows and the
+//     GW-1 rows below it (the halo: their G only; their background and
+//     position-gradient sums are taken in their own band, once per pixel);
+//   pass 2 (band b): every (source texel, plane pair) whose 5-row gather
+//     window starts in the band gathers its <= 5 x 5 pixels from G (the
+//     window lies inside band + halo), accumulating in registers over frames.
+// Each thread owns pixels tid + NT s, s = 0..3: slots 0, 1 form band 0 and
+// 2, 3 band 1; slot 2 of the first NHALO threads is also band 0's halo, so
+// targets, background values and background gradients stay in registers.
+// The source gradients are the same gather as dec_bwd_cu_k's (a fixed order,
+// no atomics); the position gradients the same fp64 sums.
+template <int K, int H>
+struct DecBand {
+  static constexpr int NT = 1024, NW = NT / 64;
+  static constexpr int h = H / 2, hp = h + 2, hh = h * h, HW = H * H;
+  static constexpr int BR = H / 2;          // output rows per band
+  static constexpr int GR = BR + GW - 1;    // G rows: band + halo
+  static constexpr int GPITCH = H + 8;      // float2 slots per G row (even columns first; 8 mod 16)
+  static constexpr int PS = HW / NT;        // pixel slots per thread
+  static constexpr int NHALO = (GW - 1) * H;
+  static constexpr int NI = K * hh * 2;     // pass-2 items: (texel, plane pair)
+  static constexpr int NIT = NI / NT;
+  static constexpr int NC = K * 2 * H, NG = K * 2 * h, TG0 = NC;   // axis / gather table threads
+  static constexpr int NR = NW * 4;         // fp64 position-gradient partials (4 row sums per wave)
+  static_assert(HW % NT == 0 && PS == 4 && K * hh == 2 * NT && NHALO <= NT && TG0 + NG <= NT && NR <= 64,
+                "decoder band geometry");
+};
+
+template <int K, int H>
+__global__ void __launch_bounds__(1024)
+dec_bwd_band_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
+               float* __restrict__ slab, int F, int Rl, int FPB) {
+  using C = DecBand<K, H>;
+  constexpr int h = C::h, hp = C::hp, hh = C::hh, HW = C::HW, NT = C::NT, PS = C::PS, BR = C::BR;
+  constexpr int GPITCH = C::GPITCH, NIT = C::NIT, NC = C::NC, NG = C::NG, TG0 = C::TG0, NR = C::NR;
+  __shared__ float4 SRC[K][hp * hp];           // (template + 5, sigmoid(content) x 3), zero border
+  __shared__ float2 G[2][K][C::GR * GPITCH];   // [plane pair][object][band row][slot]
+  __shared__ float4 AXW[K][2][H];              // per output column (0) / row (1): w0, w1, d0, d1
+  __shared__ int AXC[K][2][H];                 //   and the padded index of the first tap
+  __shared__ int J0[K][2][h];                  // gather tables: first index of the 5-wide window
+  __shared__ float WT[K][2][h][GW];            //   and its weights
+  __shared__ double RED[2 * K][NR];
+  __shared__ double BC[H];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int R = pos.grp;
+  const bool grouped = R > 0 && Rl > 0 && Rl < R;
+  const int NL = grouped ? (F / R) * Rl : F;
+  const int first = blockIdx.x * FPB;
+  const int nf = first < NL ? (NL - first < FPB ? NL - first : FPB) : 0;
+  const DecFrames FR(pos, tgt, Rl);
+
+  const int tg = tid - TG0;
+  const bool is_c = tid < NC, is_g = tg >= 0 && tg < NG;
+  const int ck = is_c ? tid / (2 * H) : (is_g ? tg / (2 * h) : 0);
+  const int cax = is_c ? (tid / H) & 1 : (is_g ? (tg / h) & 1 : 0);
+  const int cj = is_c ? tid % H : (is_g ? tg % h : 0);
+
+  float gbg[PS][3];
+  float gsrc[NIT][2];
+#pragma unroll
+  for (int s = 0; s < PS; ++s)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) gbg[s][c] = 0.f;
+#pragma unroll
+  for (int u = 0; u < NIT; ++u) gsrc[u][0] = gsrc[u][1] = 0.f;
+  DecCursor cur = FR.at(first < NL ? first : 0);
+  for (int t = tid; t < K * hp * hp; t += NT) {
+    const int k = t / (hp * hp), q = t % (hp * hp), y = q / hp - 1, x = q % hp - 1;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)h) {
+      const int o = y * h + x;
+      v.x = S.tmpl[k * hh + o] + 5.f;
+      v.y = 1.f / (1.f + expf(-S.cont[(k * 3 + 0) * hh + o]));
+      v.z = 1.f / (1.f + expf(-S.cont[(k * 3 + 1) * hh + o]));
+      v.w = 1.f / (1.f + expf(-S.cont[(k * 3 + 2) * hh + o]));
+    }
+    SRC[k][q] = v;
+  }
+  for (int j = tid; j < H; j += NT) BC[j] = base_coord(j, H);
+  if (grouped) {   // dead frames (steps Rl..R-1 of every sequence): zero position gradients
+    const int per = (R - Rl) * 2 * K, nd = (F / R) * per;
+    for (int e = blockIdx.x * NT + tid; e < nd; e += gridDim.x * NT) {
+      const int b = e / per, rem = e - b * per;
+      dpos[((long long)b * R + Rl + rem / (2 * K)) * 2 * K + rem % (2 * K)] = 0.f;
+    }
+  }
+  __syncthreads();   // SRC, BC
+
+  for (int it = 0; it < nf; ++it) {
+    const float w = dsse != nullptr ? uniform_f(dsse[cur.f]) : 0.f;
+    const float* dof = dout.p ? dout.p + (long long)cur.f * dout.fs : nullptr;
+    const DecCursor nxt = it + 1 < nf ? FR.next(cur) : cur;
+    if (w == 0.f && dof == nullptr) {   // block-uniform: no gradient flows through this frame
+      if (tid < 2 * K) dpos[(long long)cur.f * 2 * K + tid] = 0.f;
+      cur = nxt;
+      continue;
+    }
+    const float* tf = FR.tgt_of(cur);
+    // ---- the frame's axis and gather tables (the previous frame's last
+    // barrier ordered every read of the old ones)
+    if (is_c || is_g) {
+      const float l = FR.pos_of(cur)[2 * ck + cax];
+      if (is_c) {
+        const Ax x = axis(src_coord(BC[cj], (double)(((float)H / 2.f - l) / (float)h), h), h);
+        AXW[ck][cax][cj] = make_float4(x.w0, x.w1, x.d0, x.d1);
+        AXC[ck][cax][cj] = x.c;
+      } else {
+        gather_entry(l, BC, H, h, cj, &J0[ck][cax][cj], WT[ck][cax][cj]);
+      }
+    }
+    __syncthreads();
+    const float w_f = 2.f * w;
+    double sx[K], sy[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) sx[k] = sy[k] = 0.0;
+
+    // one pixel of pass 1 (slot s, band b); own: the band owns the pixel
+    // (background / position-gradient sums), else it is band 0's halo
+    auto pixel = [&](int s, int b, bool own) __attribute__((always_inline)) {
+      asm volatile("" ::: "memory");   // tables re-read per pixel (registers)
+      const int p = tid + NT * s, i = p / H, j = p % H;
+      // background and target from memory, issued before the sampling
+      // (registers hold the background gradients)
+      const float bq3[3] = {S.bg[p], S.bg[HW + p], S.bg[2 * HW + p]};
+      float tq[3] = {0.f, 0.f, 0.f};
+      if (dsse != nullptr)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tq[c] = tf[c * HW + p];
+      float sv[K][4];
+      // the texels of object k and their bilinear (derivative) weights
+      auto texels = [&](int k, float4& ax, float4& ay, float (*tv)[4]) __attribute__((always_inline)) {
+        ax = AXW[k][0][j];
+        ay = AXW[k][1][i];
+        const int bs = AXC[k][1][i] * hp + AXC[k][0][j];
+        const float4 a = SRC[k][bs], bq = SRC[k][bs + 1], c = SRC[k][bs + hp], d = SRC[k][bs + hp + 1];
+        const float4 t4[4] = {a, bq, c, d};
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          tv[n][0] = t4[n].x;
+          tv[n][1] = t4[n].y;
+          tv[n][2] = t4[n].z;
+          tv[n][3] = t4[n].w;
+        }
+      };
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float4 ax, ay;
+        float tv[4][4];
+        texels(k, ax, ay, tv);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float top = fmaf(ax.y, tv[1][q], ax.x * tv[0][q]), bot = fmaf(ax.y, tv[3][q], ax.x * tv[2][q]);
+          sv[k][q] = fmaf(ay.y, bot, ay.x * top);
+        }
+      }
+      float o[3], m[K + 1];
+      blend<K>(sv, bq3, o, m);
+      float g[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        g[c] = w_f * (o[c] - tq[c]);
+        if (dof) g[c] += dof[c * HW + p];
+        if (own) gbg[s][c] = fmaf(m[K], g[c], gbg[s][c]);
+      }
+      const int gof = (i - b * BR) * GPITCH + gslot<H>(j);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float dT = 0.f;
+        float dC[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          dC[c] = m[k] * g[c];
+          dT = fmaf(g[c], sv[k][1 + c] - o[c], dT);
+        }
+        dT *= m[k];
+        G[0][k][gof] = make_float2(dT, dC[0]);
+        G[1][k][gof] = make_float2(dC[1], dC[2]);
+        if (own) {   // d/dix, d/diy of the 4 planes re-formed from the texels (registers)
+          const float gq[4] = {dT, dC[0], dC[1], dC[2]};
+          float4 ax, ay;
+          float tv[4][4];
+          asm volatile("" ::: "memory");   // re-read, not CSE'd with the sampling reads (held across the blend)
+          texels(k, ax, ay, tv);
+          float gx = 0.f, gy = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float top = fmaf(ax.y, tv[1][q], ax.x * tv[0][q]), bot = fmaf(ax.y, tv[3][q], ax.x * tv[2][q]);
+            const float dtop = fmaf(ax.w, tv[1][q], ax.z * tv[0][q]), dbot = fmaf(ax.w, tv[3][q], ax.z * tv[2][q]);
+            gx = fmaf(gq[q], fmaf(ay.y, dbot, ay.x * dtop), gx);
+            gy = fmaf(gq[q], fmaf(ay.w, bot, ay.z * top), gy);
+          }
+          sx[k] += (double)gx;
+          sy[k] += (double)gy;
+          // pinned here: left free, the compiler sinks every pixel's fp64
+          // adds to the end of the band and holds their operands (spills)
+          asm volatile("" : "+v"(sx[k]), "+v"(sy[k]));
+        }
+      }
+    };
+    // pass 2 of band b: the items whose window starts in the band
+    auto gather = [&](int b) __attribute__((always_inline)) {
+      // the tables are re-read per band (not CSE'd across band 1's pass 1:
+      // holding them would spill)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < NIT; ++u) {
+        const int hf = u >> 1, tx = tid + NT * (u & 1);   // K hh = 2 NT: items u, u+1 share a plane pair
+        const int k = tx / hh, q = tx % hh, ys = q / h, xs = q % h;
+        const int i0 = J0[k][1][ys] - b * BR;
+        if ((unsigned)i0 < (unsigned)BR) {
+        const int c0 = J0[k][0][xs];
+        float wy[GW], wx[GW];
+#pragma unroll
+        for (int a2 = 0; a2 < GW; ++a2) {
+          wy[a2] = WT[k][1][ys][a2];
+          wx[a2] = WT[k][0][xs][a2];
+        }
+        int so[GW];
+#pragma unroll
+        for (int bb = 0; bb < GW; ++bb) so[bb] = gslot<H>(c0 + bb);
+        const float2* gk = &G[hf][k][i0 * GPITCH];
+        float ax = 0.f, ay = 0.f;
+#pragma unroll
+        for (int a2 = 0; a2 < GW; ++a2) {
+          float rx = 0.f, ry = 0.f;
+#pragma unroll
+          for (int bb = 0; bb < GW; ++bb) {
+            const float2 v = gk[a2 * GPITCH + so[bb]];
+            rx = fmaf(wx[bb], v.x, rx);
+            ry = fmaf(wx[bb], v.y, ry);
+          }
+          ax = fmaf(wy[a2], rx, ax);
+          ay = fmaf(wy[a2], ry, ay);
+        }
+        gsrc[u][0] += ax;
+        gsrc[u][1] += ay;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one item's 25 reads in flight at a time (registers)
+      }
+    };
+
+    // ---- band 0: slots 0, 1 (+ the halo: slot 2 of the first NHALO threads)
+    pixel(0, 0, true);
+    __builtin_amdgcn_sched_barrier(0);
+    pixel(1, 0, true);
+    __builtin_amdgcn_sched_barrier(0);
+    if (tid < C::NHALO) pixel(2, 0, false);
+    __syncthreads();
+    gather(0);
+    __syncthreads();
+    // ---- band 1: slots 2, 3; then the position gradients
+    pixel(2, 1, true);
+    __builtin_amdgcn_sched_barrier(0);
+    pixel(3, 1, true);
+    {
+      double sv2[2 * K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        sv2[2 * k] = sx[k];
+        sv2[2 * k + 1] = sy[k];
+      }
+      row_sums_dpp_d<2 * K>(sv2);
+      if ((lane & 15) == 0)
+#pragma unroll
+        for (int e = 0; e < 2 * K; ++e) RED[e][wv * 4 + (lane >> 4)] = sv2[e];
+    }
+    __syncthreads();
+    if (wv < 2 * K) {   // wave e finishes position gradient e
+      const double tot = wave_sum_dpp_d(lane < NR ? RED[wv][lane] : 0.0);
+      const float dth = (float)(tot * (double)h * 0.5);
+      if (lane == 0) dpos[(long long)cur.f * 2 * K + wv] = -dth / (float)h;
+    }
+    gather(1);
+    cur = nxt;
+    __syncthreads();
+  }
+  // ---- this block's partial source gradients -> its slab row
+  float* srow = slab + (long long)blockIdx.x * ((long long)K * hh * 4 + 3LL * HW);
+  float* s_tm = srow;
+  float* s_ct = srow + K * hh;
+  float* s_bg = s_ct + K * 3 * hh;
+#pragma unroll
+  for (int u = 0; u < NIT; ++u) {
+    const int hf = u >> 1, tx = tid + NT * (u & 1);
+    const int k = tx / hh, q = tx % hh;
+#pragma unroll
+    for (int q2 = 0; q2 < 2; ++q2) {
+      const int pl = 2 * hf + q2;   // 0: template, 1..3: content channel pl-1
+      if (pl == 0) s_tm[tx] = gsrc[u][q2];
+      else s_ct[(k * 3 + pl - 1) * hh + q] = gsrc[u][q2];
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < PS; ++s)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s_bg[c * HW + tid + NT * s] = gbg[s][c];
 }
 
 // ---------------------------------------------------------------------------
@@ -1554,9 +1853,9 @@ extern "C" {
 
 // Launch geometry of paig_decoder_bwd: the one-CU-per-block kernel for the
 // headline shapes, the generic kernels otherwise.
-// the one-CU backward's shapes (64 x 64 frames: the per-frame pixel-gradient
-// image alone would fill the LDS; they take the generic kernels)
-static bool dec_cu_shape(int K, int h, int H) { return H == 2 * h && ((K == 2 && H == 32) || (K == 3 && H == 36)); }
+static bool dec_cu_shape(int K, int h, int H) {
+  return H == 2 * h && ((K == 2 && (H == 32 || H == 64)) || (K == 3 && H == 36));
+}
 
 static int dec_live(int F, int grp, int live) {
   return (grp > 0 && live > 0 && live < grp) ? (F / grp) * live : F;
@@ -1644,7 +1943,10 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
     const int fpb = dec_cu_fpb(NL > 0 ? NL : 1);
     const int g = paig_decoder_bwd_blocks(F, pos_grp, live, K, h, H);
     const int rl = dec_live(F, pos_grp, live) == F ? 0 : live;
-    if (K == 2)
+    if (K == 2 && H == 64)
+      hipLaunchKernelGGL((dec_bwd_band_k<2, 64>), dim3(g), dim3(DecBand<2, 64>::NT), 0, st, pv, S, t, dsse, d, dpos, slab, F, rl,
+                         fpb);
+    else if (K == 2)
       hipLaunchKernelGGL((dec_bwd_cu_k<2, 32>), dim3(g), dim3(DecCu<2, 32>::NT), 0, st, pv, S, t, dsse, d, dpos, slab, F, rl, fpb);
     else
       hipLaunchKernelGGL((dec_bwd_cu_k<3, 36>), dim3(g), dim3(DecCu<3, 36>::NT), 0, st, pv, S, t, dsse, d, dpos, slab, F, rl, fpb);
