@@ -206,6 +206,15 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
                  long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
                  const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,
                  void* stream);
+/* The GEMM of paig_gemm_ex (alpha = 1) without its epilogue: the K-slices of
+ * its split plan written as S >= 1 partial slabs part[s][M][N] (S = 1 when
+ * the plan does not split); returns S, or a negative status.  part_floats >=
+ * paig_gemm_parts_size(M, N, K, math) keeps the plan's split (fewer than
+ * S M N floats fall back to S = 1; fewer than M N is an error).  The consumer
+ * sums the slabs in slab order (paig_dense_tail_fwd). */
+size_t paig_gemm_parts_size(int M, int N, int K, int math);
+int paig_gemm_parts(int ta, int tb, int M, int N, int K, const float* A, long long lda, const float* B,
+                    long long ldb, float* part, size_t part_floats, int math, void* stream);
 /* Dense layers on pre-split operands (psgemm.hip).  A "PS image" holds a
  * logical matrix X[R][K] (reduction dim K) split once into f16 hi + lo planes
  * ([ceil(K/32)][R rounded up to 64][32] each), one power-of-two exponent per
@@ -298,6 +307,27 @@ int paig_head_bwd_vel_vfn2(const float* h2, const float* h3, const float* dpos, 
                            const int* sig, const float* const* h, const float* const* W2, float* const* dW1,
                            float* const* db1, float* const* dW2, float* const* db2, float* const* part, const int* P,
                            void* stream);
+
+/* The localiser's dense tail, forward (blocks.py:98-102): l1's split-K slabs
+ * (paig_gemm_parts of objects x W1^T, S slabs of [K*F][IN]) summed + b1 +
+ * ReLU -> h1; h2 = ReLU(h1 W2^T + b2) in fp32 FMA; the l3 position head as
+ * paig_head_fwd -> h3, pos.  IN <= 200, a multiple of 4; W2t: IN * IN floats
+ * of scratch (8-byte aligned) for W2^T.  Two launches (the 200 x 200
+ * transpose, then one for the split-K epilogue, l2 and the head). */
+int paig_dense_tail_fwd(const float* part, int S, const float* b1, float* h1, const float* W2, float* W2t,
+                        const float* b2, float* h2, const float* W3, const float* b3, float* h3, float* pos, int F,
+                        int K, int IN, float half, void* stream);
+/* paig_head_bwd_vel_vfn2 (dX / dpos0 nullable: no velocity-encoder term; n =
+ * 0: no VFN phase 2) that also forms l2's data gradient (blocks.py:99):
+ * dh1 = (dh2 W2) * (h1 > 0), fp32 FMA, W2 [IN][IN] (8-byte aligned), IN <=
+ * 200; its [W3 | b3] slab rows are paig_head_l2_bwd_blocks(K * F). */
+int paig_head_l2_bwd_blocks(int rows);
+int paig_head_l2_bwd(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab,
+                     int F, int K, int IN, float half, const float* dX, const float* dpos0, int B, int Te, int S,
+                     int alt, const float* W2, const float* h1, float* dh1, int n, const float* const* d,
+                     const float* const* y, const int* sig, const float* const* h, const float* const* vW2,
+                     float* const* dW1, float* const* db1, float* const* dW2, float* const* db2, float* const* part,
+                     const int* P, void* stream);
 
 /* ---- velocity encoder input packing (blocks.py:33-45) */
 int paig_vel_pack(const float* pos, float* X, int B, int Te, int K, int S, int alt, void* stream);

@@ -50,7 +50,11 @@ SIGNATURES = {
     "paig_velmlp_slab_len": (I, [I]),
     "paig_velmlp_bwd": (I, [P, P, P, P, P, P, P, P, P, I, I, P]),
     "paig_head_fwd": (I, [P, P, P, P, P, I, I, I, F32, P]),
+    "paig_dense_tail_fwd": (I, [P, I, P, P, P, P, P, P, P, P, P, P, I, I, I, F32, P]),
+    "paig_head_l2_bwd": (I, [P, P, P, P, P, P, I, I, I, F32, P, P, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P,
+                             P, P, P]),
     "paig_head_bwd_blocks": (I, [I]),
+    "paig_head_l2_bwd_blocks": (I, [I]),
     "paig_head_bwd": (I, [P, P, P, P, P, P, I, I, I, F32, P]),
     "paig_head_bwd_vel": (I, [P, P, P, P, P, P, I, I, I, F32, P, P, I, I, I, I, P]),
     "paig_head_bwd_vel_vfn2": (I, [P, P, P, P, P, P, I, I, I, F32, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P,
@@ -67,6 +71,8 @@ SIGNATURES = {
     "paig_pos_head_fwd": (I, [P, P, I, I, F32, P]),
     "paig_pos_head_bwd": (I, [P, P, P, I, I, F32, P]),
     "paig_gemm_workspace": (SZ, [I, I, I]),
+    "paig_gemm_parts_size": (SZ, [I, I, I, I]),
+    "paig_gemm_parts": (I, [I, I, I, I, I, P, LL, P, LL, P, SZ, I, P]),
     "paig_gemm": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, P]),
     "paig_gemm_ex": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, I, P]),
     "paig_ps_bytes": (LL, [I, I]),
@@ -115,8 +121,8 @@ SIGNATURES = {
 
 _QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported",
           "paig_conv2d_bwd_supported", "paig_velmlp_bwd_blocks",
-          "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_mask_blocks", "paig_conv_wprep_size", "paig_gemm_workspace", "paig_colsum_workspace",
-          "paig_ps_bytes", "paig_psgemm_workspace",
+          "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_l2_bwd_blocks", "paig_head_mask_blocks", "paig_conv_wprep_size", "paig_gemm_workspace", "paig_colsum_workspace",
+          "paig_ps_bytes", "paig_psgemm_workspace", "paig_gemm_parts_size", "paig_gemm_parts",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
           "paig_decoder_bwd_scratch"}
 

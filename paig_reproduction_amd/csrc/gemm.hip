@@ -1013,6 +1013,40 @@ int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, 
                       ws_floats, 0, stream);
 }
 
+size_t paig_gemm_parts_size(int M, int N, int K, int math) {
+  if (M <= 0 || N <= 0) return 0;
+  const GemmPlan p = plan_gemm(M, N, K, math);
+  return (size_t)(p.S > 1 ? p.S : 1) * M * N;
+}
+
+int paig_gemm_parts(int ta, int tb, int M, int N, int K, const float* A, long long lda, const float* B,
+                    long long ldb, float* part, size_t part_floats, int math, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  PAIG_REQUIRE(math >= 0 && math <= 6, "paig_gemm_parts: math must be 0..6, got %d", math);
+  PAIG_REQUIRE(M > 0 && N > 0 && K > 0 && part, "paig_gemm_parts: empty shape (%d x %d x %d) or no slabs", M, N, K);
+  const int va = vec_ok(A, lda) && (ta ? M % 4 == 0 : K % 4 == 0);
+  const int vb = vec_ok(B, ldb) && (tb ? K % 4 == 0 : N % 4 == 0);
+  GemmPlan plan = plan_gemm(M, N, K, math);
+  if (plan.tile && !(va && vb)) plan = GemmPlan{0, choose_split(M, N, K)};
+  int S = plan.S;
+  if (S > 1 && part_floats < (size_t)S * M * N) S = 1;
+  PAIG_REQUIRE(part_floats >= (size_t)M * N, "paig_gemm_parts: %zu floats for a %d x %d slab", part_floats, M, N);
+  const int kchunk = S > 1 ? cdiv(cdiv(K, S), BK) * BK : K;
+  S = cdiv(K, kchunk);
+  const int bm = plan.tile == 2 ? 256 : BM, bn = plan.tile == 1 ? 256 : BN;
+  dim3 grid(cdiv(N, bn), cdiv(M, bm), S);
+#define PAIG_G(TA_, TB_)                                                                                        \
+  launch_gemm<TA_, TB_>(math, plan.tile, grid, st, M, N, K, kchunk, 1.f, A, lda, va, B, ldb, vb, nullptr, N, 0.f, \
+                        nullptr, 0, 0, nullptr, 0, part, nullptr, nullptr)
+  if (ta && tb) PAIG_G(true, true);
+  else if (ta) PAIG_G(true, false);
+  else if (tb) PAIG_G(false, true);
+  else PAIG_G(false, false);
+#undef PAIG_G
+  PAIG_CHECK_LAUNCH();
+  return S;
+}
+
 int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
                  long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
                  const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, int math,

@@ -374,14 +374,17 @@ __device__ __forceinline__ float vel_grad(const VelGrad& v, int K, int f, int k,
 }
 
 // slab row per block: [W3 (2*IN) | b3 (2)]; blk = the block's row block
+// (dstash: the block's dh2 rows also go to this LDS array [RB][IN])
+template <int RB = HEAD_RB>
 __device__ __forceinline__ void head_bwd_block(const float* __restrict__ h2, const float* __restrict__ h3,
                                                const float* __restrict__ dpos, const float* __restrict__ W3,
                                                float* __restrict__ dh2, float* __restrict__ slab, int F, int K,
-                                               int IN, float half, const VelGrad& vg, int blk) {
-  __shared__ float D3[HEAD_RB][2];
-  const int n0 = blk * HEAD_RB, rows = K * F, tid = threadIdx.x;
-  const int nr = rows - n0 < HEAD_RB ? rows - n0 : HEAD_RB;
-  if (tid < HEAD_RB * 2) {
+                                               int IN, float half, const VelGrad& vg, int blk,
+                                               float* dstash = nullptr) {
+  __shared__ float D3[RB][2];
+  const int n0 = blk * RB, rows = K * F, tid = threadIdx.x;
+  const int nr = rows - n0 < RB ? rows - n0 : RB;
+  if (tid < RB * 2) {
     const int r = tid >> 1, j = tid & 1;
     float d = 0.f;
     if (r < nr) {
@@ -404,6 +407,7 @@ __device__ __forceinline__ void head_bwd_block(const float* __restrict__ h2, con
       g1 = fmaf(D3[r][1], x, g1);
       const float g = fmaf(D3[r][0], w0, D3[r][1] * w1);
       dh2[o] = x > 0.f ? g : 0.f;                     // relu' of l2's output (blocks.py:99)
+      if (dstash) dstash[r * IN + u] = x > 0.f ? g : 0.f;
     }
     s[u] = g0;
     s[IN + u] = g1;
@@ -437,9 +441,253 @@ head_bwd_vfn2_k(const float* __restrict__ h2, const float* __restrict__ h3, cons
   }
 }
 
+// ---------------------------------------------------------------------------
+// The localiser's dense tail in one launch each way (nn/network/blocks.py:
+// 98-102: l1 -> ReLU -> l2 -> ReLU -> l3 -> tanh head).  The 200-wide l2 is
+// 2000 x 200 x 200: as an MFMA GEMM launch it is all latency (7 K-steps,
+// 128 tiles), so it runs in fp32 FMA inside the launches around it:
+//   forward: l1's split-K slabs summed (+ b1, ReLU; the order of
+//     gemm_splitk_epilogue_k) -> h1; h2 = ReLU(h1 W2^T + b2); the l3 head
+//     (head_fwd_k's per-row order) -> h3, enc_pos.  8 rows per block.
+//   backward: the head backward's blocks (16 rows, dh2 kept in LDS) also form
+//     l2's data gradient dh1 = (dh2 W2) * (h1 > 0).
+// Plain fp32 FMA throughout: at least as accurate as the split MFMA form.
+// Both launches multiply 8 rows by W2 per block (250 blocks at K*F = 2000):
+// 512 threads = (column pair, K-slice of TSL): a thread holds its two W2
+// rows' (forward) / columns' (backward) slice in registers (loaded at once,
+// one L2 round trip), reads each h1 / dh2 value once from LDS for both
+// columns (packed fp32 FMA), and the slices' partials are summed in LDS in
+// slice order.  IN <= 200 = TNP pairs x TNS slices of TSL.
+constexpr int TAIL_RB = 8, TAIL_NT = 512, TSL = 40, TNS = 5, TNP = 100, TAIL_MAXIN = 2 * TNP;
+
+// columns c0, c0+1 of M [k][IN] over rows k0 .. k0+kn (float2 per row,
+// coalesced over consecutive pairs): wa / wb[j] = the two columns at k0 + 4j + {0..3}
+__device__ __forceinline__ void load_pair_slice(const float* __restrict__ M, int IN, int c0, int k0, int kn,
+                                                float4* wa, float4* wb) {
+#pragma unroll
+  for (int j = 0; j < TSL / 4; ++j) {
+    float2 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = 4 * j < kn ? *reinterpret_cast<const float2*>(M + (long long)(k0 + 4 * j + q) * IN + c0)
+                        : make_float2(0.f, 0.f);
+    wa[j] = make_float4(v[0].x, v[1].x, v[2].x, v[3].x);
+    wb[j] = make_float4(v[0].y, v[1].y, v[2].y, v[3].y);
+  }
+}
+
+// W2t = W2^T ([IN][IN]; 32 x 32 tiles through LDS)
+__global__ void __launch_bounds__(256) transpose_sq_k(const float* __restrict__ A, float* __restrict__ At, int n) {
+  __shared__ float T[32][33];
+  const int bx = blockIdx.x * 32, by = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8)
+    if (by + y < n && bx + tx < n) T[y][tx] = A[(long long)(by + y) * n + bx + tx];
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8)
+    if (bx + y < n && by + tx < n) At[(long long)(bx + y) * n + by + tx] = T[tx][y];
+}
+
+// acc[r] += rows r of X (LDS [TAIL_RB][IN], slice k0..k0+kn) x the pair's
+// slice (wa, wb: the two columns' values at k0 + 4j + {0..3})
+__device__ __forceinline__ void pair_slice(const float* X, int IN, int k0, int kn, const float4* wa, const float4* wb,
+                                           pf32x2* acc) {
+#pragma unroll
+  for (int j = 0; j < TSL / 4; ++j) {
+    if (4 * j < kn) {
+      const pf32x2 w0 = {wa[j].x, wb[j].x}, w1 = {wa[j].y, wb[j].y}, w2 = {wa[j].z, wb[j].z}, w3 = {wa[j].w, wb[j].w};
+#pragma unroll
+      for (int r = 0; r < TAIL_RB; ++r) {
+        const float4 x = *reinterpret_cast<const float4*>(&X[r * IN + k0 + 4 * j]);
+        acc[r] += x.x * w0;
+        acc[r] += x.y * w1;
+        acc[r] += x.z * w2;
+        acc[r] += x.w * w3;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(TAIL_NT)
+dense_tail_fwd_k(const float* __restrict__ part, int S, const float* __restrict__ b1, float* __restrict__ h1,
+                 const float* __restrict__ W2t, const float* __restrict__ b2, float* __restrict__ h2,
+                 const float* __restrict__ W3, const float* __restrict__ b3, float* __restrict__ h3,
+                 float* __restrict__ pos, int F, int K, int IN, float half) {
+  __shared__ __attribute__((aligned(16))) float X1[TAIL_RB * TAIL_MAXIN];
+  __shared__ float X2[TAIL_RB * TAIL_MAXIN];
+  __shared__ float RQ[TNS * TAIL_RB * TAIL_MAXIN];
+  const int rows = K * F, n0 = blockIdx.x * TAIL_RB, tid = threadIdx.x;
+  const int nr = rows - n0 < TAIL_RB ? rows - n0 : TAIL_RB;
+  const long long MN = (long long)rows * IN;
+  // this thread's W2 rows 2p, 2p+1 over K-slice ks, from W2^T (W2t [k][c]:
+  // float2 per k, coalesced over p), loaded first (they fly behind the slab
+  // sums)
+  const int pp = tid % TNP, ks = tid / TNP, c0 = 2 * pp, k0 = ks * TSL;
+  const bool act = ks < TNS && c0 < IN && k0 < IN;
+  const int kn = act ? (IN - k0 < TSL ? IN - k0 : TSL) : 0;
+  float4 wa[TSL / 4], wb[TSL / 4];
+  load_pair_slice(W2t, IN, c0, k0, kn, wa, wb);
+  // h1 = ReLU(sum_s part[s] + b1): slab order, as the split-K epilogue
+  for (int e = tid; e < TAIL_RB * IN; e += TAIL_NT) {
+    const int r = e / IN, c = e - r * IN;
+    float v = 0.f;
+    if (r < nr) {
+      const long long o = (long long)(n0 + r) * IN + c;
+      const float* p = part + o;
+      int sq = 0;
+      for (; sq + 8 <= S; sq += 8) {   // 8 slab loads in flight, summed in slab order
+        float t[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) t[jj] = p[(sq + jj) * MN];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) v += t[jj];
+      }
+      for (; sq < S; ++sq) v += p[sq * MN];
+      v = epi(v + b1[c], ACT_RELU, AUX_NONE, nullptr, 0);
+      h1[o] = v;
+    }
+    X1[e] = v;
+  }
+  __syncthreads();
+  // h2 = ReLU(h1 W2^T + b2)
+  if (act) {
+    pf32x2 acc[TAIL_RB];
+#pragma unroll
+    for (int r = 0; r < TAIL_RB; ++r) acc[r] = pf32x2{0.f, 0.f};
+    pair_slice(X1, IN, k0, kn, wa, wb, acc);
+#pragma unroll
+    for (int r = 0; r < TAIL_RB; ++r) {
+      RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0] = acc[r].x;
+      RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0 + 1] = acc[r].y;
+    }
+  }
+  __syncthreads();
+  const int nsl = (IN + TSL - 1) / TSL;
+  for (int e = tid; e < TAIL_RB * IN; e += TAIL_NT) {
+    const int r = e / IN, c = e - r * IN;
+    float a = 0.f;
+    for (int q = 0; q < nsl; ++q) a += RQ[(q * TAIL_RB + r) * TAIL_MAXIN + c];
+    const float v = r < nr ? epi(a + b2[c], ACT_RELU, AUX_NONE, nullptr, 0) : 0.f;
+    if (r < nr) h2[(long long)(n0 + r) * IN + c] = v;
+    X2[e] = v;
+  }
+  __syncthreads();
+  // l3 + tanh head (head_fwd_k's order): wave w takes row w
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int r = wv; r < nr; r += TAIL_NT / 64) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int c = lane; c < IN; c += 64) {
+      const float v = X2[r * IN + c];
+      a0 = fmaf(v, W3[c], a0);
+      a1 = fmaf(v, W3[IN + c], a1);
+    }
+    a0 = wave_sum(a0) + b3[0];
+    a1 = wave_sum(a1) + b3[1];
+    if (lane == 0) {
+      const int n = n0 + r, k = n / F, f = n % F;
+      h3[(long long)n * 2] = a0;
+      h3[(long long)n * 2 + 1] = a1;
+      pos[(long long)f * 2 * K + 2 * k] = tanhf(a0) * half + half;
+      pos[(long long)f * 2 * K + 2 * k + 1] = tanhf(a1) * half + half;
+    }
+  }
+}
+
+// head backward (+ the velocity encoder's input gradient) of TAIL_RB rows and
+// their l2 data gradient dh1 = (dh2 W2) * (h1 > 0): (column pair, o-slice)
+// threads as in the forward, W2's columns read as float2 rows (coalesced);
+// and (nvfn > 0) the VariableFromNetwork backward's phase 2 as extra blocks
+// (head_bwd_vfn2_k's items, one per wave)
+__global__ void __launch_bounds__(TAIL_NT)
+head_l2_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const float* __restrict__ dpos,
+              const float* __restrict__ W3, float* __restrict__ dh2, float* __restrict__ slab, int F, int K, int IN,
+              float half, VelGrad vg, const float* __restrict__ W2, const float* __restrict__ h1,
+              float* __restrict__ dh1, int nhead, paig_vfn::VfnBwdTasks T, int nitems) {
+  __shared__ __attribute__((aligned(16))) float DH[TAIL_RB * TAIL_MAXIN];
+  __shared__ float RQ[TNS * TAIL_RB * TAIL_MAXIN];
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= nhead) {
+    const int item = ((int)blockIdx.x - nhead) * (TAIL_NT / 64) + (tid >> 6);
+    if (item < nitems) paig_vfn::vfn_bwd2_item(T, item, tid & 63);
+    return;
+  }
+  const int n0 = blockIdx.x * TAIL_RB, rows = K * F;
+  const int nr = rows - n0 < TAIL_RB ? rows - n0 : TAIL_RB;
+  // this thread's W2 columns 2p, 2p+1 over o-slice ks (float2 per o)
+  const int pp = tid % TNP, ks = tid / TNP, c0 = 2 * pp, k0 = ks * TSL;
+  const bool act = ks < TNS && c0 < IN && k0 < IN;
+  const int kn = act ? (IN - k0 < TSL ? IN - k0 : TSL) : 0;
+  float4 wa[TSL / 4], wb[TSL / 4];
+  load_pair_slice(W2, IN, c0, k0, kn, wa, wb);
+  for (int e = nr * IN + tid; e < TAIL_RB * IN; e += TAIL_NT) DH[e] = 0.f;
+  head_bwd_block<TAIL_RB>(h2, h3, dpos, W3, dh2, slab, F, K, IN, half, vg, blockIdx.x, DH);
+  __syncthreads();
+  if (act) {
+    pf32x2 acc[TAIL_RB];
+#pragma unroll
+    for (int r = 0; r < TAIL_RB; ++r) acc[r] = pf32x2{0.f, 0.f};
+    pair_slice(DH, IN, k0, kn, wa, wb, acc);
+#pragma unroll
+    for (int r = 0; r < TAIL_RB; ++r) {
+      RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0] = acc[r].x;
+      RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0 + 1] = acc[r].y;
+    }
+  }
+  __syncthreads();
+  const int nsl = (IN + TSL - 1) / TSL;
+  for (int e = tid; e < nr * IN; e += TAIL_NT) {
+    const int r = e / IN, c = e - r * IN;
+    float a = 0.f;
+    for (int q = 0; q < nsl; ++q) a += RQ[(q * TAIL_RB + r) * TAIL_MAXIN + c];
+    const long long o = (long long)(n0 + r) * IN + c;
+    dh1[o] = epi(a, ACT_NONE, AUX_RELU, h1, o);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int paig_dense_tail_fwd(const float* part, int S, const float* b1, float* h1, const float* W2, float* W2t,
+                        const float* b2, float* h2, const float* W3, const float* b3, float* h3, float* pos, int F,
+                        int K, int IN, float half, void* stream) {
+  const int rows = K * F;
+  if (rows <= 0) return 0;
+  PAIG_REQUIRE(S >= 1 && IN > 0 && IN <= TAIL_MAXIN && IN % 4 == 0,
+               "dense_tail_fwd: S=%d, IN=%d (<= %d, a multiple of 4)", S, IN, TAIL_MAXIN);
+  PAIG_REQUIRE(W2 && W2t && (reinterpret_cast<uintptr_t>(W2t) & 7) == 0,
+               "dense_tail_fwd: W2 and an 8-byte aligned W2t scratch (IN * IN floats) are required");
+  hipLaunchKernelGGL(transpose_sq_k, dim3(cdiv(IN, 32), cdiv(IN, 32)), dim3(256), 0, (hipStream_t)stream, W2, W2t, IN);
+  PAIG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dense_tail_fwd_k, dim3(cdiv(rows, TAIL_RB)), dim3(TAIL_NT), 0, (hipStream_t)stream, part, S, b1, h1,
+                     W2t, b2, h2, W3, b3, h3, pos, F, K, IN, half);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_head_l2_bwd(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab,
+                     int F, int K, int IN, float half, const float* dX, const float* dpos0, int B, int Te, int S,
+                     int alt, const float* W2, const float* h1, float* dh1, int n, const float* const* d,
+                     const float* const* y, const int* sig, const float* const* h, const float* const* vW2,
+                     float* const* dW1, float* const* db1, float* const* dW2, float* const* db2, float* const* part,
+                     const int* P, void* stream) {
+  const int rows = K * F;
+  if (rows <= 0) return 0;
+  PAIG_REQUIRE(IN > 0 && IN <= TAIL_MAXIN && IN % 4 == 0, "head_l2_bwd: IN=%d (<= %d, a multiple of 4)", IN, TAIL_MAXIN);
+  PAIG_REQUIRE(W2 && h1 && dh1 && (reinterpret_cast<uintptr_t>(W2) & 7) == 0,
+               "head_l2_bwd: W2 (8-byte aligned), h1 and dh1 are required");
+  PAIG_REQUIRE((dX == nullptr && dpos0 == nullptr) || (B > 0 && Te > 0 && F == B * Te && S <= Te),
+               "head_l2_bwd: F=%d != B=%d x Te=%d or S=%d > Te", F, B, Te, S);
+  PAIG_REQUIRE(n >= 0 && n <= paig_vfn::VMAX, "head_l2_bwd: n=%d (0..%d)", n, paig_vfn::VMAX);
+  paig_vfn::VfnBwdTasks T{};
+  if (n > 0) paig_vfn::vfn_bwd_tasks(T, n, d, y, sig, h, vW2, dW1, db1, dW2, db2, part, P);
+  const int nhead = cdiv(rows, TAIL_RB), nitems = paig_vfn::VH * n;
+  const VelGrad vg = (dX || dpos0) ? VelGrad{dX, dpos0, B, Te, S, alt} : VelGrad{nullptr, nullptr, 1, 1, 0, 0};
+  hipLaunchKernelGGL(head_l2_bwd_k, dim3(nhead + cdiv(nitems, TAIL_NT / 64)), dim3(TAIL_NT), 0, (hipStream_t)stream, h2,
+                     h3, dpos, W3,
+                     dh2, slab, F, K, IN, half, vg, W2, h1, dh1, nhead, T, nitems);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
 
 int paig_head_fwd(const float* h2, const float* W3, const float* b3, float* h3, float* pos, int F, int K, int IN,
                   float half, void* stream) {
@@ -452,6 +700,8 @@ int paig_head_fwd(const float* h2, const float* W3, const float* b3, float* h3, 
 }
 
 int paig_head_bwd_blocks(int rows) { return cdiv(rows, HEAD_RB); }
+
+int paig_head_l2_bwd_blocks(int rows) { return cdiv(rows, TAIL_RB); }
 
 int paig_head_bwd(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab, int F,
                   int K, int IN, float half, void* stream) {

@@ -23,7 +23,7 @@ import os
 
 import torch
 
-from ._lib import XMAX_SLOTS, lib, ptr, stream_handle, require_device
+from ._lib import XMAX_SLOTS, PaigError, lib, ptr, stream_handle, require_device
 
 # --------------------------------------------------------------------------
 # U-Net plans (buffers + ops), forward order.  A buffer is (channels, level),
@@ -401,6 +401,7 @@ class Engine:
                 self.L.paig_gemm_workspace(200, n1, K * F), self.L.paig_gemm_workspace(K * F, n1, 200), self.L.paig_gemm_workspace(200, 200, K * F),
                 self.L.paig_gemm_workspace(2, 200, K * F), self.L.paig_gemm_workspace(100, 100, K * B),
                 self.L.paig_gemm_workspace(K * B, 100, 100), 1 << 16,
+                self.L.paig_gemm_parts_size(K * F, 200, n1, self.gemm_math(self.FWD)),
                 self.L.paig_psgemm_workspace(K * F, 200, n1), self.L.paig_psgemm_workspace(200, n1, K * F),
                 self.L.paig_psgemm_workspace(K * F, n1, 200), self.L.paig_psgemm_workspace(200, 200, K * F),
                 self.L.paig_psgemm_workspace(K * F, 200, 200)]
@@ -715,12 +716,26 @@ class Engine:
             self._psgemm("gemm_fwd:encoder.l2", KF, 200, 200, ps["h1"], ps["w2"], h2, 200, ws, st,
                          bias=self.p("encoder.l2.bias"), act=1)
             S["ps"] = ps
+            enc_pos = _empty(F * 2 * K, dev)
+            L.paig_head_fwd(ptr(h2), ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
+                            ptr(enc_pos), F, K, 200, float(H / 2), st)
         else:
-            self.linear(l1_x, K * F, "encoder.l1", h1, 1, st, ws)
-            self.linear(h1, K * F, "encoder.l2", h2, 1, st, ws)
-        enc_pos = _empty(F * 2 * K, dev)
-        L.paig_head_fwd(ptr(h2), ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
-                        ptr(enc_pos), F, K, 200, float(H / 2), st)
+            # l1 (blocks.py:98) as split-K slabs, then ONE launch for its
+            # epilogue, l2 and the position head (blocks.py:99-102)
+            n1, KF = lay.l1_in, K * F
+            enc_pos = _empty(F * 2 * K, dev)
+            with self._p("gemm_fwd:encoder.l1", 2 * KF * 200 * n1, 4 * (KF * n1 + 200 * n1)):
+                nS = L.paig_gemm_parts(0, 1, KF, 200, n1, ptr(l1_x), n1, ptr(self.p("encoder.l1.weight")), n1, ptr(ws),
+                                       ws.numel(), self.gemm_math(self.FWD), st)
+            if nS <= 0:
+                raise PaigError(f"paig_gemm_parts failed (rc={nS}): {L.paig_last_error().decode(errors='replace')}")
+            with self._p("dense_tail_fwd", 2 * KF * 200 * 200 + 4 * KF * 200,
+                         4 * (nS * KF * 200 + 2 * KF * 200 + 200 * 200 + 2 * KF + 2 * KF)):
+                w2t = _empty(200 * 200, dev)
+                L.paig_dense_tail_fwd(ptr(ws), nS, ptr(self.p("encoder.l1.bias")), ptr(h1),
+                                      ptr(self.p("encoder.l2.weight")), ptr(w2t), ptr(self.p("encoder.l2.bias")), ptr(h2),
+                                      ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
+                                      ptr(enc_pos), F, K, 200, float(H / 2), st)
         S.update(masks=masks, objs=objs, l1_x=l1_x, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
 
     # -- a second stream for the per-sequence chains (PAIG_SCHED=0 only) ----
@@ -910,9 +925,22 @@ class Engine:
         S.setdefault("extra_slabs", [])
         # ---- position head + localiser MLP backward -> d masked objects
         dh2 = _empty(K * F * 200, dev)
-        hblk = L.paig_head_bwd_blocks(K * F)
+        dh1 = _empty(K * F * 200, dev)
+        fused_l2 = "ps" not in S   # l2's data gradient formed inside the head backward's launch
+        hblk = L.paig_head_l2_bwd_blocks(K * F) if fused_l2 else L.paig_head_bwd_blocks(K * F)
         hslab = _empty(hblk * (2 * 200 + 2), dev)
-        if vel is not None and vel[6] is not None:   # + the VFN backward's phase 2
+        if fused_l2:
+            dXv = dpos0 = None
+            Bv = Tev = Sv = altv = 0
+            vfn2 = None
+            if vel is not None:
+                dXv, dpos0, Bv, Tev, Sv, altv, vfn2 = vel
+            vf = vfn2 if vfn2 is not None else (0,) + (None,) * 11
+            L.paig_head_l2_bwd(ptr(S["h2"]), ptr(S["h3"]), ptr(denc), ptr(self.p("encoder.l3.weight")), ptr(dh2),
+                               ptr(hslab), F, K, 200, float(H / 2), ptr(dXv) if torch.is_tensor(dXv) else dXv,
+                               ptr(dpos0) if torch.is_tensor(dpos0) else dpos0, Bv, Tev, Sv, altv,
+                               ptr(self.p("encoder.l2.weight")), ptr(S["h1"]), ptr(dh1), *vf, st)
+        elif vel is not None and vel[6] is not None:   # + the VFN backward's phase 2
             dXv, dpos0, Bv, Tev, Sv, altv, vfn2 = vel
             L.paig_head_bwd_vel_vfn2(ptr(S["h2"]), ptr(S["h3"]), ptr(denc), ptr(self.p("encoder.l3.weight")),
                                      ptr(dh2), ptr(hslab), F, K, 200, float(H / 2), ptr(dXv), ptr(dpos0), Bv, Tev,
@@ -927,12 +955,11 @@ class Engine:
         g3 = self.g("encoder.l3.weight")
         assert self.g("encoder.l3.bias").data_ptr() == g3.data_ptr() + 400 * 4, "l3 grads not contiguous"
         S["extra_slabs"].append((hslab, hblk, 402, g3))
-        dh1 = _empty(K * F * 200, dev)
         dobjs = _empty(K * F * lay.l1_in, dev)
         if "ps" in S:
             self._dense_bwd_ps(S, dh2, dh1, dobjs, st, ws)
         else:
-            self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws)
+            self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", None, None, 0, st, ws, need_dx=False)
             self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
         # every gradient of the flat buffer's early bucket is final (queued on
         # this stream): the data-parallel all-reduce of that bucket may start
