@@ -144,6 +144,26 @@ int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, c
                     const float* xmax, int xmax_n, const float* dpool, long long dpool_fs,
                     const unsigned char* pcode, long long pcode_fs, const void* wprep, void* stream);
 
+/* ---- the whole U-Net as one call each way (csrc/unet.hip): net 0 =
+ * ShallowUNet (hidden 8, blocks.py:240-308; its c13 output ReLU'd, Q13), 1 =
+ * UNet (hidden 16, blocks.py:106-237), over F frames [F][3][H][W] (the frame
+ * view x, x_fs, x_grp, x_gs as paig_conv2d_fwd takes it) -> logits
+ * [F][K][H][W].  math: the conv arithmetic flag (128 split, 256 bf16, 0
+ * fp32).  w[i], b[i]: conv i's weight [Cout][Cin][k][k] and bias in plan
+ * order (c1, c2, ...).  The workspace (paig_unet_workspace bytes, 256-byte
+ * aligned) holds the activations, weight images and pool codes from the
+ * forward for the backward, which takes the same arguments plus the logits
+ * and d logits (d of the output after its activation) and writes every conv's
+ * [weight | bias] gradient to dwb[i] (contiguous, overwritten).  The same
+ * kernels in the same order as the Python engine's U-Net stages. */
+size_t paig_unet_workspace(int net, int F, int H, int K, int math);
+int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
+                  const float* const* w, const float* const* b, float* logits, void* ws, size_t ws_bytes,
+                  void* stream);
+int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
+                  const float* const* w, const float* logits, const float* dlogits, float* const* dwb, void* ws,
+                  size_t ws_bytes, void* stream);
+
 /* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,
                       void* stream);
