@@ -349,6 +349,38 @@ int paig_head_l2_bwd(const float* h2, const float* h3, const float* dpos, const 
                      float* const* dW1, float* const* db1, float* const* dW2, float* const* db2, float* const* part,
                      const int* P, void* stream);
 
+/* ---- composites (csrc/composite.hip): each stage as one call each way.
+ * The localiser (blocks.py:98-102): x1 [K*F][n1] masked (pooled) objects ->
+ * h1, h2 [K*F][IN], h3 [K*F][2], pos [F][2K]; the backward from d pos writes
+ * [W1 | b1], [W2 | b2], [W3 | b3] (contiguous, overwritten) and dx1 (nullable).
+ * math: paig_gemm_ex's (the step uses 6).  Workspace paig_localiser_workspace
+ * bytes (shared by both calls, nothing kept between them). */
+size_t paig_localiser_workspace(int F, int K, int n1, int IN, int math);
+int paig_localiser_fwd(const float* x1, const float* W1, const float* b1, const float* W2, const float* b2,
+                       const float* W3, const float* b3, float* h1, float* h2, float* h3, float* pos, int F, int K,
+                       int n1, int IN, float half, int math, void* ws, size_t ws_bytes, void* stream);
+int paig_localiser_bwd(const float* dpos, const float* x1, const float* h1, const float* h2, const float* h3,
+                       const float* W1, const float* W2, const float* W3, float* dl1, float* dl2, float* dl3,
+                       float* dx1, int F, int K, int n1, int IN, float half, int math, void* ws, size_t ws_bytes,
+                       void* stream);
+/* The velocity encoder MLP + the physics rollout (blocks.py:43-48, cells.py,
+ * physics_models.py:231-239): paig_velmlp_fwd then paig_rollout_fwd from the
+ * positions of step S-1.  The backward (rollout adjoint, MLP backward, the
+ * packed input gradient and d pos0 added into dpos [B][Te][2K]) writes the
+ * MLP's [W0|b0|W2|b2|W4|b4] gradient to dmlp (overwritten) and the physics
+ * parameters' to gparam0/1 (fp64; workspace paig_velmlp_rollout_bwd_workspace
+ * bytes).  alt_vel (the linear velocity encoder) is not covered. */
+int paig_velmlp_rollout_fwd(int cell, const float* pos, int B, int Te, int K, int S, const float* W0, const float* b0,
+                            const float* W2, const float* b2, const float* W4, const float* b4, float* X, float* h1,
+                            float* h2, float* vel0, const float* dt, const double* p0, const double* p1, float* pvs,
+                            int R, void* stream);
+size_t paig_velmlp_rollout_bwd_workspace(int B, int K, int S);
+int paig_velmlp_rollout_bwd(int cell, const float* pvs, const float* dpos_roll, const float* dpvs, const float* dt,
+                            const double* p0, const double* p1, const float* X, const float* h1, const float* h2,
+                            const float* W0, const float* W2, const float* W4, float* dpos, float* dmlp,
+                            double* gparam0, double* gparam1, int B, int Te, int K, int S, int R, void* ws,
+                            size_t ws_bytes, void* stream);
+
 /* ---- velocity encoder input packing (blocks.py:33-45) */
 int paig_vel_pack(const float* pos, float* X, int B, int Te, int K, int S, int alt, void* stream);
 int paig_vel_unpack_add(const float* dX, const float* dpos0, float* dpos, int B, int Te, int K, int S, int alt,

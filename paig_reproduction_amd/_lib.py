@@ -60,6 +60,12 @@ SIGNATURES = {
     "paig_head_bwd_vel_vfn2": (I, [P, P, P, P, P, P, I, I, I, F32, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P,
                                    P]),
     "paig_unet_workspace": (SZ, [I, I, I, I, I]),
+    "paig_localiser_workspace": (SZ, [I, I, I, I, I]),
+    "paig_localiser_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, F32, I, P, SZ, P]),
+    "paig_localiser_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, F32, I, P, SZ, P]),
+    "paig_velmlp_rollout_fwd": (I, [I, P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
+    "paig_velmlp_rollout_bwd_workspace": (SZ, [I, I, I]),
+    "paig_velmlp_rollout_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P, SZ, P]),
     "paig_unet_fwd": (I, [I, I, I, I, I, P, LL, I, LL, P, P, P, P, SZ, P]),
     "paig_unet_bwd": (I, [I, I, I, I, I, P, LL, I, LL, P, P, P, P, P, SZ, P]),
     "paig_maxpool2_fwd": (I, [P, LL, P, LL, I, I, I, I, P]),
@@ -125,7 +131,8 @@ SIGNATURES = {
 _QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported",
           "paig_conv2d_bwd_supported", "paig_velmlp_bwd_blocks",
           "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_l2_bwd_blocks", "paig_head_mask_blocks", "paig_conv_wprep_size", "paig_gemm_workspace", "paig_colsum_workspace",
-          "paig_ps_bytes", "paig_psgemm_workspace", "paig_gemm_parts_size", "paig_gemm_parts", "paig_unet_workspace",
+          "paig_ps_bytes", "paig_psgemm_workspace", "paig_gemm_parts_size", "paig_gemm_parts", "paig_unet_workspace", "paig_localiser_workspace",
+          "paig_velmlp_rollout_bwd_workspace",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
           "paig_decoder_bwd_scratch"}
 
