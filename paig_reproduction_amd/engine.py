@@ -374,6 +374,13 @@ class Engine:
     # fragments and issue MFMAs (the per-tile conversion of paig_gemm_ex
     # bound those launches).  Weights are split once per forward (both
     # orientations), activations / gradients where they are produced.
+    def dense_tail(self):
+        """The localiser's l2 + head as fp32 FMA inside the launches around
+        them (paig_dense_tail_fwd / paig_head_l2_bwd): in split arithmetic,
+        where the 3-MFMA l2 GEMMs were latency-bound launches of their own;
+        bf16 keeps its 1-MFMA l2 GEMMs (faster there).  PAIG_DENSE_TAIL=0: A/B."""
+        return self.gemm_math(self.FWD) == 6 and os.environ.get("PAIG_DENSE_TAIL", "1") != "0"
+
     def use_ps(self):
         return self.gemm_math(self.FWD) == 6 and os.environ.get("PAIG_DENSE_PS", "0") != "0"
 
@@ -719,9 +726,16 @@ class Engine:
             enc_pos = _empty(F * 2 * K, dev)
             L.paig_head_fwd(ptr(h2), ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
                             ptr(enc_pos), F, K, 200, float(H / 2), st)
+        elif not self.dense_tail():
+            self.linear(l1_x, K * F, "encoder.l1", h1, 1, st, ws)
+            self.linear(h1, K * F, "encoder.l2", h2, 1, st, ws)
+            enc_pos = _empty(F * 2 * K, dev)
+            L.paig_head_fwd(ptr(h2), ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
+                            ptr(enc_pos), F, K, 200, float(H / 2), st)
         else:
             # l1 (blocks.py:98) as split-K slabs, then ONE launch for its
             # epilogue, l2 and the position head (blocks.py:99-102)
+            S["dense_tail"] = True
             n1, KF = lay.l1_in, K * F
             enc_pos = _empty(F * 2 * K, dev)
             with self._p("gemm_fwd:encoder.l1", 2 * KF * 200 * n1, 4 * (KF * n1 + 200 * n1)):
@@ -926,7 +940,7 @@ class Engine:
         # ---- position head + localiser MLP backward -> d masked objects
         dh2 = _empty(K * F * 200, dev)
         dh1 = _empty(K * F * 200, dev)
-        fused_l2 = "ps" not in S   # l2's data gradient formed inside the head backward's launch
+        fused_l2 = S.get("dense_tail", False)   # l2's data gradient formed inside the head backward's launch
         hblk = L.paig_head_l2_bwd_blocks(K * F) if fused_l2 else L.paig_head_bwd_blocks(K * F)
         hslab = _empty(hblk * (2 * 200 + 2), dev)
         if fused_l2:
@@ -959,7 +973,7 @@ class Engine:
         if "ps" in S:
             self._dense_bwd_ps(S, dh2, dh1, dobjs, st, ws)
         else:
-            self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", None, None, 0, st, ws, need_dx=False)
+            self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws, need_dx=not fused_l2)
             self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
         # every gradient of the flat buffer's early bucket is final (queued on
         # this stream): the data-parallel all-reduce of that bucket may start
