@@ -100,6 +100,8 @@ int paig_conv2d_fwd_pwc(const float* in, long long in_fs, int in_grp, long long 
  * images for a kernel with cin[i] input / cout[i] output channels (dgrad,
  * dg[i] = 1: cin = the layer's Cout, cout = the layer's Cin) to out[i]
  * (16-byte aligned, paig_conv_wprep_size(cin, cout, ks) 16-bit elements).
+ * dg[i] = 2: a dense layer's weight w[i] [cout][cin] transposed into out[i]
+ * as fp32 [cin][cout] (the dense tail's W2^T, paig_dense_tail_fwd).
  * Fixed 2^8 weight scale, f16 hi/lo, |w| < 256 range-guarded (as in-kernel). */
 long long paig_conv_wprep_size(int cin, int cout, int ks);
 int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
@@ -332,8 +334,10 @@ int paig_head_bwd_vel_vfn2(const float* h2, const float* h3, const float* dpos, 
  * (paig_gemm_parts of objects x W1^T, S slabs of [K*F][IN]) summed + b1 +
  * ReLU -> h1; h2 = ReLU(h1 W2^T + b2) in fp32 FMA; the l3 position head as
  * paig_head_fwd -> h3, pos.  IN <= 200, a multiple of 4; W2t: IN * IN floats
- * of scratch (8-byte aligned) for W2^T.  Two launches (the 200 x 200
- * transpose, then one for the split-K epilogue, l2 and the head). */
+ * (8-byte aligned) holding W2^T when W2 is NULL (paig_conv_wprep's dg = 2
+ * job writes it with the step's other weight images), else scratch that
+ * receives W2^T from a first launch.  Then ONE launch for the split-K
+ * epilogue, l2 and the head. */
 int paig_dense_tail_fwd(const float* part, int S, const float* b1, float* h1, const float* W2, float* W2t,
                         const float* b2, float* h2, const float* W3, const float* b3, float* h3, float* pos, int F,
                         int K, int IN, float half, void* stream);

@@ -1369,6 +1369,18 @@ __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
   int q = 0;
   while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.blk0[q + 1]) ++q;
   const WPrepJob jb = jobs.j[q];
+  if (jb.dg == 2) {   // a dense layer's weight [cout][cin] -> out [cin][cout] fp32 (32 x 32 tiles)
+    __shared__ float T[32][33];
+    const int bl = (int)blockIdx.x - jobs.blk0[q], tx = (bl % ((jb.cin + 31) / 32)) * 32,
+              ty = (bl / ((jb.cin + 31) / 32)) * 32, c = threadIdx.x & 31, r = threadIdx.x >> 5;
+    for (int y = r; y < 32; y += WPREP_T / 32)
+      if (ty + y < jb.cout && tx + c < jb.cin) T[y][c] = jb.w[(long long)(ty + y) * jb.cin + tx + c];
+    __syncthreads();
+    float* o = reinterpret_cast<float*>(jb.out);
+    for (int y = r; y < 32; y += WPREP_T / 32)
+      if (tx + y < jb.cin && ty + c < jb.cout) o[(long long)(tx + y) * jb.cout + ty + c] = T[c][y];
+    return;
+  }
   const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16, NS = (KC + 3) / 4;
   const int NSC = (NS + WPREP_S - 1) / WPREP_S;   // k-step chunks per N-tile
   const int bl = (int)blockIdx.x - jobs.blk0[q], nt = bl / NSC, s0 = (bl % NSC) * WPREP_S;
@@ -1435,6 +1447,10 @@ int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cou
       PAIG_REQUIRE(((uintptr_t)out[i] & 15) == 0, "conv_wprep: job %d output not 16-byte aligned", i);
       jobs.j[q] = WPrepJob{w[i], static_cast<s16x8*>(out[i]), cin[i], cout[i], ks[i], dg[i]};
       jobs.blk0[q] = blocks;
+      if (dg[i] == 2) {   // dense transpose job
+        blocks += (cin[i] + 31) / 32 * ((cout[i] + 31) / 32);
+        continue;
+      }
       const int NS = (ks[i] * ks[i] * ((cin[i] + 7) / 8) + 3) / 4;
       blocks += (cout[i] + 15) / 16 * ((NS + WPREP_S - 1) / WPREP_S);
     }

@@ -654,10 +654,13 @@ int paig_dense_tail_fwd(const float* part, int S, const float* b1, float* h1, co
   if (rows <= 0) return 0;
   PAIG_REQUIRE(S >= 1 && IN > 0 && IN <= TAIL_MAXIN && IN % 4 == 0,
                "dense_tail_fwd: S=%d, IN=%d (<= %d, a multiple of 4)", S, IN, TAIL_MAXIN);
-  PAIG_REQUIRE(W2 && W2t && (reinterpret_cast<uintptr_t>(W2t) & 7) == 0,
-               "dense_tail_fwd: W2 and an 8-byte aligned W2t scratch (IN * IN floats) are required");
-  hipLaunchKernelGGL(transpose_sq_k, dim3(cdiv(IN, 32), cdiv(IN, 32)), dim3(256), 0, (hipStream_t)stream, W2, W2t, IN);
-  PAIG_CHECK_LAUNCH();
+  PAIG_REQUIRE(W2t && (reinterpret_cast<uintptr_t>(W2t) & 7) == 0,
+               "dense_tail_fwd: an 8-byte aligned W2t (IN * IN floats) is required");
+  if (W2) {   // W2^T into the W2t scratch first (else W2t already holds it: paig_conv_wprep dg = 2)
+    hipLaunchKernelGGL(transpose_sq_k, dim3(cdiv(IN, 32), cdiv(IN, 32)), dim3(256), 0, (hipStream_t)stream, W2, W2t,
+                       IN);
+    PAIG_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(dense_tail_fwd_k, dim3(cdiv(rows, TAIL_RB)), dim3(TAIL_NT), 0, (hipStream_t)stream, part, S, b1, h1,
                      W2t, b2, h2, W3, b3, h3, pos, F, K, IN, half);
   PAIG_CHECK_LAUNCH();

@@ -625,12 +625,16 @@ class Engine:
                 if op["src"][0] != "X0":   # the dgrad kernel's images (Q10: none for the input)
                     jobs.append((i, 1, W_, cout, cin, ks))
             sizes = [int(L.paig_conv_wprep_size(j[3], j[4], j[5])) for j in jobs]
-            buf = torch.empty(sum(sizes), dtype=torch.int16, device=dev)
+            if self.dense_tail():
+                # the localiser's W2^T for the fused dense tail, in the same launch
+                jobs.append((-1, 2, self.p("encoder.l2.weight"), 200, 200, 1))
+                sizes.append(2 * 200 * 200)
+            buf = torch.empty(sum(-(-n // 8) * 8 for n in sizes), dtype=torch.int16, device=dev)
             outs, off = [], 0
             for j, n in zip(jobs, sizes):
                 wp[(j[0], j[1])] = buf.data_ptr() + 2 * off
                 outs.append(wp[(j[0], j[1])])
-                off += n
+                off += -(-n // 8) * 8   # 16-byte aligned images
             n = len(jobs)
             L.paig_conv_wprep(n, (ctypes.c_void_p * n)(*[ptr(j[2]) for j in jobs]),
                               (ctypes.c_int * n)(*[j[3] for j in jobs]), (ctypes.c_int * n)(*[j[4] for j in jobs]),
@@ -745,9 +749,13 @@ class Engine:
                 raise PaigError(f"paig_gemm_parts failed (rc={nS}): {L.paig_last_error().decode(errors='replace')}")
             with self._p("dense_tail_fwd", 2 * KF * 200 * 200 + 4 * KF * 200,
                          4 * (nS * KF * 200 + 2 * KF * 200 + 200 * 200 + 2 * KF + 2 * KF)):
-                w2t = _empty(200 * 200, dev)
-                L.paig_dense_tail_fwd(ptr(ws), nS, ptr(self.p("encoder.l1.bias")), ptr(h1),
-                                      ptr(self.p("encoder.l2.weight")), ptr(w2t), ptr(self.p("encoder.l2.bias")), ptr(h2),
+                w2t = S.get("wprep", {}).get((-1, 2))   # W2^T from the step's weight-prep launch
+                w2 = None if w2t is not None else self.p("encoder.l2.weight")
+                if w2t is None:
+                    S["w2t"] = _empty(200 * 200, dev)
+                    w2t = ptr(S["w2t"])
+                L.paig_dense_tail_fwd(ptr(ws), nS, ptr(self.p("encoder.l1.bias")), ptr(h1), ptr(w2), w2t,
+                                      ptr(self.p("encoder.l2.bias")), ptr(h2),
                                       ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
                                       ptr(enc_pos), F, K, 200, float(H / 2), st)
         S.update(masks=masks, objs=objs, l1_x=l1_x, h1=h1, h2=h2, h3=h3, enc_pos=enc_pos)
