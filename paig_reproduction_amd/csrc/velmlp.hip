@@ -384,6 +384,12 @@ __device__ __forceinline__ void head_bwd_block(const float* __restrict__ h2, con
   __shared__ float D3[RB][2];
   const int n0 = blk * RB, rows = K * F, tid = threadIdx.x;
   const int nr = rows - n0 < RB ? rows - n0 : RB;
+  // this thread's first column of h2 for all the block's rows, loaded before
+  // the head's reduction so the two latencies overlap (a load per row inside
+  // the loop below cost one memory round trip per row)
+  float xv[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) xv[r] = tid < IN && r < nr ? h2[(long long)(n0 + r) * IN + tid] : 0.f;
   if (tid < RB * 2) {
     const int r = tid >> 1, j = tid & 1;
     float d = 0.f;
@@ -398,16 +404,22 @@ __device__ __forceinline__ void head_bwd_block(const float* __restrict__ h2, con
   __syncthreads();
   float* s = slab + (long long)blk * (2 * IN + 2);
   for (int u = tid; u < IN; u += blockDim.x) {
+    if (u != tid)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) xv[r] = r < nr ? h2[(long long)(n0 + r) * IN + u] : 0.f;
     const float w0 = W3[u], w1 = W3[IN + u];
     float g0 = 0.f, g1 = 0.f;
-    for (int r = 0; r < nr; ++r) {
-      const long long o = (long long)(n0 + r) * IN + u;
-      const float x = h2[o];
-      g0 = fmaf(D3[r][0], x, g0);
-      g1 = fmaf(D3[r][1], x, g1);
-      const float g = fmaf(D3[r][0], w0, D3[r][1] * w1);
-      dh2[o] = x > 0.f ? g : 0.f;                     // relu' of l2's output (blocks.py:99)
-      if (dstash) dstash[r * IN + u] = x > 0.f ? g : 0.f;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (r < nr) {
+        const long long o = (long long)(n0 + r) * IN + u;
+        const float x = xv[r];
+        g0 = fmaf(D3[r][0], x, g0);
+        g1 = fmaf(D3[r][1], x, g1);
+        const float g = fmaf(D3[r][0], w0, D3[r][1] * w1);
+        dh2[o] = x > 0.f ? g : 0.f;                     // relu' of l2's output (blocks.py:99)
+        if (dstash) dstash[r * IN + u] = x > 0.f ? g : 0.f;
+      }
     }
     s[u] = g0;
     s[IN + u] = g1;
@@ -453,27 +465,20 @@ head_bwd_vfn2_k(const float* __restrict__ h2, const float* __restrict__ h3, cons
 //     l2's data gradient dh1 = (dh2 W2) * (h1 > 0).
 // Plain fp32 FMA throughout: at least as accurate as the split MFMA form.
 // Both launches multiply 8 rows by W2 per block (250 blocks at K*F = 2000):
-// 512 threads = (column pair, K-slice of TSL): a thread holds its two W2
-// rows' (forward) / columns' (backward) slice in registers (loaded at once,
-// one L2 round trip), reads each h1 / dh2 value once from LDS for both
-// columns (packed fp32 FMA), and the slices' partials are summed in LDS in
-// slice order.  IN <= 200 = TNP pairs x TNS slices of TSL.
-constexpr int TAIL_RB = 8, TAIL_NT = 512, TSL = 40, TNS = 5, TNP = 100, TAIL_MAXIN = 2 * TNP;
+// 512 threads = (column quad, K-slice of TSL): a thread holds its four W2
+// rows' (forward, from W2^T) / columns' (backward) slice in registers
+// (float4 loads, coalesced over the quads, all issued at once: one L2 round
+// trip), reads each h1 / dh2 value once from LDS for all four columns
+// (packed fp32 FMA), and the slices' partials are summed in LDS in slice
+// order.  IN <= 200 = TNQ quads x TNS slices of TSL.
+constexpr int TAIL_RB = 8, TAIL_NT = 512, TSL = 20, TNS = 10, TNQ = 50, TAIL_MAXIN = 4 * TNQ;
 
-// columns c0, c0+1 of M [k][IN] over rows k0 .. k0+kn (float2 per row,
-// coalesced over consecutive pairs): wa / wb[j] = the two columns at k0 + 4j + {0..3}
-__device__ __forceinline__ void load_pair_slice(const float* __restrict__ M, int IN, int c0, int k0, int kn,
-                                                float4* wa, float4* wb) {
+// columns c0 .. c0+3 of M [k][IN] over rows k0 .. k0+kn (one float4 per row)
+__device__ __forceinline__ void load_quad_slice(const float* __restrict__ M, int IN, int c0, int k0, int kn,
+                                                float4* w) {
 #pragma unroll
-  for (int j = 0; j < TSL / 4; ++j) {
-    float2 v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      v[q] = 4 * j < kn ? *reinterpret_cast<const float2*>(M + (long long)(k0 + 4 * j + q) * IN + c0)
-                        : make_float2(0.f, 0.f);
-    wa[j] = make_float4(v[0].x, v[1].x, v[2].x, v[3].x);
-    wb[j] = make_float4(v[0].y, v[1].y, v[2].y, v[3].y);
-  }
+  for (int k = 0; k < TSL; ++k)
+    w[k] = k < kn ? *reinterpret_cast<const float4*>(M + (long long)(k0 + k) * IN + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // W2t = W2^T ([IN][IN]; 32 x 32 tiles through LDS)
@@ -487,24 +492,33 @@ __global__ void __launch_bounds__(256) transpose_sq_k(const float* __restrict__ 
     if (bx + y < n && by + tx < n) At[(long long)(bx + y) * n + by + tx] = T[tx][y];
 }
 
-// acc[r] += rows r of X (LDS [TAIL_RB][IN], slice k0..k0+kn) x the pair's
-// slice (wa, wb: the two columns' values at k0 + 4j + {0..3})
-__device__ __forceinline__ void pair_slice(const float* X, int IN, int k0, int kn, const float4* wa, const float4* wb,
-                                           pf32x2* acc) {
+// acc[r][0..1] += rows r of X (LDS [TAIL_RB][IN], slice k0..k0+kn) x the
+// quad's slice w[k] (columns c0 .. c0+3 at row k0 + k)
+__device__ __forceinline__ void quad_slice(const float* X, int IN, int k0, int kn, const float4* w, pf32x2 (*acc)[2]) {
 #pragma unroll
   for (int j = 0; j < TSL / 4; ++j) {
     if (4 * j < kn) {
-      const pf32x2 w0 = {wa[j].x, wb[j].x}, w1 = {wa[j].y, wb[j].y}, w2 = {wa[j].z, wb[j].z}, w3 = {wa[j].w, wb[j].w};
 #pragma unroll
       for (int r = 0; r < TAIL_RB; ++r) {
         const float4 x = *reinterpret_cast<const float4*>(&X[r * IN + k0 + 4 * j]);
-        acc[r] += x.x * w0;
-        acc[r] += x.y * w1;
-        acc[r] += x.z * w2;
-        acc[r] += x.w * w3;
+        const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 wq = w[4 * j + q];
+          acc[r][0] += xs[q] * pf32x2{wq.x, wq.y};
+          acc[r][1] += xs[q] * pf32x2{wq.z, wq.w};
+        }
       }
     }
   }
+}
+
+// the quad's partials of slice ks -> RQ [slice][row][column]
+__device__ __forceinline__ void quad_store(float* RQ, int ks, int c0, pf32x2 (*acc)[2]) {
+#pragma unroll
+  for (int r = 0; r < TAIL_RB; ++r)
+    *reinterpret_cast<float4*>(&RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0]) =
+        make_float4(acc[r][0].x, acc[r][0].y, acc[r][1].x, acc[r][1].y);
 }
 
 __global__ void __launch_bounds__(TAIL_NT)
@@ -514,51 +528,60 @@ dense_tail_fwd_k(const float* __restrict__ part, int S, const float* __restrict_
                  float* __restrict__ pos, int F, int K, int IN, float half) {
   __shared__ __attribute__((aligned(16))) float X1[TAIL_RB * TAIL_MAXIN];
   __shared__ float X2[TAIL_RB * TAIL_MAXIN];
-  __shared__ float RQ[TNS * TAIL_RB * TAIL_MAXIN];
+  __shared__ __attribute__((aligned(16))) float RQ[TNS * TAIL_RB * TAIL_MAXIN];
   const int rows = K * F, n0 = blockIdx.x * TAIL_RB, tid = threadIdx.x;
   const int nr = rows - n0 < TAIL_RB ? rows - n0 : TAIL_RB;
   const long long MN = (long long)rows * IN;
-  // this thread's W2 rows 2p, 2p+1 over K-slice ks, from W2^T (W2t [k][c]:
-  // float2 per k, coalesced over p), loaded first (they fly behind the slab
-  // sums)
-  const int pp = tid % TNP, ks = tid / TNP, c0 = 2 * pp, k0 = ks * TSL;
+  // this thread's W2 rows c0 .. c0+3 over K-slice ks, from W2^T (W2t [k][c]),
+  // loaded first (they fly behind the slab sums)
+  const int qd = tid % TNQ, ks = tid / TNQ, c0 = 4 * qd, k0 = ks * TSL;
   const bool act = ks < TNS && c0 < IN && k0 < IN;
   const int kn = act ? (IN - k0 < TSL ? IN - k0 : TSL) : 0;
-  float4 wa[TSL / 4], wb[TSL / 4];
-  load_pair_slice(W2t, IN, c0, k0, kn, wa, wb);
-  // h1 = ReLU(sum_s part[s] + b1): slab order, as the split-K epilogue
-  for (int e = tid; e < TAIL_RB * IN; e += TAIL_NT) {
-    const int r = e / IN, c = e - r * IN;
-    float v = 0.f;
-    if (r < nr) {
-      const long long o = (long long)(n0 + r) * IN + c;
-      const float* p = part + o;
-      int sq = 0;
-      for (; sq + 8 <= S; sq += 8) {   // 8 slab loads in flight, summed in slab order
-        float t[8];
+  float4 w[TSL];
+  load_quad_slice(W2t, IN, c0, k0, kn, w);
+  // h1 = ReLU(sum_s part[s] + b1): slab order, as the split-K epilogue.  A
+  // thread's TAIL_E elements x 8 slabs are loaded at once (one round trip
+  // per 8 slabs instead of one per element)
+  constexpr int TAIL_E = (TAIL_RB * TAIL_MAXIN + TAIL_NT - 1) / TAIL_NT;
+  float acc1[TAIL_E];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) t[jj] = p[(sq + jj) * MN];
+  for (int q = 0; q < TAIL_E; ++q) acc1[q] = 0.f;
+  for (int sq = 0; sq < S; sq += 8) {
+    float t[TAIL_E][8];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) v += t[jj];
-      }
-      for (; sq < S; ++sq) v += p[sq * MN];
-      v = epi(v + b1[c], ACT_RELU, AUX_NONE, nullptr, 0);
-      h1[o] = v;
+    for (int q = 0; q < TAIL_E; ++q) {
+      const int e = tid + q * TAIL_NT, r = e / IN, c = e - r * IN;
+      const bool ok = e < TAIL_RB * IN && r < nr;
+      const float* p = part + (ok ? (long long)(n0 + r) * IN + c : 0);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) t[q][jj] = ok && sq + jj < S ? p[(sq + jj) * MN] : 0.f;
     }
-    X1[e] = v;
+#pragma unroll
+    for (int q = 0; q < TAIL_E; ++q)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj)
+        if (sq + jj < S) acc1[q] += t[q][jj];
+  }
+#pragma unroll
+  for (int q = 0; q < TAIL_E; ++q) {
+    const int e = tid + q * TAIL_NT, r = e / IN, c = e - r * IN;
+    if (e < TAIL_RB * IN) {
+      float v = 0.f;
+      if (r < nr) {
+        v = epi(acc1[q] + b1[c], ACT_RELU, AUX_NONE, nullptr, 0);
+        h1[(long long)(n0 + r) * IN + c] = v;
+      }
+      X1[e] = v;
+    }
   }
   __syncthreads();
   // h2 = ReLU(h1 W2^T + b2)
   if (act) {
-    pf32x2 acc[TAIL_RB];
+    pf32x2 acc[TAIL_RB][2];
 #pragma unroll
-    for (int r = 0; r < TAIL_RB; ++r) acc[r] = pf32x2{0.f, 0.f};
-    pair_slice(X1, IN, k0, kn, wa, wb, acc);
-#pragma unroll
-    for (int r = 0; r < TAIL_RB; ++r) {
-      RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0] = acc[r].x;
-      RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0 + 1] = acc[r].y;
-    }
+    for (int r = 0; r < TAIL_RB; ++r) acc[r][0] = acc[r][1] = pf32x2{0.f, 0.f};
+    quad_slice(X1, IN, k0, kn, w, acc);
+    quad_store(RQ, ks, c0, acc);
   }
   __syncthreads();
   const int nsl = (IN + TSL - 1) / TSL;
@@ -603,7 +626,7 @@ head_l2_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const 
               float half, VelGrad vg, const float* __restrict__ W2, const float* __restrict__ h1,
               float* __restrict__ dh1, int nhead, paig_vfn::VfnBwdTasks T, int nitems) {
   __shared__ __attribute__((aligned(16))) float DH[TAIL_RB * TAIL_MAXIN];
-  __shared__ float RQ[TNS * TAIL_RB * TAIL_MAXIN];
+  __shared__ __attribute__((aligned(16))) float RQ[TNS * TAIL_RB * TAIL_MAXIN];
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= nhead) {
     const int item = ((int)blockIdx.x - nhead) * (TAIL_NT / 64) + (tid >> 6);
@@ -612,25 +635,21 @@ head_l2_bwd_k(const float* __restrict__ h2, const float* __restrict__ h3, const 
   }
   const int n0 = blockIdx.x * TAIL_RB, rows = K * F;
   const int nr = rows - n0 < TAIL_RB ? rows - n0 : TAIL_RB;
-  // this thread's W2 columns 2p, 2p+1 over o-slice ks (float2 per o)
-  const int pp = tid % TNP, ks = tid / TNP, c0 = 2 * pp, k0 = ks * TSL;
+  // this thread's W2 columns c0 .. c0+3 over o-slice ks (float4 per o)
+  const int qd = tid % TNQ, ks = tid / TNQ, c0 = 4 * qd, k0 = ks * TSL;
   const bool act = ks < TNS && c0 < IN && k0 < IN;
   const int kn = act ? (IN - k0 < TSL ? IN - k0 : TSL) : 0;
-  float4 wa[TSL / 4], wb[TSL / 4];
-  load_pair_slice(W2, IN, c0, k0, kn, wa, wb);
+  float4 w[TSL];
+  load_quad_slice(W2, IN, c0, k0, kn, w);
   for (int e = nr * IN + tid; e < TAIL_RB * IN; e += TAIL_NT) DH[e] = 0.f;
   head_bwd_block<TAIL_RB>(h2, h3, dpos, W3, dh2, slab, F, K, IN, half, vg, blockIdx.x, DH);
   __syncthreads();
   if (act) {
-    pf32x2 acc[TAIL_RB];
+    pf32x2 acc[TAIL_RB][2];
 #pragma unroll
-    for (int r = 0; r < TAIL_RB; ++r) acc[r] = pf32x2{0.f, 0.f};
-    pair_slice(DH, IN, k0, kn, wa, wb, acc);
-#pragma unroll
-    for (int r = 0; r < TAIL_RB; ++r) {
-      RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0] = acc[r].x;
-      RQ[(ks * TAIL_RB + r) * TAIL_MAXIN + c0 + 1] = acc[r].y;
-    }
+    for (int r = 0; r < TAIL_RB; ++r) acc[r][0] = acc[r][1] = pf32x2{0.f, 0.f};
+    quad_slice(DH, IN, k0, kn, w, acc);
+    quad_store(RQ, ks, c0, acc);
   }
   __syncthreads();
   const int nsl = (IN + TSL - 1) / TSL;

@@ -42,10 +42,10 @@ def main():
     def gemm():
         S[0] = L.paig_gemm_parts(0, 1, KF, IN, n1, X.data_ptr(), n1, W1.data_ptr(), n1, part.data_ptr(), nparts, 6, st)
 
-    w2t = torch.empty(IN * IN, device=dev)
+    w2t = W2.t().contiguous()   # as paig_conv_wprep's dg = 2 job leaves it
 
     def tail():
-        L.paig_dense_tail_fwd(part.data_ptr(), S[0], b1.data_ptr(), h1.data_ptr(), W2.data_ptr(), w2t.data_ptr(),
+        L.paig_dense_tail_fwd(part.data_ptr(), S[0], b1.data_ptr(), h1.data_ptr(), None, w2t.data_ptr(),
                               b2.data_ptr(),
                               h2.data_ptr(), W3.data_ptr(), b3.data_ptr(), h3.data_ptr(), pos.data_ptr(), F, K, IN,
                               float(16.0), st)
