@@ -679,10 +679,12 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       // backward, align_corners=False: source s gets outputs 2s-1 .. 2s+2
       // with weights 1/4, 3/4, 3/4, 1/4; 1 at the clamped edges), in
       // upsample_bwd_k's per-pixel order; then ReLU' of the source and the
-      // store.  Item = 4 consecutive source pixels of one row: full-resolution
-      // columns 8q-1 .. 8q+8 of 4 rows (two float4 + 2 edge values per row)
-      constexpr int HS = H / 2, WS = W / 2, WQ = WS / 4, NO = CIN * (RT / 2) * WQ;
-      static_assert(WS % 4 == 0, "4-pixel source items");
+      // store.  Item = IK (4, or 2 where the source width is not a multiple
+      // of 4: 3bp's 18) consecutive source pixels of one row: full-resolution
+      // columns 2 IK q - 1 .. 2 IK q + 2 IK of 4 rows
+      constexpr int HS = H / 2, WS = W / 2, IK = WS % 4 == 0 ? 4 : 2, WQ = WS / IK, NO = CIN * (RT / 2) * WQ;
+      static_assert(WS % IK == 0, "IK-pixel source items");
+      typedef float fIK __attribute__((ext_vector_type(IK)));
       for (int o = tid; o < NO; o += 256) {
         const int q = o % WQ, sr = (o / WQ) % (RT / 2), ci = o / (WQ * (RT / 2));
         const int sy = y0 / 2 + sr;
@@ -691,20 +693,28 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
         wy[1] = sy == 0 ? 1.f : 0.75f;
         wy[2] = sy == HS - 1 ? 1.f : 0.75f;
         wy[3] = sy <= HS - 2 ? 0.25f : 0.f;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        fIK acc;
+#pragma unroll
+        for (int k = 0; k < IK; ++k) acc[k] = 0.f;
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           // full row 2sy - 1 + a = tile dX row 2sr + a (row 0 = y0 - 1)
           if (wy[a] == 0.f) continue;
-          const float* rp = U + ci * C::UPP + (2 * sr + a) * W + 8 * q;
-          const f32x4 m0 = *reinterpret_cast<const f32x4*>(rp), m1 = *reinterpret_cast<const f32x4*>(rp + 4);
-          const float l = q > 0 ? rp[-1] : 0.f, r = q < WQ - 1 ? rp[8] : 0.f;
-          // source pixels 4q + k read columns 8q + 2k - 1 .. 8q + 2k + 2
-          const float c[10] = {l, m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3], r};
-          f32x4 row;
+          const float* rp = U + ci * C::UPP + (2 * sr + a) * W + 2 * IK * q;
+          float c[2 * IK + 2];
+          c[0] = q > 0 ? rp[-1] : 0.f;
+          c[2 * IK + 1] = q < WQ - 1 ? rp[2 * IK] : 0.f;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int sx = 4 * q + k;
+          for (int h = 0; h < IK / 2; ++h) {
+            const f32x4 m = *reinterpret_cast<const f32x4*>(rp + 4 * h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) c[1 + 4 * h + e] = m[e];
+          }
+          // source pixels IK q + k read columns 2 IK q + 2k - 1 .. 2 IK q + 2k + 2
+          fIK row;
+#pragma unroll
+          for (int k = 0; k < IK; ++k) {
+            const int sx = IK * q + k;
             float wx[4];
             wx[0] = sx >= 1 ? 0.25f : 0.f;
             wx[1] = sx == 0 ? 1.f : 0.75f;
@@ -717,18 +727,18 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
             row[k] = v;
           }
 #pragma unroll
-          for (int k = 0; k < 4; ++k) acc[k] = fmaf(wy[a], row[k], acc[k]);
+          for (int k = 0; k < IK; ++k) acc[k] = fmaf(wy[a], row[k], acc[k]);
         }
         if (f0 < F) {
-          const long long off = ((long long)ci * HS + sy) * WS + 4 * q;
+          const long long off = ((long long)ci * HS + sy) * WS + IK * q;
           float* op = dx.frame(f0) + off;
-          if (flags & 4) acc += *reinterpret_cast<const f32x4*>(op);
+          if (flags & 4) acc += *reinterpret_cast<const fIK*>(op);
           if (flags & 2) {
-            const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f0) + off);
+            const fIK m = *reinterpret_cast<const fIK*>(aux.frame(f0) + off);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k] = m[k] > 0.f ? acc[k] : 0.f;
+            for (int k = 0; k < IK; ++k) acc[k] = m[k] > 0.f ? acc[k] : 0.f;
           }
-          *reinterpret_cast<f32x4*>(op) = acc;
+          *reinterpret_cast<fIK*>(op) = acc;
         }
       }
     } else {
@@ -872,7 +882,7 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // odd rows and 32-channel tiles spill registers in the fused form)
 // the fused-upsample layers (input = the 2x bilinear upsample of a half-
 // resolution source; the upsample's transpose folded into the data gradient)
-#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32)
+#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32) X(16, 16, 36)
 // the layers whose output feeds a 2x2 max pool fused into their forward
 // (c2, c4 of the ShallowUNet): the pool's backward folded into the dY
 // staging (flags & 64).  The UNet (mnist) keeps its standalone pools (its
