@@ -192,14 +192,17 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
     *reinterpret_cast<s16x8*>(Dh + (C::ZSLOT + tid) * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (PM != 2) *reinterpret_cast<s16x8*>(Dl + (C::ZSLOT + tid) * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
-  for (int i = tid; i < FPT * ROWS * 2 * OFFX; i += 256) {
-    const int hc = i % (2 * OFFX), r = i / (2 * OFFX);
-    const int xc = hc < OFFX ? hc : W + hc;
-    for (int cq = 0; cq < CQ; ++cq) {
+  // (UPS: again at every tile's staging -- the epilogue parks the tile's
+  // full-resolution dX over the X image, halo columns included)
+  auto zero_xhalo = [&]() {
+    for (int i = tid; i < FPT * ROWS * 2 * OFFX * CQ; i += 256) {
+      const int cq = i % CQ, hc = (i / CQ) % (2 * OFFX), r = i / (CQ * 2 * OFFX);
+      const int xc = hc < OFFX ? hc : W + hc;
       *reinterpret_cast<s16x4*>(Xh + xplane(cq) + (r * TWX + xc) * 4) = s16x4{0, 0, 0, 0};
       if (PM != 2) *reinterpret_cast<s16x4*>(Xl + xplane(cq) + (r * TWX + xc) * 4) = s16x4{0, 0, 0, 0};
     }
-  }
+  };
+  zero_xhalo();
 
   // ---- scales (PM 0): X per launch (ecx), dY per tile (ecd), the
   // data-gradient weights per output channel (ewn)
@@ -537,6 +540,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       // taps and source reads), stored as two 2-pixel staging units
       const int y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
+      zero_xhalo();
       __syncthreads();
       constexpr int W4 = W / 4;
 #pragma unroll 1
@@ -890,7 +894,7 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // those that measured faster fused are listed (c2, c17: 16 -> 16 at 64 x 64;
 // c3: 16 -> 32 at 32 x 32); its wider or 1-block-per-CU shapes (c4 / c14,
 // c15's upsample, c16) measured 14-40% slower than the separate kernels
-#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16)
+#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16) X(16, 16, 64)
 #define PAIG_BWD_SHAPES(X)                                                                  \
   X(8, 8, 32) X(8, 16, 16) X(16, 16, 16) X(16, 32, 8) X(32, 32, 8) X(32, 16, 16) X(24, 8, 32) \
   X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(32, 16, 18) X(24, 8, 36)                            \

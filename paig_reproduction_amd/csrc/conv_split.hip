@@ -129,12 +129,14 @@ struct SFwdCfg {
   static constexpr int NL = (NI + 255) / 256;
   static constexpr bool VEC4 = W % 4 == 0;                   // 4-pixel epilogue stores stay in one row
   static_assert(H % RT == 0, "RT divides H");
-  // fused 2x2 max pool of the output (flags & 64): a lane's 4 pixels of row y
-  // (M-tile mt) and of row y + 1 (M-tile mt + PO) are in the same lane when
-  // rows are whole 16-pixel M-tiles and a wave holds whole row pairs
+  // fused 2x2 max pool of the output (flags & 64): rows are whole 16-pixel
+  // M-tiles (PO per row), and a pooling kernel gives each wave MW / 2 column
+  // units of row pairs (pool_mtile): its M-tile mt < MW / 2 on row 2p and
+  // mt + MW / 2 on row 2p + 1, the same columns, so a lane holds both rows of
+  // its windows (64-wide rows: half a row pair per wave)
   static constexpr int PO = W / 16;
-  static constexpr bool POOLOK = !UPS && VEC4 && W % 16 == 0 && PO >= 1 && MW % (2 * PO) == 0 &&
-                                 (MW * 16) % (2 * W) == 0 && TPXV % (2 * W) == 0 && RT % 2 == 0;
+  static constexpr bool POOLOK = !UPS && VEC4 && W % 16 == 0 && PO >= 1 && MW % 2 == 0 && NMT == 4 * MW &&
+                                 TPXV % (2 * W) == 0 && RT % 2 == 0;
 };
 
 // aten max_pool2d's window scan (rows, then columns; a later value replaces
@@ -157,6 +159,19 @@ __device__ __forceinline__ unsigned char pool_code(float a, float b, float c, fl
   if (c > m || c != c) { m = c; k = 2; }
   if (d > m || d != d) { m = d; k = 3; }
   return (unsigned char)((a > 0.f ? 1 : 0) | (b > 0.f ? 2 : 0) | (c > 0.f ? 4 : 0) | (d > 0.f ? 8 : 0) | (k << 4));
+}
+
+// M-tile of wave wv's local tile mt: contiguous, or (fused pool) column unit
+// u = wv MW/2 + mt % (MW/2) of row pair u / PO, top row for mt < MW/2
+template <int MW, int PO, bool POOL>
+__device__ __forceinline__ int fwd_mtile(int wv, int mt) {
+  if constexpr (POOL) {
+    constexpr int HM = MW / 2;
+    const int u = wv * HM + mt % HM;
+    return ((u / PO) * 2 + mt / HM) * PO + u % PO;
+  } else {
+    return wv * MW + mt;
+  }
 }
 
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false>
@@ -213,7 +228,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   int pbase[MW];
 #pragma unroll
   for (int mt = 0; mt < MW; ++mt) {
-    int pix = (wv * MW + mt) * 16 + (lane & 15);
+    int pix = fwd_mtile<MW, C::PO, POOL>(wv, mt) * 16 + (lane & 15);
     if (pix >= C::TPXV) pix = 0;   // padding rows of the last M-tile: finite data, never stored
     const int fi = pix / (RT * W), rem = pix % (RT * W);
     pbase[mt] = (fi * ROWS + rem / W) * RP + (rem % W) * PS;
@@ -497,7 +512,7 @@ if constexpr (W % 4 == 0) {
       f32x4 vv[MW];   // the stored values (fused pool)
 #pragma unroll
       for (int mt = 0; mt < MW; ++mt) {
-        const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+        const int pix = fwd_mtile<MW, C::PO, POOL>(wv, mt) * 16 + (lane >> 4) * 4;
         if constexpr (C::VEC4) {
           // 4 pixels of one row (rows hold a multiple of 4 pixels)
           if (pix >= C::TPXV) continue;
@@ -540,16 +555,16 @@ if constexpr (W % 4 == 0) {
       }
       if constexpr (POOL) {
         {
-          // rows y (M-tile mt) and y + 1 (mt + PO) -> pooled row y / 2, columns x/2, x/2 + 1
+          // rows y (local M-tile mt) and y + 1 (mt + MW/2) -> pooled row y / 2,
+          // columns x/2, x/2 + 1
 #pragma unroll
-          for (int mt = 0; mt < MW; ++mt) {
-            if ((mt / C::PO) % 2 != 0) continue;
-            const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+          for (int mt = 0; mt < MW / 2; ++mt) {
+            const int pix = fwd_mtile<MW, C::PO, POOL>(wv, mt) * 16 + (lane >> 4) * 4;
             if (pix >= C::TPXV) continue;
             const int fi = pix / (RT * W), rem = pix % (RT * W);
             const int y = y0 + rem / W, x = rem % W, f = f0 + fi;
             if (f >= F) continue;
-            const f32x4 a = vv[mt], b = vv[mt + C::PO];
+            const f32x4 a = vv[mt], b = vv[mt + MW / 2];
             const float2 o = make_float2(pool4(a[0], a[1], b[0], b[1]), pool4(a[2], a[3], b[2], b[3]));
             *reinterpret_cast<float2*>(pout.frame(f) + (long long)co * (HW / 4) + (y / 2) * (W / 2) + x / 2) = o;
             if (pout.code) {   // the two windows' codes (PoolOut): ReLU' bits + argmax

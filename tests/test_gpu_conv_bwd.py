@@ -47,12 +47,11 @@ def _wprep(w, cin, cout):
     return buf
 
 
-def _fused(x, w, dy, dx0, aux, mode, xmax, wprep=None):
+def _fused(x, w, dy, dx0, aux, mode, xmax, wprep=None, nmax=512):
     F_, cin, hw = x.shape[0], x.shape[1], x.shape[2]
     cout = w.shape[0]
     dx = dx0.clone()
     flags = mode | (4 if dx0.abs().sum() > 0 else 0) | (2 if aux is not None else 0)
-    nmax = 512
     slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
     nb = ctypes.c_int(0)
     L().paig_conv2d_bwd(p(x), cin * hw * hw, 0, 0, p(dy), cout * hw * hw, p(dx), cin * hw * hw, p(aux),
@@ -93,7 +92,8 @@ def _ref(x, w, dy, dx0, aux):
 def test_fused_backward_matches_fp64(cin, cout, hw, mode):
     assert L().paig_conv2d_bwd_supported(cin, cout, hw, hw, 3, mode) == 1
     tol = TOL[mode]
-    for F_, relu_acc in ((5, True), (3, False), (1, True)):
+    # nmax 2: two persistent blocks walk every tile
+    for F_, relu_acc, nmax in ((5, True, 512), (3, False, 512), (1, True, 512), (5, True, 2)):
         torch.manual_seed(cin * 1000 + cout * 10 + hw + F_)
         x = torch.relu(torch.randn(F_, cin, hw, hw, device=DEV))
         w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.2
@@ -102,7 +102,7 @@ def test_fused_backward_matches_fp64(cin, cout, hw, mode):
         dx0 = torch.full((F_, cin, hw, hw), 0.5, device=DEV) if relu_acc else torch.zeros(F_, cin, hw, hw, device=DEV)
         aux = x if relu_acc else None
         xmax = _xmax_of(x, w, b, mode) if mode == 128 else None
-        dx, gw, gb = _fused(x, w, dy, dx0, aux, mode, xmax)
+        dx, gw, gb = _fused(x, w, dy, dx0, aux, mode, xmax, nmax=nmax)
         rdx, rgw, rgb = _ref(x, w, dy, dx0, aux)
         assert rel_err(dx, rdx) <= tol, ("dx", F_)
         assert rel_err(gw, rgw) <= tol, ("dw", F_)
@@ -188,7 +188,9 @@ def test_fused_backward_upsample_input(cin, cout, hw, mode):
     autograd through F.interpolate + conv2d is the reference."""
     assert L().paig_conv2d_bwd_supported(cin, cout, hw, hw, 3, mode | 32) == 1
     tol = TOL[mode]
-    for F_ in (3, 1):
+    # nmax 2: two persistent blocks walk every tile (the staging of a block's
+    # later tiles must not see what its earlier tiles left in the LDS)
+    for F_, nmax in ((3, 512), (1, 512), (3, 2)):
         torch.manual_seed(cin + cout + hw + F_)
         xs = torch.relu(torch.randn(F_, cin, hw // 2, hw // 2, device=DEV))
         w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.2
@@ -207,7 +209,6 @@ def test_fused_backward_upsample_input(cin, cout, hw, mode):
             L().paig_conv2d_fwd_ex(p(xs), cin * hs * hs, 0, 0, p(out), cout * hw * hw, None, 0, p(w), p(b), F_, cin,
                                    cout, hw, hw, 3, 32 | mode, p(xmax), XMAX_SLOTS, st())
         dx = torch.full((F_, cin, hs, hs), float("nan"), device=DEV)   # write mode: every element written
-        nmax = 512
         slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
         nb = ctypes.c_int(0)
         L().paig_conv2d_bwd(p(xs), cin * hs * hs, 0, 0, p(dy), cout * hw * hw, p(dx), cin * hs * hs, p(xs),
@@ -225,7 +226,7 @@ def test_fused_backward_upsample_input(cin, cout, hw, mode):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16)])
+@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16), (16, 16, 64)])
 def test_fused_backward_pool_fold(cin, cout, hw, mode):
     """c2 / c4 (blocks.py:249-250, 253-254): the layer's ReLU'd output feeds
     the skip concat AND a 2x2 max pool.  The forward's fused pool writes one
@@ -236,7 +237,7 @@ def test_fused_backward_pool_fold(cin, cout, hw, mode):
     assert L().paig_conv2d_bwd_supported(cin, cout, hw, hw, 3, mode | 64) == 1
     tol = TOL[mode]
     hp = hw // 2
-    for F_ in (4, 1):
+    for F_, nmax in ((4, 512), (1, 512), (4, 2)):   # nmax 2: blocks walk many tiles
         torch.manual_seed(cin + cout + hw + F_ + mode)
         x = torch.relu(torch.randn(F_, cin, hw, hw, device=DEV))
         w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.2
@@ -267,7 +268,6 @@ def test_fused_backward_pool_fold(cin, cout, hw, mode):
         rdw = torch.nn.grad.conv2d_weight(xd, wd.shape, dpre, padding=1)
         rdb = dpre.sum((0, 2, 3))
         dx = torch.full((F_, cin, hw, hw), float("nan"), device=DEV)
-        nmax = 512
         slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
         nb = ctypes.c_int(0)
         L().paig_conv2d_bwd(p(x), cin * hw * hw, 0, 0, p(gy), cout * hw * hw, p(dx), cin * hw * hw, p(x),

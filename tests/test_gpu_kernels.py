@@ -599,7 +599,7 @@ def test_conv_wprep_bit_identical(cin, cout, hw, ks, up):
         assert torch.equal(dxs[0], dxs[1])
 
 
-@pytest.mark.parametrize("cin,cout,hw,mode", [(8, 8, 32, 128), (16, 16, 16, 128), (8, 8, 32, 256), (3, 8, 32, 128)])
+@pytest.mark.parametrize("cin,cout,hw,mode", [(8, 8, 32, 128), (16, 16, 16, 128), (8, 8, 32, 256), (3, 8, 32, 128), (16, 16, 64, 128), (32, 32, 32, 128), (32, 32, 32, 256), (64, 64, 16, 128)])
 def test_conv_fused_pool(cin, cout, hw, mode):
     """Split forward with the fused 2x2 max pool (flags & 64): the conv output
     is unchanged and the pooled output is bit-identical to paig_maxpool2_fwd
