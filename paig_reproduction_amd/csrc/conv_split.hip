@@ -589,6 +589,10 @@ if constexpr (W % 4 == 0) {
 }
 
 // ===================================================================== wgrad
+#ifndef PAIG_WG_UPS_OB
+#define PAIG_WG_UPS_OB 32
+#endif
+
 // waves splitting the N-tiles: as few as keep <= 40 accumulators per lane
 constexpr int swg_wn(int MT, int NT) { return MT * NT * 4 <= 40 ? 1 : (MT * ceil_div(NT, 2) * 4 <= 40 ? 2 : 4); }
 // LDS of a wgrad block staging CINB input and COUTB output-gradient channels
@@ -616,7 +620,7 @@ constexpr int swg_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM
     for (int cb : ci) {
       if (cb > CIN || CIN % cb != 0 || (cb != CIN && cb % 4 != 0)) continue;
       for (int ob : oc) {
-        if (ob > COUT || COUT % ob != 0 || (UPS && ob > 16)) continue;   // UPS: dY staging registers
+        if (ob > COUT || COUT % ob != 0 || (UPS && ob > (pass ? PAIG_WG_UPS_OB : 16))) continue;   // UPS: dY staging registers
         const int MT = ceil_div(ob, 16), NT = ceil_div(KS * KS * ceil_div(cb, 4), 4);
         if (MT * ceil_div(NT, 4) * 4 > 40 || swg_lds(cb, ob, H, W, KS, UPS, PM) > (pass == 0 ? LDS_MAX / 2 : LDS_MAX))
           continue;
@@ -689,7 +693,8 @@ struct SWgCfg {
   // (narrow whole-layer blocks only: the 32-wide / channel-sliced ones need
   // more than the 168 registers of 3 waves)
   static constexpr int MINW =
-      3 * LDS <= 160 * 1024 && NSI * NSO == 1 && (CIN <= 24 || (UPS && COUT <= 16)) && !(MT == 2 && FPT > 1) ? 3 : 2;
+      2 * LDS > 160 * 1024 ? 1
+      : 3 * LDS <= 160 * 1024 && NSI * NSO == 1 && (CIN <= 24 || (UPS && COUT <= 16)) && !(MT == 2 && FPT > 1) ? 3 : 2;
   static_assert(H % RT == 0, "RT divides H");
   static_assert(TPXV % DU == 0, "dY units");
 };

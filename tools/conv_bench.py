@@ -21,6 +21,12 @@ LAYERS = [("c1", 3, 8, 32, 3, 0), ("c2", 8, 8, 32, 3, 0), ("c3", 8, 16, 16, 3, 0
           ("c5", 16, 32, 8, 3, 0), ("c6", 32, 32, 8, 3, 0), ("c7", 32, 16, 16, 3, 1), ("c8", 32, 16, 16, 3, 0),
           ("c9", 16, 16, 16, 3, 0), ("c10", 16, 16, 32, 3, 1), ("c11", 24, 8, 32, 3, 0), ("c12", 8, 8, 32, 3, 0),
           ("c13", 8, 2, 32, 1, 0)]
+# UNet(hidden 16) at 64x64 (mnist), selected as u1 .. u18
+LAYERS += [("u%d" % (i + 1),) + l for i, l in enumerate([
+    (3, 16, 64, 3, 0), (16, 16, 64, 3, 0), (16, 32, 32, 3, 0), (32, 32, 32, 3, 0), (32, 64, 16, 3, 0),
+    (64, 64, 16, 3, 0), (64, 128, 8, 3, 0), (128, 128, 8, 3, 0), (128, 32, 16, 3, 1), (96, 64, 16, 3, 0),
+    (64, 64, 16, 3, 0), (64, 32, 32, 3, 1), (64, 32, 32, 3, 0), (32, 32, 32, 3, 0), (32, 32, 64, 3, 1),
+    (48, 16, 64, 3, 0), (16, 16, 64, 3, 0), (16, 2, 64, 1, 0)])]
 
 
 def main():
