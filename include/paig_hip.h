@@ -169,6 +169,11 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
 /* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,
                       void* stream);
+/* the same pooled values plus the window codes a folded pool backward reads
+ * (paig_conv2d_bwd flags & 64; layout and bits as paig_conv2d_fwd_pwc's fused
+ * pool writes them), for layers whose forward conv cannot pool in its epilogue */
+int paig_maxpool2_fwd_codes(const float* x, long long x_fs, float* y, long long y_fs, unsigned char* code,
+                            long long code_fs, int F, int C, int H, int W, void* stream);
 /* dx = (dx + scatter_argmax(dy)) * (x > 0) */
 int paig_maxpool2_bwd_relu(const float* x, long long x_fs, const float* dy, long long dy_fs, float* dx, long long dx_fs,
                            int F, int C, int H, int W, void* stream);

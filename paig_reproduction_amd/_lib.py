@@ -69,6 +69,7 @@ SIGNATURES = {
     "paig_unet_fwd": (I, [I, I, I, I, I, P, LL, I, LL, P, P, P, P, SZ, P]),
     "paig_unet_bwd": (I, [I, I, I, I, I, P, LL, I, LL, P, P, P, P, P, SZ, P]),
     "paig_maxpool2_fwd": (I, [P, LL, P, LL, I, I, I, I, P]),
+    "paig_maxpool2_fwd_codes": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
     "paig_maxpool2_bwd_relu": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
     "paig_upsample2_fwd": (I, [P, LL, P, LL, I, I, I, I, I, I, P]),
     "paig_upsample2_bwd": (I, [P, LL, P, LL, P, LL, I, I, I, I, I, I, I, P]),

@@ -74,9 +74,9 @@ constexpr int sbwd_minw(int CIN, int COUT, int H, int PM, bool PF) {
   if (CIN == 8 && COUT == 8 && H == 32) return PF ? 3 : 4;
   if (PM == 2 && CIN == 8 && COUT == 16 && H == 16) return 3;
   if (PM == 2 && CIN == 24 && COUT == 8 && H == 32) return 3;
-  if (CIN == 8 && COUT == 8 && H == 36) return 3;
+  if (CIN == 8 && COUT == 8 && H == 36) return PF ? 2 : 3;
   if (CIN == 8 && COUT == 16 && H == 18) return PM == 2 ? 4 : 3;
-  if (CIN == 16 && COUT == 16 && H == 18) return 3;
+  if (CIN == 16 && COUT == 16 && H == 18) return PF ? 2 : 3;
   return 2;
 }
 
@@ -894,7 +894,7 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // those that measured faster fused are listed (c2, c17: 16 -> 16 at 64 x 64;
 // c3: 16 -> 32 at 32 x 32); its wider or 1-block-per-CU shapes (c4 / c14,
 // c15's upsample, c16) measured 14-40% slower than the separate kernels
-#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16) X(16, 16, 64)
+#define PAIG_BWD_POOL_SHAPES(X) X(8, 8, 32) X(16, 16, 16) X(16, 16, 64) X(8, 8, 36) X(16, 16, 18)
 #define PAIG_BWD_SHAPES(X)                                                                  \
   X(8, 8, 32) X(8, 16, 16) X(16, 16, 16) X(16, 32, 8) X(32, 32, 8) X(32, 16, 16) X(24, 8, 32) \
   X(8, 8, 36) X(8, 16, 18) X(16, 16, 18) X(32, 16, 18) X(24, 8, 36)                            \

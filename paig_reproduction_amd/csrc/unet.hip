@@ -173,10 +173,15 @@ bool pool_fused(const UPlan& p, int i, int H, int cm) {
   return nx.kind == U_POOL && nx.src == op.dst &&
          paig_conv2d_mfma_supported(0, op.src.n, op.dst.n, Hl, Hl, op.ks, cm | 64);
 }
+// (the codes come from the fused pool, or from the standalone pool where the
+// forward cannot fuse it: paig_maxpool2_fwd_codes)
 bool pool_folded(const UPlan& p, int i, int H, int cm) {
   const UOp& op = p.ops[i];
+  if (op.kind != U_CONV || i + 1 >= (int)p.ops.size() || cm == 0 || p.fused_up[i] >= 0) return false;
+  const UOp& nx = p.ops[i + 1];
   const int Hl = H / p.bufs[op.dst.buf].lvl;
-  return pool_fused(p, i, H, cm) && paig_conv2d_bwd_supported(op.src.n, op.dst.n, Hl, Hl, op.ks, cm | 64);
+  return nx.kind == U_POOL && nx.src == op.dst &&
+         paig_conv2d_bwd_supported(op.src.n, op.dst.n, Hl, Hl, op.ks, cm | 64);
 }
 
 constexpr int NBLK_MAX = 1024;   // slab rows per conv (engine.py: nblk_max)
@@ -342,7 +347,11 @@ int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long l
       int slvl;
       const View sv = view(op.src, slvl);
       const int Hl = H / slvl;
-      rc = paig_maxpool2_fwd(sv.p, sv.fs, const_cast<float*>(dv.p), dv.fs, F, op.src.n, Hl, Hl, stream);
+      rc = L.pcode[i] != (size_t)-1
+               ? paig_maxpool2_fwd_codes(sv.p, sv.fs, const_cast<float*>(dv.p), dv.fs,
+                                         reinterpret_cast<unsigned char*>(base + L.pcode[i]), L.pcode_fs[i], F,
+                                         op.src.n, Hl, Hl, stream)
+               : paig_maxpool2_fwd(sv.p, sv.fs, const_cast<float*>(dv.p), dv.fs, F, op.src.n, Hl, Hl, stream);
     } else {
       int slvl;
       const View sv = view(op.src, slvl);

@@ -12,12 +12,16 @@
 namespace {
 
 // ---------------------------------------------------------------- maxpool ----
+// The scalar (any-width) kernels are templated on the flat index type: 32-bit
+// wherever the element count allows (3bp's 18 / 9-wide levels; 64-bit integer
+// division is a long instruction sequence per element)
+template <typename I>
 __global__ void maxpool_fwd_k(FView x, FViewW y, int F, int C, int H, int W) {
   const int Ho = H / 2, Wo = W / 2;
-  const long long n = (long long)F * C * Ho * Wo;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+  const I n = (I)F * C * Ho * Wo;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < n; i += (I)gridDim.x * blockDim.x) {
     int j = i % Wo;
-    long long t = i / Wo;
+    I t = i / Wo;
     int ii = t % Ho;
     t /= Ho;
     int c = t % C;
@@ -36,12 +40,13 @@ __global__ void maxpool_fwd_k(FView x, FViewW y, int F, int C, int H, int W) {
 }
 
 // dx = (dx_existing + [argmax] * dy) * (x > 0), one thread per input pixel.
+template <typename I>
 __global__ void maxpool_bwd_relu_k(FView x, FView dy, FViewW dx, int F, int C, int H, int W) {
   const int Ho = H / 2, Wo = W / 2;
-  const long long n = (long long)F * C * H * W;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+  const I n = (I)F * C * H * W;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < n; i += (I)gridDim.x * blockDim.x) {
     int xx = i % W;
-    long long t = i / W;
+    I t = i / W;
     int yy = t % H;
     t /= H;
     int c = t % C;
@@ -94,6 +99,29 @@ __global__ void maxpool_fwd_v_k(FView x, FViewW y, int F, int C, int H, int W) {
   }
 }
 
+// The standalone pool's forward for a layer whose backward folds the pool
+// (paig_conv2d_bwd flags & 64) where the conv's forward cannot pool in its
+// epilogue (rows not whole 16-pixel M-tiles: 3bp's 36 / 18): the pooled
+// values (maxpool_fwd_k's scan order, bit-identical) and one code byte per
+// (channel, window) in the layout the fused pool writes (conv_split.hip
+// pool_code): ReLU' bits of the window's pixels (y, x), (y, x+1), (y+1, x),
+// (y+1, x+1) in bits 0..3, the argmax in bits 4..5; [C/8][H/2][W/2][C%8]
+__global__ void maxpool_fwd_codes_k(FView x, FViewW y, unsigned char* __restrict__ code, long long code_fs, int F, int C,
+                                    int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int n = F * C * Ho * Wo;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int j = i % Wo, t = i / Wo, pi = t % Ho, fc = t / Ho, c = fc % C, f = fc / C;
+    const float* xp = x.frame(f) + ((long long)c * H + 2 * pi) * W + 2 * j;
+    const float a = xp[0], b = xp[1], cc = xp[W], d = xp[W + 1];
+    float m;
+    const int am = argmax4(a, b, cc, d, m);
+    y.frame(f)[((long long)c * Ho + pi) * Wo + j] = m;
+    code[(long long)f * code_fs + (((long long)(c >> 3) * Ho + pi) * Wo + j) * 8 + (c & 7)] =
+        (unsigned char)((a > 0.f ? 1 : 0) | (b > 0.f ? 2 : 0) | (cc > 0.f ? 4 : 0) | (d > 0.f ? 8 : 0) | (am << 4));
+  }
+}
+
 // dx = (dx + [argmax] * dy) * (x > 0)
 __global__ void maxpool_bwd_relu_v_k(FView x, FView dy, FViewW dx, int F, int C, int H, int W) {
   const int Ho = H / 2, Q = W / 4;
@@ -140,11 +168,12 @@ __device__ __forceinline__ void up_taps(int dst, int in, int out, int& i0, int& 
   l0 = 1.f - l1;
 }
 
+template <typename I>
 __global__ void upsample_fwd_k(FView s, FViewW u, int F, int C, int Hs, int Ws, int Ho, int Wo) {
-  const long long n = (long long)F * C * Ho * Wo;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+  const I n = (I)F * C * Ho * Wo;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < n; i += (I)gridDim.x * blockDim.x) {
     int x = i % Wo;
-    long long t = i / Wo;
+    I t = i / Wo;
     int y = t % Ho;
     t /= Ho;
     int c = t % C;
@@ -162,12 +191,13 @@ __global__ void upsample_fwd_k(FView s, FViewW u, int F, int C, int Hs, int Ws, 
 
 // ds[sy][sx] = sum over outputs using it (gather form, deterministic), then
 // optionally * (s > 0) (ReLU'd source).
+template <typename I>
 __global__ void upsample_bwd_k(FView du, FView s, FViewW ds, int F, int C, int Hs, int Ws, int Ho, int Wo,
                                int relu_mask) {
-  const long long n = (long long)F * C * Hs * Ws;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+  const I n = (I)F * C * Hs * Ws;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < n; i += (I)gridDim.x * blockDim.x) {
     int sx = i % Ws;
-    long long t = i / Ws;
+    I t = i / Ws;
     int sy = t % Hs;
     t /= Hs;
     int c = t % C;
@@ -882,8 +912,26 @@ int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, 
     return 0;
   }
   long long n = (long long)F * C * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(maxpool_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
+  if (n < (1ll << 31))
+    hipLaunchKernelGGL(maxpool_fwd_k<int>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
                      FViewW{y, y_fs}, F, C, H, W);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_k<long long>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
+                     FViewW{y, y_fs}, F, C, H, W);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_maxpool2_fwd_codes(const float* x, long long x_fs, float* y, long long y_fs, unsigned char* code,
+                            long long code_fs, int F, int C, int H, int W, void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(H % 2 == 0 && W % 2 == 0 && code && code_fs >= (long long)(C + 7) / 8 * 8 * (H / 2) * (W / 2) &&
+                   (long long)F * C * H * W < (1ll << 31),
+               "paig_maxpool2_fwd_codes: needs even H, W, a code frame of C/8 x H/2 x W/2 x 8 bytes (C=%d H=%d W=%d)",
+               C, H, W);
+  const long long n = (long long)F * C * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(maxpool_fwd_codes_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
+                     FViewW{y, y_fs}, code, code_fs, F, C, H, W);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -901,7 +949,11 @@ int paig_maxpool2_bwd_relu(const float* x, long long x_fs, const float* dy, long
     return 0;
   }
   long long n = (long long)F * C * H * W;
-  hipLaunchKernelGGL(maxpool_bwd_relu_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
+  if (n < (1ll << 31))
+    hipLaunchKernelGGL(maxpool_bwd_relu_k<int>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
+                     FView{dy, dy_fs, 0, 0}, FViewW{dx, dx_fs}, F, C, H, W);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_relu_k<long long>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
                      FView{dy, dy_fs, 0, 0}, FViewW{dx, dx_fs}, F, C, H, W);
   PAIG_CHECK_LAUNCH();
   return 0;
@@ -911,7 +963,11 @@ int paig_upsample2_fwd(const float* s, long long s_fs, float* u, long long u_fs,
                        int Wo, void* stream) {
   if (F <= 0) return 0;
   long long n = (long long)F * C * Ho * Wo;
-  hipLaunchKernelGGL(upsample_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{s, s_fs, 0, 0},
+  if (n < (1ll << 31))
+    hipLaunchKernelGGL(upsample_fwd_k<int>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{s, s_fs, 0, 0},
+                     FViewW{u, u_fs}, F, C, Hs, Ws, Ho, Wo);
+  else
+    hipLaunchKernelGGL(upsample_fwd_k<long long>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{s, s_fs, 0, 0},
                      FViewW{u, u_fs}, F, C, Hs, Ws, Ho, Wo);
   PAIG_CHECK_LAUNCH();
   return 0;
@@ -931,7 +987,11 @@ int paig_upsample2_bwd(const float* du, long long du_fs, const float* s, long lo
     return 0;
   }
   long long n = (long long)F * C * Hs * Ws;
-  hipLaunchKernelGGL(upsample_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{du, du_fs, 0, 0},
+  if (n < (1ll << 31))
+    hipLaunchKernelGGL(upsample_bwd_k<int>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{du, du_fs, 0, 0},
+                     FView{s, s_fs, 0, 0}, FViewW{ds, ds_fs}, F, C, Hs, Ws, Ho, Wo, relu_mask);
+  else
+    hipLaunchKernelGGL(upsample_bwd_k<long long>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{du, du_fs, 0, 0},
                      FView{s, s_fs, 0, 0}, FViewW{ds, ds_fs}, F, C, Hs, Ws, Ho, Wo, relu_mask);
   PAIG_CHECK_LAUNCH();
   return 0;

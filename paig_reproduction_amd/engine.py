@@ -657,18 +657,23 @@ class Engine:
                 pool_v = (None, 0)
                 nxt = ops[i + 1] if i + 1 < len(ops) else None
                 pcode = (None, 0)
-                if (nxt is not None and nxt["op"] == "pool" and nxt["src"] == op["dst"] and not xfl and cm
-                        and L.paig_conv2d_mfma_supported(0, op["src"][2], op["dst"][2], Hl, Hl, op["ks"], cm | 64)):
+                pool_next = nxt is not None and nxt["op"] == "pool" and nxt["src"] == op["dst"] and not xfl and cm
+                if pool_next and self._fused_bwd(op["src"][2], op["dst"][2], Hl, op["ks"], cm | 64):
+                    # the pool windows' codes (ReLU' bits + argmax): the
+                    # backward folds the pool into this layer's dY staging.
+                    # Written by this conv's fused pool, or (widths whose rows
+                    # are not whole M-tiles: 3bp) by the standalone pool
+                    cfs = -(-op["dst"][2] // 8) * 8 * (Hl // 2) ** 2
+                    cb = torch.empty(F * cfs, dtype=torch.uint8, device=dev)
+                    S.setdefault("pcode", {})[i + 1] = (cb, cfs)
+                    pcode = (cb.data_ptr(), cfs)
+                if pool_next and L.paig_conv2d_mfma_supported(0, op["src"][2], op["dst"][2], Hl, Hl, op["ks"],
+                                                              cm | 64):
                     pv, _ = view(nxt["dst"])
                     pool_v = (pv[0], pv[1])
                     pooled.add(i + 1)
-                    if self._fused_bwd(op["src"][2], op["dst"][2], Hl, op["ks"], cm | 64):
-                        # the pool windows' codes (ReLU' bits + argmax): the
-                        # backward folds the pool into this layer's dY staging
-                        cfs = -(-op["dst"][2] // 8) * 8 * (Hl // 2) ** 2
-                        cb = torch.empty(F * cfs, dtype=torch.uint8, device=dev)
-                        S.setdefault("pcode", {})[i + 1] = (cb, cfs)
-                        pcode = (cb.data_ptr(), cfs)
+                else:
+                    pcode = (None, 0)
                 W_ = self.p(lay.prefix + op["name"] + ".weight")
                 b_ = self.p(lay.prefix + op["name"] + ".bias")
                 fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
@@ -682,7 +687,12 @@ class Engine:
             elif op["op"] == "pool":
                 sv, slvl = view(op["src"])
                 Hl = H // slvl
-                L.paig_maxpool2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hl, Hl, st)
+                if i in S.get("pcode", {}):
+                    cb, cfs = S["pcode"][i]
+                    L.paig_maxpool2_fwd_codes(sv[0], sv[1], dv[0], dv[1], cb.data_ptr(), cfs, F, op["src"][2], Hl, Hl,
+                                              st)
+                else:
+                    L.paig_maxpool2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hl, Hl, st)
             else:
                 sv, slvl = view(op["src"])
                 Hs, Ho = H // slvl, H // dlvl

@@ -226,7 +226,7 @@ def test_fused_backward_upsample_input(cin, cout, hw, mode):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16), (16, 16, 64)])
+@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16), (16, 16, 64), (8, 8, 36), (16, 16, 18)])
 def test_fused_backward_pool_fold(cin, cout, hw, mode):
     """c2 / c4 (blocks.py:249-250, 253-254): the layer's ReLU'd output feeds
     the skip concat AND a 2x2 max pool.  The forward's fused pool writes one
@@ -250,9 +250,22 @@ def test_fused_backward_pool_fold(cin, cout, hw, mode):
         cfs = -(-cout // 8) * 8 * hp * hp
         code = torch.empty(F_ * cfs, dtype=torch.uint8, device=DEV)
         xmax = torch.zeros(XMAX_SLOTS, device=DEV)
-        L().paig_conv2d_fwd_pwc(p(x), cin * hw * hw, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout,
-                                hw, hw, 3, 1 | 64 | mode, p(xmax) if mode == 128 else None,
-                                XMAX_SLOTS if mode == 128 else 0, p(pool), cout * hp * hp, p(code), cfs, None, st())
+        if L().paig_conv2d_mfma_supported(0, cin, cout, hw, hw, 3, mode | 64):
+            L().paig_conv2d_fwd_pwc(p(x), cin * hw * hw, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), F_, cin,
+                                    cout, hw, hw, 3, 1 | 64 | mode, p(xmax) if mode == 128 else None,
+                                    XMAX_SLOTS if mode == 128 else 0, p(pool), cout * hp * hp, p(code), cfs, None, st())
+        else:
+            # 3bp's 36 / 18: the conv cannot pool in its epilogue; the
+            # standalone pool writes the same codes (paig_maxpool2_fwd_codes)
+            L().paig_conv2d_fwd_pwc(p(x), cin * hw * hw, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), F_, cin,
+                                    cout, hw, hw, 3, 1 | mode, p(xmax) if mode == 128 else None,
+                                    XMAX_SLOTS if mode == 128 else 0, None, 0, None, 0, None, st())
+            assert L().paig_maxpool2_fwd_codes(p(y), cout * hw * hw, p(pool), cout * hp * hp, p(code), cfs, F_, cout,
+                                               hw, hw, st()) == 0
+            ref = torch.empty_like(pool)
+            L().paig_maxpool2_fwd(p(y), cout * hw * hw, p(ref), cout * hp * hp, F_, cout, hw, hw, st())
+            torch.cuda.synchronize()
+            assert torch.equal(pool, ref)   # bit-identical pooled values
         torch.cuda.synchronize()
         xd, wd = x.double().cpu(), w.double().cpu()
         assert rel_err(pool, F.max_pool2d(torch.relu(F.conv2d(xd, wd, b.double().cpu(), padding="same")), 2)) <= tol

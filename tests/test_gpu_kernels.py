@@ -624,6 +624,19 @@ def test_conv_fused_pool(cin, cout, hw, mode):
     assert torch.equal(y0, y1)
     assert torch.equal(pool, ref)
     assert L().paig_conv2d_mfma_supported(0, cin, cout, 36, 36, 3, mode | 64) == 0   # 36-wide rows: no in-lane windows
+    # window codes: the fused pool's and the standalone pool's
+    # (paig_maxpool2_fwd_codes, 3bp's layers) are the same bytes
+    cfs = -(-cout // 8) * 8 * h2 * h2
+    c1 = torch.zeros(F_ * cfs, dtype=torch.uint8, device=DEV)
+    c2 = torch.ones(F_ * cfs, dtype=torch.uint8, device=DEV)
+    pool2 = torch.empty_like(pool)
+    L().paig_conv2d_fwd_pwc(p(x), cin * hw * hw, 0, 0, p(y1), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout, hw,
+                            hw, 3, 1 | mode | 64, None, 0, p(pool), cout * h2 * h2, p(c1), cfs, None, st())
+    L().paig_maxpool2_fwd_codes(p(y0), cout * hw * hw, p(pool2), cout * h2 * h2, p(c2), cfs, F_, cout, hw, hw, st())
+    torch.cuda.synchronize()
+    assert torch.equal(pool2, ref)
+    if cout % 8 == 0:   # (padding channels of a partial 8-channel group are not written)
+        assert torch.equal(c1, c2)
 
 
 @pytest.mark.parametrize("R", [6, 46, 64, 65, 70])
