@@ -140,7 +140,7 @@ struct SBwdCfg {
   static constexpr int MINW = MW0 < LDSB ? MW0 : LDSB;
   static_assert(H % RT == 0, "RT divides H");
   static_assert(KS == 3, "3x3 layers (the 1x1 heads are fused elsewhere)");
-  static_assert(!UPS || (FPT == 1 && RT % 2 == 0 && W % 4 == 0), "fused upsample: whole even row blocks of one frame");
+  static_assert(!UPS || (FPT == 1 && RT % 2 == 0 && W % 2 == 0), "fused upsample: whole even row blocks of one frame");
   // PF: the 2x2 max pool of this layer's output folded into the dY staging
   // (a staging unit's pixel pair is one pooling window's columns)
   static_assert(!PF || (!UPS && UPX == 2 && COUT % 8 == 0 && H % 2 == 0), "pool fold: even widths, 8-channel chunks");
@@ -542,24 +542,41 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       up.commit(Sl, tid);
       zero_xhalo();
       __syncthreads();
-      constexpr int W4 = W / 4;
+      if constexpr (W % 4 == 0) {
+        constexpr int W4 = W / 4;
 #pragma unroll 1
-      for (int i = tid; i < NIX / 2; i += 256) {
-        const int q = i % W4, r = (i / W4) % ROWS, cq = (i / (W4 * ROWS)) % CQ;
-        const int gy = y0 + r - PADL;
-        const bool ok = f0 < F && gy >= 0 && gy < H;
-        f32x4 o[4];
+        for (int i = tid; i < NIX / 2; i += 256) {
+          const int q = i % W4, r = (i / W4) % ROWS, cq = (i / (W4 * ROWS)) % CQ;
+          const int gy = y0 + r - PADL;
+          const bool ok = f0 < F && gy >= 0 && gy < H;
+          f32x4 o[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          o[c] = (ok && cq * 4 + c < CIN) ? UP::row4(Sl, 0, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
-        const int ia = (cq * ROWS + r) * W2 + 2 * q;
-        float2 v[4];
+          for (int c = 0; c < 4; ++c)
+            o[c] = (ok && cq * 4 + c < CIN) ? UP::row4(Sl, 0, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const int ia = (cq * ROWS + r) * W2 + 2 * q;
+          float2 v[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][0], o[c][1]);
-        put_x(ia, v);
+          for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][0], o[c][1]);
+          put_x(ia, v);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][2], o[c][3]);
-        put_x(ia + 1, v);
+          for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][2], o[c][3]);
+          put_x(ia + 1, v);
+        }
+      } else {
+        // 3bp's 18-wide c7 (a 9-wide source): one 2-pixel staging unit per item
+#pragma unroll 1
+        for (int i = tid; i < NIX; i += 256) {
+          const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ;
+          const int gy = y0 + r - PADL;
+          const bool ok = f0 < F && gy >= 0 && gy < H;
+          float2 v[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            v[c] = (ok && cq * 4 + c < CIN)
+                       ? make_float2(UP::px1(Sl, 0, cq * 4 + c, gy, y0, xp), UP::px1(Sl, 0, cq * 4 + c, gy, y0, xp + 1))
+                       : make_float2(0.f, 0.f);
+          put_x(i, v);
+        }
       }
     } else if constexpr (C::XPIPE) {
 #pragma unroll
@@ -683,10 +700,11 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       // backward, align_corners=False: source s gets outputs 2s-1 .. 2s+2
       // with weights 1/4, 3/4, 3/4, 1/4; 1 at the clamped edges), in
       // upsample_bwd_k's per-pixel order; then ReLU' of the source and the
-      // store.  Item = IK (4, or 2 where the source width is not a multiple
-      // of 4: 3bp's 18) consecutive source pixels of one row: full-resolution
+      // store.  Item = IK (4; 2 or 1 where the source width is not a multiple
+      // of 4: 3bp's 18 / 9) consecutive source pixels of one row: full-resolution
       // columns 2 IK q - 1 .. 2 IK q + 2 IK of 4 rows
-      constexpr int HS = H / 2, WS = W / 2, IK = WS % 4 == 0 ? 4 : 2, WQ = WS / IK, NO = CIN * (RT / 2) * WQ;
+      constexpr int HS = H / 2, WS = W / 2, IK = WS % 4 == 0 ? 4 : (WS % 2 == 0 ? 2 : 1), WQ = WS / IK;
+      constexpr int NO = CIN * (RT / 2) * WQ;
       static_assert(WS % IK == 0, "IK-pixel source items");
       typedef float fIK __attribute__((ext_vector_type(IK)));
       for (int o = tid; o < NO; o += 256) {
@@ -708,11 +726,16 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
           float c[2 * IK + 2];
           c[0] = q > 0 ? rp[-1] : 0.f;
           c[2 * IK + 1] = q < WQ - 1 ? rp[2 * IK] : 0.f;
+          if constexpr (IK == 1) {
+            c[1] = rp[0];
+            c[2] = rp[1];
+          } else {
 #pragma unroll
-          for (int h = 0; h < IK / 2; ++h) {
-            const f32x4 m = *reinterpret_cast<const f32x4*>(rp + 4 * h);
+            for (int h = 0; h < IK / 2; ++h) {
+              const f32x4 m = *reinterpret_cast<const f32x4*>(rp + 4 * h);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) c[1 + 4 * h + e] = m[e];
+              for (int e = 0; e < 4; ++e) c[1 + 4 * h + e] = m[e];
+            }
           }
           // source pixels IK q + k read columns 2 IK q + 2k - 1 .. 2 IK q + 2k + 2
           fIK row;
@@ -886,7 +909,7 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
 // odd rows and 32-channel tiles spill registers in the fused form)
 // the fused-upsample layers (input = the 2x bilinear upsample of a half-
 // resolution source; the upsample's transpose folded into the data gradient)
-#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32) X(16, 16, 36)
+#define PAIG_BWD_UP_SHAPES(X) X(32, 16, 16) X(16, 16, 32) X(16, 16, 36) X(32, 16, 18)
 // the layers whose output feeds a 2x2 max pool fused into their forward
 // (c2, c4 of the ShallowUNet): the pool's backward folded into the dY
 // staging (flags & 64).  The UNet (mnist) keeps its standalone pools (its

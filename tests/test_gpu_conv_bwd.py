@@ -179,7 +179,7 @@ def test_fused_backward_matches_separate_kernels(cin, cout, hw):
 
 
 @pytest.mark.parametrize("mode", [128, 256])
-@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (16, 16, 36)])
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (16, 16, 36), (32, 16, 18)])
 def test_fused_backward_upsample_input(cin, cout, hw, mode):
     """c7 / c10 (blocks.py:289-290,298-299): the conv input is the 2x bilinear
     upsample (torchvision Resize) of a ReLU'd half-resolution source.  One
