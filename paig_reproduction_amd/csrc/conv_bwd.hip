@@ -118,6 +118,15 @@ struct SBwdCfg {
   static constexpr int XIMG = CQ * XPL;
   // ---- weight gradient: D[co][(tap, ci)], K = pixels in k-blocks of 32
   static constexpr int MT = ceil_div(COUT, 16), NTW = ceil_div(NTX, 4);
+  // balanced N-tiles: NTF whole N-tiles per wave (wv + 4 j); the NTR = NTX % 4
+  // tail N-tiles are split by k-blocks (wave wv takes kb % 4 == wv) instead of
+  // going whole to waves 0 .. NTR-1, whose extra MFMAs every barrier waited
+  // for (c12: 2 : 1 N-tiles); the tail partials are summed over the 4 waves
+  // in LDS at the end, in wave order.  Not where the extra accumulators
+  // spill (bf16 images; 3bp's 36-wide non-fused layers): whole tail N-tiles
+  // to waves 0 .. NTR-1 there, as before
+  static constexpr bool BAL = PM != 2 && !(H == 36 && !UPS && !PF);
+  static constexpr int NTF = BAL ? NTX / 4 : ceil_div(NTX, 4), NTR = BAL ? NTX % 4 : 0;
   static constexpr int KB = ceil_div(TPXV, 32);
   static constexpr int NCOL = CIN * KK, SLAB = COUT * NCOL + COUT;
   // ---- staging units: UPX pixels x (8 dY | 4 X) channels, pixel fastest
@@ -162,7 +171,8 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   constexpr int EXT = C::EXT, RTD = C::RTD, ROWSD = C::ROWSD, TPXD = C::TPXD;
   constexpr int CCD = C::CCD, PSD = C::PSD, RPD = C::RPD, KC = C::KC, NS = C::NS, NTD = C::NTD, MW = C::MW;
   constexpr int CQ = C::CQ, NQ = C::NQ, NTX = C::NTX, OFFX = C::OFFX, TWX = C::TWX, XPL = C::XPL;
-  constexpr int MT = C::MT, NTW = C::NTW, KB = C::KB, NCOL = C::NCOL, UPX = C::UPX, W2 = C::W2;
+  constexpr int MT = C::MT, NTF = C::NTF, NTR = C::NTR, KB = C::KB, NCOL = C::NCOL, UPX = C::UPX, W2 = C::W2;
+  constexpr int NF1 = NTF > 0 ? NTF : 1, NR1 = NTR > 0 ? NTR : 1;
   constexpr int NID = C::NID, NLD = C::NLD, NIX = C::NIX, NLX = C::NLX;
   constexpr long long HW = (long long)H * W;
   constexpr long long XPLANE = UPS ? (long long)(H / 2) * (W / 2) : HW;
@@ -297,14 +307,17 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   // 16-lane group supplies row q (pixel 8g + 4h + q of the k-block) of
   // column quad pl
   const int qq = (lane >> 2) & 3, pl = lane & 3;
-  int colt[NTW];
-#pragma unroll
-  for (int jn = 0; jn < NTW; ++jn) {
-    int cq = (wv + jn * 4) * 4 + pl;
+  auto colt_of = [&](int nt) {
+    int cq = nt * 4 + pl;
     if (cq >= NQ) cq = 0;   // padded columns: finite data, never stored
     const int tap = cq / CQ, ciq = cq % CQ;
-    colt[jn] = xplane(ciq) + ((tap / KS) * TWX + tap % KS) * 4;
-  }
+    return xplane(ciq) + ((tap / KS) * TWX + tap % KS) * 4;
+  };
+  int colt[NF1], coltr[NR1];
+#pragma unroll
+  for (int jn = 0; jn < NTF; ++jn) colt[jn] = colt_of(wv + jn * 4);
+#pragma unroll
+  for (int t = 0; t < NTR; ++t) coltr[t] = colt_of(NTF * 4 + t);
   // dY slot of tile pixel j (its centre position in the halo'd image); the
   // zero slot past the valid pixels
   auto dslot = [&](int j) {
@@ -318,11 +331,14 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
     return ((fi * ROWS + rem / W) * TWX + rem % W + (OFFX - PADL)) * 4;
   };
 
-  f32x4 accw[MT][NTW];
+  f32x4 accw[MT][NF1], accr[MT][NR1];   // whole N-tiles, tail N-tiles (this wave's k-blocks)
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int m = 0; m < MT; ++m) {
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) accw[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NF1; ++j) accw[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NR1; ++t) accr[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   float bacc[NLD][8];   // bias partials of this thread's dY units (centre rows), unscaled fp32
 #pragma unroll
   for (int l = 0; l < NLD; ++l)
@@ -514,9 +530,12 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int j = 0; j < NTW; ++j)
+          for (int r = 0; r < 4; ++r) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) accw[m][j][r] = __builtin_amdgcn_ldexpf(accw[m][j][r], td - ecd);
+            for (int j = 0; j < NF1; ++j) accw[m][j][r] = __builtin_amdgcn_ldexpf(accw[m][j][r], td - ecd);
+#pragma unroll
+            for (int t = 0; t < NR1; ++t) accr[m][t][r] = __builtin_amdgcn_ldexpf(accr[m][t][r], td - ecd);
+          }
         ecd = td;
         dsc = __builtin_amdgcn_ldexpf(1.f, ecd);
       }
@@ -625,7 +644,8 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
     __syncthreads();
     issue(tile_of(lt + gridDim.x));
 
-    // ---- weight gradient: all 4 waves over all k-blocks, each its N-tiles
+    // ---- weight gradient: all 4 waves over all k-blocks, each its whole
+    // N-tiles; the tail N-tiles over every 4th k-block
 #pragma unroll 2
     for (int kb = 0; kb < KB; ++kb) {
       const int p0 = kb * 32;
@@ -641,16 +661,32 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
         al[m] = PM != 2 ? __builtin_shufflevector(tr_read(Dl + a0), tr_read(Dl + a1), 0, 1, 2, 3, 4, 5, 6, 7) : ah[m];
       }
       const int r0 = xpos(p0 + 8 * g + qq), r1 = xpos(p0 + 8 * g + 4 + qq);
+      auto ntile = [&](int ct, f32x4* acc) __attribute__((always_inline)) {
+        const s16x8 bh = __builtin_shufflevector(tr_read(Xh + r0 + ct), tr_read(Xh + r1 + ct), 0, 1, 2, 3, 4, 5, 6, 7);
+        const s16x8 bl =
+            PM != 2 ? __builtin_shufflevector(tr_read(Xl + r0 + ct), tr_read(Xl + r1 + ct), 0, 1, 2, 3, 4, 5, 6, 7) : bh;
 #pragma unroll
-      for (int jn = 0; jn < NTW; ++jn) {
-        if (wv + jn * 4 < NTX) {   // wave-uniform: EXEC stays full for the transposed reads
-          const s16x8 bh = __builtin_shufflevector(tr_read(Xh + r0 + colt[jn]), tr_read(Xh + r1 + colt[jn]), 0, 1,
-                                                   2, 3, 4, 5, 6, 7);
-          const s16x8 bl = PM != 2 ? __builtin_shufflevector(tr_read(Xl + r0 + colt[jn]),
-                                                             tr_read(Xl + r1 + colt[jn]), 0, 1, 2, 3, 4, 5, 6, 7)
-                                   : bh;
+        for (int m = 0; m < MT; ++m) acc[m] = mma3<PM>(ah[m], al[m], bh, bl, acc[m]);
+      };
 #pragma unroll
-          for (int m = 0; m < MT; ++m) accw[m][jn] = mma3<PM>(ah[m], al[m], bh, bl, accw[m][jn]);
+      for (int jn = 0; jn < NTF; ++jn) {
+        if (!C::BAL && wv + jn * 4 >= NTX) continue;   // wave-uniform
+        f32x4 a[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) a[m] = accw[m][jn];
+        ntile(colt[jn], a);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) accw[m][jn] = a[m];
+      }
+      if (NTR > 0 && (kb & 3) == wv) {   // wave-uniform: EXEC stays full for the transposed reads
+#pragma unroll
+        for (int t = 0; t < NTR; ++t) {
+          f32x4 a[MT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) a[m] = accr[m][t];
+          ntile(coltr[t], a);
+#pragma unroll
+          for (int m = 0; m < MT; ++m) accr[m][t] = a[m];
         }
       }
     }
@@ -816,22 +852,38 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   // ---- this block's slab row: weight gradients (each wave its N-tiles,
   // scaled back exactly), then the bias
   float* s = slab + (long long)blockIdx.x * C::SLAB;
+  auto put_w = [&](int m, int nt, const f32x4& acc) __attribute__((always_inline)) {
+    const int col = nt * 16 + (lane & 15), cq = col >> 2;
+    const int tap = cq / CQ, ci = (cq % CQ) * 4 + (col & 3);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = m * 16 + (lane >> 4) * 4 + r;
+      float v = acc[r];
+      if constexpr (PM == 0) v = __builtin_amdgcn_ldexpf(v, -(ecx + ecd));
+      if (co < COUT && cq < NQ && ci < CIN) s[co * NCOL + ci * KK + tap] = v;
+    }
+  };
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int nt = wv + j * 4;
-      if (nt >= NTX) continue;
-      const int col = nt * 16 + (lane & 15), cq = col >> 2;
-      const int tap = cq / CQ, ci = (cq % CQ) * 4 + (col & 3);
+    for (int j = 0; j < NTF; ++j)
+      if (wv + j * 4 < NTX) put_w(m, wv + j * 4, accw[m][j]);
+  if constexpr (NTR > 0) {
+    // tail N-tiles: the 4 waves' k-block partials, summed in wave order
+    f32x4* Rt = reinterpret_cast<f32x4*>(lds16);   // [4][MT][NTR][64]
+    __syncthreads();   // the last tile's LDS reads are done
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = m * 16 + (lane >> 4) * 4 + r;
-        float v = accw[m][j][r];
-        if constexpr (PM == 0) v = __builtin_amdgcn_ldexpf(v, -(ecx + ecd));
-        if (co < COUT && cq < NQ && ci < CIN) s[co * NCOL + ci * KK + tap] = v;
-      }
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int t = 0; t < NTR; ++t) Rt[((wv * MT + m) * NTR + t) * 64 + lane] = accr[m][t];
+    __syncthreads();
+    for (int u = wv; u < MT * NTR; u += 4) {
+      f32x4 v = Rt[u * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) v += Rt[(w * MT * NTR + u) * 64 + lane];
+      put_w(u / NTR, NTF * 4 + u % NTR, v);
     }
+  }
   // bias: unit i of thread i % 256 (slot i / 256) kept the partials of its 8
   // channels.  Two fixed-order stages: thread (channel co, part q) sums the
   // units q, q + NP, ... of co's chunk; thread co then sums its NP parts
