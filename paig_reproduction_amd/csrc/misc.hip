@@ -178,7 +178,8 @@ __global__ void rmsprop_k(T* __restrict__ p, const T* __restrict__ g, T* __restr
 // parameters) -- rmsprop_k's arithmetic in each precision
 __global__ void rmsprop_mixed_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ sa, long long n,
                                 float lr, float alpha, float eps, double* __restrict__ pd, const double* __restrict__ gd,
-                                double* __restrict__ sd, long long nd, double lrd, double alphad, double epsd) {
+                                double* __restrict__ sd, long long nd, double lrd, double alphad, double epsd,
+                                int vec) {
   if (blockIdx.x == 0)
     for (long long i = threadIdx.x; i < nd; i += blockDim.x) {
       const double gi = gd[i];
@@ -187,13 +188,34 @@ __global__ void rmsprop_mixed_k(float* __restrict__ p, const float* __restrict__
       sd[i] = s;
       pd[i] = pd[i] - lrd * gi / (sqrt(s) + epsd);
     }
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float gi = g[i];
-    float s = sa[i] * alpha;
+  auto upd = [&](float pi, float gi, float si, float& po, float& so) __attribute__((always_inline)) {
+    float s = si * alpha;
     s = s + (1.f - alpha) * gi * gi;
-    sa[i] = s;
-    p[i] = p[i] - lr * gi / (sqrtf(s) + eps);
+    so = s;
+    po = pi - lr * gi / (sqrtf(s) + eps);
+  };
+  if (vec) {
+    // float4 per thread (the flat buffers are 16-byte aligned), the n % 4
+    // tail by the first threads; the same operations per element
+    const int n4 = (int)(n / 4);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+      const float4 gv = reinterpret_cast<const float4*>(g)[i];
+      const float4 sv = reinterpret_cast<const float4*>(sa)[i];
+      const float4 pv = reinterpret_cast<const float4*>(p)[i];
+      float4 po, so;
+      upd(pv.x, gv.x, sv.x, po.x, so.x);
+      upd(pv.y, gv.y, sv.y, po.y, so.y);
+      upd(pv.z, gv.z, sv.z, po.z, so.z);
+      upd(pv.w, gv.w, sv.w, po.w, so.w);
+      reinterpret_cast<float4*>(sa)[i] = so;
+      reinterpret_cast<float4*>(p)[i] = po;
+    }
+    const long long t = 4ll * n4 + blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (t < n) upd(p[t], g[t], sa[t], p[t], sa[t]);
+    return;
   }
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    upd(p[i], g[i], sa[i], p[i], sa[i]);
 }
 
 template <typename T>
@@ -356,9 +378,10 @@ int paig_rmsprop_f32(float* p, const float* g, float* sa, long long n, float lr,
 int paig_rmsprop_mixed(float* p32, const float* g32, float* s32, long long n32, double* p64, const double* g64,
                        double* s64, long long n64, double lr, double alpha, double eps, void* stream) {
   if (n32 <= 0 && n64 <= 0) return 0;
-  const long long nb = n32 > 0 ? n32 : 1;
+  const int vec = n32 < (1ll << 31) && ((uintptr_t)p32 | (uintptr_t)g32 | (uintptr_t)s32) % 16 == 0;
+  const long long nb = n32 > 0 ? (vec ? n32 / 4 + 1 : n32) : 1;
   hipLaunchKernelGGL(rmsprop_mixed_k, dim3(grid_for(nb)), dim3(256), 0, (hipStream_t)stream, p32, g32, s32, n32,
-                     (float)lr, (float)alpha, (float)eps, p64, g64, s64, n64, lr, alpha, eps);
+                     (float)lr, (float)alpha, (float)eps, p64, g64, s64, n64, lr, alpha, eps, vec);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
