@@ -125,7 +125,7 @@ struct SBwdCfg {
   // in LDS at the end, in wave order.  Not where the extra accumulators
   // spill (bf16 images; 3bp's 36-wide non-fused layers): whole tail N-tiles
   // to waves 0 .. NTR-1 there, as before
-  static constexpr bool BAL = PM != 2 && !(H == 36 && !UPS && !PF);
+  static constexpr bool BAL = !(PM == 2 && (CIN == 24 || (UPS && CIN == 32) || H == 36 || H == 18)) && !(H == 36 && !UPS && !PF);
   static constexpr int NTF = BAL ? NTX / 4 : ceil_div(NTX, 4), NTR = BAL ? NTX % 4 : 0;
   static constexpr int KB = ceil_div(TPXV, 32);
   static constexpr int NCOL = CIN * KK, SLAB = COUT * NCOL + COUT;
