@@ -157,7 +157,9 @@ int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, c
  * forward for the backward, which takes the same arguments plus the logits
  * and d logits (d of the output after its activation) and writes every conv's
  * [weight | bias] gradient to dwb[i] (contiguous, overwritten).  The same
- * kernels in the same order as the Python engine's U-Net stages. */
+ * kernels in the same order as the Python engine's U-Net stages (its
+ * default configuration: the engine's A/B switches such as PAIG_FUSED_BWD=0
+ * do not apply here; the fused layer backwards are always taken). */
 size_t paig_unet_workspace(int net, int F, int H, int K, int math);
 int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
                   const float* const* w, const float* const* b, float* logits, void* ws, size_t ws_bytes,
@@ -242,27 +244,6 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
 size_t paig_gemm_parts_size(int M, int N, int K, int math);
 int paig_gemm_parts(int ta, int tb, int M, int N, int K, const float* A, long long lda, const float* B,
                     long long ldb, float* part, size_t part_floats, int math, void* stream);
-/* Dense layers on pre-split operands (psgemm.hip).  A "PS image" holds a
- * logical matrix X[R][K] (reduction dim K) split once into f16 hi + lo planes
- * ([ceil(K/32)][R rounded up to 64][32] each), one power-of-two exponent per
- * row (max_k |X[r][k]| 2^e in [2^14, 2^15)).
- * paig_ps_split fills up to 8 images in one launch; job i reads
- * op(X)[r][k] = src[i][r * sr[i] + k * sk[i]] (sk == 1 or sr == 1), R[i] x K[i],
- * into dst[i] (paig_ps_bytes(R, K) bytes, 256-byte aligned) and, when rowsum
- * and rowsum[i] are not NULL, its fp32 row sums into rowsum[i] (R floats: for
- * an image of dY^T, the bias gradient of dW = dY^T X).
- * paig_psgemm: C[M][N] = alpha sum_k A[m][k] B[n][k] (+beta C) (+bias[n]) -> act
- * -> * aux' (the paig_gemm_ex epilogue) from the images of A (M x K) and B
- * (N x K); 3 f16 MFMAs per product, fp32-accurate like paig_gemm_ex math 6.
- * Replaces the per-tile operand conversion of the split GEMMs for
- * nn/network/blocks.py:71-75,98-100 (l1, l2: forward, dgrad, wgrad). */
-long long paig_ps_bytes(int R, int K);
-int paig_ps_split(int n, const float* const* src, const long long* sr, const long long* sk, const int* R,
-                  const int* K, void* const* dst, float* const* rowsum, void* stream);
-size_t paig_psgemm_workspace(int M, int N, int K);
-int paig_psgemm(int M, int N, int K, const void* A_img, const void* B_img, float alpha, float* C, long long ldc,
-                float beta, const float* bias, int act, int auxm, const float* aux, long long ldaux, float* ws,
-                size_t ws_floats, void* stream);
 size_t paig_colsum_workspace(int M, int N);
 int paig_colsum(const float* X, int M, int N, long long ld, float* out, int accumulate, float* ws, void* stream);
 int paig_slab_reduce(const float* slab, int nblk, long long ld, int len, float* out, int accumulate, void* stream);
@@ -339,7 +320,7 @@ int paig_head_bwd_vel_vfn2(const float* h2, const float* h3, const float* dpos, 
  * (paig_gemm_parts of objects x W1^T, S slabs of [K*F][IN]) summed + b1 +
  * ReLU -> h1; h2 = ReLU(h1 W2^T + b2) in fp32 FMA; the l3 position head as
  * paig_head_fwd -> h3, pos.  IN <= 200, a multiple of 4; W2t: IN * IN floats
- * (8-byte aligned) holding W2^T when W2 is NULL (paig_conv_wprep's dg = 2
+ * (16-byte aligned) holding W2^T when W2 is NULL (paig_conv_wprep's dg = 2
  * job writes it with the step's other weight images), else scratch that
  * receives W2^T from a first launch.  Then ONE launch for the split-K
  * epilogue, l2 and the head. */
@@ -348,7 +329,7 @@ int paig_dense_tail_fwd(const float* part, int S, const float* b1, float* h1, co
                         int K, int IN, float half, void* stream);
 /* paig_head_bwd_vel_vfn2 (dX / dpos0 nullable: no velocity-encoder term; n =
  * 0: no VFN phase 2) that also forms l2's data gradient (blocks.py:99):
- * dh1 = (dh2 W2) * (h1 > 0), fp32 FMA, W2 [IN][IN] (8-byte aligned), IN <=
+ * dh1 = (dh2 W2) * (h1 > 0), fp32 FMA, W2 [IN][IN] (16-byte aligned), IN <=
  * 200; its [W3 | b3] slab rows are paig_head_l2_bwd_blocks(K * F). */
 int paig_head_l2_bwd_blocks(int rows);
 int paig_head_l2_bwd(const float* h2, const float* h3, const float* dpos, const float* W3, float* dh2, float* slab,

@@ -85,10 +85,6 @@ SIGNATURES = {
     "paig_gemm_parts": (I, [I, I, I, I, I, P, LL, P, LL, P, SZ, I, P]),
     "paig_gemm": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, P]),
     "paig_gemm_ex": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, I, P]),
-    "paig_ps_bytes": (LL, [I, I]),
-    "paig_ps_split": (I, [I, P, P, P, P, P, P, P, P]),
-    "paig_psgemm_workspace": (SZ, [I, I, I]),
-    "paig_psgemm": (I, [I, I, I, P, P, F32, P, LL, F32, P, I, I, P, LL, P, SZ, P]),
     "paig_colsum_workspace": (SZ, [I, I]),
     "paig_colsum": (I, [P, I, I, LL, P, I, P, P]),
     "paig_slab_reduce": (I, [P, I, LL, I, P, I, P]),
@@ -132,7 +128,7 @@ SIGNATURES = {
 _QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported",
           "paig_conv2d_bwd_supported", "paig_velmlp_bwd_blocks",
           "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_l2_bwd_blocks", "paig_head_mask_blocks", "paig_conv_wprep_size", "paig_gemm_workspace", "paig_colsum_workspace",
-          "paig_ps_bytes", "paig_psgemm_workspace", "paig_gemm_parts_size", "paig_gemm_parts", "paig_unet_workspace", "paig_localiser_workspace",
+          "paig_gemm_parts_size", "paig_gemm_parts", "paig_unet_workspace", "paig_localiser_workspace",
           "paig_velmlp_rollout_bwd_workspace",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
           "paig_decoder_bwd_scratch"}

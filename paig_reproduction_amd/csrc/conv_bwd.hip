@@ -40,6 +40,29 @@
 #ifndef PAIG_BWD_MINW
 #define PAIG_BWD_MINW 0   // A/B builds: force the blocks per CU the kernels are compiled for
 #endif
+#ifndef PAIG_BWD_AUXP
+#define PAIG_BWD_AUXP 1   // A/B builds: 0 = the epilogue loads its ReLU' mask when it needs it
+#endif
+
+// Diagnostic build only (-DPAIG_BWD_STAMPS, tools/bwd_bench.py): per wave,
+// s_memtime cycle sums of the tile loop's phases (0 setup, 1 prefetch wait +
+// max + barrier, 2 commit, 3 issue, 4 weight gradient, 5 data gradient, 6
+// epilogue, 7 slab write; inside the commit: 8 dY staging, 9 UPS window +
+// halo, 10 its barrier, 11 the upsampled X staging) and the tile count, stored
+// by lane 0 (vector stores)
+#ifdef PAIG_BWD_STAMPS
+__device__ unsigned long long paig_bwd_stamps[4096][4][13];
+#define PAIG_BSTAMP(k)                                      \
+  do {                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t_ - st_last;                              \
+    st_last = t_;                                           \
+  } while (0)
+#else
+#define PAIG_BSTAMP(k) \
+  do {                 \
+  } while (0)
+#endif
 
 namespace {
 
@@ -71,13 +94,25 @@ constexpr int sbwd_tpx(int CIN, int COUT, int H, int W, bool UPS, int PM) {
 // waves per SIMD (= blocks per CU) each shape compiles for without spilling
 // (measured: -Rpass-analysis=kernel-resource-usage at 2 / 3 / 4)
 constexpr int sbwd_minw(int CIN, int COUT, int H, int PM, bool PF) {
-  if (CIN == 8 && COUT == 8 && H == 32) return PF ? 3 : 4;
+  if (CIN == 8 && COUT == 8 && H == 32) return PF || PAIG_BWD_AUXP == 2 ? 3 : 4;
   if (PM == 2 && CIN == 8 && COUT == 16 && H == 16) return 3;
   if (PM == 2 && CIN == 24 && COUT == 8 && H == 32) return 3;
   if (CIN == 8 && COUT == 8 && H == 36) return PF ? 2 : 3;
   if (CIN == 8 && COUT == 16 && H == 18) return PM == 2 ? 4 : 3;
   if (CIN == 16 && COUT == 16 && H == 18) return PF ? 2 : 3;
   return 2;
+}
+
+// the shapes whose ReLU'-mask prefetch (AUXP) would spill registers at their
+// blocks per CU (-Rpass-analysis=kernel-resource-usage); PAIG_BWD_AUXP=2
+// (A/B builds) prefetches everywhere, c12's 8 -> 8 at three blocks per CU
+constexpr bool sbwd_auxp(int CIN, int COUT, int H, int PM, bool UPS, bool PF) {
+  if (PAIG_BWD_AUXP == 2) return true;
+  if (CIN == 8 && COUT == 8 && (H == 32 || H == 36) && !PF) return false;
+  if (CIN == 24 && COUT == 8 && (H == 36 || PM == 2)) return false;
+  if (UPS && H == 36) return false;
+  if (PM == 0) return !(PF && CIN == 16 && COUT == 16 && H == 16);
+  return !((UPS && CIN == 32 && H == 16) || (CIN == 8 && COUT == 16 && H == 16));
 }
 
 // 4 waves split the weight-gradient N-tiles (each wave owns every 4th one
@@ -159,6 +194,14 @@ struct SBwdCfg {
   // the 16 channels of one epilogue store land on distinct bank groups
   static constexpr int UPP = rup(TPXD, 64) + 4;
   static_assert(!UPS || CIN * UPP * 4 <= XREG, "fused upsample: dX tile does not fit the X region");
+  // UPS epilogue items: IKU consecutive source pixels of one source row
+  static constexpr int WSU = W / 2, IKU = WSU % 4 == 0 ? 4 : (WSU % 2 == 0 ? 2 : 1), WQU = WSU / IKU;
+  static constexpr int NOU = UPS ? CIN * (RT / 2) * WQU : 0, NOI = NOU > 0 ? ceil_div(NOU, 256) : 1;
+  // the epilogue's ReLU' mask (flags & 2) is loaded before the next tile's
+  // prefetch is issued, so its latency hides behind the tile's MFMAs instead
+  // of stalling the epilogue (MW x NTD float4 per lane; UPS: NOI items)
+  static constexpr bool AUXP =
+      PAIG_BWD_AUXP && (UPS || (VEC4 && MW * NTD <= 8)) && sbwd_auxp(CIN, COUT, H, PM, UPS, PF);
 };
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM, bool PF>
@@ -187,6 +230,9 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   float* Sl = reinterpret_cast<float*>(reinterpret_cast<char*>(Xh) + C::XREG);   // UPS window
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4;
   __shared__ float smax[4];
+#ifdef PAIG_BWD_STAMPS
+  unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime(), st_n = 0;
+#endif
 
   auto xplane = [](int cq) { return cq * XPL + ((cq & 1) ? 16 : 0) + ((cq & 2) ? 64 : 0); };
   // ---- zero what the staging never writes: the dY image's halo columns,
@@ -364,7 +410,11 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       const int i = tid + l * 256;
       const int xp = UPX * (i % W2), r = (i / W2) % ROWSD, cc = (i / (W2 * ROWSD)) % CCD, fi = i / (W2 * ROWSD * CCD);
       const int gy = y0 + r - PADL - EXT;
+#ifdef PAIG_BWD_NOLOAD   // diagnostic builds only (wrong results): dY reads from a hot zero buffer
+      const bool ok = false;
+#else
       const bool ok = i < NID && f0 + fi < F && gy >= 0 && gy < H;
+#endif
       const int off = fi * (int)dy.fs + cc * 8 * (int)HW + gy * W + xp;
       static_assert(8 * HW <= 8 * 4096, "paig_zero_planes covers the unit");
       const float* base = ok ? fb + off : paig_zero_planes;
@@ -553,6 +603,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
         for (int c = 0; c < 8; ++c) bacc[l][c] += pd[l][c].x + pd[l][c].y;
       }
     }
+    PAIG_BSTAMP(8);
     if constexpr (UPS) {
       // the half-resolution window (prefetched) -> LDS, then the upsampled
       // rows: units of 4 pixels x 4 channels (one row4 per channel: shared
@@ -560,18 +611,34 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       const int y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
       zero_xhalo();
+      PAIG_BSTAMP(9);
       __syncthreads();
+      PAIG_BSTAMP(10);
       if constexpr (W % 4 == 0) {
         constexpr int W4 = W / 4;
 #pragma unroll 1
         for (int i = tid; i < NIX / 2; i += 256) {
+#ifdef PAIG_BWD_NOUPS   // diagnostic builds only (wrong results): no upsampled X staging
+          if (i >= 0) break;
+#endif
           const int q = i % W4, r = (i / W4) % ROWS, cq = (i / (W4 * ROWS)) % CQ;
           const int gy = y0 + r - PADL;
           const bool ok = f0 < F && gy >= 0 && gy < H;
           f32x4 o[4];
+          // whole waves walk the items (their count a multiple of 64): the
+          // neighbouring columns come from the adjacent lanes (row4n); the
+          // halo rows' window addresses stay inside the window, the data is
+          // selected away afterwards
+          constexpr bool DPP = (NIX / 2) % 64 == 0 && 16 % W4 == 0 && CIN % 4 == 0;
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            o[c] = (ok && cq * 4 + c < CIN) ? UP::row4(Sl, 0, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int c = 0; c < 4; ++c) {
+            if constexpr (DPP) {
+              const f32x4 u = UP::row4n(Sl, 0, cq * 4 + c, gy, y0, q);
+              o[c] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
+            } else {
+              o[c] = (ok && cq * 4 + c < CIN) ? UP::row4(Sl, 0, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
           const int ia = (cq * ROWS + r) * W2 + 2 * q;
           float2 v[4];
 #pragma unroll
@@ -581,6 +648,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
           for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][2], o[c][3]);
           put_x(ia + 1, v);
         }
+        PAIG_BSTAMP(11);
       } else {
         // 3bp's 18-wide c7 (a 9-wide source): one 2-pixel staging unit per item
 #pragma unroll 1
@@ -634,15 +702,54 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
   if constexpr (PM == 0) xsc = __builtin_amdgcn_ldexpf(1.f, ecx);
   else ecx = 0;
 
+  PAIG_BSTAMP(0);
   for (; lt < ntiles; lt += gridDim.x) {
     const int tile = xcd_tile(lt, ntiles);
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
     if constexpr (PF) fold(tile);
     if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) tile_max();
     __syncthreads();   // the previous tile's fragment reads are done
+    PAIG_BSTAMP(1);
     commit(tile);
     __syncthreads();
+    PAIG_BSTAMP(2);
+    // this tile's ReLU' mask for the epilogue (AUXP), issued before the next
+    // tile's prefetch: the epilogue then waits for it alone
+    typedef float fIKU __attribute__((ext_vector_type(C::IKU)));
+    f32x4 auxv[C::AUXP && !UPS ? MW : 1][C::AUXP && !UPS ? NTD : 1];
+    fIKU auxu[C::AUXP && UPS ? C::NOI : 1];
+    if constexpr (C::AUXP) {
+      if (flags & 2) {
+        if constexpr (UPS) {
+#pragma unroll
+          for (int k = 0; k < C::NOI; ++k) {
+            const int o = tid + 256 * k;
+            const int q = o % C::WQU, sr = (o / C::WQU) % (RT / 2), ci = o / (C::WQU * (RT / 2));
+            const bool ok = o < C::NOU && f0 < F;
+            const float* ap = ok ? aux.frame(f0) + ((long long)ci * (H / 2) + y0 / 2 + sr) * C::WSU + C::IKU * q
+                                 : paig_zero_planes;
+            auxu[k] = *reinterpret_cast<const fIKU*>(ap);
+          }
+        } else {
+#pragma unroll
+          for (int nt = 0; nt < NTD; ++nt) {
+            const int ci = nt * 16 + (lane & 15);
+#pragma unroll
+            for (int mt = 0; mt < MW; ++mt) {
+              const int pix = (wv * MW + mt) * 16 + (lane >> 4) * 4;
+              const int fi = pix / (RT * W), rem = pix % (RT * W);
+              const int f = f0 + fi;
+              const bool ok = ci < CIN && pix < TPXV && f < F;
+              const float* ap = ok ? aux.frame(f) + ci * HW + (long long)(y0 + rem / W) * W + rem % W
+                                   : paig_zero_planes;
+              auxv[mt][nt] = *reinterpret_cast<const f32x4*>(ap);
+            }
+          }
+        }
+      }
+    }
     issue(tile_of(lt + gridDim.x));
+    PAIG_BSTAMP(3);
 
     // ---- weight gradient: all 4 waves over all k-blocks, each its whole
     // N-tiles; the tail N-tiles over every 4th k-block
@@ -691,6 +798,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       }
     }
 
+    PAIG_BSTAMP(4);
     // ---- data gradient of the tile's pixels
     f32x4 accd[MW][NTD];
 #pragma unroll
@@ -715,6 +823,7 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
         for (int nt = 0; nt < NTD; ++nt) accd[mt][nt] = mma3<PM>(ah, al, bh[nt], bl[nt], accd[mt][nt]);
       }
     }
+    PAIG_BSTAMP(5);
     if constexpr (UPS) {
       // full-resolution dX rows y0-1 .. y0+RT of the tile -> LDS [ci][RTD][W]
       // (the X image is free once every wave's weight-gradient reads are done)
@@ -739,11 +848,12 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       // store.  Item = IK (4; 2 or 1 where the source width is not a multiple
       // of 4: 3bp's 18 / 9) consecutive source pixels of one row: full-resolution
       // columns 2 IK q - 1 .. 2 IK q + 2 IK of 4 rows
-      constexpr int HS = H / 2, WS = W / 2, IK = WS % 4 == 0 ? 4 : (WS % 2 == 0 ? 2 : 1), WQ = WS / IK;
-      constexpr int NO = CIN * (RT / 2) * WQ;
+      constexpr int HS = H / 2, WS = W / 2, IK = C::IKU, WQ = C::WQU;
+      constexpr int NO = C::NOU;
       static_assert(WS % IK == 0, "IK-pixel source items");
-      typedef float fIK __attribute__((ext_vector_type(IK)));
-      for (int o = tid; o < NO; o += 256) {
+      typedef fIKU fIK;
+      // item o; mp: its prefetched ReLU' mask (AUXP)
+      auto item = [&](int o, const fIK& mp) __attribute__((always_inline)) {
         const int q = o % WQ, sr = (o / WQ) % (RT / 2), ci = o / (WQ * (RT / 2));
         const int sy = y0 / 2 + sr;
         float wy[4];
@@ -797,12 +907,24 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
           float* op = dx.frame(f0) + off;
           if (flags & 4) acc += *reinterpret_cast<const fIK*>(op);
           if (flags & 2) {
-            const fIK m = *reinterpret_cast<const fIK*>(aux.frame(f0) + off);
+            fIK m;
+            if constexpr (C::AUXP) m = mp;
+            else m = *reinterpret_cast<const fIK*>(aux.frame(f0) + off);
 #pragma unroll
             for (int k = 0; k < IK; ++k) acc[k] = m[k] > 0.f ? acc[k] : 0.f;
           }
           *reinterpret_cast<fIK*>(op) = acc;
         }
+      };
+      if constexpr (C::AUXP) {
+#pragma unroll
+        for (int it = 0; it < C::NOI; ++it) {
+          const int o = tid + 256 * it;
+          if (NO % 256 != 0 && o >= NO) break;
+          item(o, auxu[it]);
+        }
+      } else {
+        for (int o = tid; o < NO; o += 256) item(o, auxu[0]);
       }
     } else {
     // epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for input
@@ -824,7 +946,9 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
           f32x4 v = accd[mt][nt] * tinv;
           if (flags & 4) v += *reinterpret_cast<const f32x4*>(op);
           if (flags & 2) {
-            const f32x4 a = *reinterpret_cast<const f32x4*>(aux.frame(f) + ci * HW + (long long)y * W + xx);
+            f32x4 a;
+            if constexpr (C::AUXP) a = auxv[mt][nt];
+            else a = *reinterpret_cast<const f32x4*>(aux.frame(f) + ci * HW + (long long)y * W + xx);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
           }
@@ -847,6 +971,10 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       }
     }
     }   // !UPS
+    PAIG_BSTAMP(6);
+#ifdef PAIG_BWD_STAMPS
+    ++st_n;
+#endif
   }
 
   // ---- this block's slab row: weight gradients (each wave its N-tiles,
@@ -912,6 +1040,14 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
     s[COUT * NCOL + tid] = v;
   }
   if constexpr (PM == 0) f16_range_note(rmax);
+#ifdef PAIG_BWD_STAMPS
+  PAIG_BSTAMP(7);
+  if (lane == 0 && blockIdx.x < 4096) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) paig_bwd_stamps[blockIdx.x][wv][k] = st_acc[k];
+    paig_bwd_stamps[blockIdx.x][wv][12] = st_n;
+  }
+#endif
 }
 
 template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM, bool PF = false>
@@ -1048,6 +1184,12 @@ int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, c
 #undef PAIG_CASE
   return PAIG_E_UNSUPPORTED;
 }
+
+#ifdef PAIG_BWD_STAMPS
+int paig_bwd_stamps_read(void* host, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(paig_bwd_stamps), bytes);
+}
+#endif
 
 }  // extern "C"
 

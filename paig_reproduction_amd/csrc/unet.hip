@@ -9,7 +9,9 @@
 // C ABI alone.  The same kernels run in the same order with the same
 // arguments (fused pools / upsamples, weight images, max-|x| slots, fused
 // layer backwards, one batched slab reduction), so the results are
-// bit-identical to the Python engine's (tests/test_gpu_unet_abi.py).
+// bit-identical to the Python engine's (tests/test_gpu_unet_abi.py) in its
+// default configuration (the engine's A/B switch PAIG_FUSED_BWD=0 has no
+// counterpart here: the fused layer backwards are always taken).
 // Host code only; the caller's workspace holds every activation, gradient
 // and partial-gradient slab (paig_unet_workspace), the library allocates
 // nothing.
@@ -482,6 +484,9 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
         const unsigned char* pcode = nullptr;
         long long pcode_fs = 0;
         if (i + 1 < no && L.pcode[i + 1] != (size_t)-1) {   // the max pool of this output, folded
+          // the kernel reads this output's skip-path gradient (dY): the
+          // concat partner must have written it
+          PAIG_REQUIRE(state(op.dst) == 1, "paig_unet_bwd: pool fold before the skip gradient (op %d)", i);
           const View pdv = dview(p.ops[i + 1].dst);
           dpool = pdv.p;
           dpool_fs = pdv.fs;

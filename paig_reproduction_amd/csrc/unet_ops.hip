@@ -889,6 +889,9 @@ __global__ void axpby_k(const float* __restrict__ x, float* __restrict__ y, long
     y[i] = a * x[i] + (b == 0.f ? 0.f : b * y[i]);
 }
 
+// the 32-bit instantiation: the grid-stride step (<= 8192 x 256 threads) must
+// not overflow past the last element either
+static inline bool int_index_ok(long long n) { return n + 8192LL * 256 < (1ll << 31); }
 static inline int grid_for(long long n, int bs = 256) {
   long long g = (n + bs - 1) / bs;
   if (g > 8192) g = 8192;
@@ -912,7 +915,7 @@ int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, 
     return 0;
   }
   long long n = (long long)F * C * (H / 2) * (W / 2);
-  if (n < (1ll << 31))
+  if (int_index_ok(n))
     hipLaunchKernelGGL(maxpool_fwd_k<int>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
                      FViewW{y, y_fs}, F, C, H, W);
   else
@@ -949,7 +952,7 @@ int paig_maxpool2_bwd_relu(const float* x, long long x_fs, const float* dy, long
     return 0;
   }
   long long n = (long long)F * C * H * W;
-  if (n < (1ll << 31))
+  if (int_index_ok(n))
     hipLaunchKernelGGL(maxpool_bwd_relu_k<int>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{x, x_fs, 0, 0},
                      FView{dy, dy_fs, 0, 0}, FViewW{dx, dx_fs}, F, C, H, W);
   else
@@ -963,7 +966,7 @@ int paig_upsample2_fwd(const float* s, long long s_fs, float* u, long long u_fs,
                        int Wo, void* stream) {
   if (F <= 0) return 0;
   long long n = (long long)F * C * Ho * Wo;
-  if (n < (1ll << 31))
+  if (int_index_ok(n))
     hipLaunchKernelGGL(upsample_fwd_k<int>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{s, s_fs, 0, 0},
                      FViewW{u, u_fs}, F, C, Hs, Ws, Ho, Wo);
   else
@@ -987,7 +990,7 @@ int paig_upsample2_bwd(const float* du, long long du_fs, const float* s, long lo
     return 0;
   }
   long long n = (long long)F * C * Hs * Ws;
-  if (n < (1ll << 31))
+  if (int_index_ok(n))
     hipLaunchKernelGGL(upsample_bwd_k<int>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, FView{du, du_fs, 0, 0},
                      FView{s, s_fs, 0, 0}, FViewW{ds, ds_fs}, F, C, Hs, Ws, Ho, Wo, relu_mask);
   else

@@ -673,8 +673,8 @@ int paig_dense_tail_fwd(const float* part, int S, const float* b1, float* h1, co
   if (rows <= 0) return 0;
   PAIG_REQUIRE(S >= 1 && IN > 0 && IN <= TAIL_MAXIN && IN % 4 == 0,
                "dense_tail_fwd: S=%d, IN=%d (<= %d, a multiple of 4)", S, IN, TAIL_MAXIN);
-  PAIG_REQUIRE(W2t && (reinterpret_cast<uintptr_t>(W2t) & 7) == 0,
-               "dense_tail_fwd: an 8-byte aligned W2t (IN * IN floats) is required");
+  PAIG_REQUIRE(W2t && (reinterpret_cast<uintptr_t>(W2t) & 15) == 0,
+               "dense_tail_fwd: a 16-byte aligned W2t (IN * IN floats) is required");
   if (W2) {   // W2^T into the W2t scratch first (else W2t already holds it: paig_conv_wprep dg = 2)
     hipLaunchKernelGGL(transpose_sq_k, dim3(cdiv(IN, 32), cdiv(IN, 32)), dim3(256), 0, (hipStream_t)stream, W2, W2t,
                        IN);
@@ -695,8 +695,8 @@ int paig_head_l2_bwd(const float* h2, const float* h3, const float* dpos, const 
   const int rows = K * F;
   if (rows <= 0) return 0;
   PAIG_REQUIRE(IN > 0 && IN <= TAIL_MAXIN && IN % 4 == 0, "head_l2_bwd: IN=%d (<= %d, a multiple of 4)", IN, TAIL_MAXIN);
-  PAIG_REQUIRE(W2 && h1 && dh1 && (reinterpret_cast<uintptr_t>(W2) & 7) == 0,
-               "head_l2_bwd: W2 (8-byte aligned), h1 and dh1 are required");
+  PAIG_REQUIRE(W2 && h1 && dh1 && (reinterpret_cast<uintptr_t>(W2) & 15) == 0,
+               "head_l2_bwd: W2 (16-byte aligned: float4 loads), h1 and dh1 are required");
   PAIG_REQUIRE((dX == nullptr && dpos0 == nullptr) || (B > 0 && Te > 0 && F == B * Te && S <= Te),
                "head_l2_bwd: F=%d != B=%d x Te=%d or S=%d > Te", F, B, Te, S);
   PAIG_REQUIRE(n >= 0 && n <= paig_vfn::VMAX, "head_l2_bwd: n=%d (0..%d)", n, paig_vfn::VMAX);

@@ -368,38 +368,12 @@ class Engine:
                 self.L.paig_gemm_ex(0, 0, rows, I, O, 1.0, ptr(dy), O, ptr(W), I, 0.0, ptr(dx), I, None, 0, auxm,
                                     ptr(aux), I, None, ptr(ws), n_ws, self.gemm_math(self.DGRAD), st)
 
-    # -- dense layers on pre-split operands (csrc/psgemm.hip) ---------------
-    # In split arithmetic every dense-layer operand is split ONCE into an f16
-    # hi + lo "PS image" with per-row exponents and the GEMMs only load
-    # fragments and issue MFMAs (the per-tile conversion of paig_gemm_ex
-    # bound those launches).  Weights are split once per forward (both
-    # orientations), activations / gradients where they are produced.
     def dense_tail(self):
         """The localiser's l2 + head as fp32 FMA inside the launches around
         them (paig_dense_tail_fwd / paig_head_l2_bwd): in split arithmetic,
         where the 3-MFMA l2 GEMMs were latency-bound launches of their own;
         bf16 keeps its 1-MFMA l2 GEMMs (faster there).  PAIG_DENSE_TAIL=0: A/B."""
         return self.gemm_math(self.FWD) == 6 and os.environ.get("PAIG_DENSE_TAIL", "1") != "0"
-
-    def use_ps(self):
-        return self.gemm_math(self.FWD) == 6 and os.environ.get("PAIG_DENSE_PS", "0") != "0"
-
-    def _ps_img(self, R, K, dev):
-        return _empty(self.L.paig_ps_bytes(R, K) // 4, dev)
-
-    def _ps_split(self, jobs, st):
-        """jobs: [(src ptr, sr, sk, R, K, dst image, rowsum ptr | None)]"""
-        n = len(jobs)
-        self.L.paig_ps_split(n, _parr([j[0] for j in jobs]), (ctypes.c_longlong * n)(*[j[1] for j in jobs]),
-                             (ctypes.c_longlong * n)(*[j[2] for j in jobs]), _iarr([j[3] for j in jobs]),
-                             _iarr([j[4] for j in jobs]), _parr([ptr(j[5]) for j in jobs]),
-                             _parr([j[6] for j in jobs]), st)
-
-    def _psgemm(self, tag, M, N, K, ia, ib, C, ldc, ws, st, bias=None, act=0, auxm=0, aux=None, nbytes=None):
-        fl = 2 * M * N * K
-        with self._p(tag, fl, nbytes if nbytes is not None else 4 * (M * K + N * K + M * N)):
-            self.L.paig_psgemm(M, N, K, ptr(ia), ptr(ib), 1.0, ptr(C), ldc, 0.0, ptr(bias), act, auxm, ptr(aux),
-                               ldc, ptr(ws), ws.numel(), st)
 
     def workspace_floats(self, lay):
         K, F, B = lay.K, lay.F, lay.B
@@ -408,10 +382,7 @@ class Engine:
                 self.L.paig_gemm_workspace(200, n1, K * F), self.L.paig_gemm_workspace(K * F, n1, 200), self.L.paig_gemm_workspace(200, 200, K * F),
                 self.L.paig_gemm_workspace(2, 200, K * F), self.L.paig_gemm_workspace(100, 100, K * B),
                 self.L.paig_gemm_workspace(K * B, 100, 100), 1 << 16,
-                self.L.paig_gemm_parts_size(K * F, 200, n1, self.gemm_math(self.FWD)),
-                self.L.paig_psgemm_workspace(K * F, 200, n1), self.L.paig_psgemm_workspace(200, n1, K * F),
-                self.L.paig_psgemm_workspace(K * F, n1, 200), self.L.paig_psgemm_workspace(200, 200, K * F),
-                self.L.paig_psgemm_workspace(K * F, 200, 200)]
+                self.L.paig_gemm_parts_size(K * F, 200, n1, self.gemm_math(self.FWD))]
         return int(max(need))
 
     # -- forward ---------------------------------------------------------
@@ -427,7 +398,7 @@ class Engine:
         x = x.contiguous()
         K, F, HW, H, h, D = lay.K, lay.F, lay.HW, lay.H, lay.h, lay.D
         ws = _empty(self.workspace_floats(lay), dev)
-        S = {"lay": lay, "x": x, "ws": ws, "dev": dev}
+        S = {"lay": lay, "x": x, "ws": ws, "dev": dev, "need_saved": need_saved}
         cm = self.conv_flags()
         S["cm"] = cm
 
@@ -555,6 +526,9 @@ class Engine:
         buf = S.pop("xmax_buf", None)
         if buf is not None:
             self._xmax.setdefault(S["xmax_key"], []).append(buf)
+        # the slots may now be another forward's: this forward's saved state
+        # admits no second backward (retain_graph=True)
+        S["consumed"] = True
 
     def _unet_forward(self, S, lay, x_view, st, fuse_head=False):
         """The U-Net plan over F frames addressed by x_view (frame view
@@ -658,7 +632,8 @@ class Engine:
                 nxt = ops[i + 1] if i + 1 < len(ops) else None
                 pcode = (None, 0)
                 pool_next = nxt is not None and nxt["op"] == "pool" and nxt["src"] == op["dst"] and not xfl and cm
-                if pool_next and self._fused_bwd(op["src"][2], op["dst"][2], Hl, op["ks"], cm | 64):
+                if pool_next and S.get("need_saved", True) and self._fused_bwd(op["src"][2], op["dst"][2], Hl,
+                                                                                 op["ks"], cm | 64):
                     # the pool windows' codes (ReLU' bits + argmax): the
                     # backward folds the pool into this layer's dY staging.
                     # Written by this conv's fused pool, or (widths whose rows
@@ -720,27 +695,7 @@ class Engine:
         h1 = _empty(K * F * 200, dev)
         h2 = _empty(K * F * 200, dev)
         h3 = _empty(K * F * 2, dev)
-        if self.use_ps():
-            n1, KF = lay.l1_in, K * F
-            W1, W2 = self.p("encoder.l1.weight"), self.p("encoder.l2.weight")
-            ps = {"x1": self._ps_img(KF, n1, dev), "w1": self._ps_img(200, n1, dev), "w1t": self._ps_img(n1, 200, dev),
-                  "w2": self._ps_img(200, 200, dev), "w2t": self._ps_img(200, 200, dev), "h1": self._ps_img(KF, 200, dev)}
-            # the weights in both orientations (the transposed ones serve the
-            # data gradients) and the masked objects, one launch
-            with self._p("ps_split:l1_fwd", 0, 8 * KF * n1):
-                self._ps_split([(ptr(l1_x), n1, 1, KF, n1, ps["x1"], None), (ptr(W1), n1, 1, 200, n1, ps["w1"], None),
-                                (ptr(W1), 1, n1, n1, 200, ps["w1t"], None), (ptr(W2), 200, 1, 200, 200, ps["w2"], None),
-                                (ptr(W2), 1, 200, 200, 200, ps["w2t"], None)], st)
-            self._psgemm("gemm_fwd:encoder.l1", KF, 200, n1, ps["x1"], ps["w1"], h1, 200, ws, st,
-                         bias=self.p("encoder.l1.bias"), act=1)
-            self._ps_split([(ptr(h1), 200, 1, KF, 200, ps["h1"], None)], st)
-            self._psgemm("gemm_fwd:encoder.l2", KF, 200, 200, ps["h1"], ps["w2"], h2, 200, ws, st,
-                         bias=self.p("encoder.l2.bias"), act=1)
-            S["ps"] = ps
-            enc_pos = _empty(F * 2 * K, dev)
-            L.paig_head_fwd(ptr(h2), ptr(self.p("encoder.l3.weight")), ptr(self.p("encoder.l3.bias")), ptr(h3),
-                            ptr(enc_pos), F, K, 200, float(H / 2), st)
-        elif not self.dense_tail():
+        if not self.dense_tail():
             self.linear(l1_x, K * F, "encoder.l1", h1, 1, st, ws)
             self.linear(h1, K * F, "encoder.l2", h2, 1, st, ws)
             enc_pos = _empty(F * 2 * K, dev)
@@ -813,6 +768,7 @@ class Engine:
         sequence have a loss weight (the others' d_sse_roll entries are zero
         and there is no dense d_out): the rollout decoder backward reads only
         those frames."""
+        self._check_fresh(S)
         lay = S["lay"]
         L = self.L
         x = S["x"]
@@ -988,11 +944,8 @@ class Engine:
         assert self.g("encoder.l3.bias").data_ptr() == g3.data_ptr() + 400 * 4, "l3 grads not contiguous"
         S["extra_slabs"].append((hslab, hblk, 402, g3))
         dobjs = _empty(K * F * lay.l1_in, dev)
-        if "ps" in S:
-            self._dense_bwd_ps(S, dh2, dh1, dobjs, st, ws)
-        else:
-            self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws, need_dx=not fused_l2)
-            self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
+        self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws, need_dx=not fused_l2)
+        self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
         # every gradient of the flat buffer's early bucket is final (queued on
         # this stream): the data-parallel all-reduce of that bucket may start
         if hook and self.bucket_hook is not None:
@@ -1025,30 +978,6 @@ class Engine:
             dacts["LG"] = dLG
         self._unet_backward(S, dacts, st)
 
-    def _dense_bwd_ps(self, S, dh2, dh1, dobjs, st, ws):
-        """l2 and l1 backward (blocks.py:98-100) on PS images: dW = dY^T X
-        (db = the row sums of dY^T, written by the split), dX = dY W, the
-        l1 ReLU' fused into l2's data gradient."""
-        lay = S["lay"]
-        dev = S["dev"]
-        ps = S["ps"]
-        n1, KF = lay.l1_in, lay.K * lay.F
-        h1, l1_x = S["h1"], S["l1_x"]
-        i_dh2, i_dh2t, i_h1t = self._ps_img(KF, 200, dev), self._ps_img(200, KF, dev), self._ps_img(200, KF, dev)
-        self._ps_split([(ptr(dh2), 200, 1, KF, 200, i_dh2, None),
-                        (ptr(dh2), 1, 200, 200, KF, i_dh2t, ptr(self.g("encoder.l2.bias"))),
-                        (ptr(h1), 1, 200, 200, KF, i_h1t, None)], st)
-        self._psgemm("gemm_wgrad:encoder.l2", 200, 200, KF, i_dh2t, i_h1t, self.g("encoder.l2.weight"), 200, ws, st)
-        self._psgemm("gemm_dgrad:encoder.l2", KF, 200, 200, i_dh2, ps["w2t"], dh1, 200, ws, st, auxm=1, aux=h1,
-                     nbytes=4 * (2 * KF * 200 + 200 * 200 + KF * 200))
-        i_dh1, i_dh1t, i_xt = self._ps_img(KF, 200, dev), self._ps_img(200, KF, dev), self._ps_img(n1, KF, dev)
-        with self._p("ps_split:l1_bwd", 0, 8 * KF * n1):
-            self._ps_split([(ptr(dh1), 200, 1, KF, 200, i_dh1, None),
-                            (ptr(dh1), 1, 200, 200, KF, i_dh1t, ptr(self.g("encoder.l1.bias"))),
-                            (ptr(l1_x), 1, n1, n1, KF, i_xt, None)], st)
-        self._psgemm("gemm_wgrad:encoder.l1", 200, n1, KF, i_dh1t, i_xt, self.g("encoder.l1.weight"), n1, ws, st)
-        self._psgemm("gemm_dgrad:encoder.l1", KF, n1, 200, i_dh1, ps["w1t"], dobjs, n1, ws, st)
-
     def _fused_bwd(self, cin, cout, Hl, ks, cm):
         """The layer backward runs as one fused launch (paig_conv2d_bwd)
         where the library has the shape; PAIG_FUSED_BWD=0 keeps the separate
@@ -1057,7 +986,14 @@ class Engine:
             return False
         return bool(self.L.paig_conv2d_bwd_supported(cin, cout, Hl, Hl, ks, cm))
 
+    @staticmethod
+    def _check_fresh(S):
+        if S.get("consumed"):
+            raise PaigError("a second backward through one forward (retain_graph=True) is not supported: the "
+                            "forward's saved state (activation maxima slots) was released by the first backward")
+
     def _unet_backward(self, S, dacts, st):
+        self._check_fresh(S)
         lay = S["lay"]
         L = self.L
         dev = S["x"].device
@@ -1161,6 +1097,9 @@ class Engine:
                     fold = (None, 0, None, 0)
                     pj = i + 1
                     if pj in S.get("pcode", {}):
+                        # the kernel reads this output's skip-path gradient
+                        # (dY): its concat partner must have written it
+                        assert state(dst) == "accum", f"{op['name']}: pool fold before the skip gradient (plan error)"
                         pdv, _ = dview(lay.ops[pj]["dst"])
                         cb, cfs = S["pcode"][pj]
                         fold = (pdv[0], pdv[1], cb.data_ptr(), cfs)
