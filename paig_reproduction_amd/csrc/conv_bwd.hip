@@ -625,20 +625,9 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
           const int gy = y0 + r - PADL;
           const bool ok = f0 < F && gy >= 0 && gy < H;
           f32x4 o[4];
-          // whole waves walk the items (their count a multiple of 64): the
-          // neighbouring columns come from the adjacent lanes (row4n); the
-          // halo rows' window addresses stay inside the window, the data is
-          // selected away afterwards
-          constexpr bool DPP = (NIX / 2) % 64 == 0 && 16 % W4 == 0 && CIN % 4 == 0;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if constexpr (DPP) {
-              const f32x4 u = UP::row4n(Sl, 0, cq * 4 + c, gy, y0, q);
-              o[c] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
-            } else {
-              o[c] = (ok && cq * 4 + c < CIN) ? UP::row4(Sl, 0, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-          }
+          for (int c = 0; c < 4; ++c)
+            o[c] = (ok && cq * 4 + c < CIN) ? UP::row4(Sl, 0, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
           const int ia = (cq * ROWS + r) * W2 + 2 * q;
           float2 v[4];
 #pragma unroll

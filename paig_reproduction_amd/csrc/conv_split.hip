@@ -347,18 +347,9 @@ if constexpr (W % 4 == 0) {
           const int gy = y0 + r - PADL;
           const bool ok = f0 + fi < F && gy >= 0 && gy < H;
           f32x4 o[8];
-          // whole waves over the items: edge columns from the adjacent lanes
-          // (row4n, conv_bwd.hip's staging); in-window addresses, data selected
-          constexpr bool DPP = (NI / 2) % 64 == 0 && 16 % W4 == 0 && CIN % 8 == 0;
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            if constexpr (DPP) {
-              const f32x4 u = UP::row4n(Sl, fi, cc * 8 + c, gy, y0, q);
-              o[c] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
-            } else {
-              o[c] = (ok && cc * 8 + c < CIN) ? UP::row4(Sl, fi, cc * 8 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-          }
+          for (int c = 0; c < 8; ++c)
+            o[c] = (ok && cc * 8 + c < CIN) ? UP::row4(Sl, fi, cc * 8 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
           const int ia = ((fi * CC + cc) * ROWS + r) * W2 + 2 * q;
           float2 v[8];
 #pragma unroll
@@ -974,17 +965,9 @@ if constexpr (W % 4 == 0) {
           const int gy = y0 + r - PADL;
           const bool ok = f0 + fi < F && gy >= 0 && gy < H;
           f32x4 o[4];
-          // whole waves over the items: edge columns from the adjacent lanes (row4n)
-          constexpr bool DPP = (NIX / 2) % 64 == 0 && 16 % W4 == 0 && CINB % 4 == 0;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if constexpr (DPP) {
-              const f32x4 u = UP::row4n(Sl, fi, cq * 4 + c, gy, y0, q);
-              o[c] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
-            } else {
-              o[c] = (ok && cq * 4 + c < CINB) ? UP::row4(Sl, fi, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-          }
+          for (int c = 0; c < 4; ++c)
+            o[c] = (ok && cq * 4 + c < CINB) ? UP::row4(Sl, fi, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
           const int ia = ((fi * CQ + cq) * ROWS + r) * W2 + 2 * q;
           float2 v[4];
 #pragma unroll

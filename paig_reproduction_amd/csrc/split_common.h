@@ -164,31 +164,6 @@ struct UpStage {
     o[3] = wa * (0.75f * m0.y + 0.25f * a3) + wb * (0.75f * m1.y + 0.25f * b3);
     return o;
   }
-  // row4 with the edge columns 2q-1 / 2q+2 taken from the neighbouring lanes'
-  // float2 reads (DPP row shifts) instead of four more LDS reads: lanes hold
-  // consecutive q of one output row in groups that tile the 16-lane DPP rows
-  // (WS / 2 divides 16), and every lane of the wave executes it (DPP reads
-  // inactive lanes as 0).  Bit-identical to row4.
-  static __device__ __forceinline__ f32x4 row4n(const float* Sl, int fi, int c, int gy, int y0, int q) {
-    static_assert(16 % (WS / 2) == 0, "q groups tile the DPP rows");
-    int ya, yb;
-    float wa, wb;
-    up2_taps(gy, HS, ya, yb, wa, wb);
-    const float* p = Sl + (fi * CIN + c) * SRN * WS;
-    const float2 m0 = *reinterpret_cast<const float2*>(p + (ya - (y0 / 2 - 1)) * WS + 2 * q);
-    const float2 m1 = *reinterpret_cast<const float2*>(p + (yb - (y0 / 2 - 1)) * WS + 2 * q);
-    const float l0 = dpp_f<0x111>(m0.y), l1 = dpp_f<0x111>(m1.y);   // row_shr:1 -> lane q-1's column 2q-1
-    const float h0 = dpp_f<0x101>(m0.x), h1 = dpp_f<0x101>(m1.x);   // row_shl:1 -> lane q+1's column 2q+2
-    const bool lo = q > 0, hi = 2 * q + 2 < WS;
-    const float a0 = lo ? l0 : m0.x, b0 = lo ? l1 : m1.x, a3 = hi ? h0 : m0.y, b3 = hi ? h1 : m1.y;
-    const float w0 = lo ? 0.25f : 0.f, w1 = lo ? 0.75f : 1.f;
-    f32x4 o;
-    o[0] = wa * (w0 * a0 + w1 * m0.x) + wb * (w0 * b0 + w1 * m1.x);
-    o[1] = wa * (0.75f * m0.x + 0.25f * m0.y) + wb * (0.75f * m1.x + 0.25f * m1.y);
-    o[2] = wa * (0.25f * m0.x + 0.75f * m0.y) + wb * (0.25f * m1.x + 0.75f * m1.y);
-    o[3] = wa * (0.75f * m0.y + 0.25f * a3) + wb * (0.75f * m1.y + 0.25f * b3);
-    return o;
-  }
 };
 
 // LDS available to one block (gfx950: 160 KB per CU)

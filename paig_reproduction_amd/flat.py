@@ -212,9 +212,15 @@ class FlatParams:
                 continue
             p.grad = self.grad_view(n)
 
+    # tests only: run the data-parallel path (early-bucket all-reduce, late
+    # bucket + fp64 scalars) in a world of one process, the only RCCL run a
+    # one-GPU box allows (tests/test_gpu_dp.py::test_rccl_world1_step_bit_identical)
+    FORCE_DP = False
+
     @staticmethod
     def _dp(group):
-        return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        return dist.is_available() and dist.is_initialized() and (dist.get_world_size(group) > 1 or
+                                                                   FlatParams.FORCE_DP)
 
     @staticmethod
     def _mean(t, group, async_op=False):

@@ -86,3 +86,25 @@ def test_dp_step_equals_single_process(kind, tmp_path):
         print(f"{kind} step {i}: updated parameters rel err fp32 {ep:.3g} fp64 {e64:.3g}")
         if kind == "momentum":
             assert ep <= 6e-6 and e64 <= 6e-6, (i, ep, e64)
+
+
+@pytest.mark.parametrize("kind", ["rmsprop", "momentum"])
+def test_rccl_world1_step_bit_identical(kind, tmp_path):
+    """RCCL executed on the DP step's own path: a world-1
+    `nccl` process group with FlatParams.FORCE_DP, so the split HIP graph
+    runs, allreduce_early issues the asynchronous AVG of the early bucket on
+    RCCL's stream between the two replays, and FlatOptimizer.step reduces the
+    late bucket and the fp64 scalars and waits for the early work.  AVG over
+    one rank is exact: every step's flat gradients and updated parameters must
+    be bit-identical to the single-process step from the same state.  (No
+    scaling claim: one GPU box holds one rank.)"""
+    dp, single = tmp_path / "dp", tmp_path / "single"
+    dp.mkdir()
+    single.mkdir()
+    _wait([_run(["--mode", "dp", "--rank", "0", "--world", "1", "--port", str(_free_port()), "--backend", "nccl",
+                 "--force_dp", "--kind", kind, "--out", str(dp)])])
+    _wait([_run(["--mode", "single", "--kind", kind, "--out", str(single), "--src", str(dp)])])
+    for i in range(3):
+        for nm in ("g32", "g64", "p32", "p64"):
+            a, b = np.load(dp / f"post_{nm}_{i}.npy"), np.load(single / f"post_{nm}_{i}.npy")
+            assert np.array_equal(a, b), f"{kind} step {i}: {nm} differs (max {np.abs(a - b).max():.3g})"

@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 GRAD_RTOL = 1e-4
 GRAD_RTOL_3BP = 3e-5
 GRAD_RTOL_MNIST = 1.6e-3
-ROLLOUT_RTOL_3BP = 2e-3
+ROLLOUT_RTOL_3BP = 1e-5   # ~3x the largest measured: 4.9e-7 on the fixture, 2.8e-6 at B=512
 SUPPORTED = list(GOLDEN)
 
 

@@ -4,6 +4,13 @@ single-process reference on the concatenated batch.
 
   python tests/workers/dp_step_worker.py --mode dp --rank R --world 2 --port P --kind K --out DIR
   python tests/workers/dp_step_worker.py --mode single --kind K --out DIR --src DPDIR
+  python tests/workers/dp_step_worker.py --mode dp --world 1 --backend nccl --force_dp --kind K --out DIR
+
+The last form runs the data-parallel path (split graph, RCCL all-reduce of
+the early bucket between the replays, FlatOptimizer.step with the late
+bucket and the fp64 scalars) in a world of one process: RCCL's AVG over one
+rank must leave every gradient and parameter bit-identical to the
+single-process step.
 
 Both run 3 steps (3 fixed global batches of 2B sequences, synthetic
 spring_color, seq 12) through paig_reproduction_amd.graph_step (bench.py's
@@ -41,6 +48,8 @@ def main():
     ap.add_argument("--kind", default="momentum")
     ap.add_argument("--out", required=True)
     ap.add_argument("--src", default="", help="single mode: the DP run's output directory")
+    ap.add_argument("--backend", default="gloo")
+    ap.add_argument("--force_dp", action="store_true", help="the DP path at world 1 (FlatParams.FORCE_DP)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -48,8 +57,10 @@ def main():
     if a.mode == "dp":
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(a.port)
-        dist.init_process_group("gloo", rank=a.rank, world_size=world)
+        dist.init_process_group(a.backend, rank=a.rank, world_size=world)
+    from paig_reproduction_amd.flat import FlatParams
     from paig_reproduction_amd.graph_step import GraphStep
+    FlatParams.FORCE_DP = a.force_dp
     from paig_reproduction_amd.nn.datasets.synth import as_model_input, render_sequences
     from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
 
@@ -65,8 +76,8 @@ def main():
     xs = torch.from_numpy(as_model_input(u8)).view(STEPS, 2 * B_RANK, SEQ, 3, 32, 32)
     nb = B_RANK if world > 1 else 2 * B_RANK
     xbuf = torch.empty((nb, SEQ, 3, 32, 32), device=dev)
-    step = GraphStep(m, xbuf, world, graph=True)
-    if world > 1:
+    step = GraphStep(m, xbuf, world, graph=True, split=True if a.force_dp else None)
+    if world > 1 or a.force_dp:
         assert step.split, "the DP step must use the split graph"
     # warm-up on the first batch, then capture; re-initialise the parameters
     # and optimizer state afterwards so the 3 timed steps start from the same point
@@ -113,6 +124,8 @@ def main():
         torch.cuda.synchronize()
         if save:
             dump("post", i, {"g32": flat.g32, "g64": flat.g64, "p32": flat.p32, "p64": flat.p64})
+    if a.mode == "dp" and world == 1:
+        dist.destroy_process_group()
     if world > 1:
         # every rank holds the same parameters
         t = flat.p32.clone()
