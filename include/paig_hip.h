@@ -167,6 +167,54 @@ int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long l
 int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
                   const float* const* w, const float* logits, const float* dlogits, float* const* dwb, void* ws,
                   size_t ws_bytes, void* stream);
+/* The same with the Python engine's step options (_ex forms; the engine's
+ * U-Net stages ARE these calls, so the plan and its fusions live only here).
+ * flags:
+ *   PAIG_UNET_HEAD_FUSED    the forward stops before the 1x1 head, which the
+ *     caller runs fused into the mask softmax (paig_head_mask_fwd_ex / _bwd_ex);
+ *     the backward starts from the head input's gradient, written by the
+ *     caller into the workspace (paig_unet_buffer(.., 1, paig_unet_query(net,
+ *     K, 2))); logits / dlogits unused;
+ *   PAIG_UNET_SEPARATE_BWD  (A/B) separate data- and weight-gradient kernels
+ *     instead of the fused layer backward (and no pool fold);
+ *   PAIG_UNET_INFERENCE     forward only: no gradient buffers, slabs or pool
+ *     codes in the workspace;
+ *   PAIG_UNET_EXT_WPREP     split arithmetic: the caller built every conv's
+ *     weight images (paig_conv_wprep, dg 0 / 1) and passes them per conv
+ *     (wprep_fwd[c], wprep_dg[c]; c = conv index, wprep_dg[0] unused).
+ * The workspace layout depends on the flags (the same flags for the query,
+ * the forward and its backward).  probe (nullable) is called on the host
+ * around every conv launch (event 0 before, 1 after; kind PAIG_PROBE_*; the
+ * launch's (Cin, Cout, H, flags)): the engine's per-launch HIP-event timing.
+ * bwd: n_extra more partial-gradient slabs (extra_src[e]: extra_nblk[e] rows
+ * of extra_len[e] floats, summed into extra_dst[e]) join the U-Net's batched
+ * slab reduction (one launch for the step's weight gradients). */
+#define PAIG_UNET_HEAD_FUSED 1
+#define PAIG_UNET_SEPARATE_BWD 2
+#define PAIG_UNET_INFERENCE 4
+#define PAIG_UNET_EXT_WPREP 8
+#define PAIG_PROBE_CONV_FWD 0
+#define PAIG_PROBE_CONV_BWD 1
+#define PAIG_PROBE_CONV_WGRAD 2
+#define PAIG_PROBE_CONV_DGRAD 3
+typedef void (*paig_unet_probe_fn)(void* ctx, int event, int op, int conv, int kind, int cin, int cout, int H,
+                                   int flags);
+size_t paig_unet_workspace_ex(int net, int F, int H, int K, int math, int flags);
+/* byte offset in the workspace of buffer buf's activation (which 0) or
+ * gradient (which 1), or -1 (none: the input, the logits, a fused upsample) */
+long long paig_unet_buffer(int net, int F, int H, int K, int math, int flags, int which, int buf);
+/* plan facts: what 0 = convs, 1 = buffers, 2 = the head's input buffer, 3 =
+ * its channels, 4 = the logits buffer */
+int paig_unet_query(int net, int K, int what);
+int paig_unet_fwd_ex(int net, int F, int H, int K, int math, int flags, const float* x, long long x_fs, int x_grp,
+                     long long x_gs, const float* const* w, const float* const* b, float* logits,
+                     const void* const* wprep_fwd, const void* const* wprep_dg, void* ws, size_t ws_bytes,
+                     paig_unet_probe_fn probe, void* probe_ctx, void* stream);
+int paig_unet_bwd_ex(int net, int F, int H, int K, int math, int flags, const float* x, long long x_fs, int x_grp,
+                     long long x_gs, const float* const* w, const float* logits, const float* dlogits,
+                     float* const* dwb, int n_extra, const float* const* extra_src, const int* extra_nblk,
+                     const int* extra_len, float* const* extra_dst, const void* const* wprep_dg, void* ws,
+                     size_t ws_bytes, paig_unet_probe_fn probe, void* probe_ctx, void* stream);
 
 /* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,
@@ -210,6 +258,22 @@ int paig_head_mask_fwd(const float* x12, const float* w, const float* b, const f
 int paig_head_mask_bwd(const float* x12, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
                        long long x_gs, const float* masks, const float* dobjs, float* dx12, float* slab, int F, int K,
                        int H, int W, void* stream);
+/* The same for either U-Net's head (the _ex forms; the two above are the
+ * ShallowUNet case): CI = the head's input width, flags 1 = ReLU'd logits,
+ * 2 = pooled objects.  (CI, flags) = (8, 1): ShallowUNet c13 as above;
+ * (16, 2): UNet c18 (1x1 conv 16 -> K, not ReLU'd; blocks.py:170,236) with
+ * the masked objects' AvgPool2d(2) (blocks.py:94-96): fwd also writes pobjs
+ * [K*F][3][H/2][W/2] (8-byte aligned; H even, W % 4 == 0), bwd takes dobjs as
+ * the pooled objects' gradient.  xl = the head's input [F][CI][H][W] (c12's /
+ * c17's output), dxl its gradient (that layer's ReLU' applied); slab rows of
+ * K*CI weight + K bias partials.  Replace the head conv's fwd / dgrad / wgrad
+ * and paig_mask_softmax_fwd/bwd. */
+int paig_head_mask_fwd_ex(const float* xl, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                          long long x_gs, float* masks, float* objs, float* pobjs, int F, int K, int CI, int H, int W,
+                          int flags, void* stream);
+int paig_head_mask_bwd_ex(const float* xl, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                          long long x_gs, const float* masks, const float* dobjs, float* dxl, float* slab, int F, int K,
+                          int CI, int H, int W, int flags, void* stream);
 int paig_pos_head_fwd(const float* h3, float* pos, int N, int K, float half, void* stream);
 int paig_pos_head_bwd(const float* h3, const float* dpos, float* dh3, int N, int K, float half, void* stream);
 

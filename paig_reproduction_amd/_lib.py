@@ -68,6 +68,11 @@ SIGNATURES = {
     "paig_velmlp_rollout_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P, SZ, P]),
     "paig_unet_fwd": (I, [I, I, I, I, I, P, LL, I, LL, P, P, P, P, SZ, P]),
     "paig_unet_bwd": (I, [I, I, I, I, I, P, LL, I, LL, P, P, P, P, P, SZ, P]),
+    "paig_unet_workspace_ex": (SZ, [I, I, I, I, I, I]),
+    "paig_unet_buffer": (LL, [I, I, I, I, I, I, I, I]),
+    "paig_unet_query": (I, [I, I, I]),
+    "paig_unet_fwd_ex": (I, [I, I, I, I, I, I, P, LL, I, LL, P, P, P, P, P, P, SZ, P, P, P]),
+    "paig_unet_bwd_ex": (I, [I, I, I, I, I, I, P, LL, I, LL, P, P, P, P, I, P, P, P, P, P, P, SZ, P, P, P]),
     "paig_maxpool2_fwd": (I, [P, LL, P, LL, I, I, I, I, P]),
     "paig_maxpool2_fwd_codes": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
     "paig_maxpool2_bwd_relu": (I, [P, LL, P, LL, P, LL, I, I, I, I, P]),
@@ -78,6 +83,8 @@ SIGNATURES = {
     "paig_head_mask_blocks": (I, [I, I, I]),
     "paig_head_mask_fwd": (I, [P, P, P, P, LL, I, LL, P, P, I, I, I, I, P]),
     "paig_head_mask_bwd": (I, [P, P, P, P, LL, I, LL, P, P, P, P, I, I, I, I, P]),
+    "paig_head_mask_fwd_ex": (I, [P, P, P, P, LL, I, LL, P, P, P, I, I, I, I, I, I, P]),
+    "paig_head_mask_bwd_ex": (I, [P, P, P, P, LL, I, LL, P, P, P, P, I, I, I, I, I, I, P]),
     "paig_pos_head_fwd": (I, [P, P, I, I, F32, P]),
     "paig_pos_head_bwd": (I, [P, P, P, I, I, F32, P]),
     "paig_gemm_workspace": (SZ, [I, I, I]),
@@ -128,7 +135,8 @@ SIGNATURES = {
 _QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported",
           "paig_conv2d_bwd_supported", "paig_velmlp_bwd_blocks",
           "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_l2_bwd_blocks", "paig_head_mask_blocks", "paig_conv_wprep_size", "paig_gemm_workspace", "paig_colsum_workspace",
-          "paig_gemm_parts_size", "paig_gemm_parts", "paig_unet_workspace", "paig_localiser_workspace",
+          "paig_gemm_parts_size", "paig_gemm_parts", "paig_unet_workspace", "paig_unet_workspace_ex",
+          "paig_unet_buffer", "paig_unet_query", "paig_localiser_workspace",
           "paig_velmlp_rollout_bwd_workspace",
           "paig_vfn_bwd_blocks", "paig_rollout_bwd_blocks", "paig_decoder_bwd_blocks", "paig_decoder_slab_len",
           "paig_decoder_bwd_scratch"}

@@ -40,6 +40,10 @@
 //   are summed exactly in fp32 from the staging registers.
 #include "split_common.h"
 
+#ifndef PAIG_FWD_AUXP
+#define PAIG_FWD_AUXP 1   // A/B builds: 0 = the dgrad epilogue loads its ReLU' mask when it needs it
+#endif
+
 namespace {
 
 // ============================================================ forward / dgrad
@@ -479,6 +483,27 @@ if constexpr (W % 4 == 0) {
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
     __syncthreads();
+    // dgrad: this tile's ReLU' mask for the epilogue (AUXP), loaded before the
+    // next tile's prefetch so that its latency hides behind the MFMAs
+    constexpr bool AUXP = PAIG_FWD_AUXP && DG && C::VEC4 && !POOL && MW * NT <= 8;
+    f32x4 auxv[AUXP ? MW : 1][AUXP ? NT : 1];
+    if constexpr (AUXP) {
+      if (flags & 2) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int co = co0 + nt * 16 + (lane & 15);
+#pragma unroll
+          for (int mt = 0; mt < MW; ++mt) {
+            const int pix = fwd_mtile<MW, C::PO, POOL>(wv, mt) * 16 + (lane >> 4) * 4;
+            const int fi = pix / (RT * W), rem = pix % (RT * W);
+            const int f = f0 + fi;
+            const bool ok = co < COUT && pix < C::TPXV && f < F;
+            const float* ap = ok ? aux.frame(f) + co * HW + (long long)(y0 + rem / W) * W + rem % W : paig_zero_planes;
+            auxv[mt][nt] = *reinterpret_cast<const f32x4*>(ap);
+          }
+        }
+      }
+    }
     issue(tile_of(lt + gridDim.x));
     f32x4 acc[MW][NT];
 #pragma unroll
@@ -530,7 +555,9 @@ if constexpr (W % 4 == 0) {
           }
           if (flags & 4) v += *reinterpret_cast<const f32x4*>(op);
           if (flags & 2) {
-            const f32x4 m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
+            f32x4 m;
+            if constexpr (AUXP) m = auxv[mt][nt];
+            else m = *reinterpret_cast<const f32x4*>(aux.frame(f) + co * HW + (long long)y * W + x);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
           }

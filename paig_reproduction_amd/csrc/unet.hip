@@ -177,8 +177,9 @@ bool pool_fused(const UPlan& p, int i, int H, int cm) {
 }
 // (the codes come from the fused pool, or from the standalone pool where the
 // forward cannot fuse it: paig_maxpool2_fwd_codes)
-bool pool_folded(const UPlan& p, int i, int H, int cm) {
+bool pool_folded(const UPlan& p, int i, int H, int cm, int flags) {
   const UOp& op = p.ops[i];
+  if (flags & (PAIG_UNET_SEPARATE_BWD | PAIG_UNET_INFERENCE)) return false;
   if (op.kind != U_CONV || i + 1 >= (int)p.ops.size() || cm == 0 || p.fused_up[i] >= 0) return false;
   const UOp& nx = p.ops[i + 1];
   const int Hl = H / p.bufs[op.dst.buf].lvl;
@@ -196,7 +197,10 @@ struct ULayout {
   size_t xmax = 0, total = 0;
 };
 
-void layout(const UPlan& p, ULayout& L, int F, int H, int cm) {
+// flags: PAIG_UNET_INFERENCE -> no gradient buffers, slabs or pool codes;
+// PAIG_UNET_EXT_WPREP -> no weight images (the caller's)
+void layout(const UPlan& p, ULayout& L, int F, int H, int cm, int flags) {
+  const bool train = !(flags & PAIG_UNET_INFERENCE);
   const size_t NONE = (size_t)-1;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -211,7 +215,7 @@ void layout(const UPlan& p, ULayout& L, int F, int H, int cm) {
     const size_t hw = (size_t)(H / p.bufs[b].lvl) * (H / p.bufs[b].lvl);
     const size_t bytes = (size_t)F * p.bufs[b].C * hw * 4;
     if (b != p.X0 && b != p.LG && !p.fused_buf[b]) L.act[b] = take(bytes);
-    if (b != p.X0) L.grad[b] = take(bytes);
+    if (b != p.X0 && train) L.grad[b] = take(bytes);
   }
   L.xmax = take((size_t)no * PAIG_XMAX_SLOTS * 4);
   L.slab.assign(no, NONE);
@@ -223,12 +227,12 @@ void layout(const UPlan& p, ULayout& L, int F, int H, int cm) {
     const UOp& op = p.ops[i];
     if (op.kind != U_CONV) continue;
     const int cin = op.src.n, cout = op.dst.n, ks = op.ks;
-    L.slab[i] = take((size_t)NBLK_MAX * (cout * cin * ks * ks + cout) * 4);
-    if (cm == 128) {
+    if (train) L.slab[i] = take((size_t)NBLK_MAX * (cout * cin * ks * ks + cout) * 4);
+    if (cm == 128 && !(flags & PAIG_UNET_EXT_WPREP)) {
       L.wprep0[i] = take((size_t)paig_conv_wprep_size(cin, cout, ks) * 2);
       if (op.src.buf != p.X0) L.wprep1[i] = take((size_t)paig_conv_wprep_size(cout, cin, ks) * 2);
     }
-    if (pool_folded(p, i, H, cm)) {
+    if (pool_folded(p, i, H, cm, flags)) {
       const int Hl = H / p.bufs[op.dst.buf].lvl;
       L.pcode_fs[i + 1] = (long long)((cout + 7) / 8 * 8) * (Hl / 2) * (Hl / 2);
       L.pcode[i + 1] = take((size_t)F * L.pcode_fs[i + 1]);
@@ -251,33 +255,29 @@ int check_args(int net, int F, int H, int K, int cm) {
   return 0;
 }
 
-}  // namespace
+// per-launch probe (the engine's HIP-event timing of one conv launch;
+// bench.py's roofline): event 0 before, 1 after the launch
+struct UProbe {
+  paig_unet_probe_fn fn;
+  void* ctx;
+  void operator()(int ev, int op, int conv, int kind, int cin, int cout, int Hl, int fl) const {
+    if (fn) fn(ctx, ev, op, conv, kind, cin, cout, Hl, fl);
+  }
+};
 
-extern "C" {
-
-size_t paig_unet_workspace(int net, int F, int H, int K, int math) {
-  if (check_args(net, F, H, K, math)) return 0;
-  UPlan p;
-  build_plan(p, net, K);
-  derive(p, H, math);
-  ULayout L;
-  layout(p, L, F, H, math);
-  return L.total;
-}
-
-int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
-                  const float* const* w, const float* const* b, float* logits, void* ws, size_t ws_bytes,
-                  void* stream) {
+int fwd_impl(int net, int F, int H, int K, int math, int flags, const float* x, long long x_fs, int x_grp,
+             long long x_gs, const float* const* w, const float* const* b, float* logits, const void* const* wpf,
+             const void* const* wpd, void* ws, size_t ws_bytes, UProbe pr, void* stream) {
   if (int rc = check_args(net, F, H, K, math)) return rc;
   UPlan p;
   build_plan(p, net, K);
   derive(p, H, math);
   ULayout L;
-  layout(p, L, F, H, math);
-  PAIG_REQUIRE(ws && ws_bytes >= L.total && x && logits && w && b,
+  layout(p, L, F, H, math, flags);
+  const bool head = (flags & PAIG_UNET_HEAD_FUSED) != 0, ext = (flags & PAIG_UNET_EXT_WPREP) != 0;
+  PAIG_REQUIRE(ws && ws_bytes >= L.total && x && (logits || head) && w && b && (!ext || math != 128 || (wpf && wpd)),
                "paig_unet_fwd: workspace %zu bytes < %zu, or a null operand", ws_bytes, L.total);
   char* base = static_cast<char*>(ws);
-  hipStream_t st = (hipStream_t)stream;
   const int cm = math;
   auto view = [&](const Reg& r, int& lvl) {
     lvl = p.bufs[r.buf].lvl;
@@ -286,11 +286,16 @@ int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long l
     float* t = r.buf == p.LG ? logits : reinterpret_cast<float*>(base + L.act[r.buf]);
     return View{t + r.off * hw, p.bufs[r.buf].C * hw, 0, 0};
   };
+  // the per-block max |x| slots (the split forward writes its layer's; a slot
+  // no forward wrote must read zero: the wgrad then takes the guarded fixed
+  // scale instead of a garbage exponent)
   float* xmax = reinterpret_cast<float*>(base + L.xmax);
-  // every slot zero (a slot no forward wrote falls back to the guarded fixed scale)
-  UNET_HIP(hipMemsetAsync(xmax, 0, p.ops.size() * PAIG_XMAX_SLOTS * 4, st));
-  const int no = (int)p.ops.size();
-  if (cm == 128) {   // every conv's forward / dgrad weight images, one launch
+  UNET_HIP(hipMemsetAsync(xmax, 0, p.ops.size() * PAIG_XMAX_SLOTS * 4, (hipStream_t)stream));
+  const int no = (int)p.ops.size(), nrun = head ? no - 1 : no;   // HEAD_FUSED: the 1x1 head is the caller's
+  auto wimg0 = [&](int i) -> const void* {
+    return cm != 128 ? nullptr : (ext ? wpf[p.ops[i].conv] : base + L.wprep0[i]);
+  };
+  if (cm == 128 && !ext) {   // every conv's forward / dgrad weight images, one launch
     std::vector<const float*> jw;
     std::vector<int> jci, jco, jks, jdg;
     std::vector<void*> jout;
@@ -308,7 +313,7 @@ int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long l
       return rc;
   }
   std::vector<bool> pooled(no, false);
-  for (int i = 0; i < no; ++i) {
+  for (int i = 0; i < nrun; ++i) {
     const UOp& op = p.ops[i];
     if ((op.kind == U_UP && p.fused_buf[op.dst.buf]) || pooled[i]) continue;
     int dlvl;
@@ -329,7 +334,7 @@ int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long l
       long long pool_fs = 0;
       unsigned char* pcode = nullptr;
       long long pcode_fs = 0;
-      if (pool_fused(p, i, H, cm)) {
+      if (pool_fused(p, i, H, cm) && i + 1 < nrun) {
         int pl;
         const View pv = view(p.ops[i + 1].dst, pl);
         pool_out = const_cast<float*>(pv.p);
@@ -340,11 +345,13 @@ int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long l
           pcode_fs = L.pcode_fs[i + 1];
         }
       }
+      const int fl = (op.relu ? 1 : 0) | xfl | cm | (pool_out ? 64 : 0);
+      pr(0, i, op.conv, PAIG_PROBE_CONV_FWD, op.src.n, op.dst.n, Hl, fl);
       rc = paig_conv2d_fwd_pwc(sv.p, sv.fs, sv.grp, sv.gs, const_cast<float*>(dv.p), dv.fs, nullptr, 0, w[op.conv],
-                               b[op.conv], F, op.src.n, op.dst.n, Hl, Hl, op.ks,
-                               (op.relu ? 1 : 0) | xfl | cm | (pool_out ? 64 : 0), xmax + (size_t)i * PAIG_XMAX_SLOTS,
-                               PAIG_XMAX_SLOTS, pool_out, pool_fs, pcode, pcode_fs,
-                               cm == 128 ? base + L.wprep0[i] : nullptr, stream);
+                               b[op.conv], F, op.src.n, op.dst.n, Hl, Hl, op.ks, fl,
+                               xmax + (size_t)i * PAIG_XMAX_SLOTS, PAIG_XMAX_SLOTS, pool_out, pool_fs, pcode, pcode_fs,
+                               wimg0(i), stream);
+      pr(1, i, op.conv, PAIG_PROBE_CONV_FWD, op.src.n, op.dst.n, Hl, fl);
     } else if (op.kind == U_POOL) {
       int slvl;
       const View sv = view(op.src, slvl);
@@ -365,16 +372,21 @@ int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long l
   return 0;
 }
 
-int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
-                  const float* const* w, const float* logits, const float* dlogits, float* const* dwb, void* ws,
-                  size_t ws_bytes, void* stream) {
+int bwd_impl(int net, int F, int H, int K, int math, int flags, const float* x, long long x_fs, int x_grp,
+             long long x_gs, const float* const* w, const float* logits, const float* dlogits, float* const* dwb,
+             int n_extra, const float* const* e_src, const int* e_nb, const int* e_len, float* const* e_dst,
+             const void* const* wpd, void* ws, size_t ws_bytes, UProbe pr, void* stream) {
   if (int rc = check_args(net, F, H, K, math)) return rc;
   UPlan p;
   build_plan(p, net, K);
   derive(p, H, math);
   ULayout L;
-  layout(p, L, F, H, math);
-  PAIG_REQUIRE(ws && ws_bytes >= L.total && x && logits && dlogits && w && dwb,
+  layout(p, L, F, H, math, flags);
+  const bool head = (flags & PAIG_UNET_HEAD_FUSED) != 0, ext = (flags & PAIG_UNET_EXT_WPREP) != 0;
+  const bool sep = (flags & PAIG_UNET_SEPARATE_BWD) != 0;
+  PAIG_REQUIRE(!(flags & PAIG_UNET_INFERENCE), "paig_unet_bwd: the forward ran in inference mode (no gradients)");
+  PAIG_REQUIRE(ws && ws_bytes >= L.total && x && (head || (logits && dlogits)) && w && dwb &&
+                   (!ext || math != 128 || wpd) && n_extra >= 0 && (n_extra == 0 || (e_src && e_nb && e_len && e_dst)),
                "paig_unet_bwd: workspace %zu bytes < %zu, or a null operand", ws_bytes, L.total);
   char* base = static_cast<char*>(ws);
   hipStream_t st = (hipStream_t)stream;
@@ -392,15 +404,25 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
     float* t = reinterpret_cast<float*>(base + L.grad[r.buf]);
     return View{t + r.off * hw, p.bufs[r.buf].C * hw, 0, 0};
   };
-  // d logits: the caller's gradient, with ShallowUNet c13's ReLU' (Q13)
-  float* dlg = reinterpret_cast<float*>(base + L.grad[p.LG]);
-  const long long nlg = (long long)F * K * H * H;
-  UNET_HIP(hipMemcpyAsync(dlg, dlogits, nlg * 4, hipMemcpyDeviceToDevice, st));
-  if (net == 0)
-    if (int rc = paig_relu_mask(logits, dlg, nlg, stream)) return rc;
   // write / accumulate state of every gradient region (engine.py state/mark)
   std::vector<std::vector<std::pair<int, int>>> written(p.bufs.size());
-  written[p.LG].push_back({0, K});
+  int first;
+  if (head) {
+    // the caller's fused head backward wrote the head input's gradient (its
+    // producer's ReLU' applied) into the workspace (paig_unet_buffer)
+    const Reg hs = p.ops[no - 1].src;
+    written[hs.buf].push_back({hs.off, hs.n});
+    first = no - 2;
+  } else {
+    // d logits: the caller's gradient, with ShallowUNet c13's ReLU' (Q13)
+    float* dlg = reinterpret_cast<float*>(base + L.grad[p.LG]);
+    const long long nlg = (long long)F * K * H * H;
+    UNET_HIP(hipMemcpyAsync(dlg, dlogits, nlg * 4, hipMemcpyDeviceToDevice, st));
+    if (net == 0)
+      if (int rc = paig_relu_mask(logits, dlg, nlg, stream)) return rc;
+    written[p.LG].push_back({0, K});
+    first = no - 1;
+  }
   auto state = [&](const Reg& r) {
     int cov = 0;
     for (auto& s : written[r.buf]) {
@@ -415,7 +437,7 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
   std::vector<int> s_nb, s_len;
   std::vector<float*> s_dst;
   std::vector<bool> folded_up(no, false);
-  for (int i = no - 1; i >= 0; --i) {
+  for (int i = first; i >= 0; --i) {
     if (folded_up[i]) continue;
     const UOp& op = p.ops[i];
     if (op.kind == U_POOL && L.pcode[i] != (size_t)-1) continue;   // folded into the pooled conv's backward
@@ -438,14 +460,14 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
       const int n_w = cout * cin * ks * ks;
       int nb = 0;
       const float* xm = xmax + (size_t)i * PAIG_XMAX_SLOTS;
-      const void* wp1 = cm == 128 && L.wprep1[i] != (size_t)-1 ? base + L.wprep1[i] : nullptr;
-      if (xfl && cm && paig_conv2d_bwd_supported(cin, cout, Hl, Hl, ks, cm | 32)) {
+      const void* wp1 = cm != 128 || op.src.buf == p.X0 ? nullptr : (ext ? wpd[op.conv] : base + L.wprep1[i]);
+      if (xfl && cm && !sep && paig_conv2d_bwd_supported(cin, cout, Hl, Hl, ks, cm | 32)) {
         // fused-upsample input: the layer backward and the upsample's backward in one launch
         const int ui = p.fused_up[i];
         const Reg usrc = p.ops[ui].src;
         const View dxv = dview(usrc);
         PAIG_REQUIRE(state(usrc) == 0, "paig_unet_bwd: upsample source gradient already written (op %d)", i);
-        int flags = cm | 32, alvl;
+        int flags2 = cm | 32, alvl;
         const float* aux = nullptr;
         long long aux_fs = 0;
         for (auto& f : p.fin[ui])
@@ -453,23 +475,25 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
             const View a = view(usrc, alvl);
             aux = a.p;
             aux_fs = a.fs;
-            flags |= 2;
+            flags2 |= 2;
           }
+        pr(0, i, op.conv, PAIG_PROBE_CONV_BWD, cin, cout, Hl, flags2);
         rc = paig_conv2d_bwd(sv.p, sv.fs, sv.grp, sv.gs, dyv.p, dyv.fs, const_cast<float*>(dxv.p), dxv.fs, aux, aux_fs,
-                             w[op.conv], slab, NBLK_MAX, &nb, F, cin, cout, Hl, Hl, ks, flags, xm, PAIG_XMAX_SLOTS,
+                             w[op.conv], slab, NBLK_MAX, &nb, F, cin, cout, Hl, Hl, ks, flags2, xm, PAIG_XMAX_SLOTS,
                              nullptr, 0, nullptr, 0, wp1, stream);
+        pr(1, i, op.conv, PAIG_PROBE_CONV_BWD, cin, cout, Hl, flags2);
         if (rc) return rc;
         s_src.push_back(slab), s_nb.push_back(nb), s_len.push_back(n_w + cout), s_dst.push_back(dwb[op.conv]);
         mark(usrc);
         folded_up[ui] = true;
         continue;
       }
-      if (op.src.buf != p.X0 && !xfl && cm && paig_conv2d_bwd_supported(cin, cout, Hl, Hl, ks, cm)) {
+      if (op.src.buf != p.X0 && !xfl && cm && !sep && paig_conv2d_bwd_supported(cin, cout, Hl, Hl, ks, cm)) {
         // data and weight gradients in one launch
         const View dxv = dview(op.src);
         const int mode = state(op.src);
         PAIG_REQUIRE(mode >= 0, "paig_unet_bwd: partially written gradient region (op %d)", i);
-        int flags = cm | (mode == 1 ? 4 : 0), alvl;
+        int flags2 = cm | (mode == 1 ? 4 : 0), alvl;
         const float* aux = nullptr;
         long long aux_fs = 0;
         if (relu_fin) {
@@ -477,7 +501,7 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
           const View a = view(op.src, alvl);
           aux = a.p;
           aux_fs = a.fs;
-          flags |= 2;
+          flags2 |= 2;
         }
         const float* dpool = nullptr;
         long long dpool_fs = 0;
@@ -492,25 +516,29 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
           dpool_fs = pdv.fs;
           pcode = reinterpret_cast<const unsigned char*>(base + L.pcode[i + 1]);
           pcode_fs = L.pcode_fs[i + 1];
-          flags |= 64;
+          flags2 |= 64;
         }
+        pr(0, i, op.conv, PAIG_PROBE_CONV_BWD, cin, cout, Hl, flags2);
         rc = paig_conv2d_bwd(sv.p, sv.fs, sv.grp, sv.gs, dyv.p, dyv.fs, const_cast<float*>(dxv.p), dxv.fs, aux, aux_fs,
-                             w[op.conv], slab, NBLK_MAX, &nb, F, cin, cout, Hl, Hl, ks, cm | (flags & 70), xm,
+                             w[op.conv], slab, NBLK_MAX, &nb, F, cin, cout, Hl, Hl, ks, cm | (flags2 & 70), xm,
                              PAIG_XMAX_SLOTS, dpool, dpool_fs, pcode, pcode_fs, wp1, stream);
+        pr(1, i, op.conv, PAIG_PROBE_CONV_BWD, cin, cout, Hl, flags2);
         if (rc) return rc;
         s_src.push_back(slab), s_nb.push_back(nb), s_len.push_back(n_w + cout), s_dst.push_back(dwb[op.conv]);
         mark(op.src);
         continue;
       }
+      pr(0, i, op.conv, PAIG_PROBE_CONV_WGRAD, cin, cout, Hl, xfl | cm);
       rc = paig_conv2d_wgrad_ex(sv.p, sv.fs, sv.grp, sv.gs, dyv.p, dyv.fs, slab, NBLK_MAX, &nb, F, cin, cout, Hl, Hl,
                                 ks, xfl | cm, xm, PAIG_XMAX_SLOTS, stream);
+      pr(1, i, op.conv, PAIG_PROBE_CONV_WGRAD, cin, cout, Hl, xfl | cm);
       if (rc) return rc;
       s_src.push_back(slab), s_nb.push_back(nb), s_len.push_back(n_w + cout), s_dst.push_back(dwb[op.conv]);
       if (op.src.buf == p.X0) continue;   // no input gradient (Q10)
       const View dxv = dview(op.src);
       const int mode = state(op.src);
       PAIG_REQUIRE(mode >= 0, "paig_unet_bwd: partially written gradient region (op %d)", i);
-      int flags = 8 | (mode == 1 ? 4 : 0), alvl;
+      int flags2 = 8 | (mode == 1 ? 4 : 0), alvl;
       const float* aux = nullptr;
       long long aux_fs = 0;
       if (relu_fin) {
@@ -518,10 +546,12 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
         const View a = view(op.src, alvl);
         aux = a.p;
         aux_fs = a.fs;
-        flags |= 2;
+        flags2 |= 2;
       }
+      pr(0, i, op.conv, PAIG_PROBE_CONV_DGRAD, cin, cout, Hl, flags2 | cm);
       rc = paig_conv2d_fwd_pw(dyv.p, dyv.fs, 0, 0, const_cast<float*>(dxv.p), dxv.fs, aux, aux_fs, w[op.conv], nullptr,
-                              F, cout, cin, Hl, Hl, ks, flags | cm, nullptr, 0, nullptr, 0, wp1, stream);
+                              F, cout, cin, Hl, Hl, ks, flags2 | cm, nullptr, 0, nullptr, 0, wp1, stream);
+      pr(1, i, op.conv, PAIG_PROBE_CONV_DGRAD, cin, cout, Hl, flags2 | cm);
       mark(op.src);
     } else if (op.kind == U_POOL) {
       int slvl;
@@ -547,8 +577,86 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
     }
     if (rc) return rc;
   }
-  // every conv's weight + bias gradient: one batched deterministic reduction
+  // every conv's weight + bias gradient and the caller's extra partial-
+  // gradient slabs: one batched deterministic reduction
+  for (int e = 0; e < n_extra; ++e)
+    s_src.push_back(e_src[e]), s_nb.push_back(e_nb[e]), s_len.push_back(e_len[e]), s_dst.push_back(e_dst[e]);
   return paig_slab_reduce_multi((int)s_src.size(), s_src.data(), s_nb.data(), s_len.data(), s_dst.data(), 0, stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t paig_unet_workspace_ex(int net, int F, int H, int K, int math, int flags) {
+  if (check_args(net, F, H, K, math)) return 0;
+  UPlan p;
+  build_plan(p, net, K);
+  derive(p, H, math);
+  ULayout L;
+  layout(p, L, F, H, math, flags);
+  return L.total;
+}
+
+size_t paig_unet_workspace(int net, int F, int H, int K, int math) {
+  return paig_unet_workspace_ex(net, F, H, K, math, 0);
+}
+
+long long paig_unet_buffer(int net, int F, int H, int K, int math, int flags, int which, int buf) {
+  if (check_args(net, F, H, K, math)) return -1;
+  UPlan p;
+  build_plan(p, net, K);
+  derive(p, H, math);
+  if (buf < 0 || buf >= (int)p.bufs.size() || (which != 0 && which != 1)) return -1;
+  ULayout L;
+  layout(p, L, F, H, math, flags);
+  const size_t o = which == 0 ? L.act[buf] : L.grad[buf];
+  return o == (size_t)-1 ? -1 : (long long)o;
+}
+
+int paig_unet_query(int net, int K, int what) {
+  if (net != 0 && net != 1) return -1;
+  UPlan p;
+  build_plan(p, net, K);
+  switch (what) {
+    case 0: return p.nconv;
+    case 1: return (int)p.bufs.size();
+    case 2: return p.ops.back().src.buf;   // the 1x1 head's input buffer
+    case 3: return p.ops.back().src.n;     // ... and its channels
+    case 4: return p.LG;
+    default: return -1;
+  }
+}
+
+int paig_unet_fwd_ex(int net, int F, int H, int K, int math, int flags, const float* x, long long x_fs, int x_grp,
+                     long long x_gs, const float* const* w, const float* const* b, float* logits,
+                     const void* const* wprep_fwd, const void* const* wprep_dg, void* ws, size_t ws_bytes,
+                     paig_unet_probe_fn probe, void* probe_ctx, void* stream) {
+  return fwd_impl(net, F, H, K, math, flags, x, x_fs, x_grp, x_gs, w, b, logits, wprep_fwd, wprep_dg, ws, ws_bytes,
+                  UProbe{probe, probe_ctx}, stream);
+}
+
+int paig_unet_bwd_ex(int net, int F, int H, int K, int math, int flags, const float* x, long long x_fs, int x_grp,
+                     long long x_gs, const float* const* w, const float* logits, const float* dlogits,
+                     float* const* dwb, int n_extra, const float* const* extra_src, const int* extra_nblk,
+                     const int* extra_len, float* const* extra_dst, const void* const* wprep_dg, void* ws,
+                     size_t ws_bytes, paig_unet_probe_fn probe, void* probe_ctx, void* stream) {
+  return bwd_impl(net, F, H, K, math, flags, x, x_fs, x_grp, x_gs, w, logits, dlogits, dwb, n_extra, extra_src,
+                  extra_nblk, extra_len, extra_dst, wprep_dg, ws, ws_bytes, UProbe{probe, probe_ctx}, stream);
+}
+
+int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
+                  const float* const* w, const float* const* b, float* logits, void* ws, size_t ws_bytes,
+                  void* stream) {
+  return fwd_impl(net, F, H, K, math, 0, x, x_fs, x_grp, x_gs, w, b, logits, nullptr, nullptr, ws, ws_bytes,
+                  UProbe{nullptr, nullptr}, stream);
+}
+
+int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
+                  const float* const* w, const float* logits, const float* dlogits, float* const* dwb, void* ws,
+                  size_t ws_bytes, void* stream) {
+  return bwd_impl(net, F, H, K, math, 0, x, x_fs, x_grp, x_gs, w, logits, dlogits, dwb, 0, nullptr, nullptr, nullptr,
+                  nullptr, nullptr, ws, ws_bytes, UProbe{nullptr, nullptr}, stream);
 }
 
 }  // extern "C"

@@ -512,34 +512,66 @@ __global__ void mask_softmax_bwd_v_k(const float* __restrict__ lg, FView x, cons
   }
 }
 
-// ------------------------------------- fused ShallowUNet head + mask softmax ----
-// ShallowUNet's last layer c13 (1x1 conv, 8 -> K, ReLU'd, Q13; blocks.py:276,
-// 307) fused into the mask softmax (blocks.py:84-93): the logits are formed
-// per pixel in fp32 FMAs from c12's output and never stored.  Forward: logits
-// -> softmax -> masks, masked objects.  Backward: the softmax backward, the
-// c13 ReLU' (the logits recomputed with the forward's exact operation order),
-// c13's input gradient with c12's ReLU' (dX12, the c12 backward's dY) and
-// c13's weight/bias gradient as one slab row per block (deterministic order,
-// reduced with the U-Net's slabs).  Replaces the c13 conv fwd/dgrad/wgrad and
-// the separate softmax kernels: the logits' write and re-reads, and 3 launches.
-constexpr int HEAD_CI = 8;   // ShallowUNet hidden width (c13's input channels)
-
-template <int K>
+// ------------------------------------------- fused U-Net head + mask softmax ----
+// The U-Net's last layer (a 1x1 conv, CI -> K) fused into the mask softmax
+// (blocks.py:84-96): the logits are formed per pixel in fp32 FMAs from the
+// previous layer's output and never stored.
+//   * ShallowUNet (H < 40): c13, 8 -> K, ReLU'd (Q13; blocks.py:276,307);
+//   * UNet (H >= 40): c18, 16 -> K, not ReLU'd (blocks.py:170,236), and the
+//     masked objects' AvgPool2d(2) (blocks.py:94-96) that feeds l1.
+// Forward: logits -> softmax -> masks, masked objects (+ pooled objects).
+// Backward: the softmax backward (from the pooled objects' gradient on the
+// UNet), the ReLU' of the logits where they are ReLU'd (recomputed in the
+// forward's exact operation order), the head's input gradient with the
+// previous layer's ReLU' (dXl: that layer's dY) and the head's weight / bias
+// gradient as one slab row per block (deterministic order, reduced with the
+// U-Net's slabs).  Replaces the head conv's forward / dgrad / wgrad and the
+// separate softmax kernels: the logits' write and re-reads and 3 launches
+// (mnist: 1.05 ms per step of separate kernels).
+template <int K, int CI>
 __device__ __forceinline__ void head_logits(const float* __restrict__ w, const float* __restrict__ b, const m4* xv,
                                             m4* l) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     m4 a = m4{b[k], b[k], b[k], b[k]};
 #pragma unroll
-    for (int c = 0; c < HEAD_CI; ++c)
+    for (int c = 0; c < CI; ++c)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] = fmaf(w[k * HEAD_CI + c], xv[c][j], a[j]);
+      for (int j = 0; j < 4; ++j) a[j] = fmaf(w[k * CI + c], xv[c][j], a[j]);
     l[k] = a;
   }
 }
 
-template <int K>
-__global__ void __launch_bounds__(256) head_mask_fwd_k(const float* __restrict__ x12, const float* __restrict__ w,
+// logits -> (ReLU) -> softmax with the constant background logit 1, in
+// mask_softmax_fwd_v_k's operation order: mk[0..K] (4 pixels each)
+template <int K, bool RELU>
+__device__ __forceinline__ void head_softmax(m4* l, m4* mk) {
+  m4 m = m4{1.f, 1.f, 1.f, 1.f}, e[K + 1];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (RELU) l[k][j] = l[k][j] < 0.f ? 0.f : l[k][j];   // c13's ReLU (Q13)
+      m[j] = fmaxf(m[j], l[k][j]);
+    }
+  m4 s = m4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[k][j] = expf(l[k][j] - m[j]);
+    s += e[k];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) e[K][j] = expf(1.f - m[j]);
+  s += e[K];
+#pragma unroll
+  for (int k = 0; k <= K; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mk[k][j] = e[k][j] / s[j];
+}
+
+template <int K, int CI, bool RELU>
+__global__ void __launch_bounds__(256) head_mask_fwd_k(const float* __restrict__ xl, const float* __restrict__ w,
                                                        const float* __restrict__ b, FView x, float* __restrict__ masks,
                                                        float* __restrict__ objs, int F, int HW) {
   const int Q = HW / 4;
@@ -547,54 +579,92 @@ __global__ void __launch_bounds__(256) head_mask_fwd_k(const float* __restrict__
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const int p = (int)(i % Q) * 4;
     const int f = (int)(i / Q);
-    m4 hv[HEAD_CI];
+    m4 hv[CI];
 #pragma unroll
-    for (int c = 0; c < HEAD_CI; ++c) hv[c] = *reinterpret_cast<const m4*>(x12 + ((long long)f * HEAD_CI + c) * HW + p);
+    for (int c = 0; c < CI; ++c) hv[c] = *reinterpret_cast<const m4*>(xl + ((long long)f * CI + c) * HW + p);
     const float* xp = x.frame(f);
     m4 xv[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) xv[c] = *reinterpret_cast<const m4*>(xp + c * HW + p);
-    m4 l[K], e[K + 1];
-    head_logits<K>(w, b, hv, l);
-    m4 m = m4{1.f, 1.f, 1.f, 1.f};
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        l[k][j] = l[k][j] < 0.f ? 0.f : l[k][j];   // c13's ReLU (Q13)
-        m[j] = fmaxf(m[j], l[k][j]);
-      }
-    m4 s = m4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) e[k][j] = expf(l[k][j] - m[j]);
-      s += e[k];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) e[K][j] = expf(1.f - m[j]);
-    s += e[K];
+    m4 l[K], mk[K + 1];
+    head_logits<K, CI>(w, b, hv, l);
+    head_softmax<K, RELU>(l, mk);
 #pragma unroll
     for (int k = 0; k <= K; ++k) {
-      m4 mk;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) mk[j] = e[k][j] / s[j];
-      *reinterpret_cast<m4*>(masks + ((long long)f * (K + 1) + k) * HW + p) = mk;
+      *reinterpret_cast<m4*>(masks + ((long long)f * (K + 1) + k) * HW + p) = mk[k];
       if (k < K)
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-          *reinterpret_cast<m4*>(objs + ((long long)k * F + f) * 3 * HW + (long long)c * HW + p) = mk * xv[c];
+          *reinterpret_cast<m4*>(objs + ((long long)k * F + f) * 3 * HW + (long long)c * HW + p) = mk[k] * xv[c];
     }
   }
 }
 
-template <int K>
-__global__ void __launch_bounds__(256) head_mask_bwd_k(const float* __restrict__ x12, const float* __restrict__ w,
+// UNet: item = columns 4u .. 4u+3 of the row pair 2py, 2py+1 (two 2x2
+// windows): masks and objects of both rows, and the windows' average in
+// mask_softmax_pool_fwd_k's order ((0,0), (0,1), (1,0), (1,1), then * 1/4)
+template <int K, int CI, bool RELU>
+__global__ void __launch_bounds__(256) head_mask_pool_fwd_k(const float* __restrict__ xl, const float* __restrict__ w,
+                                                            const float* __restrict__ b, FView x,
+                                                            float* __restrict__ masks, float* __restrict__ objs,
+                                                            float* __restrict__ pobjs, int F, int H, int W) {
+  const int HW = H * W, W2 = W / 2, W4 = W / 4, HW4 = (H / 2) * W2;
+  const long long n = (long long)F * (H / 2) * W4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int u = (int)(i % W4), py = (int)((i / W4) % (H / 2)), f = (int)(i / ((long long)W4 * (H / 2)));
+    const float* xp = x.frame(f);
+    float2 pa[K][3];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pa[k][c] = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int p = (2 * py + rr) * W + 4 * u;
+      m4 hv[CI];
+#pragma unroll
+      for (int c = 0; c < CI; ++c) hv[c] = *reinterpret_cast<const m4*>(xl + ((long long)f * CI + c) * HW + p);
+      m4 xv[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) xv[c] = *reinterpret_cast<const m4*>(xp + c * HW + p);
+      m4 l[K], mk[K + 1];
+      head_logits<K, CI>(w, b, hv, l);
+      head_softmax<K, RELU>(l, mk);
+#pragma unroll
+      for (int k = 0; k <= K; ++k) {
+        *reinterpret_cast<m4*>(masks + ((long long)f * (K + 1) + k) * HW + p) = mk[k];
+        if (k < K)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const m4 o = mk[k] * xv[c];
+            *reinterpret_cast<m4*>(objs + ((long long)k * F + f) * 3 * HW + (long long)c * HW + p) = o;
+            pa[k][c].x += o[0];
+            pa[k][c].x += o[1];
+            pa[k][c].y += o[2];
+            pa[k][c].y += o[3];
+          }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        *reinterpret_cast<float2*>(pobjs + ((long long)k * F + f) * 3 * HW4 + (long long)c * HW4 + py * W2 + 2 * u) =
+            make_float2(pa[k][c].x * 0.25f, pa[k][c].y * 0.25f);
+  }
+}
+
+// POOL: dobjs is the gradient of the pooled objects [K][F][3][H/2][W/2]
+// (each pixel takes 1/4 of its window's, mask_softmax_bwd_k's order)
+template <int K, int CI, bool RELU, bool POOL>
+__global__ void __launch_bounds__(256) head_mask_bwd_k(const float* __restrict__ xl, const float* __restrict__ w,
                                                        const float* __restrict__ b, FView x,
                                                        const float* __restrict__ masks, const float* __restrict__ dobjs,
-                                                       float* __restrict__ dx12, float* __restrict__ slab, int F,
-                                                       int HW) {
-  constexpr int NW = K * HEAD_CI + K;   // slab row: dW[k][c], then db[k]
+                                                       float* __restrict__ dxl, float* __restrict__ slab, int F, int H,
+                                                       int W) {
+  constexpr int NW = K * CI + K;   // slab row: dW[k][c], then db[k]
+  const int HW = H * W, W2 = W / 2, HW4 = (H / 2) * W2;
+  const int DHW = POOL ? HW4 : HW;
   const int Q = HW / 4;
   const long long n = (long long)F * Q;
   float acc[NW];
@@ -603,14 +673,15 @@ __global__ void __launch_bounds__(256) head_mask_bwd_k(const float* __restrict__
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const int p = (int)(i % Q) * 4;
     const int f = (int)(i / Q);
-    m4 hv[HEAD_CI];
+    const int pq = POOL ? ((p / W) >> 1) * W2 + ((p % W) >> 1) : p;   // (pooled) index of the first pixel
+    m4 hv[CI];
 #pragma unroll
-    for (int c = 0; c < HEAD_CI; ++c) hv[c] = *reinterpret_cast<const m4*>(x12 + ((long long)f * HEAD_CI + c) * HW + p);
+    for (int c = 0; c < CI; ++c) hv[c] = *reinterpret_cast<const m4*>(xl + ((long long)f * CI + c) * HW + p);
     const float* xp = x.frame(f);
     m4 xv[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) xv[c] = *reinterpret_cast<const m4*>(xp + c * HW + p);
-    // softmax backward (mask_softmax_bwd_v_k's order)
+    // softmax backward (mask_softmax_bwd_v_k's / mask_softmax_bwd_k's order)
     m4 dm[K], mk[K];
     m4 dot = m4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -618,7 +689,14 @@ __global__ void __launch_bounds__(256) head_mask_bwd_k(const float* __restrict__
       m4 a = m4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const m4 d = *reinterpret_cast<const m4*>(dobjs + ((long long)k * F + f) * 3 * HW + (long long)c * HW + p);
+        const float* dp = dobjs + ((long long)k * F + f) * 3 * DHW + (long long)c * DHW + pq;
+        m4 d;
+        if constexpr (POOL) {
+          const float2 dq = *reinterpret_cast<const float2*>(dp);
+          d = m4{dq.x, dq.x, dq.y, dq.y} * 0.25f;
+        } else {
+          d = *reinterpret_cast<const m4*>(dp);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) a[j] = fmaf(d[j], xv[c][j], a[j]);
       }
@@ -627,34 +705,41 @@ __global__ void __launch_bounds__(256) head_mask_bwd_k(const float* __restrict__
 #pragma unroll
       for (int j = 0; j < 4; ++j) dot[j] = fmaf(mk[k][j], a[j], dot[j]);
     }
-    m4 l[K], g[K];
-    head_logits<K>(w, b, hv, l);
+    m4 g[K];
+    if constexpr (RELU) {
+      m4 l[K];
+      head_logits<K, CI>(w, b, hv, l);
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      g[k] = mk[k] * (dm[k] - dot);
+      for (int k = 0; k < K; ++k) {
+        g[k] = mk[k] * (dm[k] - dot);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) g[k][j] = l[k][j] > 0.f ? g[k][j] : 0.f;   // c13's ReLU'
+        for (int j = 0; j < 4; ++j) g[k][j] = l[k][j] > 0.f ? g[k][j] : 0.f;   // c13's ReLU'
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) g[k] = mk[k] * (dm[k] - dot);
     }
-    // c13 input gradient (c12's ReLU' applied) and the weight / bias partials
+    // the head's input gradient (the previous layer's ReLU' applied) and the
+    // weight / bias partials
 #pragma unroll
-    for (int c = 0; c < HEAD_CI; ++c) {
+    for (int c = 0; c < CI; ++c) {
       m4 d = m4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < K; ++k)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) d[j] = fmaf(w[k * HEAD_CI + c], g[k][j], d[j]);
+        for (int j = 0; j < 4; ++j) d[j] = fmaf(w[k * CI + c], g[k][j], d[j]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) d[j] = hv[c][j] > 0.f ? d[j] : 0.f;
-      *reinterpret_cast<m4*>(dx12 + ((long long)f * HEAD_CI + c) * HW + p) = d;
+      *reinterpret_cast<m4*>(dxl + ((long long)f * CI + c) * HW + p) = d;
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
 #pragma unroll
-      for (int c = 0; c < HEAD_CI; ++c)
+      for (int c = 0; c < CI; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[k * HEAD_CI + c] = fmaf(g[k][j], hv[c][j], acc[k * HEAD_CI + c]);
+        for (int j = 0; j < 4; ++j) acc[k * CI + c] = fmaf(g[k][j], hv[c][j], acc[k * CI + c]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[K * HEAD_CI + k] += g[k][j];
+      for (int j = 0; j < 4; ++j) acc[K * CI + k] += g[k][j];
     }
   }
   // block reduction in a fixed order: wave butterflies, then the 4 waves
@@ -1053,6 +1138,12 @@ static bool head_mask_ok(const void* a, const void* b, const void* c, const void
   return (H * W) % 4 == 0 && (K == 2 || K == 3) && x_fs % 4 == 0 && x_gs % 4 == 0 &&
          ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)d | (uintptr_t)e) % 16 == 0;
 }
+// the two heads: ShallowUNet (CI 8, ReLU'd logits: flags 1), UNet (CI 16,
+// pooled objects: flags 2)
+static bool head_mask_kind(int CI, int flags, int H, int W, const void* pobjs) {
+  if (CI == 8 && flags == 1) return true;
+  return CI == 16 && flags == 2 && H % 2 == 0 && W % 4 == 0 && ((uintptr_t)pobjs % 8) == 0;
+}
 
 int paig_head_mask_blocks(int F, int H, int W) {
   const long long n = (long long)F * H * W / 4;
@@ -1060,37 +1151,62 @@ int paig_head_mask_blocks(int F, int H, int W) {
   return (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
 }
 
-int paig_head_mask_fwd(const float* x12, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
-                       long long x_gs, float* masks, float* objs, int F, int K, int H, int W, void* stream) {
+int paig_head_mask_fwd_ex(const float* xl, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                          long long x_gs, float* masks, float* objs, float* pobjs, int F, int K, int CI, int H, int W,
+                          int flags, void* stream) {
   if (F <= 0) return 0;
-  PAIG_REQUIRE(head_mask_ok(x12, x, masks, objs, nullptr, x_fs, x_gs, K, H, W),
+  PAIG_REQUIRE(head_mask_ok(xl, x, masks, objs, nullptr, x_fs, x_gs, K, H, W),
                "head_mask_fwd: needs K in {2,3}, H*W %% 4 == 0 and 16-byte aligned buffers (K=%d H=%d W=%d)", K, H, W);
-  const dim3 g(grid_for((long long)F * H * W / 4));
-  if (K == 2)
-    hipLaunchKernelGGL(head_mask_fwd_k<2>, g, dim3(256), 0, (hipStream_t)stream, x12, w, b, FView{x, x_fs, x_gs, x_grp},
-                       masks, objs, F, H * W);
-  else
-    hipLaunchKernelGGL(head_mask_fwd_k<3>, g, dim3(256), 0, (hipStream_t)stream, x12, w, b, FView{x, x_fs, x_gs, x_grp},
-                       masks, objs, F, H * W);
+  PAIG_REQUIRE(head_mask_kind(CI, flags, H, W, pobjs) && (!(flags & 2) || pobjs),
+               "head_mask_fwd: (CI=%d, flags=%d) is neither the ShallowUNet head (8, 1) nor the UNet's (16, 2)", CI,
+               flags);
+  const FView xv{x, x_fs, x_gs, x_grp};
+  hipStream_t st = (hipStream_t)stream;
+  if (flags & 2) {
+    const dim3 g(grid_for((long long)F * (H / 2) * (W / 4)));
+    if (K == 2) hipLaunchKernelGGL((head_mask_pool_fwd_k<2, 16, false>), g, dim3(256), 0, st, xl, w, b, xv, masks, objs, pobjs, F, H, W);
+    else hipLaunchKernelGGL((head_mask_pool_fwd_k<3, 16, false>), g, dim3(256), 0, st, xl, w, b, xv, masks, objs, pobjs, F, H, W);
+  } else {
+    const dim3 g(grid_for((long long)F * H * W / 4));
+    if (K == 2) hipLaunchKernelGGL((head_mask_fwd_k<2, 8, true>), g, dim3(256), 0, st, xl, w, b, xv, masks, objs, F, H * W);
+    else hipLaunchKernelGGL((head_mask_fwd_k<3, 8, true>), g, dim3(256), 0, st, xl, w, b, xv, masks, objs, F, H * W);
+  }
   PAIG_CHECK_LAUNCH();
   return 0;
+}
+
+int paig_head_mask_bwd_ex(const float* xl, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                          long long x_gs, const float* masks, const float* dobjs, float* dxl, float* slab, int F, int K,
+                          int CI, int H, int W, int flags, void* stream) {
+  if (F <= 0) return 0;
+  PAIG_REQUIRE(head_mask_ok(xl, x, masks, (flags & 2) ? nullptr : dobjs, dxl, x_fs, x_gs, K, H, W),
+               "head_mask_bwd: needs K in {2,3}, H*W %% 4 == 0 and 16-byte aligned buffers (K=%d H=%d W=%d)", K, H, W);
+  PAIG_REQUIRE(head_mask_kind(CI, flags, H, W, dobjs),
+               "head_mask_bwd: (CI=%d, flags=%d) is neither the ShallowUNet head (8, 1) nor the UNet's (16, 2)", CI,
+               flags);
+  const dim3 g(paig_head_mask_blocks(F, H, W));
+  const FView xv{x, x_fs, x_gs, x_grp};
+  hipStream_t st = (hipStream_t)stream;
+  if (flags & 2) {
+    if (K == 2) hipLaunchKernelGGL((head_mask_bwd_k<2, 16, false, true>), g, dim3(256), 0, st, xl, w, b, xv, masks, dobjs, dxl, slab, F, H, W);
+    else hipLaunchKernelGGL((head_mask_bwd_k<3, 16, false, true>), g, dim3(256), 0, st, xl, w, b, xv, masks, dobjs, dxl, slab, F, H, W);
+  } else {
+    if (K == 2) hipLaunchKernelGGL((head_mask_bwd_k<2, 8, true, false>), g, dim3(256), 0, st, xl, w, b, xv, masks, dobjs, dxl, slab, F, H, W);
+    else hipLaunchKernelGGL((head_mask_bwd_k<3, 8, true, false>), g, dim3(256), 0, st, xl, w, b, xv, masks, dobjs, dxl, slab, F, H, W);
+  }
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
+int paig_head_mask_fwd(const float* x12, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
+                       long long x_gs, float* masks, float* objs, int F, int K, int H, int W, void* stream) {
+  return paig_head_mask_fwd_ex(x12, w, b, x, x_fs, x_grp, x_gs, masks, objs, nullptr, F, K, 8, H, W, 1, stream);
 }
 
 int paig_head_mask_bwd(const float* x12, const float* w, const float* b, const float* x, long long x_fs, int x_grp,
                        long long x_gs, const float* masks, const float* dobjs, float* dx12, float* slab, int F, int K,
                        int H, int W, void* stream) {
-  if (F <= 0) return 0;
-  PAIG_REQUIRE(head_mask_ok(x12, x, masks, dobjs, dx12, x_fs, x_gs, K, H, W),
-               "head_mask_bwd: needs K in {2,3}, H*W %% 4 == 0 and 16-byte aligned buffers (K=%d H=%d W=%d)", K, H, W);
-  const dim3 g(paig_head_mask_blocks(F, H, W));
-  if (K == 2)
-    hipLaunchKernelGGL(head_mask_bwd_k<2>, g, dim3(256), 0, (hipStream_t)stream, x12, w, b, FView{x, x_fs, x_gs, x_grp},
-                       masks, dobjs, dx12, slab, F, H * W);
-  else
-    hipLaunchKernelGGL(head_mask_bwd_k<3>, g, dim3(256), 0, (hipStream_t)stream, x12, w, b, FView{x, x_fs, x_gs, x_grp},
-                       masks, dobjs, dx12, slab, F, H * W);
-  PAIG_CHECK_LAUNCH();
-  return 0;
+  return paig_head_mask_bwd_ex(x12, w, b, x, x_fs, x_grp, x_gs, masks, dobjs, dx12, slab, F, K, 8, H, W, 1, stream);
 }
 
 int paig_pos_head_fwd(const float* h3, float* pos, int N, int K, float half, void* stream) {

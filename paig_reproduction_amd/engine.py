@@ -23,103 +23,13 @@ import os
 
 import torch
 
-from ._lib import XMAX_SLOTS, PaigError, lib, ptr, stream_handle, require_device
+from ._lib import PaigError, lib, ptr, stream_handle, require_device
 
-# --------------------------------------------------------------------------
-# U-Net plans (buffers + ops), forward order.  A buffer is (channels, level),
-# level = spatial divisor.  An op's src/dst are (buffer, channel offset, count).
-# --------------------------------------------------------------------------
-
-
-def _conv(name, src, dst, relu, ks=3):
-    return {"op": "conv", "name": name, "src": src, "dst": dst, "relu": relu, "ks": ks}
-
-
-def _pool(src, dst):
-    return {"op": "pool", "src": src, "dst": dst}
-
-
-def _up(src, dst):
-    return {"op": "up", "src": src, "dst": dst}
-
-
-def shallow_unet_plan(c, K):
-    """ShallowUNet, nn/network/blocks.py:240-308 (hidden c=8; c13 ReLU'd, Q13)."""
-    bufs = {"X0": (3, 1), "A1": (c, 1), "CAT2": (3 * c, 1), "P1": (c, 2), "A3": (2 * c, 2), "CAT1": (4 * c, 2),
-            "P2": (2 * c, 4), "A5": (4 * c, 4), "A6": (4 * c, 4), "U1": (4 * c, 2), "A8": (2 * c, 2),
-            "A9": (2 * c, 2), "U2": (2 * c, 1), "A11": (c, 1), "A12": (c, 1), "LG": (K, 1)}
-    ops = [
-        _conv("c1", ("X0", 0, 3), ("A1", 0, c), True),
-        _conv("c2", ("A1", 0, c), ("CAT2", 2 * c, c), True),
-        _pool(("CAT2", 2 * c, c), ("P1", 0, c)),
-        _conv("c3", ("P1", 0, c), ("A3", 0, 2 * c), True),
-        _conv("c4", ("A3", 0, 2 * c), ("CAT1", 2 * c, 2 * c), True),
-        _pool(("CAT1", 2 * c, 2 * c), ("P2", 0, 2 * c)),
-        _conv("c5", ("P2", 0, 2 * c), ("A5", 0, 4 * c), True),
-        _conv("c6", ("A5", 0, 4 * c), ("A6", 0, 4 * c), True),
-        _up(("A6", 0, 4 * c), ("U1", 0, 4 * c)),
-        _conv("c7", ("U1", 0, 4 * c), ("CAT1", 0, 2 * c), False),
-        _conv("c8", ("CAT1", 0, 4 * c), ("A8", 0, 2 * c), True),
-        _conv("c9", ("A8", 0, 2 * c), ("A9", 0, 2 * c), True),
-        _up(("A9", 0, 2 * c), ("U2", 0, 2 * c)),
-        _conv("c10", ("U2", 0, 2 * c), ("CAT2", 0, 2 * c), False),
-        _conv("c11", ("CAT2", 0, 3 * c), ("A11", 0, c), True),
-        _conv("c12", ("A11", 0, c), ("A12", 0, c), True),
-        _conv("c13", ("A12", 0, c), ("LG", 0, K), True, ks=1),
-    ]
-    return bufs, ops
-
-
-def unet_plan(h, K):
-    """UNet, nn/network/blocks.py:106-237 (hidden h=16; c9/c12/c15/c18 un-ReLU'd)."""
-    bufs = {"X0": (3, 1), "A1": (h, 1), "CAT3": (3 * h, 1), "P1": (h, 2), "A3": (2 * h, 2), "CAT2": (4 * h, 2),
-            "P2": (2 * h, 4), "A5": (4 * h, 4), "CAT1": (6 * h, 4), "P3": (4 * h, 8), "A7": (8 * h, 8),
-            "A8": (8 * h, 8), "U1": (8 * h, 4), "A10": (4 * h, 4), "A11": (4 * h, 4), "U2": (4 * h, 2),
-            "A13": (2 * h, 2), "A14": (2 * h, 2), "U3": (2 * h, 1), "A16": (h, 1), "A17": (h, 1), "LG": (K, 1)}
-    ops = [
-        _conv("c1", ("X0", 0, 3), ("A1", 0, h), True),
-        _conv("c2", ("A1", 0, h), ("CAT3", 2 * h, h), True),
-        _pool(("CAT3", 2 * h, h), ("P1", 0, h)),
-        _conv("c3", ("P1", 0, h), ("A3", 0, 2 * h), True),
-        _conv("c4", ("A3", 0, 2 * h), ("CAT2", 2 * h, 2 * h), True),
-        _pool(("CAT2", 2 * h, 2 * h), ("P2", 0, 2 * h)),
-        _conv("c5", ("P2", 0, 2 * h), ("A5", 0, 4 * h), True),
-        _conv("c6", ("A5", 0, 4 * h), ("CAT1", 2 * h, 4 * h), True),
-        _pool(("CAT1", 2 * h, 4 * h), ("P3", 0, 4 * h)),
-        _conv("c7", ("P3", 0, 4 * h), ("A7", 0, 8 * h), True),
-        _conv("c8", ("A7", 0, 8 * h), ("A8", 0, 8 * h), True),
-        _up(("A8", 0, 8 * h), ("U1", 0, 8 * h)),
-        _conv("c9", ("U1", 0, 8 * h), ("CAT1", 0, 2 * h), False),
-        _conv("c10", ("CAT1", 0, 6 * h), ("A10", 0, 4 * h), True),
-        _conv("c11", ("A10", 0, 4 * h), ("A11", 0, 4 * h), True),
-        _up(("A11", 0, 4 * h), ("U2", 0, 4 * h)),
-        _conv("c12", ("U2", 0, 4 * h), ("CAT2", 0, 2 * h), False),
-        _conv("c13", ("CAT2", 0, 4 * h), ("A13", 0, 2 * h), True),
-        _conv("c14", ("A13", 0, 2 * h), ("A14", 0, 2 * h), True),
-        _up(("A14", 0, 2 * h), ("U3", 0, 2 * h)),
-        _conv("c15", ("U3", 0, 2 * h), ("CAT3", 0, 2 * h), False),
-        _conv("c16", ("CAT3", 0, 3 * h), ("A16", 0, h), True),
-        _conv("c17", ("A16", 0, h), ("A17", 0, h), True),
-        _conv("c18", ("A17", 0, h), ("LG", 0, K), False, ks=1),
-    ]
-    return bufs, ops
-
-
-def _overlap(a, b):
-    return a[0] == b[0] and a[1] < b[1] + b[2] and b[1] < a[1] + a[2]
-
-
-def backward_plan(ops):
-    """For every op, the producer regions of its source that it FINALIZES
-    (it is their earliest consumer in forward order = last in reverse), so a
-    ReLU derivative is applied exactly once, after all contributions."""
-    producers = [(i, op["dst"], op.get("relu", False)) for i, op in enumerate(ops)]
-    fin = {i: [] for i in range(len(ops))}
-    for pi, region, relu in producers:
-        consumers = [i for i, op in enumerate(ops) if i > pi and _overlap(op["src"], region)]
-        if consumers:
-            fin[min(consumers)].append((region, relu))
-    return fin
+# The U-Net plans (ShallowUNet blocks.py:240-308, UNet :106-237: buffers,
+# ops, which upsamples / pools fuse into which convs, the backward's
+# write / accumulate / ReLU' bookkeeping) live in ONE place: csrc/unet.hip,
+# whose C-ABI interpreter (paig_unet_fwd_ex / paig_unet_bwd_ex) IS the
+# engine's U-Net stage.  Python only names the convs (c1..cN, plan order).
 
 
 class Layout:
@@ -146,42 +56,27 @@ class Layout:
         self.alt_vel = model.alt_vel
         self.cell = {"spring_ode_cell": 0, "bouncing_ode_cell": 1, "gravity_ode_cell": 2}[model.cell_type]
         self.unet = self.H >= 40 if net is None else net == "unet"
-        if self.unet:       # UNet(hidden 16), blocks.py:106-237; c18 not ReLU'd
-            self.bufs, self.ops = unet_plan(16, self.K)
-            self.prefix = "encoder.unet."
-        else:               # ShallowUNet(hidden 8), blocks.py:240-308; c13 ReLU'd (Q13)
-            self.bufs, self.ops = shallow_unet_plan(8, self.K)
-            self.prefix = "encoder.shallow_unet."
-        self.lg_relu = not self.unet
+        L = lib()
+        self.net = 1 if self.unet else 0   # paig_unet_*: 0 ShallowUNet(hidden 8), 1 UNet(hidden 16)
+        self.prefix = "encoder.unet." if self.unet else "encoder.shallow_unet."
+        self.nconv = L.paig_unet_query(self.net, self.K, 0)
+        self.lg_relu = not self.unet   # ShallowUNet's c13 output is ReLU'd (Q13), UNet's c18 not
         # l1 input: the masked objects, AvgPool2d(2)'d first for H >= 40 (blocks.py:92-96)
         self.l1_in = 3 * (self.H // 2) ** 2 if self.unet else 3 * self.H * self.H
-        self.fin = backward_plan(self.ops)
-        # an upsample consumed by exactly one conv is fused into that conv's
-        # input staging (fwd and wgrad) when the MFMA path has the shape; only
-        # the gradient buffer of the upsampled tensor remains (dgrad output ->
-        # upsample backward)
-        L = lib()
-        self.fused_up, self.fused_bufs = {}, set()
-        for i, op in enumerate(self.ops):
-            if op["op"] != "up":
-                continue
-            consumers = [j for j, o in enumerate(self.ops) if o["src"][0] == op["dst"][0]]
-            if len(consumers) != 1 or self.ops[consumers[0]]["op"] != "conv":
-                continue
-            c = self.ops[consumers[0]]
-            Hc = self.H // self.bufs[op["dst"][0]][1]
-            cm = Engine.CONV_MATH.get(getattr(model, "conv_math", "split"), 0)
-            if all(L.paig_conv2d_mfma_supported(w, c["src"][2], c["dst"][2], Hc, Hc, c["ks"], 32 | cm) for w in (0, 1)):
-                self.fused_up[consumers[0]] = op
-                self.fused_bufs.add(op["dst"][0])
         self.HW = self.H * self.H
         self.frame = 3 * self.HW
-        # ShallowUNet: c13 (1x1, 8 -> K) is fused into the mask softmax
-        # (paig_head_mask_fwd/bwd) in the encoder; the standalone U-Net call
-        # keeps it as a conv (its logits are the output)
-        last = self.ops[-1]
-        self.fuse_head = (not self.unet and last["name"] == "c13" and last["ks"] == 1 and last["src"][2] == 8
-                          and self.K in (2, 3) and self.HW % 4 == 0)
+        # the U-Net's last layer, a 1x1 head (ShallowUNet c13, 8 -> K, ReLU'd;
+        # UNet c18, 16 -> K, with the objects' AvgPool2d), is fused into the
+        # mask softmax (paig_head_mask_fwd_ex / _bwd_ex) in the encoder; the
+        # standalone U-Net call keeps it as a conv (its logits are the output).
+        # PAIG_FUSE_HEAD=0: the separate conv + softmax kernels (A/B)
+        self.head_buf = L.paig_unet_query(self.net, self.K, 2)
+        self.head_ci = L.paig_unet_query(self.net, self.K, 3)
+        self.head_name = f"c{self.nconv}"
+        self.head_flags = (1 if self.lg_relu else 0) | (2 if self.unet else 0)
+        self.fuse_head = (self.K in (2, 3) and self.HW % 4 == 0 and os.environ.get("PAIG_FUSE_HEAD", "1") != "0" and
+                          ((not self.unet and self.head_ci == 8) or (self.unet and self.head_ci == 16 and
+                                                                     self.H % 4 == 0)))
 
 
 class KernelProbe:
@@ -289,7 +184,6 @@ class Engine:
         self.probe = None
         self.last_masked_objs = None
         self._side = None   # second stream (see _fork)
-        self._xmax = {}     # per-layout xmax slots (see _unet_forward)
         # called once per backward when the early gradient bucket is final
         # (FlatParams.allreduce_early by default; bench.py splits its HIP graph here)
         self.bucket_hook = model._flat.allreduce_early
@@ -516,91 +410,89 @@ class Engine:
             "background_content": bgp.view(1, 3, H, H),
         }
         if not need_saved:
-            self._release_xmax(S)
+            self._release(S)
         return res, (S if need_saved else None)
 
-    def _release_xmax(self, S):
-        """Return a forward's xmax slots to the free list (its backward has
-        been queued, or there is none); stream order keeps the next user
-        behind every kernel that reads them."""
-        buf = S.pop("xmax_buf", None)
-        if buf is not None:
-            self._xmax.setdefault(S["xmax_key"], []).append(buf)
-        # the slots may now be another forward's: this forward's saved state
-        # admits no second backward (retain_graph=True)
+    def _release(self, S):
+        """Drop a forward's U-Net workspace (activations, gradients, max-|x|
+        slots, pool codes) once its backward has been queued, or there is
+        none; stream order keeps the allocator's next user behind every kernel
+        that reads it.  The saved state then admits no second backward
+        (retain_graph=True)."""
+        S.pop("unet_ws", None)
         S["consumed"] = True
 
+    # probe kinds of paig_unet_*_ex (include/paig_hip.h PAIG_PROBE_*) -> tag prefix
+    _PROBE_TAG = {0: "conv_fwd", 1: "conv_bwd", 2: "conv_wgrad", 3: "conv_dgrad"}
+    _PROBE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int)
+
+    def _unet_probe(self, S):
+        """The per-launch probe callback of the C U-Net interpreter: HIP
+        events around every conv launch (KernelProbe) with its algorithmic
+        FLOPs and HBM bytes (bench.py's roofline); None when not probing."""
+        if self.probe is None:
+            return None
+        lay, F = S["lay"], S["lay"].F
+        open_ = {}
+
+        def cb(ctx, ev, op, conv, kind, cin, cout, Hl, fl):
+            if ev == 1:
+                open_.pop(op).__exit__(None, None, None)
+                return
+            ks = self.p(lay.prefix + f"c{conv + 1}.weight").shape[-1]
+            flops = 2 * F * cin * cout * ks * ks * Hl * Hl
+            up = bool(fl & 32)
+            hin = Hl // 2 if up else Hl
+            if kind == 0 or kind == 2:     # forward / weight gradient: X and Y (dY) once
+                nbytes = 4 * F * (cin * hin * hin + cout * Hl * Hl)
+            elif kind == 1:                # fused layer backward: data + weight gradients
+                flops *= 2
+                if up:   # the half-resolution source (and its ReLU' mask) and dY read, its gradient written
+                    nbytes = 4 * F * (cin * hin * hin * (2 if fl & 2 else 1) + cout * Hl * Hl)
+                else:    # X and dY read, dX written (+ read when accumulating)
+                    nbytes = 4 * F * Hl * Hl * (cin + cout + cin * (2 if fl & 4 else 1))
+                    if fl & 64:   # the folded max pool: pooled gradient + window codes
+                        nbytes += F * (4 * cout + cout) * (Hl // 2) ** 2
+            else:                          # data gradient: dY read, dX written (+ mask, + accumulate)
+                nbytes = 4 * F * Hl * Hl * (cout + cin * (1 + (1 if fl & 2 else 0) + (1 if fl & 4 else 0)))
+            c = self._p(f"{self._PROBE_TAG[kind]}:c{conv + 1}", flops, nbytes)
+            c.__enter__()
+            open_[op] = c
+
+        f = self._PROBE_FN(cb)
+        S["_probe_cb"] = f   # alive as long as the saved state
+        return ctypes.cast(f, ctypes.c_void_p)
+
     def _unet_forward(self, S, lay, x_view, st, fuse_head=False):
-        """The U-Net plan over F frames addressed by x_view (frame view
-        pointer, stride, group, group stride): fills S["acts"] (LG = logits).
-        fuse_head: stop before the last op (ShallowUNet's c13), which the
-        encoder runs fused into the mask softmax (no LG buffer)."""
+        """The U-Net over F frames addressed by x_view (frame view pointer,
+        stride, group, group stride): the C interpreter of csrc/unet.hip
+        (paig_unet_fwd_ex) in one workspace that the backward reuses; S["acts"]
+        holds the logits ("LG"), or, fuse_head, the 1x1 head's input ("head":
+        c12's / c17's output, which the encoder's fused mask softmax reads)."""
         L = self.L
-        F, H = lay.F, lay.H
+        F, H, K = lay.F, lay.H, lay.K
         dev = S["dev"]
         cm = S["cm"]
-        acts = {}
-        S["head_fused"] = fuse_head
-        ops = lay.ops[:-1] if fuse_head else lay.ops
-        for name, (C, lvl) in lay.bufs.items():
-            if fuse_head and name == "LG":
-                continue
-            if name != "X0" and name not in lay.fused_bufs:
-                acts[name] = _empty(F * C * (H // lvl) * (H // lvl), dev)
-        S["acts"] = acts
-
-        def view(region):
-            buf, off, n = region
-            C, lvl = lay.bufs[buf]
-            hw = (H // lvl) ** 2
-            if buf == "X0":
-                return (x_view[0] + off * hw * 4, x_view[1], x_view[2], x_view[3]), lvl
-            t = acts[buf]
-            return (t.data_ptr() + off * hw * 4, C * hw, 0, 0), lvl
-
-        def conv_input(i, op):
-            """(view, level of the conv, extra flags): a fused upsample reads its
-            half-resolution source and forms the 2x bilinear rows while staging."""
-            up = lay.fused_up.get(i)
-            if up is None:
-                v, lvl = view(op["src"])
-                return v, lvl, 0
-            v, lvl = view(up["src"])
-            return v, lvl // 2, 32
-
-        S["view"] = view
-        S["conv_input"] = conv_input
-        # per conv: the split forward's per-block max |input| slots, which
-        # set the X scale of the same input's wgrad (every slot is written;
-        # zeroed so that a slot no forward wrote falls back to the guarded
-        # fixed scale instead of a garbage exponent).  Each forward owns its
-        # buffer until its backward has consumed it (a second forward before
-        # the first one's backward takes another); buffers return to a
-        # per-(device, layout) free list, so steady-state steps reuse one
-        # buffer (a step of the same shape rewrites exactly the same slots)
-        # and the zero fill (an extra launch) happens once.
-        key = (str(dev), len(lay.ops), lay.F, lay.H)
-        free = self._xmax.setdefault(key, [])
-        xmax = free.pop() if free else torch.zeros(len(lay.ops) * XMAX_SLOTS, device=dev)
-        S["xmax"] = lambda i: ptr(xmax) + i * XMAX_SLOTS * 4
-        S["xmax_buf"] = xmax
-        S["xmax_key"] = key
-        # split path: every conv's forward and dgrad weight images, pre-split
-        # in one launch per step (paig_conv_wprep) and copied by the kernels
+        flags = ((1 if fuse_head else 0) | (0 if S.get("need_saved", True) else 4) |
+                 (2 if os.environ.get("PAIG_FUSED_BWD", "1") == "0" else 0))
+        Ws = [self.p(lay.prefix + f"c{c + 1}.weight") for c in range(lay.nconv)]
+        Bs = [self.p(lay.prefix + f"c{c + 1}.bias") for c in range(lay.nconv)]
+        # split path: every conv's forward and dgrad weight images (and the
+        # localiser's W2^T for the fused dense tail) in one launch per step
+        # (paig_conv_wprep); the interpreter takes them per conv
         wp = {}
+        wpf = wpd = None
         if cm == self.CONV_MATH["split"]:
+            flags |= 8
             jobs = []
-            for i, op in enumerate(ops):
-                if op["op"] != "conv":
-                    continue
-                W_ = self.p(lay.prefix + op["name"] + ".weight")
-                cin, cout, ks = op["src"][2], op["dst"][2], op["ks"]
-                jobs.append((i, 0, W_, cin, cout, ks))
-                if op["src"][0] != "X0":   # the dgrad kernel's images (Q10: none for the input)
-                    jobs.append((i, 1, W_, cout, cin, ks))
+            for c, W_ in enumerate(Ws):
+                cout, cin, ks = W_.shape[0], W_.shape[1], W_.shape[-1]
+                jobs.append((c, 0, W_, cin, cout, ks))
+                if c > 0:   # the dgrad kernel's images (Q10: none for the input layer)
+                    jobs.append((c, 1, W_, cout, cin, ks))
             sizes = [int(L.paig_conv_wprep_size(j[3], j[4], j[5])) for j in jobs]
             if self.dense_tail():
-                # the localiser's W2^T for the fused dense tail, in the same launch
                 jobs.append((-1, 2, self.p("encoder.l2.weight"), 200, 200, 1))
                 sizes.append(2 * 200 * 200)
             buf = torch.empty(sum(-(-n // 8) * 8 for n in sizes), dtype=torch.int16, device=dev)
@@ -615,63 +507,31 @@ class Engine:
                               (ctypes.c_int * n)(*[j[5] for j in jobs]), (ctypes.c_int * n)(*[j[1] for j in jobs]),
                               (ctypes.c_void_p * n)(*outs), st)
             S["wprep_buf"] = buf
+            wpf = _parr([wp[(c, 0)] for c in range(lay.nconv)])
+            wpd = _parr([wp.get((c, 1), 0) for c in range(lay.nconv)])
         S["wprep"] = wp
-        pooled = set()   # pools written by their producing conv's epilogue
-        for i, op in enumerate(ops):
-            if op["op"] == "up" and op["dst"][0] in lay.fused_bufs:
-                continue   # formed inside the consuming conv's staging
-            if i in pooled:
-                continue
-            dv, dlvl = view(op["dst"])
-            if op["op"] == "conv":
-                sv, clvl, xfl = conv_input(i, op)
-                Hl = H // clvl
-                # a 2x2 max pool of exactly this output, next in the plan, is
-                # fused into the conv's epilogue where the split kernel has it
-                pool_v = (None, 0)
-                nxt = ops[i + 1] if i + 1 < len(ops) else None
-                pcode = (None, 0)
-                pool_next = nxt is not None and nxt["op"] == "pool" and nxt["src"] == op["dst"] and not xfl and cm
-                if pool_next and S.get("need_saved", True) and self._fused_bwd(op["src"][2], op["dst"][2], Hl,
-                                                                                 op["ks"], cm | 64):
-                    # the pool windows' codes (ReLU' bits + argmax): the
-                    # backward folds the pool into this layer's dY staging.
-                    # Written by this conv's fused pool, or (widths whose rows
-                    # are not whole M-tiles: 3bp) by the standalone pool
-                    cfs = -(-op["dst"][2] // 8) * 8 * (Hl // 2) ** 2
-                    cb = torch.empty(F * cfs, dtype=torch.uint8, device=dev)
-                    S.setdefault("pcode", {})[i + 1] = (cb, cfs)
-                    pcode = (cb.data_ptr(), cfs)
-                if pool_next and L.paig_conv2d_mfma_supported(0, op["src"][2], op["dst"][2], Hl, Hl, op["ks"],
-                                                              cm | 64):
-                    pv, _ = view(nxt["dst"])
-                    pool_v = (pv[0], pv[1])
-                    pooled.add(i + 1)
-                else:
-                    pcode = (None, 0)
-                W_ = self.p(lay.prefix + op["name"] + ".weight")
-                b_ = self.p(lay.prefix + op["name"] + ".bias")
-                fl = 2 * F * op["src"][2] * op["dst"][2] * op["ks"] ** 2 * Hl * Hl
-                nbytes = 4 * F * (op["src"][2] * (Hl // (2 if xfl else 1)) ** 2 + op["dst"][2] * Hl * Hl)
-                with self._p("conv_fwd:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_fwd_pwc(sv[0], sv[1], sv[2], sv[3], dv[0], dv[1], None, 0, ptr(W_), ptr(b_), F,
-                                          op["src"][2], op["dst"][2], Hl, Hl, op["ks"],
-                                          (1 if op["relu"] else 0) | xfl | cm | (64 if pool_v[0] else 0),
-                                          S["xmax"](i), XMAX_SLOTS, pool_v[0], pool_v[1], pcode[0], pcode[1],
-                                          wp.get((i, 0)), st)
-            elif op["op"] == "pool":
-                sv, slvl = view(op["src"])
-                Hl = H // slvl
-                if i in S.get("pcode", {}):
-                    cb, cfs = S["pcode"][i]
-                    L.paig_maxpool2_fwd_codes(sv[0], sv[1], dv[0], dv[1], cb.data_ptr(), cfs, F, op["src"][2], Hl, Hl,
-                                              st)
-                else:
-                    L.paig_maxpool2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hl, Hl, st)
-            else:
-                sv, slvl = view(op["src"])
-                Hs, Ho = H // slvl, H // dlvl
-                L.paig_upsample2_fwd(sv[0], sv[1], dv[0], dv[1], F, op["src"][2], Hs, Hs, Ho, Ho, st)
+        nb = int(L.paig_unet_workspace_ex(lay.net, F, H, K, cm, flags))
+        if nb <= 0:
+            raise PaigError(f"paig_unet_workspace_ex: no U-Net for net={lay.net} F={F} H={H} K={K} math={cm}")
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        logits = None if fuse_head else _empty(F * K * lay.HW, dev)
+        probe = self._unet_probe(S)
+        L.paig_unet_fwd_ex(lay.net, F, H, K, cm, flags, *x_view, _parr([ptr(t) for t in Ws]),
+                           _parr([ptr(t) for t in Bs]), ptr(logits), wpf, wpd, ptr(ws), nb, probe, None, st)
+        acts = {}
+        if fuse_head:
+            off = int(L.paig_unet_buffer(lay.net, F, H, K, cm, flags, 0, lay.head_buf))
+            acts["head"] = ws[off:off + F * lay.head_ci * lay.HW * 4].view(torch.float32)
+        else:
+            acts["LG"] = logits
+        S.update(acts=acts, head_fused=fuse_head, unet_ws=ws, unet_flags=flags, unet_wp=(wpf, wpd))
+
+    def _unet_grad(self, S, buf, n):
+        """The U-Net workspace's gradient buffer `buf` (n floats)."""
+        lay = S["lay"]
+        off = int(self.L.paig_unet_buffer(lay.net, lay.F, lay.H, lay.K, S["cm"], S["unet_flags"], 1, buf))
+        assert off >= 0, f"no gradient buffer {buf} in the U-Net workspace"
+        return S["unet_ws"][off:off + n * 4].view(torch.float32)
 
     def _encoder_forward(self, S, lay, x_view, ws, st):
         """ConvolutionalEncoder.forward (nn/network/blocks.py:77-103) over the
@@ -686,9 +546,11 @@ class Engine:
         masks = _empty(F * (K + 1) * HW, dev)
         objs = _empty(K * F * 3 * HW, dev)
         pobjs = _empty(K * F * lay.l1_in, dev) if lay.unet else None
-        if lay.fuse_head:   # c13 + cat(ones) + softmax + mask x image, one launch
-            L.paig_head_mask_fwd(ptr(acts["A12"]), ptr(self.p(lay.prefix + "c13.weight")),
-                                 ptr(self.p(lay.prefix + "c13.bias")), *x_view, ptr(masks), ptr(objs), F, K, H, H, st)
+        if lay.fuse_head:   # the head conv + cat(ones) + softmax + mask x image (+ AvgPool2d), one launch
+            hn = lay.prefix + lay.head_name
+            L.paig_head_mask_fwd_ex(ptr(acts["head"]), ptr(self.p(hn + ".weight")), ptr(self.p(hn + ".bias")),
+                                    *x_view, ptr(masks), ptr(objs), ptr(pobjs), F, K, lay.head_ci, H, H,
+                                    lay.head_flags, st)
         else:
             L.paig_mask_softmax_fwd(ptr(acts["LG"]), *x_view, ptr(masks), ptr(objs), ptr(pobjs), F, K, 3, H, H, st)
         l1_x = pobjs if lay.unet else objs
@@ -954,218 +816,59 @@ class Engine:
         # ---- mask softmax backward (incl. ReLU' of ShallowUNet's c13, Q13, and
         # the AvgPool2d backward of the UNet path)
         acts = S["acts"]
-        dacts = {}
         if S.get("head_fused"):
-            # fused c13 + softmax backward: c12's dY (ReLU' applied) and c13's
-            # weight/bias partials (one slab row per block)
-            c = lay.ops[-1]["src"][2]
-            dX12 = _empty(F * c * HW, dev)
+            # fused head + softmax backward: the head input's dY (its
+            # producer's ReLU' applied), written straight into the U-Net
+            # workspace's gradient buffer, and the head's weight/bias partials
+            # (one slab row per block)
+            hn, c = lay.prefix + lay.head_name, lay.head_ci
+            dXl = self._unet_grad(S, lay.head_buf, F * c * HW)
             nb = L.paig_head_mask_blocks(F, H, H)
             nw = K * c + K
             hs = _empty(nb * nw, dev)
-            L.paig_head_mask_bwd(ptr(acts["A12"]), ptr(self.p(lay.prefix + "c13.weight")),
-                                 ptr(self.p(lay.prefix + "c13.bias")), *x_view, ptr(S["masks"]), ptr(dobjs), ptr(dX12),
-                                 ptr(hs), F, K, H, H, st)
-            g13 = self.g(lay.prefix + "c13.weight")
-            assert self.g(lay.prefix + "c13.bias").data_ptr() == g13.data_ptr() + K * c * 4, "c13 grads not contiguous"
-            S["extra_slabs"].append((hs, nb, nw, g13))
-            dacts["A12"] = dX12
+            L.paig_head_mask_bwd_ex(ptr(acts["head"]), ptr(self.p(hn + ".weight")), ptr(self.p(hn + ".bias")),
+                                    *x_view, ptr(S["masks"]), ptr(dobjs), ptr(dXl), ptr(hs), F, K, c, H, H,
+                                    lay.head_flags, st)
+            gh = self.g(hn + ".weight")
+            assert self.g(hn + ".bias").data_ptr() == gh.data_ptr() + K * c * 4, "head grads not contiguous"
+            S["extra_slabs"].append((hs, nb, nw, gh))
+            self._unet_backward(S, None, st)
         else:
             dLG = _empty(F * K * HW, dev)
             L.paig_mask_softmax_bwd(ptr(acts["LG"]), x_view[0], x_view[1], x_view[2], x_view[3], ptr(S["masks"]),
                                     ptr(dobjs), ptr(dLG), F, K, 3, H, H,
                                     (1 if lay.lg_relu else 0) | (2 if lay.unet else 0), st)
-            dacts["LG"] = dLG
-        self._unet_backward(S, dacts, st)
-
-    def _fused_bwd(self, cin, cout, Hl, ks, cm):
-        """The layer backward runs as one fused launch (paig_conv2d_bwd)
-        where the library has the shape; PAIG_FUSED_BWD=0 keeps the separate
-        data- and weight-gradient kernels (A/B)."""
-        if os.environ.get("PAIG_FUSED_BWD", "1") == "0" or not cm:
-            return False
-        return bool(self.L.paig_conv2d_bwd_supported(cin, cout, Hl, Hl, ks, cm))
+            self._unet_backward(S, dLG, st)
 
     @staticmethod
     def _check_fresh(S):
         if S.get("consumed"):
             raise PaigError("a second backward through one forward (retain_graph=True) is not supported: the "
-                            "forward's saved state (activation maxima slots) was released by the first backward")
+                            "forward's saved state (its U-Net workspace) was released by the first backward")
 
-    def _unet_backward(self, S, dacts, st):
+    def _unet_backward(self, S, dlogits, st):
+        """The U-Net backward (paig_unet_bwd_ex, the same C interpreter as the
+        forward) from d logits, or (fused head) from the head input's
+        gradient already in the workspace; every conv's weight and bias
+        gradient, with the step's other partial-gradient slabs (extra_slabs:
+        head, l3, velocity MLP) in one batched deterministic reduction."""
         self._check_fresh(S)
         lay = S["lay"]
         L = self.L
-        dev = S["x"].device
-        acts = S["acts"]
-        view = S["view"]
-        F, H = lay.F, lay.H
-        fused = S.get("head_fused", False)
-        # the fused head wrote c12's dY (dacts["A12"]); otherwise dLG is the start
-        written = {"A12": [(0, lay.ops[-1]["src"][2])]} if fused else {"LG": [(0, lay.K)]}
-        nops = len(lay.ops) - 1 if fused else len(lay.ops)
-        cm = S["cm"]
-
-        def dview(region):
-            buf, off, n = region
-            C, lvl = lay.bufs[buf]
-            hw = (H // lvl) ** 2
-            if buf not in dacts:
-                dacts[buf] = _empty(F * C * hw, dev)
-            t = dacts[buf]
-            return (t.data_ptr() + off * hw * 4, C * hw), lvl
-
-        def state(region):
-            buf, off, n = region
-            spans = written.get(buf, [])
-            cov = sum(max(0, min(off + n, a + c) - max(off, a)) for a, c in spans)
-            if cov == 0:
-                return "write"
-            if cov == n:
-                return "accum"
-            raise RuntimeError(f"partially written gradient region {region}")
-
-        def mark(region):
-            written.setdefault(region[0], []).append((region[1], region[2]))
-
-        slabs = []
-        folded_ups = set()   # upsample ops whose backward a fused conv backward did
-        for i in range(nops - 1, -1, -1):
-            if i in folded_ups:
-                continue
-            op = lay.ops[i]
-            if op["op"] == "pool" and i in S.get("pcode", {}):
-                continue   # folded into the pooled conv's backward (its dY staging), below
-            fin = lay.fin[i]
-            relu_fin = [r for r, relu in fin if relu]
-            src, dst = op["src"], op["dst"]
-            dyv, dlvl = dview(dst)
-            if op["op"] == "conv":
-                sv, slvl, xfl = S["conv_input"](i, op)
-                Hl = H // slvl
-                cin, cout, ks = src[2], dst[2], op["ks"]
-                # weight + bias gradient: per-block partials, then one reduction
-                nblk_max = 1024
-                slab = _empty(nblk_max * (cout * cin * ks * ks + cout), dev)
-                nb = ctypes.c_int(0)
-                fl = 2 * F * cin * cout * ks * ks * Hl * Hl
-                gw = self.g(lay.prefix + op["name"] + ".weight")
-                n_w = cout * cin * ks * ks
-                if xfl and self._fused_bwd(cin, cout, Hl, ks, cm | 32):
-                    # fused-upsample input (c7 / c10): the layer backward AND the
-                    # upsample's backward in one launch -- the data gradient of
-                    # the upsampled tensor never reaches memory; the launch
-                    # writes the half-resolution source's gradient
-                    up = lay.fused_up[i]
-                    ui = lay.ops.index(up)
-                    usrc = up["src"]
-                    dxv, _ = dview(usrc)
-                    mode = state(usrc)
-                    assert mode == "write", f"{op['name']}: upsample source gradient already written"
-                    flags = cm | 32
-                    aux = (None, 0)
-                    if any(relu for r, relu in lay.fin[ui] if r == usrc):
-                        a = view(usrc)[0]
-                        aux = (a[0], a[1])
-                        flags |= 2
-                    nbytes = 4 * F * (cin * (Hl // 2) ** 2 * (2 if flags & 2 else 1) + cout * Hl * Hl)
-                    with self._p("conv_bwd:" + op["name"], 2 * fl, nbytes):
-                        L.paig_conv2d_bwd(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], dxv[0], dxv[1], aux[0], aux[1],
-                                          ptr(self.p(lay.prefix + op["name"] + ".weight")), ptr(slab), nblk_max,
-                                          ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, flags, S["xmax"](i), XMAX_SLOTS,
-                                          None, 0, None, 0, S["wprep"].get((i, 1)), st)
-                    slabs.append((slab, nb.value, n_w + cout, gw))
-                    mark(usrc)
-                    folded_ups.add(ui)
-                    continue
-                if src[0] != "X0" and not xfl and self._fused_bwd(cin, cout, Hl, ks, cm):
-                    # the layer's data and weight gradients in ONE launch from
-                    # one staging of dY and X (csrc/conv_bwd.hip)
-                    dxv, _ = dview(src)
-                    mode = state(src)
-                    flags = cm | (4 if mode == "accum" else 0)
-                    aux = (None, 0)
-                    if relu_fin:
-                        assert len(fin) == 1 and fin[0][0] == src, f"{op['name']}: mixed ReLU finalization"
-                        a = view(src)[0]
-                        aux = (a[0], a[1])
-                        flags |= 2
-                    # algorithmic bytes: X and dY read, dX written (+ read when accumulating)
-                    nbytes = 4 * F * Hl * Hl * (cin + cout + cin * (2 if mode == "accum" else 1))
-                    # the max pool of this output (next op), folded: its
-                    # gradient and window codes join the dY staging
-                    fold = (None, 0, None, 0)
-                    pj = i + 1
-                    if pj in S.get("pcode", {}):
-                        # the kernel reads this output's skip-path gradient
-                        # (dY): its concat partner must have written it
-                        assert state(dst) == "accum", f"{op['name']}: pool fold before the skip gradient (plan error)"
-                        pdv, _ = dview(lay.ops[pj]["dst"])
-                        cb, cfs = S["pcode"][pj]
-                        fold = (pdv[0], pdv[1], cb.data_ptr(), cfs)
-                        flags |= 64
-                        nbytes += F * (4 * cout + cout) * (Hl // 2) ** 2   # pooled gradient + codes
-                    with self._p("conv_bwd:" + op["name"], 2 * fl, nbytes):
-                        L.paig_conv2d_bwd(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], dxv[0], dxv[1], aux[0], aux[1],
-                                          ptr(self.p(lay.prefix + op["name"] + ".weight")), ptr(slab), nblk_max,
-                                          ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, cm | (flags & 70),
-                                          S["xmax"](i), XMAX_SLOTS, *fold, S["wprep"].get((i, 1)), st)
-                    slabs.append((slab, nb.value, n_w + cout, gw))
-                    mark(src)
-                    continue
-                nbytes = 4 * F * (cin * (Hl // (2 if xfl else 1)) ** 2 + cout * Hl * Hl)
-                with self._p("conv_wgrad:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_wgrad_ex(sv[0], sv[1], sv[2], sv[3], dyv[0], dyv[1], ptr(slab), nblk_max,
-                                           ctypes.byref(nb), F, cin, cout, Hl, Hl, ks, xfl | cm, S["xmax"](i),
-                                           XMAX_SLOTS, st)
-                gb = self.g(lay.prefix + op["name"] + ".bias")
-                assert gb.data_ptr() == gw.data_ptr() + n_w * 4, "flat grads: weight and bias must be adjacent"
-                slabs.append((slab, nb.value, n_w + cout, gw))
-                if src[0] == "X0":
-                    continue
-                dxv, _ = dview(src)
-                mode = state(src)
-                flags = 8 | (4 if mode == "accum" else 0)
-                aux = (0, 0)
-                if relu_fin:
-                    assert len(fin) == 1 and fin[0][0] == src, f"{op['name']}: mixed ReLU finalization"
-                    a = view(src)[0]
-                    aux = (a[0], a[1])
-                    flags |= 2
-                W_ = self.p(lay.prefix + op["name"] + ".weight")
-                nbytes = 4 * F * Hl * Hl * (cout + cin * (1 + (1 if flags & 2 else 0) + (1 if flags & 4 else 0)))
-                with self._p("conv_dgrad:" + op["name"], fl, nbytes):
-                    L.paig_conv2d_fwd_pw(dyv[0], dyv[1], 0, 0, dxv[0], dxv[1], aux[0] or None, aux[1], ptr(W_), None,
-                                         F, cout, cin, Hl, Hl, ks, flags | cm, None, 0, None, 0,
-                                         S["wprep"].get((i, 1)), st)
-                mark(src)
-            elif op["op"] == "pool":
-                sv, slvl = view(src)
-                Hl = H // slvl
-                dxv, _ = dview(src)
-                # the pool kernel accumulates into the concat partner's gradient
-                assert state(src) == "accum", "maxpool backward reached before its concat partner (plan error)"
-                relu = any(relu for r, relu in fin if r == src)
-                assert relu, "pool sources are ReLU'd activations in both U-Nets"
-                L.paig_maxpool2_bwd_relu(sv[0], sv[1], dyv[0], dyv[1], dxv[0], dxv[1], F, src[2], Hl, Hl, st)
-                mark(src)
-            else:
-                sv, slvl = view(src)
-                Hs, Ho = H // slvl, H // dlvl
-                dxv, _ = dview(src)
-                assert state(src) == "write"
-                relu = any(relu for r, relu in fin if r == src)
-                L.paig_upsample2_bwd(dyv[0], dyv[1], sv[0], sv[1], dxv[0], dxv[1], F, src[2], Hs, Hs, Ho, Ho,
-                                     int(relu), st)
-                mark(src)
-        # all conv weight/bias gradients (+ the velocity MLP's): one batched
-        # deterministic reduction
-        slabs = slabs + S.get("extra_slabs", [])
-        n = len(slabs)
-        srcs = (ctypes.c_void_p * n)(*[ptr(s[0]) for s in slabs])
-        nbs = (ctypes.c_int * n)(*[s[1] for s in slabs])
-        lens = (ctypes.c_int * n)(*[s[2] for s in slabs])
-        dsts = (ctypes.c_void_p * n)(*[ptr(s[3]) for s in slabs])
-        L.paig_slab_reduce_multi(n, srcs, nbs, lens, dsts, 0, st)
-        S["_slabs"] = slabs
-        self._release_xmax(S)
+        Ws = [self.p(lay.prefix + f"c{c + 1}.weight") for c in range(lay.nconv)]
+        dwb = []
+        for c in range(lay.nconv):
+            gw = self.g(lay.prefix + f"c{c + 1}.weight")
+            assert self.g(lay.prefix + f"c{c + 1}.bias").data_ptr() == gw.data_ptr() + gw.numel() * 4, \
+                "flat grads: weight and bias must be adjacent"
+            dwb.append(ptr(gw))
+        extra = S.get("extra_slabs", [])
+        n = len(extra)
+        ws = S["unet_ws"]
+        _, wpd = S["unet_wp"]
+        L.paig_unet_bwd_ex(lay.net, lay.F, lay.H, lay.K, S["cm"], S["unet_flags"], *S["x_view"],
+                           _parr([ptr(t) for t in Ws]), ptr(S["acts"].get("LG")), ptr(dlogits), _parr(dwb), n,
+                           _parr([ptr(e[0]) for e in extra]), _iarr([e[1] for e in extra]),
+                           _iarr([e[2] for e in extra]), _parr([ptr(e[3]) for e in extra]), wpd, ptr(ws), ws.numel(),
+                           self._unet_probe(S), None, st)
+        self._release(S)

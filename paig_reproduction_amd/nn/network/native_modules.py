@@ -356,11 +356,10 @@ class _Encoder(torch.autograd.Function):
             with model._flat.partial_backward(("encoder.",)):
                 eng._encoder_backward(S, denc.float().contiguous(), st, hook=False)
         else:
-            dLG = grads[0].float().contiguous().clone()
-            if lay.lg_relu:   # ShallowUNet's c13 output is ReLU'd (Q13): its derivative first
-                lib().paig_relu_mask(ptr(S["acts"]["LG"]), ptr(dLG), dLG.numel(), st)
+            # (paig_unet_bwd_ex applies ShallowUNet c13's ReLU' itself, Q13)
+            dLG = grads[0].float().contiguous()
             with model._flat.partial_backward((lay.prefix,)):
-                eng._unet_backward(S, {"LG": dLG}, st)
+                eng._unet_backward(S, dLG, st)
         return None, None, None, None
 
 

@@ -24,7 +24,7 @@ def header_protos():
         for a in args:
             t = re.sub(r"\b\w+$", "", a).strip()  # drop the parameter name
             t = t.replace("const ", "").strip()
-            types.append("ptr" if "*" in t else t)
+            types.append("ptr" if "*" in t or t.endswith("_fn") else t)   # (callback typedefs: pointers)
         out[m.group(2)] = types
     return out
 
@@ -56,6 +56,17 @@ def test_library_loads_and_exports_every_symbol():
     fmin = max(1, int(os.environ.get("PAIG_DEC_FPB_MIN", "3")))
     assert L.paig_decoder_bwd_blocks(4600, 46, 6, 2, 16, 32) == -(-600 // max(fmin, 3))
     assert L.paig_vfn_bwd_blocks(3072) == 384
+    # the U-Net plan facts the engine reads (csrc/unet.hip is the one plan):
+    # convs, buffers, the 1x1 head's input buffer and width
+    assert [L.paig_unet_query(0, 2, w) for w in range(5)] == [13, 16, 14, 8, 15]   # ShallowUNet: c13 on A12
+    assert [L.paig_unet_query(1, 2, w) for w in range(5)] == [18, 22, 20, 16, 21]  # UNet: c18 on A17
+    # workspace layouts: inference holds no gradients; a head-input gradient exists for training
+    for net, H in ((0, 32), (1, 64)):
+        full = L.paig_unet_workspace_ex(net, 10, H, 2, 128, 1)
+        assert 0 < L.paig_unet_workspace_ex(net, 10, H, 2, 128, 1 | 4) < full
+        hb = L.paig_unet_query(net, 2, 2)
+        assert 0 <= L.paig_unet_buffer(net, 10, H, 2, 128, 1, 1, hb) < full
+        assert L.paig_unet_buffer(net, 10, H, 2, 128, 1 | 4, 1, hb) == -1
 
 
 def test_product_path_refuses_cpu_tensors():

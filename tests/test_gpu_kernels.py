@@ -559,6 +559,56 @@ def test_head_mask_fused(K, hw, F_):
     assert rel_err(part[K * 8:], br.grad) <= 1e-5
 
 
+@pytest.mark.parametrize("K,hw,F_", [(2, 64, 9), (3, 64, 3), (2, 40, 5)])
+def test_head_mask_fused_unet(K, hw, F_):
+    """paig_head_mask_fwd_ex/_bwd_ex with the UNet head (c18: 1x1 conv 16 -> K,
+    not ReLU'd; cat(ones), softmax, mask x image and the masked objects'
+    AvgPool2d(2); blocks.py:84-96,170,236) against the same ops in fp64 torch:
+    masks, masked objects, pooled objects, c17's input gradient (c17's ReLU'
+    applied) from the pooled objects' gradient, c18's weight / bias gradient."""
+    torch.manual_seed(K * 1000 + hw)
+    HW = hw * hw
+    x17 = torch.relu(torch.randn(F_, 16, hw, hw))
+    x17[:, :, :2] = 0.0   # dead pixels: c17's ReLU' must zero them
+    img = torch.rand(F_, 3, hw, hw)
+    w = torch.randn(K, 16) * 0.4
+    b = torch.randn(K) * 0.2
+    dpobjs = torch.randn(K, F_, 3, hw // 2, hw // 2)
+    xr = x17.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    lg = F.conv2d(xr, wr.view(K, 16, 1, 1), br)   # c18: no ReLU (blocks.py:236)
+    masks_ref = torch.softmax(torch.cat([lg, torch.ones(F_, 1, hw, hw, dtype=torch.float64)], 1), 1)
+    objs_ref = torch.stack([masks_ref[:, k:k + 1] * img.double() for k in range(K)], 0)
+    pobjs_ref = F.avg_pool2d(objs_ref.reshape(K * F_, 3, hw, hw), 2).view(K, F_, 3, hw // 2, hw // 2)
+    (pobjs_ref * dpobjs.double()).sum().backward()
+    dx_ref = xr.grad * (x17 > 0)
+    g = {n: t.to(DEV).contiguous() for n, t in dict(x17=x17, img=img, w=w, b=b, dp=dpobjs).items()}
+    masks = torch.empty(F_, K + 1, hw, hw, device=DEV)
+    objs = torch.empty(K, F_, 3, hw, hw, device=DEV)
+    pobjs = torch.empty(K, F_, 3, hw // 2, hw // 2, device=DEV)
+    L().paig_head_mask_fwd_ex(p(g["x17"]), p(g["w"]), p(g["b"]), p(g["img"]), 3 * HW, 0, 0, p(masks), p(objs),
+                              p(pobjs), F_, K, 16, hw, hw, 2, st())
+    nb = L().paig_head_mask_blocks(F_, hw, hw)
+    slab = torch.empty(nb, K * 16 + K, device=DEV)
+    dx = torch.full((F_, 16, hw, hw), float("nan"), device=DEV)
+    L().paig_head_mask_bwd_ex(p(g["x17"]), p(g["w"]), p(g["b"]), p(g["img"]), 3 * HW, 0, 0, p(masks), p(g["dp"]),
+                              p(dx), p(slab), F_, K, 16, hw, hw, 2, st())
+    torch.cuda.synchronize()
+    part = slab.double().sum(0).cpu()
+    assert rel_err(masks, masks_ref.detach()) <= 1e-6
+    assert rel_err(objs, objs_ref.detach()) <= 1e-6
+    assert rel_err(pobjs, pobjs_ref.detach()) <= 1e-6
+    assert torch.isfinite(dx).all()
+    assert rel_err(dx, dx_ref) <= 1e-5
+    assert rel_err(part[:K * 16].view(K, 16), wr.grad) <= 1e-5
+    assert rel_err(part[K * 16:], br.grad) <= 1e-5
+    # the (CI, flags) pairs are the two heads only
+    with pytest.raises(Exception):
+        L().paig_head_mask_fwd_ex(p(g["x17"]), p(g["w"]), p(g["b"]), p(g["img"]), 3 * HW, 0, 0, p(masks), p(objs),
+                                  p(pobjs), F_, K, 16, hw, hw, 1, st())
+
+
 @pytest.mark.parametrize("cin,cout,hw,ks,up", [(8, 8, 32, 3, 0), (32, 32, 8, 3, 0), (24, 8, 32, 3, 0), (8, 24, 32, 3, 0),
                                                (64, 128, 16, 3, 0), (32, 16, 16, 3, 1), (8, 2, 32, 1, 0)])
 def test_conv_wprep_bit_identical(cin, cout, hw, ks, up):
