@@ -40,6 +40,9 @@
 #ifndef PAIG_BWD_MINW
 #define PAIG_BWD_MINW 0   // A/B builds: force the blocks per CU the kernels are compiled for
 #endif
+#ifndef PAIG_BWD_UPS2
+#define PAIG_BWD_UPS2 1   // A/B builds: 0 = one-row upsample staging items
+#endif
 #ifndef PAIG_BWD_AUXP
 #define PAIG_BWD_AUXP 1   // A/B builds: 0 = the epilogue loads its ReLU' mask when it needs it
 #endif
@@ -614,7 +617,43 @@ conv_bwd_split_k(FView x, FView dy, FViewW dx, FView aux, const float* __restric
       PAIG_BSTAMP(9);
       __syncthreads();
       PAIG_BSTAMP(10);
-      if constexpr (W % 4 == 0) {
+      if constexpr (W % 4 == 0 && ROWS % 2 == 0 && PAIG_BWD_UPS2 && PM == 0 && H != 36) {   // (spills there)
+        // items of 4 pixels x 4 channels x a ROW PAIR (image rows 2rp, 2rp+1:
+        // output rows y0 - 1 + 2rp (odd) and y0 + 2rp, which interpolate the
+        // same two source rows): half the items of the one-row form, each
+        // sharing its row reads and horizontal interpolations (c10: 160 items,
+        // one pass of the block instead of 320 in one and a quarter passes)
+        constexpr int W4 = W / 4, RP2 = ROWS / 2;
+#pragma unroll 1
+        for (int i = tid; i < CQ * RP2 * W4; i += 256) {
+          const int q = i % W4, rp = (i / W4) % RP2, cq = i / (W4 * RP2);
+          const int gy = y0 + 2 * rp - PADL;
+          const bool ok0 = f0 < F && gy >= 0 && gy < H, ok1 = f0 < F && gy + 1 >= 0 && gy + 1 < H;
+          f32x4 o0[4], o1[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (cq * 4 + c < CIN) {
+              UP::row4x2(Sl, 0, cq * 4 + c, gy, y0, q, ok0, ok1, o0[c], o1[c]);
+            } else {
+              o0[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+              o1[c] = o0[c];
+            }
+          }
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const int ia = (cq * ROWS + 2 * rp + h2) * W2 + 2 * q;
+            const f32x4* o = h2 ? o1 : o0;
+            float2 v[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][0], o[c][1]);
+            put_x(ia, v);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][2], o[c][3]);
+            put_x(ia + 1, v);
+          }
+        }
+        PAIG_BSTAMP(11);
+      } else if constexpr (W % 4 == 0) {
         constexpr int W4 = W / 4;
 #pragma unroll 1
         for (int i = tid; i < NIX / 2; i += 256) {

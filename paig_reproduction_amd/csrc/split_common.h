@@ -164,6 +164,39 @@ struct UpStage {
     o[3] = wa * (0.75f * m0.y + 0.25f * a3) + wb * (0.75f * m1.y + 0.25f * b3);
     return o;
   }
+  // output rows gy (odd) and gy + 1 at once (pixels 4q..4q+3): 2x bilinear
+  // output rows 2k+1 and 2k+2 interpolate the same source rows k, k+1, so the
+  // row reads and the horizontal interpolations are shared; each row's
+  // vertical weights are its own (row4's operation order).  ok0 / ok1: the
+  // rows lie in the frame (else 0; the taps then come from the valid row)
+  static __device__ __forceinline__ void row4x2(const float* Sl, int fi, int c, int gy, int y0, int q, bool ok0,
+                                                bool ok1, f32x4& o0, f32x4& o1) {
+    int ya, yb, ya1, yb1;
+    float wa0, wb0, wa1, wb1;
+    up2_taps(gy, HS, ya, yb, wa0, wb0);
+    up2_taps(gy + 1, HS, ya1, yb1, wa1, wb1);
+    if (!ok0) {
+      ya = ya1;
+      yb = yb1;
+    }
+    const float* p = Sl + (fi * CIN + c) * SRN * WS;
+    const float* r0 = p + (ya - (y0 / 2 - 1)) * WS;
+    const float* r1 = p + (yb - (y0 / 2 - 1)) * WS;
+    const int c0 = q > 0 ? 2 * q - 1 : 0, c3 = 2 * q + 2 < WS ? 2 * q + 2 : WS - 1;
+    const float2 m0 = *reinterpret_cast<const float2*>(r0 + 2 * q);
+    const float2 m1 = *reinterpret_cast<const float2*>(r1 + 2 * q);
+    const float a0 = r0[c0], a3 = r0[c3], b0 = r1[c0], b3 = r1[c3];
+    const float w0 = q > 0 ? 0.25f : 0.f, w1 = q > 0 ? 0.75f : 1.f;
+    const float h0[4] = {w0 * a0 + w1 * m0.x, 0.75f * m0.x + 0.25f * m0.y, 0.25f * m0.x + 0.75f * m0.y,
+                         0.75f * m0.y + 0.25f * a3};
+    const float h1[4] = {w0 * b0 + w1 * m1.x, 0.75f * m1.x + 0.25f * m1.y, 0.25f * m1.x + 0.75f * m1.y,
+                         0.75f * m1.y + 0.25f * b3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o0[j] = ok0 ? wa0 * h0[j] + wb0 * h1[j] : 0.f;
+      o1[j] = ok1 ? wa1 * h0[j] + wb1 * h1[j] : 0.f;
+    }
+  }
 };
 
 // LDS available to one block (gfx950: 160 KB per CU)

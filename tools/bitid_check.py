@@ -65,6 +65,13 @@ def main():
             d = (ra[k] - rb[k]).abs().max().item()
             bad += not same
             print(f"({cin},{cout},{H}) {k:7s} {'bit-identical' if same else f'DIFFERS max |d| {d:.3g}'}", flush=True)
+            if not same and k in ("wgrad", "bwd_dw") and d > 1e-3:
+                # where: max |d| per tap (ky, kx) and per input channel
+                n = cout * cin * 9
+                dd = (ra[k] - rb[k])[:n].abs().view(cout, cin, 3, 3)
+                print("    per tap:", [[round(dd[:, :, ky, kx].max().item(), 3) for kx in range(3)] for ky in range(3)])
+                print("    per cin:", [round(v, 2) for v in dd.amax((0, 2, 3)).tolist()])
+                print("    per cout:", [round(v, 2) for v in dd.amax((1, 2, 3)).tolist()])
     print("BITID_OK" if bad == 0 else f"BITID_FAIL {bad}")
 
 
