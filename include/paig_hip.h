@@ -78,7 +78,14 @@ int paig_conv2d_fwd_ex(const float* in, long long in_fs, int in_grp, long long i
  * flags & 64: the output's 2x2 max pool (nn.MaxPool2d((2,2)), blocks.py:250,
  * 254) also written to pool_out [F][Cout][H/2][W/2] (frame stride pool_fs),
  * bit-identical to paig_maxpool2_fwd; forward split shapes for which
- * paig_conv2d_mfma_supported(0, .., flags | 64) says 1. */
+ * paig_conv2d_mfma_supported(0, .., flags | 64) says 1.
+ * flags & 512 (dgrad, flags & 8 | 128): the layer's input was the 2x
+ * bilinear upsample of a half-resolution source (blocks.py:206,219,229), and
+ * out [F][Cout][H/2][W/2] receives that source's gradient (the upsample's
+ * backward in the dgrad's epilogue; aux with flags & 2: the source's ReLU'
+ * input, same shape), bit-identical to this dgrad followed by
+ * paig_upsample2_bwd; shapes for which paig_conv2d_mfma_supported(0, ..,
+ * flags) says 1 (the UNet's c9 / c12 / c15). */
 int paig_conv2d_fwd_pw(const float* in, long long in_fs, int in_grp, long long in_gs, float* out, long long out_fs,
                        const float* aux, long long aux_fs, const float* w, const float* bias, int F, int Cin,
                        int Cout, int H, int W, int ks, int flags, float* xmax, int xmax_n, float* pool_out,
@@ -181,7 +188,11 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
  *     codes in the workspace;
  *   PAIG_UNET_EXT_WPREP     split arithmetic: the caller built every conv's
  *     weight images (paig_conv_wprep, dg 0 / 1) and passes them per conv
- *     (wprep_fwd[c], wprep_dg[c]; c = conv index, wprep_dg[0] unused).
+ *     (wprep_fwd[c], wprep_dg[c]; c = conv index, wprep_dg[0] unused);
+ *   PAIG_UNET_STANDALONE_UP (A/B) the backward of an upsample whose consumer
+ *     has separate data- and weight-gradient launches runs as its own kernel
+ *     (paig_upsample2_bwd) instead of in that dgrad's epilogue (flags & 512
+ *     of paig_conv2d_fwd_pw; bit-identical results).
  * The workspace layout depends on the flags (the same flags for the query,
  * the forward and its backward).  probe (nullable) is called on the host
  * around every conv launch (event 0 before, 1 after; kind PAIG_PROBE_*; the
@@ -193,6 +204,7 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
 #define PAIG_UNET_SEPARATE_BWD 2
 #define PAIG_UNET_INFERENCE 4
 #define PAIG_UNET_EXT_WPREP 8
+#define PAIG_UNET_STANDALONE_UP 16
 #define PAIG_PROBE_CONV_FWD 0
 #define PAIG_PROBE_CONV_BWD 1
 #define PAIG_PROBE_CONV_WGRAD 2

@@ -401,6 +401,15 @@ int paig_conv2d_fwd_pwc(const float* in, long long in_fs, int in_grp, long long 
   const int fl = flags & 7;
   if (F <= 0) return 0;
   int rc = 0;
+  if (flags & 512) {   // dgrad with the transposed-upsample epilogue: split path only
+    if (!(flags & 16) && paig_conv_split_fwd(vin, vout, vaux, w, bias, F, Cin, Cout, H, W, ks, flags, st, &rc,
+                                             XMax{xmax, xmax_n}, wprep, PoolOut{pool_out, pool_fs, pool_code,
+                                                                                 pool_code_fs}))
+      return rc;
+    paig_set_error("paig_conv2d_fwd: no transposed-upsample dgrad (flags & 512) for Cin=%d Cout=%d H=%d flags=%d", Cin,
+                   Cout, H, flags);
+    return PAIG_E_UNSUPPORTED;
+  }
   if ((flags & 64) && (flags & 16)) {
     paig_set_error("paig_conv2d_fwd: the fused pool (flags & 64) needs the split path");
     return PAIG_E_UNSUPPORTED;

@@ -51,6 +51,14 @@ namespace {
 
 // ============================================================ forward / dgrad
 
+// the fused-upsample window in the LDS of the lo image (SLA): staged, read
+// by the interpolation, and overwritten by the lo pieces after a barrier (the
+// interpolating threads hold them in registers meanwhile).  64 x 64 layers
+// (the UNet's c15): two blocks per CU on 128-pixel tiles where the window's
+// own LDS would leave one
+constexpr bool sfwd_sla(bool UPS, int PM, int H, int W, int ups_bytes, int lo_bytes) {
+  return UPS && PM == 0 && H * W >= 4096 && ups_bytes <= lo_bytes;
+}
 // bytes of LDS a forward block needs for a tile of <= tpxm pixels and ntb
 // 16-channel output tiles (weights of that COUT slice + the operand images +
 // the fused-upsample window)
@@ -63,7 +71,7 @@ constexpr int sfwd_lds(int CIN, int H, int W, int KS, bool UPS, int PM, int tpxm
   const int RP = W == 8 ? to_mod16(TWPX * PS, 8) : TWPX * PS;
   const int img = FPT * (RT + KS - 1) * RP * 8, wimg = NS * ntb * 64 * 8;
   const int ups = UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0;
-  return (img + wimg) * 2 * (PM == 2 ? 1 : 2) + ups;
+  return (img + wimg) * 2 * (PM == 2 ? 1 : 2) + (sfwd_sla(UPS, PM, H, W, ups, img * 2) ? 0 : ups);
 }
 // VGPRs per lane of a forward block (fitted to the compiler's allocation):
 // accumulators, A fragments, B fragments, k-step offsets, and the staging
@@ -89,7 +97,7 @@ constexpr int sfwd_vgprs(int CIN, int H, int W, int KS, bool UPS, int tpxm, int 
 // 64-pixel tiles).
 constexpr int sfwd_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM) {
   const int base = W == 8 ? 128 : 256, NT = ceil_div(COUT, 16);
-  for (int pass = UPS ? 1 : 0; pass < 3; ++pass)
+  for (int pass = UPS && !(PM == 0 && H * W >= 4096) ? 1 : 0; pass < 3; ++pass)
     for (int nb = 1; nb <= NT; ++nb) {
       if (NT % nb != 0 || NT / nb > 4) continue;
       for (int tp = base; tp >= (pass == 1 ? base / 2 : 64); tp /= 2)
@@ -127,7 +135,9 @@ struct SFwdCfg {
   static constexpr int RP = W == 8 ? to_mod16(TWPX * PS, 8) : TWPX * PS;
   static constexpr int IMG = FPT * ROWS * RP * 8;            // 16-bit elements per image
   static constexpr int WIMG = NS * NT * 64 * 8;
-  static constexpr int LDS = (IMG + WIMG) * 2 * NIMG;
+  static constexpr int SLB = UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0;   // upsample window
+  static constexpr bool SLA = sfwd_sla(UPS, PM, H, W, SLB, IMG * 2);
+  static constexpr int LDS = (IMG + WIMG) * 2 * NIMG + (SLA ? 0 : SLB);   // incl. the upsample window
   // staging unit = UPX pixels x 8 channels, consecutive lanes on consecutive
   // pixels (coalesced loads, b128 LDS writes PS slots apart: conflict-free)
   static constexpr int UPX = W % 2 == 0 ? 2 : 1;
@@ -181,11 +191,22 @@ __device__ __forceinline__ int fwd_mtile(int wv, int mt) {
   }
 }
 
-template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false>
+// UPT (dgrad only): the layer's input was the 2x bilinear upsample of a
+// half-resolution source (blocks.py:206,219,229 feeding c9 / c12 / c15), and
+// the kernel writes that SOURCE's gradient: the transposed upsample of the
+// dX tile, in the epilogue.  A block walks whole frames top to bottom (its
+// frames b, b + G, ...), so each half-resolution row's four full-resolution
+// rows are summed in a fixed order in registers, two rows carried from one
+// tile to the next; out / aux are the source's gradient and its ReLU' input
+// (H/2 x W/2 planes).  Same operation order as upsample_bwd_v_k on the
+// dgrad's output: bit-identical to the two-launch form.
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false, bool UPT = false>
 __global__ void __launch_bounds__(256, 2)
 conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
                  int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp, PoolOut pout) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
+  static_assert(!UPT || (DG && !UPS && !POOL && C::FPT == 1 && C::RT % 2 == 0 && C::VEC4 && W % 2 == 0),
+                "transposed-upsample epilogue: dgrad tiles of whole row pairs");
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
   constexpr int RT = C::RT, FPT = C::FPT, ROWS = C::ROWS, PS = C::PS, RP = C::RP;
   constexpr int NI = C::NI, NL = C::NL, PADL = C::PADL, W2 = C::W2;
@@ -221,16 +242,20 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) ewn[nt] = 0;
   __shared__ int sew[PM == 0 ? NT * 16 : 1];   // in-kernel staging: the slice's channel exponents
-  // ---- zero the halo columns (never written by the staging)
-  if (PADL > 0) {
-    for (int i = tid; i < FPT * ROWS * 2 * PADL * CC; i += 256) {
-      const int cc = i % CC, hc = (i / CC) % (2 * PADL), r = i / (CC * 2 * PADL);
-      const int xc = hc < PADL ? hc : W + hc;
-      const int o = (r * RP + xc * PS + cc) * 8;
-      *reinterpret_cast<s16x8*>(Xh + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  // ---- zero the halo columns (never written by the staging; again after
+  // UPT's epilogue, which keeps its dX tile in the images' LDS)
+  auto zero_halo = [&]() {
+    if (PADL > 0) {
+      for (int i = tid; i < FPT * ROWS * 2 * PADL * CC; i += 256) {
+        const int cc = i % CC, hc = (i / CC) % (2 * PADL), r = i / (CC * 2 * PADL);
+        const int xc = hc < PADL ? hc : W + hc;
+        const int o = (r * RP + xc * PS + cc) * 8;
+        *reinterpret_cast<s16x8*>(Xh + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
-  }
+  };
+  zero_halo();
   // ---- per-lane fragment slot offsets: pixel base per M-tile, (tap, chunk) per k-step
   int pbase[MW];
 #pragma unroll
@@ -252,8 +277,28 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   // ---- staging: unit i = (frame fi, row r, chunk cc, pixel xp), xp fastest;
   // the next tile's loads are in flight during this tile's MFMAs
   using UP = UpStage<UPS ? CIN : 1, H, W, FPT, RT>;
-  float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::IMG + C::WIMG));
+  float* Sl = reinterpret_cast<float*>(C::SLA ? Xl : lds16 + C::NIMG * (C::IMG + C::WIMG));
   constexpr int UPX = C::UPX;
+  // staging unit i's hi / lo pieces (both pixels) and its image offset
+  auto split_px = [&](int i, const float2* v, float sc, s16x8& h0, s16x8& l0, s16x8& h1, s16x8& l1) {
+    const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
+    if constexpr (PM == 0) {
+      pf32x2 sv[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) sv[c] = pf32x2{v[c].x, v[c].y} * sc;
+      u32x4 a0, b0, a1, b1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        { const HiLo q_ = split_pk(sv[2 * k].x, sv[2 * k + 1].x); a0[k] = q_.h; b0[k] = q_.l; }
+        { const HiLo q_ = split_pk(sv[2 * k].y, sv[2 * k + 1].y); a1[k] = q_.h; b1[k] = q_.l; }
+      }
+      h0 = __builtin_bit_cast(s16x8, a0);
+      l0 = __builtin_bit_cast(s16x8, b0);
+      h1 = __builtin_bit_cast(s16x8, a1);
+      l1 = __builtin_bit_cast(s16x8, b1);
+    }
+    return ((fi * ROWS + r) * RP + (xp + PADL) * PS + cc) * 8;
+  };
   auto put_px = [&](int i, const float2* v, float sc) {
     const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cc = (i / (W2 * ROWS)) % CC, fi = i / (W2 * ROWS * CC);
     const int o = ((fi * ROWS + r) * RP + (xp + PADL) * PS + cc) * 8;
@@ -340,6 +385,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   };
   auto commit = [&](int t) {
     if constexpr (DYN) tile_scale();
+    if constexpr (UPT) zero_halo();
     if constexpr (UPS) {
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
@@ -378,6 +424,54 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
             for (int c = 0; c < 8; ++c) v[c] = make_float2(o[c][2], o[c][3]);
             put_px(ia + 1, v, tsc);
+          }
+        }
+      } else if constexpr (C::SLA) {
+        // the window lives in the lo image's LDS: hi pieces stored now, lo
+        // pieces held in registers until every thread has read the window
+        static_assert(W % 4 == 0 && UPX == 2, "SLA: 4-pixel items");
+        constexpr int W4 = W / 4, NIT = ceil_div(NI / 2, 256);
+        s16x8 lk[NIT][4];
+        int lo_off[NIT][2];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int i = tid + it * 256;
+          lo_off[it][0] = -1;
+          if ((NI / 2) % 256 != 0 && i >= NI / 2) break;
+          const int q = i % W4, r = (i / W4) % ROWS, cc = (i / (W4 * ROWS)) % CC, fi = i / (W4 * ROWS * CC);
+          const int gy = y0 + r - PADL;
+          const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+          f32x4 o[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            o[c] = (ok && cc * 8 + c < CIN) ? UP::row4(Sl, fi, cc * 8 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const int ia = ((fi * CC + cc) * ROWS + r) * W2 + 2 * q;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            float2 v[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) v[c] = make_float2(o[c][2 * u], o[c][2 * u + 1]);
+            s16x8 h0, h1;
+            const int off = split_px(ia + u, v, tsc, h0, lk[it][2 * u], h1, lk[it][2 * u + 1]);
+            *reinterpret_cast<s16x8*>(Xh + off) = h0;
+            *reinterpret_cast<s16x8*>(Xh + off + PS * 8) = h1;
+            lo_off[it][u] = off;
+          }
+        }
+        __syncthreads();   // every read of the window is done
+        // the lo image's halo columns (the window overwrote them)
+        for (int i = tid; i < FPT * ROWS * 2 * PADL * CC; i += 256) {
+          const int cc = i % CC, hc = (i / CC) % (2 * PADL), r = i / (CC * 2 * PADL);
+          const int xc = hc < PADL ? hc : W + hc;
+          *reinterpret_cast<s16x8*>(Xl + (r * RP + xc * PS + cc) * 8) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          if (lo_off[it][0] < 0) break;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            *reinterpret_cast<s16x8*>(Xl + lo_off[it][u]) = lk[it][2 * u];
+            *reinterpret_cast<s16x8*>(Xl + lo_off[it][u] + PS * 8) = lk[it][2 * u + 1];
           }
         }
       } else if constexpr (W % 4 == 0) {
@@ -448,8 +542,17 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   // logical tile lt; xcd_tile() gives the physical one; past the last tile,
   // tile ntiles lies beyond frame F and every lane reads paig_zeros (the
   // prefetch stays unconditional: branch-free for the load counting)
-  int lt = blockIdx.x;
-  auto tile_of = [&](int l) { return l < ntiles ? xcd_tile(l, ntiles) : ntiles; };
+  // UPT: logical tile l of this block is band l % NRB of its (l / NRB)-th frame
+  int lt = UPT ? 0 : blockIdx.x;
+  const int lstep = UPT ? 1 : gridDim.x;
+  auto tile_of = [&](int l) {
+    if constexpr (UPT) {
+      const int f = blockIdx.x + (l / NRB) * gridDim.x;
+      return f < F ? f * NRB + l % NRB : ntiles;
+    } else {
+      return l < ntiles ? xcd_tile(l, ntiles) : ntiles;
+    }
+  };
   issue(tile_of(lt));
   if (PM == 0 && wp != nullptr) {
     // pre-split images of the whole COUT (paig_conv_wprep, once per step):
@@ -515,8 +618,102 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     bvs[nt] = *(bias && co < COUT ? bias + co : paig_zeros);
     asm volatile("" ::"v"(bvs[nt]));   // arrived before the loop: no wait on it behind a prefetch
   }
-  for (; lt < ntiles; lt += gridDim.x) {
-    const int tile = xcd_tile(lt, ntiles);
+  // UPT: this thread's items (channel, source column) and their carried
+  // partial sums of source rows kB (the tile's last) and kB + 1
+  constexpr int WS2 = W / 2, NCL = NT * 16, NUI = UPT ? ceil_div(NCL * WS2, 256) : 1;
+  float car0[NUI], car1[NUI];
+  float auxu[UPT ? NUI : 1][UPT ? RT / 2 + 1 : 1];   // ReLU' inputs of the rows the tile completes
+  // loaded before the tile's MFMAs (their latency hides behind them)
+  auto upt_aux = [&](int tile) {
+    if constexpr (UPT) {
+      if (flags & 2) {
+        const int f = tile / NRB, kA = (tile % NRB) * (RT / 2);
+#pragma unroll
+        for (int u = 0; u < NUI; ++u) {
+          const int item = tid + u * 256;
+          const int cl = item / WS2, j = item % WS2;
+          const bool ok = (NCL * WS2) % 256 == 0 || item < NCL * WS2;
+#pragma unroll
+          for (int i = 0; i <= RT / 2; ++i) {
+            const int k = kA - 1 + i;
+            const float* ap = aux.frame(f) + (long long)(co0 + cl) * ((H / 2) * WS2) + (long long)k * WS2 + j;
+            auxu[u][i] = *(ok && k >= 0 && k < H / 2 ? ap : paig_zeros);
+          }
+        }
+      }
+    }
+  };
+  auto upt_epilogue = [&](int tile, f32x4 (&a)[MW][NT]) {
+    constexpr int HS = H / 2, KR = RT / 2 + 2;   // P[i]: source row kA - 1 + i
+    static_assert(!UPT || RT * NCL * W * 4 <= C::NIMG * C::IMG * 2, "the dX tile fits the image's LDS");
+    const int f = tile / NRB, band = tile % NRB, kA = band * (RT / 2);
+    __syncthreads();   // every wave's fragment reads of the image are done
+    float* RB = reinterpret_cast<float*>(lds16);   // the dX tile, [row][channel][x]
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int cl = nt * 16 + (lane & 15);
+#pragma unroll
+      for (int mt = 0; mt < MW; ++mt) {
+        const int pix = fwd_mtile<MW, C::PO, false>(wv, mt) * 16 + (lane >> 4) * 4;
+        if (pix >= C::TPXV) continue;
+        f32x4 v = a[mt][nt];
+        if constexpr (SCL) v *= tinv[nt];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bvs[nt];
+        *reinterpret_cast<f32x4*>(RB + ((pix / W) * NCL + cl) * W + pix % W) = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NUI; ++u) {
+      const int item = tid + u * 256;
+      if ((NCL * WS2) % 256 != 0 && item >= NCL * WS2) break;
+      const int cl = item / WS2, j = item % WS2, co = co0 + cl;
+      float P[KR];
+      P[0] = band == 0 ? 0.f : car0[u];
+      P[1] = band == 0 ? 0.f : car1[u];
+#pragma unroll
+      for (int i = 2; i < KR; ++i) P[i] = 0.f;
+      // upsample_bwd_v_k's taps and order: each full row's columns 2j-1 ..
+      // 2j+2, then the rows 2k-1 .. 2k+2 of source row k in increasing order
+      const float wxa = j >= 1 ? 0.25f : 0.f, wxb = j == 0 ? 1.f : 0.75f;
+      const float wxc = j == WS2 - 1 ? 1.f : 0.75f, wxd = j <= WS2 - 2 ? 0.25f : 0.f;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const float* rp = RB + (r * NCL + cl) * W + 2 * j;
+        const float2 m2 = *reinterpret_cast<const float2*>(rp);
+        float hs = 0.f;
+        if (wxa != 0.f) hs = fmaf(wxa, rp[-1], hs);
+        hs = fmaf(wxb, m2.x, hs);
+        hs = fmaf(wxc, m2.y, hs);
+        if (wxd != 0.f) hs = fmaf(wxd, rp[2], hs);
+        const int m = kA + r / 2;   // full row 2m (r even) or 2m + 1 (r odd)
+        if (r % 2 == 0) {
+          if (m >= 1) P[r / 2] = fmaf(0.25f, hs, P[r / 2]);                 // row 2k+2 of k = m - 1
+          P[r / 2 + 1] = fmaf(m == 0 ? 1.f : 0.75f, hs, P[r / 2 + 1]);      // row 2k of k = m
+        } else {
+          P[r / 2 + 1] = fmaf(m == HS - 1 ? 1.f : 0.75f, hs, P[r / 2 + 1]);  // row 2k+1 of k = m
+          if (m + 1 <= HS - 1) P[r / 2 + 2] = fmaf(0.25f, hs, P[r / 2 + 2]);  // row 2k-1 of k = m + 1
+        }
+      }
+      // complete: rows kA - 1 .. kB - 1, and kB on the frame's last band
+      const bool last = band == NRB - 1;
+      const long long po = (long long)co * (HS * WS2) + j;
+#pragma unroll
+      for (int i = 0; i <= RT / 2; ++i) {
+        const int k = kA - 1 + i;
+        if (k < 0 || (i == RT / 2 && !last)) continue;
+        float v = P[i];
+        if (flags & 2) v = auxu[u][i] > 0.f ? v : 0.f;
+        out.frame(f)[po + k * WS2] = v;
+      }
+      car0[u] = P[RT / 2];
+      car1[u] = P[RT / 2 + 1];
+    }
+  };
+  for (;; lt += lstep) {
+    const int tile = tile_of(lt);
+    if (tile >= ntiles) break;
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
     if constexpr (DYN) tile_max();
     __syncthreads();   // previous tile's fragment reads are done
@@ -524,7 +721,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     __syncthreads();
     // dgrad: this tile's ReLU' mask for the epilogue (AUXP), loaded before the
     // next tile's prefetch so that its latency hides behind the MFMAs
-    constexpr bool AUXP = PAIG_FWD_AUXP && DG && C::VEC4 && !POOL && MW * NT <= 8;
+    constexpr bool AUXP = PAIG_FWD_AUXP && DG && C::VEC4 && !POOL && !UPT && MW * NT <= 8;
     f32x4 auxv[AUXP ? MW : 1][AUXP ? NT : 1];
     if constexpr (AUXP) {
       if (flags & 2) {
@@ -543,7 +740,8 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
         }
       }
     }
-    issue(tile_of(lt + gridDim.x));
+    upt_aux(tile);
+    issue(tile_of(lt + lstep));
     f32x4 acc[MW][NT];
 #pragma unroll
     for (int mt = 0; mt < MW; ++mt)
@@ -566,6 +764,10 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mma3<PM>(ah, al, bh[nt], bl[nt], acc[mt][nt]);
       }
+    }
+    if constexpr (UPT) {
+      upt_epilogue(tile, acc);
+      continue;
     }
     // ---- epilogue: lane holds pixels (lane>>4)*4 + r of each M-tile for co = nt*16 + (lane&15)
 #pragma unroll
@@ -1232,17 +1434,19 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
   if constexpr (PM == 0) f16_range_note(rmax);
 }
 
-template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM>
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool UPT = false>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
                        hipStream_t st, XMax xm, const void* wp, PoolOut pout) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
-  constexpr int LDS = C::LDS + (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0);
+  constexpr int LDS = C::LDS;
+  static_assert(C::SLB == (UPS ? UpStage<CIN, H, W, C::FPT, C::RT>::SL * 4 : 0), "upsample window bytes");
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   // the fused-pool variant (its own instantiation: keeping the stored tile
   // live for the pool costs ~20 VGPRs, which the other launches must not pay)
   constexpr bool POOLABLE = C::POOLOK && !DG;
-  auto k = (POOLABLE && (flags & 64)) ? conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, POOLABLE>
-                                      : conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, false>;
+  auto k = UPT ? conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, false, UPT>
+              : (POOLABLE && (flags & 64)) ? conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, POOLABLE>
+                                           : conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, false>;
   static int resident[2] = {0, 0};
   const int kv = (POOLABLE && (flags & 64)) ? 1 : 0;
   if (!resident[kv]) {
@@ -1250,7 +1454,7 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
     resident[kv] = persistent_grid((const void*)k, LDS);
   }
   int nb = resident[kv] / C::NB;   // persistent blocks per COUT slice
-  if (nb > ntiles) nb = ntiles;
+  if (nb > (UPT ? F : ntiles)) nb = UPT ? F : ntiles;   // UPT: whole frames per block
   if (nb < 1) nb = 1;
   if (PM != 0 || DG) xm.p = nullptr;
   PAIG_REQUIRE(!xm.p || nb <= xm.n, "conv split fwd: %d blocks need more than %d xmax slots", nb, xm.n);
@@ -1301,6 +1505,9 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
 #define PAIG_SPLIT_UP(X)                                                                                  \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(32, 16, 18, 3) X(16, 16, 36, 3) X(128, 32, 16, 3) X(64, 32, 32, 3) \
   X(32, 32, 64, 3)
+// dgrad shapes (layer Cout, layer Cin) of the UNet convs whose input is the
+// 2x upsample (c9, c12, c15) with the transposed-upsample epilogue (UPT)
+#define PAIG_SPLIT_UPT(X) X(32, 128, 16, 3) X(32, 64, 32, 3) X(32, 32, 64, 3)
 // 3bp_color (ShallowUNet hidden 8 on 36 x 36 frames, K = 3 objects): levels
 // 36 / 18 / 9; tiles of 6 rows (36), 9 rows (18) or 3 frames (9 x 9)
 #define PAIG_SPLIT_FWD_3BP(X)                                                                             \
@@ -1332,6 +1539,17 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
   const int fl = flags & (7 | 64);
   if (H != W || !(flags & (128 | 256))) return 0;
   if (in.grp > 0 && H * W < 256) return 0;   // multi-frame tiles step frames by a plain stride
+  if (flags & 512) {   // dgrad writing the transposed upsample of dX (UPT)
+    if (!dg || up || b16 || (flags & (4 | 64))) return 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                                          \
+    if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
+      *rc = sfwd_launch<CI, CO, HH, HH, K, true, false, 0, true>(in, out, aux, w, b, F, fl, st, xm, wp, pout); \
+      return 1;                                                                                           \
+    }
+    PAIG_SPLIT_UPT(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
   if (up) {
     if (dg) return 0;
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
@@ -1402,6 +1620,11 @@ int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks,
   }
 #define PAIG_CASE(CI, CO, HH, K) \
   if (Cin == CI && Cout == CO && H == HH && ks == K) return 1;
+  if (flags & 512) {
+    if (what != 0 || !dg || up || (flags & (4 | 64 | 256)) || !(flags & 128)) return 0;
+    PAIG_SPLIT_UPT(PAIG_CASE)
+    return 0;
+  }
   if (up) {
     if (dg) return 0;
     PAIG_SPLIT_UP(PAIG_CASE)

@@ -535,6 +535,33 @@ int bwd_impl(int net, int F, int H, int K, int math, int flags, const float* x, 
       if (rc) return rc;
       s_src.push_back(slab), s_nb.push_back(nb), s_len.push_back(n_w + cout), s_dst.push_back(dwb[op.conv]);
       if (op.src.buf == p.X0) continue;   // no input gradient (Q10)
+      const int ui = p.fused_up[i];
+      if (ui >= 0 && cm == 128 && !(flags & PAIG_UNET_STANDALONE_UP) &&
+          paig_conv2d_mfma_supported(0, cout, cin, Hl, Hl, ks, 8 | 128 | 512)) {
+        // the dgrad writes the upsample SOURCE's gradient: the upsample's
+        // backward in its epilogue (one launch, no full-resolution gradient)
+        const Reg usrc = p.ops[ui].src;
+        const View dxv = dview(usrc);
+        PAIG_REQUIRE(state(usrc) == 0, "paig_unet_bwd: upsample source gradient already written (op %d)", i);
+        int flags2 = 8 | 512, alvl;
+        const float* aux = nullptr;
+        long long aux_fs = 0;
+        for (auto& f : p.fin[ui])
+          if (f.first == usrc && f.second) {
+            const View a = view(usrc, alvl);
+            aux = a.p;
+            aux_fs = a.fs;
+            flags2 |= 2;
+          }
+        pr(0, i, op.conv, PAIG_PROBE_CONV_DGRAD, cin, cout, Hl, flags2 | cm);
+        rc = paig_conv2d_fwd_pw(dyv.p, dyv.fs, 0, 0, const_cast<float*>(dxv.p), dxv.fs, aux, aux_fs, w[op.conv],
+                                nullptr, F, cout, cin, Hl, Hl, ks, flags2 | cm, nullptr, 0, nullptr, 0, wp1, stream);
+        pr(1, i, op.conv, PAIG_PROBE_CONV_DGRAD, cin, cout, Hl, flags2 | cm);
+        if (rc) return rc;
+        mark(usrc);
+        folded_up[ui] = true;
+        continue;
+      }
       const View dxv = dview(op.src);
       const int mode = state(op.src);
       PAIG_REQUIRE(mode >= 0, "paig_unet_bwd: partially written gradient region (op %d)", i);

@@ -454,6 +454,8 @@ class Engine:
                     nbytes = 4 * F * Hl * Hl * (cin + cout + cin * (2 if fl & 4 else 1))
                     if fl & 64:   # the folded max pool: pooled gradient + window codes
                         nbytes += F * (4 * cout + cout) * (Hl // 2) ** 2
+            elif fl & 512:                 # data gradient into the upsample source: dY read, its gradient (+ mask)
+                nbytes = 4 * F * (cout * Hl * Hl + cin * (Hl // 2) ** 2 * (2 if fl & 2 else 1))
             else:                          # data gradient: dY read, dX written (+ mask, + accumulate)
                 nbytes = 4 * F * Hl * Hl * (cout + cin * (1 + (1 if fl & 2 else 0) + (1 if fl & 4 else 0)))
             c = self._p(f"{self._PROBE_TAG[kind]}:c{conv + 1}", flops, nbytes)
@@ -475,7 +477,8 @@ class Engine:
         dev = S["dev"]
         cm = S["cm"]
         flags = ((1 if fuse_head else 0) | (0 if S.get("need_saved", True) else 4) |
-                 (2 if os.environ.get("PAIG_FUSED_BWD", "1") == "0" else 0))
+                 (2 if os.environ.get("PAIG_FUSED_BWD", "1") == "0" else 0) |
+                 (16 if os.environ.get("PAIG_UPT", "1") == "0" else 0))   # A/B: standalone upsample backward
         Ws = [self.p(lay.prefix + f"c{c + 1}.weight") for c in range(lay.nconv)]
         Bs = [self.p(lay.prefix + f"c{c + 1}.bias") for c in range(lay.nconv)]
         # split path: every conv's forward and dgrad weight images (and the

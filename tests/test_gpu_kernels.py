@@ -180,6 +180,25 @@ def test_conv_split_fused_upsample(cin, cout, hw, mode):
         assert rel_err(dx, xr.grad) <= tb
 
 
+def test_conv_split_fused_upsample_many_tiles():
+    """c15's fused-upsample forward (window in the lo image's LDS, two blocks
+    per CU) with every persistent block walking many tiles: vs float64."""
+    tf, _ = SPLIT_TOL[128]
+    cin, cout, hw, F_ = 32, 32, 64, 200
+    torch.manual_seed(5)
+    xs = torch.relu(torch.randn(F_, cin, hw // 2, hw // 2))
+    w = torch.randn(cout, cin, 3, 3) * 0.2
+    b = torch.randn(cout)
+    xu = F.interpolate(xs.double(), size=(hw, hw), mode="bilinear", align_corners=False)
+    y = F.conv2d(xu, w.double(), b.double(), padding=1)
+    xg, wg, bg = xs.to(DEV), w.to(DEV), b.to(DEV)
+    out = torch.empty(F_, cout, hw, hw, device=DEV)
+    L().paig_conv2d_fwd(p(xg), cin * hw * hw // 4, 0, 0, p(out), cout * hw * hw, None, 0, p(wg), p(bg), F_, cin, cout,
+                        hw, hw, 3, 32 | 128, st())
+    torch.cuda.synchronize()
+    assert rel_err(out.double().cpu(), y) <= tf
+
+
 def test_conv_grouped_input_view():
     """The first conv reads frames (b, t < Te) of a [B, T, C, H, W] input in place."""
     B, T, Te, H = 3, 7, 4, 32

@@ -81,3 +81,78 @@ def test_unet_abi_rejects_bad_arguments():
     with pytest.raises(PaigError):   # workspace too small
         L.paig_unet_fwd(0, 4, 32, 2, 128, x.data_ptr(), 3 * 1024, 0, 0, _parr([0] * 13), _parr([0] * 13),
                         x.data_ptr(), x.data_ptr(), 16, torch.cuda.current_stream().cuda_stream)
+
+
+@pytest.mark.parametrize("N", [3, 40])
+def test_unet_upsample_backward_in_dgrad_epilogue_is_bit_identical(N):
+    """The UNet's c9 / c12 / c15 data gradients with the upsample's backward
+    in their epilogue (paig_conv2d_fwd_pw flags & 512, the default) against
+    the same dgrads followed by paig_upsample2_bwd (PAIG_UNET_STANDALONE_UP):
+    every conv's weight and bias gradient bit-identical (c1 .. c14 see the
+    upsample sources' gradients).  Reference: blocks.py:206,219,229."""
+    from paig_reproduction_amd._lib import lib
+    L = lib()
+    H, K, net, nconv, math = 64, 2, 1, 18, 128
+    torch.manual_seed(7)
+    ws_ = [None] * nconv
+    chans = [(3, 16, 3), (16, 16, 3), (16, 32, 3), (32, 32, 3), (32, 64, 3), (64, 64, 3), (64, 128, 3), (128, 128, 3),
+             (128, 32, 3), (96, 64, 3), (64, 64, 3), (64, 32, 3), (64, 32, 3), (32, 32, 3), (32, 32, 3), (48, 16, 3),
+             (16, 16, 3), (16, K, 1)]
+    ws_ = [torch.randn(co, ci, k, k, device=DEV) * (2.0 / (ci * k * k)) ** 0.5 for ci, co, k in chans]
+    bs_ = [torch.randn(co, device=DEV) * 0.1 for _, co, _ in chans]
+    x = torch.rand(N, 3, H, H, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for flags in (0, 16):
+        nbytes = int(L.paig_unet_workspace_ex(net, N, H, K, math, flags))
+        ws = torch.empty(nbytes // 4 + 1, device=DEV)
+        lg = torch.empty(N, K, H, H, device=DEV)
+        L.paig_unet_fwd_ex(net, N, H, K, math, flags, x.data_ptr(), 3 * H * H, 0, 0,
+                           _parr([t.data_ptr() for t in ws_]), _parr([t.data_ptr() for t in bs_]), lg.data_ptr(), None,
+                           None, ws.data_ptr(), nbytes, None, None, st)
+        torch.manual_seed(11)
+        R = torch.randn(N, K, H, H, device=DEV)
+        dwb = [torch.full((w.numel() + w.shape[0],), float("nan"), device=DEV) for w in ws_]
+        L.paig_unet_bwd_ex(net, N, H, K, math, flags, x.data_ptr(), 3 * H * H, 0, 0,
+                           _parr([t.data_ptr() for t in ws_]), lg.data_ptr(), R.data_ptr(),
+                           _parr([t.data_ptr() for t in dwb]), 0, None, None, None, None, None, ws.data_ptr(), nbytes,
+                           None, None, st)
+        torch.cuda.synchronize()
+        out[flags] = (lg.clone(), dwb)
+    assert torch.equal(out[0][0], out[16][0])
+    for i in range(nconv):
+        a, b = out[0][1][i], out[16][1][i]
+        assert torch.isfinite(a).all(), f"c{i + 1}"
+        assert torch.equal(a, b), f"c{i + 1}: max |d| {(a - b).abs().max().item():.3e}"
+
+
+@pytest.mark.parametrize("cin,cout,H", [(128, 32, 16), (64, 32, 32), (32, 32, 64)])
+@pytest.mark.parametrize("F", [5, 700])
+def test_dgrad_upsample_epilogue_kernel(cin, cout, H, F):
+    """paig_conv2d_fwd_pw flags & 512 (dgrad of a conv whose input was the 2x
+    upsample, writing the upsample source's gradient with its ReLU' mask)
+    bit-identical to the dgrad then paig_upsample2_bwd; F = 700 gives every
+    persistent block several frames (the carried rows)."""
+    from paig_reproduction_amd._lib import lib
+    L = lib()
+    torch.manual_seed(cin + H + F)
+    hs = H // 2
+    dy = torch.randn(F, cout, H, H, device=DEV)
+    w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.1
+    src = torch.randn(F, cin, hs, hs, device=DEV)   # the upsample source (ReLU output: mask src > 0)
+    st = torch.cuda.current_stream().cuda_stream
+    full = torch.empty(F, cin, H, H, device=DEV)
+    rc = L.paig_conv2d_fwd_pw(dy.data_ptr(), cout * H * H, 0, 0, full.data_ptr(), cin * H * H, None, 0, w.data_ptr(),
+                              None, F, cout, cin, H, H, 3, 8 | 128, None, 0, None, 0, None, st)
+    assert rc == 0
+    ref = torch.empty(F, cin, hs, hs, device=DEV)
+    L.paig_upsample2_bwd(full.data_ptr(), cin * H * H, src.data_ptr(), cin * hs * hs, ref.data_ptr(), cin * hs * hs, F,
+                         cin, hs, hs, H, H, 1, st)
+    got = torch.full((F, cin, hs, hs), float("nan"), device=DEV)
+    assert L.paig_conv2d_mfma_supported(0, cout, cin, H, H, 3, 8 | 128 | 512) == 1
+    rc = L.paig_conv2d_fwd_pw(dy.data_ptr(), cout * H * H, 0, 0, got.data_ptr(), cin * hs * hs, src.data_ptr(),
+                              cin * hs * hs, w.data_ptr(), None, F, cout, cin, H, H, 3, 8 | 128 | 512 | 2, None, 0,
+                              None, 0, None, st)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), f"max |d| {(got - ref).abs().max().item():.3e}"
