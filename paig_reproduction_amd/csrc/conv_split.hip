@@ -40,9 +40,6 @@
 //   are summed exactly in fp32 from the staging registers.
 #include "split_common.h"
 
-#ifndef PAIG_UPS2_FWD
-#define PAIG_UPS2_FWD 1   // A/B builds: 0 = one-row upsample staging items (forward)
-#endif
 #ifndef PAIG_FWD_AUXP
 #define PAIG_FWD_AUXP 1   // A/B builds: 0 = the dgrad epilogue loads its ReLU' mask when it needs it
 #endif
@@ -390,43 +387,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
       __syncthreads();
-      if constexpr (W % 4 == 0 && ROWS % 2 == 0 && PAIG_UPS2_FWD && CIN <= 32 && !(H == 64 && PM == 0)) {
-        // (the 8-channel row-pair item's 64 outputs spill on the UNet's wide
-        // / 64-wide upsample layers: those keep the one-row items)
-        // units of 4 pixels x 8 channels x a ROW PAIR (output rows y0 - 1 +
-        // 2rp, y0 + 2rp interpolate the same two source rows: shared reads and
-        // horizontal interpolations, half the items; conv_bwd.hip's form)
-        constexpr int W4 = W / 4, RP2 = ROWS / 2;
-#pragma unroll 1
-        for (int i = tid; i < FPT * CC * RP2 * W4; i += 256) {
-          const int q = i % W4, rp = (i / W4) % RP2, cc = (i / (W4 * RP2)) % CC, fi = i / (W4 * RP2 * CC);
-          const int gy = y0 + 2 * rp - PADL;
-          const bool okf = f0 + fi < F;
-          const bool ok0 = okf && gy >= 0 && gy < H, ok1 = okf && gy + 1 >= 0 && gy + 1 < H;
-          f32x4 o0[8], o1[8];
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            if (cc * 8 + c < CIN) {
-              UP::row4x2(Sl, fi, cc * 8 + c, gy, y0, q, ok0, ok1, o0[c], o1[c]);
-            } else {
-              o0[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-              o1[c] = o0[c];
-            }
-          }
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            const int ia = ((fi * CC + cc) * ROWS + 2 * rp + h2) * W2 + 2 * q;
-            const f32x4* o = h2 ? o1 : o0;
-            float2 v[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) v[c] = make_float2(o[c][0], o[c][1]);
-            put_px(ia, v, tsc);
-#pragma unroll
-            for (int c = 0; c < 8; ++c) v[c] = make_float2(o[c][2], o[c][3]);
-            put_px(ia + 1, v, tsc);
-          }
-        }
-      } else if constexpr (C::SLA) {
+      if constexpr (C::SLA) {
         // the window lives in the lo image's LDS: hi pieces stored now, lo
         // pieces held in registers until every thread has read the window
         static_assert(W % 4 == 0 && UPX == 2, "SLA: 4-pixel items");
