@@ -92,8 +92,12 @@ constexpr int sfwd_vgprs(int CIN, int H, int W, int KS, bool UPS, int tpxm, int 
 // MFMAs serialised (the UNet's 32..128-channel layers: 1.2-1.7x faster).
 // Not for the fused upsample (its 64 x 64 layer measured 1.2x slower on
 // 64-pixel tiles).
+#ifndef PAIG_FWD_UPS_TP
+#define PAIG_FWD_UPS_TP 256   // A/B builds: the largest tile of the sub-64x64 fused-upsample forwards
+#endif
 constexpr int sfwd_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM) {
-  const int base = W == 8 ? 128 : 256, NT = ceil_div(COUT, 16);
+  const int base = UPS && H * W < 4096 && PAIG_FWD_UPS_TP < 256 ? PAIG_FWD_UPS_TP : (W == 8 ? 128 : 256);
+  const int NT = ceil_div(COUT, 16);
   for (int pass = UPS && !(PM == 0 && H * W >= 4096) ? 1 : 0; pass < 3; ++pass)
     for (int nb = 1; nb <= NT; ++nb) {
       if (NT % nb != 0 || NT / nb > 4) continue;
@@ -1414,7 +1418,13 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
     if (LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     resident[kv] = persistent_grid((const void*)k, LDS);
   }
-  int nb = resident[kv] / C::NB;   // persistent blocks per COUT slice
+  static const int bpc = [] {   // A/B: PAIG_FWD_BPC caps the forward's blocks per CU
+    const char* e = getenv("PAIG_FWD_BPC");
+    return e ? atoi(e) : 0;
+  }();
+  int res = resident[kv];
+  if (bpc > 0 && res > bpc * 256) res = bpc * 256;
+  int nb = res / C::NB;   // persistent blocks per COUT slice
   if (nb > (UPT ? F : ntiles)) nb = UPT ? F : ntiles;   // UPT: whole frames per block
   if (nb < 1) nb = 1;
   if (PM != 0 || DG) xm.p = nullptr;
