@@ -79,7 +79,7 @@ constexpr int sbwd_lds(int CIN, int COUT, int H, int W, bool UPS, int PM, int tp
   const int XIMG = rup(CIN, 4) / 4 * rup(FPT * ROWS * (W + 4) * 4 + 80, 128) * 2 * (PM == 2 ? 1 : 2);
   const int UPB = UPS ? CIN * (rup(FPT * (RT + 2) * W, 64) + 4) * 4 : 0;
   const int XREG = XIMG > UPB ? XIMG : UPB;
-  return (IMGD + WIMG) * 2 * (PM == 2 ? 1 : 2) + XREG + (UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0);
+  return (IMGD + WIMG) * 2 * (PM == 2 ? 1 : 2) + XREG + (UPS ? up_window_floats(CIN, FPT, RT, W) * 4 : 0);
 }
 // pixels per tile: the largest of 256 / 128 / 64 whose staging lets two
 // blocks share a CU (the 8 x 8 / 9 x 9 levels' multi-frame tiles and the
@@ -171,7 +171,7 @@ struct SBwdCfg {
   static constexpr int UPX = W % 2 == 0 ? 2 : 1, W2 = W / UPX;
   static constexpr int NID = FPT * ROWSD * W2 * CCD, NLD = ceil_div(NID, 256);
   static constexpr int NIX = FPT * ROWS * W2 * CQ, NLX = ceil_div(NIX, 256);
-  static constexpr int UPW = FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2);   // fused-upsample window (floats)
+  static constexpr int UPW = up_window_floats(CIN, FPT, RT, W);   // fused-upsample window (floats)
   // the X image's region (UPS: it later holds the tile's full-resolution dX)
   static constexpr int UPB = UPS ? CIN * (rup(FPT * (RT + 2) * W, 64) + 4) * 4 : 0;   // the dX tile's bytes
   static constexpr int XREG = XIMG * 2 * NIMG > UPB ? XIMG * 2 * NIMG : UPB;

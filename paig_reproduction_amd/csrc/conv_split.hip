@@ -67,7 +67,7 @@ constexpr int sfwd_lds(int CIN, int H, int W, int KS, bool UPS, int PM, int tpxm
   const int TWPX = W + 2 * (KS / 2);
   const int RP = W == 8 ? to_mod16(TWPX * PS, 8) : TWPX * PS;
   const int img = FPT * (RT + KS - 1) * RP * 8, wimg = NS * ntb * 64 * 8;
-  const int ups = UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0;
+  const int ups = UPS ? up_window_floats(CIN, FPT, RT, W) * 4 : 0;
   return (img + wimg) * 2 * (PM == 2 ? 1 : 2) + (sfwd_sla(UPS, PM, H, W, ups, img * 2) ? 0 : ups);
 }
 // VGPRs per lane of a forward block (fitted to the compiler's allocation):
@@ -136,7 +136,7 @@ struct SFwdCfg {
   static constexpr int RP = W == 8 ? to_mod16(TWPX * PS, 8) : TWPX * PS;
   static constexpr int IMG = FPT * ROWS * RP * 8;            // 16-bit elements per image
   static constexpr int WIMG = NS * NT * 64 * 8;
-  static constexpr int SLB = UPS ? FPT * CIN * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0;   // upsample window
+  static constexpr int SLB = UPS ? up_window_floats(CIN, FPT, RT, W) * 4 : 0;   // upsample window
   static constexpr bool SLA = sfwd_sla(UPS, PM, H, W, SLB, IMG * 2);
   static constexpr int LDS = (IMG + WIMG) * 2 * NIMG + (SLA ? 0 : SLB);   // incl. the upsample window
   // staging unit = UPX pixels x 8 channels, consecutive lanes on consecutive
@@ -835,7 +835,7 @@ constexpr int swg_lds(int CINB, int COUTB, int H, int W, int KS, bool UPS, int P
   const int TWPX = W + 2 * (KS / 2 > 0 ? 2 : 0);
   const int XPL = rup(FPT * (RT + KS - 1) * TWPX * 4 + 80, 128);
   const int stg = (CQ * XPL + COUTB * 264) * 2 * (PM == 2 ? 1 : 2) +
-                  (UPS ? FPT * CINB * (RT / 2 + 2 + (RT & 1)) * (W / 2) * 4 : 0);
+                  (UPS ? up_window_floats(CINB, FPT, RT, W) * 4 : 0);
   const int MT = ceil_div(COUTB, 16), NT = ceil_div(KS * KS * CQ, 4);
   const int red = 4 * MT * ceil_div(NT, swg_wn(MT, NT)) * 4 * 64 * 4;
   return stg > red ? stg : red;

@@ -89,6 +89,15 @@ __device__ __forceinline__ s16x4 tr_read(const short* p) {
 // window (rows y0/2 - 1 .. y0/2 + RT/2, all columns, fp32) is prefetched a
 // tile ahead into registers, parked in LDS, and the upsampled rows are formed
 // from LDS while building the 16-bit operand image.
+#ifndef PAIG_UPS_CPAD
+#define PAIG_UPS_CPAD 0   // A/B builds: floats of padding after each channel's window rows (4 measured neutral)
+#endif
+// the window's LDS floats: each channel's rows, then PAIG_UPS_CPAD floats
+// (16 B of padding moves the interpolation's reads of channels 4 apart onto
+// other banks; whole-step A/B: no change on spring / 3bp / mnist)
+constexpr int up_pitch(int RT, int W) { return (RT / 2 + 2 + (RT & 1)) * (W / 2) + PAIG_UPS_CPAD; }
+constexpr int up_window_floats(int CIN, int FPT, int RT, int W) { return FPT * CIN * up_pitch(RT, W); }
+
 template <int CIN, int H, int W, int FPT, int RT>
 struct UpStage {
   // window rows y0/2 - 1 .. : RT/2 + 2 rows for an even tile height, one more
@@ -97,7 +106,8 @@ struct UpStage {
   static constexpr int VS = WS % 4 == 0 ? 4 : 1;               // floats per load unit
   static constexpr int QS = WS / VS;
   static constexpr int NSU = FPT * CIN * SRN * QS, NLS = (NSU + 255) / 256;
-  static constexpr int SL = FPT * CIN * SRN * WS;   // floats of LDS
+  static constexpr int CP = up_pitch(RT, W);         // floats per (frame, channel)
+  static constexpr int SL = up_window_floats(CIN, FPT, RT, W);   // floats of LDS
   f32x4 v[VS == 4 ? NLS : 1];
   float v1[VS == 1 ? NLS : 1];
   __device__ __forceinline__ void issue(const FView& x, int F, int f0, int y0, int tid) {
@@ -126,10 +136,11 @@ struct UpStage {
   __device__ __forceinline__ void commit(float* Sl, int tid) const {
 #pragma unroll
     for (int l = 0; l < NLS; ++l) {
-      const int i = tid + l * 256;   // Sl is [fi][c][sr][WS]: unit i sits at VS*i
+      const int i = tid + l * 256;   // Sl is [fi][c][CP]: rows sr of WS floats, then the padding
       if (NSU % 256 != 0 && i >= NSU) break;
-      if constexpr (VS == 4) *reinterpret_cast<f32x4*>(Sl + 4 * i) = v[l];
-      else Sl[i] = v1[l];
+      const int fc = i / (QS * SRN), r = i % (QS * SRN);
+      if constexpr (VS == 4) *reinterpret_cast<f32x4*>(Sl + fc * CP + 4 * r) = v[l];
+      else Sl[fc * CP + r] = v1[l];
     }
   }
   // output pixel (row gy, column x) of channel c of frame fi (0 <= gy < H), in
@@ -139,7 +150,7 @@ struct UpStage {
     float wa, wb, ua, ub;
     up2_taps(gy, HS, ya, yb, wa, wb);
     up2_taps(x, WS, xa, xb, ua, ub);
-    const float* p = Sl + (fi * CIN + c) * SRN * WS;
+    const float* p = Sl + (fi * CIN + c) * CP;
     const float* r0 = p + (ya - (y0 / 2 - 1)) * WS;
     const float* r1 = p + (yb - (y0 / 2 - 1)) * WS;
     return wa * (ua * r0[xa] + ub * r0[xb]) + wb * (ua * r1[xa] + ub * r1[xb]);
@@ -149,7 +160,7 @@ struct UpStage {
     int ya, yb;
     float wa, wb;
     up2_taps(gy, HS, ya, yb, wa, wb);
-    const float* p = Sl + (fi * CIN + c) * SRN * WS;
+    const float* p = Sl + (fi * CIN + c) * CP;
     const float* r0 = p + (ya - (y0 / 2 - 1)) * WS;
     const float* r1 = p + (yb - (y0 / 2 - 1)) * WS;
     const int c0 = q > 0 ? 2 * q - 1 : 0, c3 = 2 * q + 2 < WS ? 2 * q + 2 : WS - 1;
@@ -179,7 +190,7 @@ struct UpStage {
       ya = ya1;
       yb = yb1;
     }
-    const float* p = Sl + (fi * CIN + c) * SRN * WS;
+    const float* p = Sl + (fi * CIN + c) * CP;
     const float* r0 = p + (ya - (y0 / 2 - 1)) * WS;
     const float* r1 = p + (yb - (y0 / 2 - 1)) * WS;
     const int c0 = q > 0 ? 2 * q - 1 : 0, c3 = 2 * q + 2 < WS ? 2 * q + 2 : WS - 1;
