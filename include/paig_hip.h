@@ -192,7 +192,10 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
  *   PAIG_UNET_STANDALONE_UP (A/B) the backward of an upsample whose consumer
  *     has separate data- and weight-gradient launches runs as its own kernel
  *     (paig_upsample2_bwd) instead of in that dgrad's epilogue (flags & 512
- *     of paig_conv2d_fwd_pw; bit-identical results).
+ *     of paig_conv2d_fwd_pw; bit-identical results);
+ *   PAIG_UNET_STANDALONE_POOL (A/B) the same for a max pool whose conv has
+ *     separate data- and weight-gradient launches (paig_maxpool2_bwd_relu
+ *     instead of the fold in paig_conv2d_wgrad_pf / the dgrad's staging).
  * The workspace layout depends on the flags (the same flags for the query,
  * the forward and its backward).  probe (nullable) is called on the host
  * around every conv launch (event 0 before, 1 after; kind PAIG_PROBE_*; the
@@ -205,6 +208,7 @@ int paig_unet_bwd(int net, int F, int H, int K, int math, const float* x, long l
 #define PAIG_UNET_INFERENCE 4
 #define PAIG_UNET_EXT_WPREP 8
 #define PAIG_UNET_STANDALONE_UP 16
+#define PAIG_UNET_STANDALONE_POOL 32
 #define PAIG_PROBE_CONV_FWD 0
 #define PAIG_PROBE_CONV_BWD 1
 #define PAIG_PROBE_CONV_WGRAD 2
@@ -227,6 +231,21 @@ int paig_unet_bwd_ex(int net, int F, int H, int K, int math, int flags, const fl
                      float* const* dwb, int n_extra, const float* const* extra_src, const int* extra_nblk,
                      const int* extra_len, float* const* extra_dst, const void* const* wprep_dg, void* ws,
                      size_t ws_bytes, paig_unet_probe_fn probe, void* probe_ctx, void* stream);
+
+/* paig_conv2d_wgrad_ex of a layer whose output (ReLU'd) a 2x2 max pool also
+ * read (the UNet's c4 / c6, blocks.py:186-197), with the pool's backward
+ * folded into the dY staging: dY = ReLU'(y) * (dy + dpool at each window's
+ * argmax), from the window codes the forward's fused pool wrote
+ * (paig_conv2d_fwd_pwc: the same bytes and layout); dy is the skip path's
+ * gradient, unmasked.  flags: 64 | 128 (+ the usual), shapes for which
+ * paig_conv2d_mfma_supported(1, .., 64 | 128) says 1.  The matching data
+ * gradient is paig_conv2d_fwd_pwc with flags 8 | 64 | 128, pool_out = dpool
+ * and pool_code = the codes.  Both are bit-identical to paig_maxpool2_bwd_relu
+ * followed by the plain kernels. */
+int paig_conv2d_wgrad_pf(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
+                         const float* dpool, long long dpool_fs, const unsigned char* pcode, long long pcode_fs,
+                         float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
+                         int flags, const float* xmax, int xmax_n, void* stream);
 
 /* ---- U-Net glue: max_pool2d (blocks.py:250,254), Resize bilinear (:260,269) */
 int paig_maxpool2_fwd(const float* x, long long x_fs, float* y, long long y_fs, int F, int C, int H, int W,

@@ -38,6 +38,7 @@ SIGNATURES = {
     "paig_conv_wprep_size": (LL, [I, I, I]),
     "paig_conv_wprep": (I, [I, P, P, P, P, P, P, P]),
     "paig_conv2d_wgrad_ex": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
+    "paig_conv2d_wgrad_pf": (I, [P, LL, I, LL, P, LL, P, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
     "paig_conv2d_bwd_supported": (I, [I, I, I, I, I, I]),
     "paig_conv2d_bwd": (I, [P, LL, I, LL, P, LL, P, LL, P, LL, P, P, I, P, I, I, I, I, I, I, I, P, I, P, LL, P, LL,

@@ -286,5 +286,6 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
                         int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr,
                         PoolOut pout = PoolOut{nullptr, 0, nullptr, 0});
 int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout,
-                          int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm);
+                          int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm,
+                          PoolOut pin = PoolOut{nullptr, 0, nullptr, 0});
 int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags);

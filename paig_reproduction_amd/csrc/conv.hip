@@ -470,4 +470,21 @@ int paig_conv2d_wgrad_ex(const float* x, long long x_fs, int x_grp, long long x_
   return PAIG_E_UNSUPPORTED;
 }
 
+int paig_conv2d_wgrad_pf(const float* x, long long x_fs, int x_grp, long long x_gs, const float* dy, long long dy_fs,
+                         const float* dpool, long long dpool_fs, const unsigned char* pcode, long long pcode_fs,
+                         float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout, int H, int W, int ks,
+                         int flags, const float* xmax, int xmax_n, void* stream) {
+  *nblk_out = 0;
+  if (F <= 0) return 0;
+  PAIG_REQUIRE((flags & 64) && (flags & 128) && dpool && pcode,
+               "paig_conv2d_wgrad_pf: needs flags 64 | 128, the pooled gradient and the window codes");
+  int rc = 0;
+  if (paig_conv_split_wgrad(FView{x, x_fs, x_gs, x_grp}, FView{dy, dy_fs, 0, 0}, slab, nblk_max, nblk_out, F, Cin, Cout,
+                            H, W, ks, flags, (hipStream_t)stream, &rc, XMax{const_cast<float*>(xmax), xmax_n},
+                            PoolOut{const_cast<float*>(dpool), dpool_fs, const_cast<unsigned char*>(pcode), pcode_fs}))
+    return rc;
+  paig_set_error("paig_conv2d_wgrad_pf: no pool-fold instantiation for Cin=%d Cout=%d H=%d", Cin, Cout, H);
+  return PAIG_E_UNSUPPORTED;
+}
+
 }  // extern "C"

@@ -201,11 +201,19 @@ __device__ __forceinline__ int fwd_mtile(int wv, int mt) {
 // tile to the next; out / aux are the source's gradient and its ReLU' input
 // (H/2 x W/2 planes).  Same operation order as upsample_bwd_v_k on the
 // dgrad's output: bit-identical to the two-launch form.
-template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false, bool UPT = false>
+// PF (dgrad only): the input dY is the gradient of a ReLU'd output that a 2x2
+// max pool also read (the UNet's c4 / c6): the pool's backward is folded into
+// the staging -- dY = ReLU'(y) * (dy + the pooled gradient at each window's
+// argmax), from pout = (the pooled gradient, the forward's window codes), in
+// maxpool_bwd_relu's arithmetic (conv_bwd.hip's fold)
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false, bool UPT = false,
+          bool PF = false>
 __global__ void __launch_bounds__(256, 2)
 conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
                  int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp, PoolOut pout) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
+  static_assert(!PF || (DG && !UPS && !POOL && !UPT && C::UPX == 2 && H % 2 == 0 && CIN % 8 == 0),
+                "pool fold: dgrad staging units of one window's pixel pair");
   static_assert(!UPT || (DG && !UPS && !POOL && C::FPT == 1 && C::RT % 2 == 0 && C::VEC4 && W % 2 == 0),
                 "transposed-upsample epilogue: dgrad tiles of whole row pairs");
   constexpr int KK = C::KK, CC = C::CC, KC = C::KC, NS = C::NS, NT = C::NT, MW = C::MW;
@@ -339,6 +347,9 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     }
   };
   float2 pre[UPS ? 1 : NL][8];
+  // PF: each staging unit's window (8 channels): pooled gradients and codes
+  float dpv[PF ? NL : 1][8];
+  uint2 pcv[PF ? NL : 1];
   UP up;
   // f16 pieces (PM 0): the operand image (activations, or dgrad's gradients:
   // any magnitude) is scaled per tile by one power of two from the tile's
@@ -380,6 +391,38 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
           // channels past CIN (CIN % 8 != 0 only) read a zero of their own
           const float* q = CIN % 8 == 0 || cc * 8 + c < CIN ? base + c * (int)PLANE : paig_zeros;
           pre[l][c] = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
+        }
+        if constexpr (PF) {
+          constexpr int HP = H / 2, WP = W / 2;
+          const int pw = (gy >> 1) * WP + (xp >> 1);
+          const float* pb = ok ? pout.frame(f0) + fi * (int)pout.fs + cc * 8 * (HP * WP) + pw : paig_zero_planes;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) dpv[l][c] = pb[c * (HP * WP)];
+          const unsigned char* cb = ok ? pout.code + (long long)(f0 + fi) * pout.code_fs + ((long long)cc * HP * WP + pw) * 8
+                                       : reinterpret_cast<const unsigned char*>(paig_zeros);
+          pcv[l] = *reinterpret_cast<const uint2*>(cb);
+        }
+      }
+    }
+  };
+  // PF: the max pool's backward on the prefetched units of tile t (before
+  // their max and staging)
+  auto fold = [&](int t) {
+    if constexpr (PF) {
+      const int y0 = (t % NRB) * RT;
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        const int i = tid + l * 256;
+        const int r = (i / W2) % ROWS;
+        const int pr = ((y0 + r - PADL) & 1) * 2;   // window row of this unit: bits pr, pr + 1
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const unsigned b = ((c < 4 ? pcv[l].x : pcv[l].y) >> (8 * (c & 3))) & 255u;
+          const int am = (int)(b >> 4) & 3;
+          const float vx = pre[l][c].x + (am == pr ? dpv[l][c] : 0.f);
+          const float vy = pre[l][c].y + (am == pr + 1 ? dpv[l][c] : 0.f);
+          pre[l][c].x = (b >> pr) & 1u ? vx : 0.f;
+          pre[l][c].y = (b >> (pr + 1)) & 1u ? vy : 0.f;
         }
       }
     }
@@ -680,6 +723,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
     const int tile = tile_of(lt);
     if (tile >= ntiles) break;
     const int f0 = (tile / NRB) * FPT, y0 = (tile % NRB) * RT;
+    fold(tile);
     if constexpr (DYN) tile_max();
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
@@ -932,10 +976,16 @@ struct SWgCfg {
   static_assert(TPXV % DU == 0, "dY units");
 };
 
-template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
+// PF: dY is the gradient of a ReLU'd output that a 2x2 max pool also read
+// (the UNet's c4 / c6, blocks.py:186-197): the pool's backward is folded into
+// the dY staging -- dY = ReLU'(y) * (dy + the pooled gradient pin at each
+// window's argmax), from the window codes the forward's fused pool wrote
+// (paig_conv2d_fwd_pwc), in maxpool_bwd_relu's arithmetic
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM, bool PF = false>
 __global__ void __launch_bounds__(256, (SWgCfg<CIN, COUT, H, W, KS, UPS, PM>::MINW))
-conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int ntiles, XMax xm) {
+conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int ntiles, XMax xm, PoolOut pin) {
   using C = SWgCfg<CIN, COUT, H, W, KS, UPS, PM>;
+  static_assert(!PF || (!UPS && C::DU == 4 && C::FPT == 1 && W % 4 == 0 && H % 2 == 0), "pool fold: 4-pixel dY units");
   constexpr int CINB = C::CINB, COUTB = C::COUTB;
   constexpr int KK = C::KK, CQ = C::CQ, NQ = C::NQ, NT = C::NT, NCOL = C::NCOL, MT = C::MT, COP = C::COP;
   constexpr int WN = C::WN, WP = C::WP, NTW = C::NTW, RT = C::RT, FPT = C::FPT, ROWS = C::ROWS;
@@ -1103,6 +1153,42 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
   };
   constexpr bool DPIPE = XPIPE || UPS || NLD * 4 <= 16;
   f32x4 sd[DPIPE ? NLD : 1];
+  // PF: each dY unit's two windows: pooled gradients and code bytes
+  constexpr int HPL = H / 2, WPL = W / 2;   // the pooled plane
+  float2 pdp[PF ? NLD : 1];
+  unsigned pcd[PF ? NLD : 1];
+  auto load_pf = [&](int t, int l) {
+    if constexpr (PF) {
+      const int f0 = t / NRB, y0 = (t % NRB) * RT;
+      const int i = tid + l * 256;
+      const int co = i / NPU, pt = DU * (i % NPU);
+      const int y = y0 + pt / W, xx = pt % W;
+      const bool ok = i < NID && f0 < F;
+      const int pw = (y >> 1) * WPL + (xx >> 1), c = co0 + co;
+      const float* pp = ok ? pin.frame(f0) + (long long)c * (HPL * WPL) + pw : paig_zeros;
+      pdp[l] = *reinterpret_cast<const float2*>(pp);
+      const unsigned char* cb = ok ? pin.code + (long long)f0 * pin.code_fs + ((long long)(c >> 3) * (HPL * WPL) + pw) * 8 + (c & 7)
+                                   : reinterpret_cast<const unsigned char*>(paig_zeros);
+      pcd[l] = (unsigned)cb[0] | ((unsigned)cb[8] << 8);
+    }
+  };
+  // dY unit l of tile t := ReLU'(y) * (dy + pooled gradient at the argmax)
+  auto fold = [&](int t, int l, f32x4& v) {
+    if constexpr (PF) {
+      const int i = tid + l * 256;
+      const int pr = ((((t % NRB) * RT) + (DU * (i % NPU)) / W) & 1) * 2;   // window row bits pr, pr + 1
+#pragma unroll
+      for (int w2 = 0; w2 < 2; ++w2) {
+        const unsigned b = (pcd[l] >> (8 * w2)) & 255u;
+        const int am = (int)(b >> 4) & 3;
+        const float g = w2 ? pdp[l].y : pdp[l].x;
+        const float vx = v[2 * w2] + (am == pr ? g : 0.f);
+        const float vy = v[2 * w2 + 1] + (am == pr + 1 ? g : 0.f);
+        v[2 * w2] = (b >> pr) & 1u ? vx : 0.f;
+        v[2 * w2 + 1] = (b >> (pr + 1)) & 1u ? vy : 0.f;
+      }
+    }
+  };
   auto issue = [&](int t) {
     if constexpr (UPS) {
       up.issue(x, F, (t / NRB) * FPT, (t % NRB) * RT, tid);
@@ -1112,7 +1198,17 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
     }
     if constexpr (DPIPE) {
 #pragma unroll
-      for (int l = 0; l < NLD; ++l) sd[l] = load_d(t, l);
+      for (int l = 0; l < NLD; ++l) {
+        sd[l] = load_d(t, l);
+        load_pf(t, l);
+      }
+    }
+  };
+  // PF with prefetched dY: fold the tile before its max and staging
+  auto fold_all = [&](int t) {
+    if constexpr (PF && DPIPE) {
+#pragma unroll
+      for (int l = 0; l < NLD; ++l) fold(t, l, sd[l]);
     }
   };
   // PM 0 dY exponent.  dY held in registers before the barrier (prefetched)
@@ -1143,8 +1239,13 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
       if (NID % 256 != 0 && i >= NID) break;
       const int co = i / NPU, pt = DU * (i % NPU);
       f32x4 dv;
-      if constexpr (DPIPE) dv = sd[l];
-      else dv = load_d(t, l);
+      if constexpr (DPIPE) {
+        dv = sd[l];
+      } else {
+        dv = load_d(t, l);
+        load_pf(t, l);
+        fold(t, l, dv);
+      }
       if (first) bacc[l] += (dv[0] + dv[1]) + (dv[2] + dv[3]);   // zeros past DU; unscaled
       s16x4 hv, lv;
       if constexpr (PM == 0) {
@@ -1293,6 +1394,7 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
   xsc = __builtin_amdgcn_ldexpf(1.f, ecx);
   for (int lt = blockIdx.x; lt < ntiles; lt += gridDim.x) {
     const int tile = xcd_tile(lt, ntiles);
+    fold_all(tile);
     if constexpr (PM == 0 && PAIG_SCALE_MODE < 2) tile_max(tile);
     __syncthreads();   // previous tile's fragment reads are done
     commit(tile);
@@ -1399,7 +1501,7 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
   if constexpr (PM == 0) f16_range_note(rmax);
 }
 
-template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool UPT = false>
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool UPT = false, bool PF = false>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
                        hipStream_t st, XMax xm, const void* wp, PoolOut pout) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
@@ -1409,7 +1511,8 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
   // the fused-pool variant (its own instantiation: keeping the stored tile
   // live for the pool costs ~20 VGPRs, which the other launches must not pay)
   constexpr bool POOLABLE = C::POOLOK && !DG;
-  auto k = UPT ? conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, false, UPT>
+  auto k = PF ? conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, false, false, PF>
+         : UPT ? conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, false, UPT>
               : (POOLABLE && (flags & 64)) ? conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, POOLABLE>
                                            : conv_fwd_split_k<CIN, COUT, H, W, KS, DG, UPS, PM, false>;
   static int resident[2] = {0, 0};
@@ -1429,20 +1532,23 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
   if (nb < 1) nb = 1;
   if (PM != 0 || DG) xm.p = nullptr;
   PAIG_REQUIRE(!xm.p || nb <= xm.n, "conv split fwd: %d blocks need more than %d xmax slots", nb, xm.n);
-  if (flags & 64) PAIG_REQUIRE(C::POOLOK && pout.p, "conv split fwd: no fused pool for Cin=%d Cout=%d H=%d", CIN, COUT, H);
+  if (PF) PAIG_REQUIRE(pout.p && pout.code, "conv split dgrad: the pool fold needs the pooled gradient and codes");
+  else if (flags & 64) PAIG_REQUIRE(C::POOLOK && pout.p, "conv split fwd: no fused pool for Cin=%d Cout=%d H=%d", CIN, COUT, H);
   hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles, xm,
                      PM == 0 ? static_cast<const s16x8*>(wp) : nullptr, pout);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
 
-template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM>
-static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st, XMax xm) {
+template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM, bool PF = false>
+static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st, XMax xm,
+                      PoolOut pin = PoolOut{nullptr, 0, nullptr, 0}) {
   using C = SWgCfg<CIN, COUT, H, W, KS, UPS, PM>;
   constexpr int STG = C::STG + (UPS ? UpStage<C::CINB, H, W, C::FPT, C::RT>::SL * 4 : 0);
   constexpr int LDS = STG > C::RED ? STG : C::RED;
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
-  auto k = conv_wgrad_split_k<CIN, COUT, H, W, KS, UPS, PM>;
+  auto k = conv_wgrad_split_k<CIN, COUT, H, W, KS, UPS, PM, PF>;
+  if constexpr (PF) PAIG_REQUIRE(pin.p && pin.code, "conv split wgrad: the pool fold needs the pooled gradient and codes");
   static int resident = 0;
   if (!resident) {
     if (LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -1456,7 +1562,7 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
   *nblk_out = nb;
   PAIG_REQUIRE(!xm.p || (xm.n % 4 == 0 && (reinterpret_cast<uintptr_t>(xm.p) & 15) == 0),
                "conv split wgrad: xmax needs 16-byte alignment and a multiple of 4 slots (%d)", xm.n);
-  hipLaunchKernelGGL(k, dim3(nb, C::NSI, C::NSO), dim3(256), LDS, st, x, dy, slab, F, ntiles, xm);
+  hipLaunchKernelGGL(k, dim3(nb, C::NSI, C::NSO), dim3(256), LDS, st, x, dy, slab, F, ntiles, xm, pin);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -1476,6 +1582,12 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
 #define PAIG_SPLIT_UP(X)                                                                                  \
   X(32, 16, 16, 3) X(16, 16, 32, 3) X(32, 16, 18, 3) X(16, 16, 36, 3) X(128, 32, 16, 3) X(64, 32, 32, 3) \
   X(32, 32, 64, 3)
+// UNet convs whose output's max pool is folded into their separate weight
+// gradient's dY staging and their data gradient's input staging (flags & 64;
+// c4: too wide for the fused layer backward): (Cin, Cout) of the layer.  c6
+// (64 -> 64 @ 16^2) keeps the standalone pool backward: its folding dgrad
+// spills 32 VGPRs (the plain one already takes 240)
+#define PAIG_SPLIT_PF(X) X(32, 32, 32, 3)
 // dgrad shapes (layer Cout, layer Cin) of the UNet convs whose input is the
 // 2x upsample (c9, c12, c15) with the transposed-upsample epilogue (UPT)
 #define PAIG_SPLIT_UPT(X) X(32, 128, 16, 3) X(32, 64, 32, 3) X(32, 32, 64, 3)
@@ -1510,6 +1622,17 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
   const int fl = flags & (7 | 64);
   if (H != W || !(flags & (128 | 256))) return 0;
   if (in.grp > 0 && H * W < 256) return 0;   // multi-frame tiles step frames by a plain stride
+  if (dg && (flags & 64)) {   // dgrad with the output max pool's backward folded into its input staging (PF)
+    if (up || b16 || (flags & 512)) return 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                                          \
+    if (Cin == CO && Cout == CI && H == HH && ks == K) {                                                  \
+      *rc = sfwd_launch<CO, CI, HH, HH, K, true, false, 0, false, true>(in, out, aux, w, b, F, fl & 7, st, xm, wp, pout); \
+      return 1;                                                                                           \
+    }
+    PAIG_SPLIT_PF(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
   if (flags & 512) {   // dgrad writing the transposed upsample of dX (UPT)
     if (!dg || up || b16 || (flags & (4 | 64))) return 0;
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
@@ -1549,10 +1672,21 @@ int paig_conv_split_fwd(FView in, FViewW out, FView aux, const float* w, const f
 }
 
 int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, int Cin, int Cout,
-                          int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm) {
+                          int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, PoolOut pin) {
   const bool up = (flags & 32) != 0, b16 = (flags & 256) != 0;
   if (H != W || !(flags & (128 | 256))) return 0;
   if (x.grp > 0 && H * W < 256) return 0;   // multi-frame tiles step frames by a plain stride
+  if (flags & 64) {   // the 2x2 max pool of the layer's output folded into the dY staging
+    if (up || b16) return 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                                          \
+    if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
+      *rc = swg_launch<CI, CO, HH, HH, K, false, 0, true>(x, dy, slab, nblk_max, nblk_out, F, st, xm, pin);  \
+      return 1;                                                                                           \
+    }
+    PAIG_SPLIT_PF(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
   if (up) {
 #define PAIG_CASE(CI, CO, HH, K)                                                                          \
     if (Cin == CI && Cout == CO && H == HH && ks == K) {                                                  \
@@ -1579,6 +1713,16 @@ int paig_conv_split_wgrad(FView x, FView dy, float* slab, int nblk_max, int* nbl
 int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags) {
   if (H != W) return 0;
   const bool up = (flags & 32) != 0, dg = (flags & 8) != 0;
+  if ((flags & 64) && (what == 1 || dg)) {   // the output max pool's backward folded (wgrad / dgrad staging)
+    if (up || !(flags & 128) || (flags & (256 | 512))) return 0;
+#define PAIG_CASE(CI, CO, HH, K)                                                                         \
+    if (what == 1 ? (Cin == CI && Cout == CO) : (Cin == CO && Cout == CI)) {                             \
+      if (H == HH && ks == K) return 1;                                                                  \
+    }
+    PAIG_SPLIT_PF(PAIG_CASE)
+#undef PAIG_CASE
+    return 0;
+  }
   if (flags & 64) {   // forward with the fused 2x2 max pool of its output
     if (what != 0 || up || dg || !(flags & (128 | 256))) return 0;
     const bool b16 = (flags & 256) != 0;

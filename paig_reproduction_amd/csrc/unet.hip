@@ -175,6 +175,22 @@ bool pool_fused(const UPlan& p, int i, int H, int cm) {
   return nx.kind == U_POOL && nx.src == op.dst &&
          paig_conv2d_mfma_supported(0, op.src.n, op.dst.n, Hl, Hl, op.ks, cm | 64);
 }
+// the pool's backward folded into the fused layer backward's dY staging, or
+// (layers too wide for it: the UNet's c4) into the separate weight gradient's
+// and data gradient's staging (paig_conv2d_wgrad_pf, paig_conv2d_fwd_pwc
+// flags 8 | 64)
+bool pool_fold_fused(const UPlan& p, int i, int H, int cm) {
+  const UOp& op = p.ops[i];
+  const int Hl = H / p.bufs[op.dst.buf].lvl;
+  return paig_conv2d_bwd_supported(op.src.n, op.dst.n, Hl, Hl, op.ks, cm | 64);
+}
+bool pool_fold_split(const UPlan& p, int i, int H, int cm, int flags) {
+  const UOp& op = p.ops[i];
+  const int Hl = H / p.bufs[op.dst.buf].lvl;
+  return cm == 128 && !(flags & PAIG_UNET_STANDALONE_POOL) && op.src.buf != p.X0 && !pool_fold_fused(p, i, H, cm) &&
+         paig_conv2d_mfma_supported(1, op.src.n, op.dst.n, Hl, Hl, op.ks, 128 | 64) &&
+         paig_conv2d_mfma_supported(0, op.dst.n, op.src.n, Hl, Hl, op.ks, 8 | 128 | 64);
+}
 // (the codes come from the fused pool, or from the standalone pool where the
 // forward cannot fuse it: paig_maxpool2_fwd_codes)
 bool pool_folded(const UPlan& p, int i, int H, int cm, int flags) {
@@ -183,8 +199,7 @@ bool pool_folded(const UPlan& p, int i, int H, int cm, int flags) {
   if (op.kind != U_CONV || i + 1 >= (int)p.ops.size() || cm == 0 || p.fused_up[i] >= 0) return false;
   const UOp& nx = p.ops[i + 1];
   const int Hl = H / p.bufs[op.dst.buf].lvl;
-  return nx.kind == U_POOL && nx.src == op.dst &&
-         paig_conv2d_bwd_supported(op.src.n, op.dst.n, Hl, Hl, op.ks, cm | 64);
+  return nx.kind == U_POOL && nx.src == op.dst && (pool_fold_fused(p, i, H, cm) || pool_fold_split(p, i, H, cm, flags));
 }
 
 constexpr int NBLK_MAX = 1024;   // slab rows per conv (engine.py: nblk_max)
@@ -528,12 +543,30 @@ int bwd_impl(int net, int F, int H, int K, int math, int flags, const float* x, 
         mark(op.src);
         continue;
       }
-      pr(0, i, op.conv, PAIG_PROBE_CONV_WGRAD, cin, cout, Hl, xfl | cm);
-      rc = paig_conv2d_wgrad_ex(sv.p, sv.fs, sv.grp, sv.gs, dyv.p, dyv.fs, slab, NBLK_MAX, &nb, F, cin, cout, Hl, Hl,
-                                ks, xfl | cm, xm, PAIG_XMAX_SLOTS, stream);
-      pr(1, i, op.conv, PAIG_PROBE_CONV_WGRAD, cin, cout, Hl, xfl | cm);
+      // the max pool of this output folded into both launches' dY staging
+      // (pool_fold_split): the pooled gradient and the forward's codes
+      const bool pf = !xfl && i + 1 < no && L.pcode[i + 1] != (size_t)-1;
+      const float* dpool = nullptr;
+      long long dpool_fs = 0;
+      const unsigned char* pcode = nullptr;
+      long long pcode_fs = 0;
+      if (pf) {
+        PAIG_REQUIRE(state(op.dst) == 1, "paig_unet_bwd: pool fold before the skip gradient (op %d)", i);
+        const View pdv = dview(p.ops[i + 1].dst);
+        dpool = pdv.p;
+        dpool_fs = pdv.fs;
+        pcode = reinterpret_cast<const unsigned char*>(base + L.pcode[i + 1]);
+        pcode_fs = L.pcode_fs[i + 1];
+      }
+      pr(0, i, op.conv, PAIG_PROBE_CONV_WGRAD, cin, cout, Hl, xfl | cm | (pf ? 64 : 0));
+      rc = pf ? paig_conv2d_wgrad_pf(sv.p, sv.fs, sv.grp, sv.gs, dyv.p, dyv.fs, dpool, dpool_fs, pcode, pcode_fs, slab,
+                                     NBLK_MAX, &nb, F, cin, cout, Hl, Hl, ks, cm | 64, xm, PAIG_XMAX_SLOTS, stream)
+              : paig_conv2d_wgrad_ex(sv.p, sv.fs, sv.grp, sv.gs, dyv.p, dyv.fs, slab, NBLK_MAX, &nb, F, cin, cout, Hl, Hl,
+                                     ks, xfl | cm, xm, PAIG_XMAX_SLOTS, stream);
+      pr(1, i, op.conv, PAIG_PROBE_CONV_WGRAD, cin, cout, Hl, xfl | cm | (pf ? 64 : 0));
       if (rc) return rc;
       s_src.push_back(slab), s_nb.push_back(nb), s_len.push_back(n_w + cout), s_dst.push_back(dwb[op.conv]);
+      PAIG_REQUIRE(!pf || op.src.buf != p.X0, "paig_unet_bwd: pool fold on the input layer (op %d)", i);
       if (op.src.buf == p.X0) continue;   // no input gradient (Q10)
       const int ui = p.fused_up[i];
       if (ui >= 0 && cm == 128 && !(flags & PAIG_UNET_STANDALONE_UP) &&
@@ -575,9 +608,11 @@ int bwd_impl(int net, int F, int H, int K, int math, int flags, const float* x, 
         aux_fs = a.fs;
         flags2 |= 2;
       }
+      if (pf) flags2 |= 64;
       pr(0, i, op.conv, PAIG_PROBE_CONV_DGRAD, cin, cout, Hl, flags2 | cm);
-      rc = paig_conv2d_fwd_pw(dyv.p, dyv.fs, 0, 0, const_cast<float*>(dxv.p), dxv.fs, aux, aux_fs, w[op.conv], nullptr,
-                              F, cout, cin, Hl, Hl, ks, flags2 | cm, nullptr, 0, nullptr, 0, wp1, stream);
+      rc = paig_conv2d_fwd_pwc(dyv.p, dyv.fs, 0, 0, const_cast<float*>(dxv.p), dxv.fs, aux, aux_fs, w[op.conv], nullptr,
+                               F, cout, cin, Hl, Hl, ks, flags2 | cm, nullptr, 0, const_cast<float*>(dpool), dpool_fs,
+                               const_cast<unsigned char*>(pcode), pcode_fs, wp1, stream);
       pr(1, i, op.conv, PAIG_PROBE_CONV_DGRAD, cin, cout, Hl, flags2 | cm);
       mark(op.src);
     } else if (op.kind == U_POOL) {

@@ -478,7 +478,8 @@ class Engine:
         cm = S["cm"]
         flags = ((1 if fuse_head else 0) | (0 if S.get("need_saved", True) else 4) |
                  (2 if os.environ.get("PAIG_FUSED_BWD", "1") == "0" else 0) |
-                 (16 if os.environ.get("PAIG_UPT", "1") == "0" else 0))   # A/B: standalone upsample backward
+                 (16 if os.environ.get("PAIG_UPT", "1") == "0" else 0) |   # A/B: standalone upsample backward
+                 (32 if os.environ.get("PAIG_POOL_FOLD", "1") == "0" else 0))   # A/B: standalone pool backward
         Ws = [self.p(lay.prefix + f"c{c + 1}.weight") for c in range(lay.nconv)]
         Bs = [self.p(lay.prefix + f"c{c + 1}.bias") for c in range(lay.nconv)]
         # split path: every conv's forward and dgrad weight images (and the

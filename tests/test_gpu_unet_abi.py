@@ -83,13 +83,18 @@ def test_unet_abi_rejects_bad_arguments():
                         x.data_ptr(), x.data_ptr(), 16, torch.cuda.current_stream().cuda_stream)
 
 
+@pytest.mark.parametrize("alt", [16, 32])
 @pytest.mark.parametrize("N", [3, 40])
-def test_unet_upsample_backward_in_dgrad_epilogue_is_bit_identical(N):
-    """The UNet's c9 / c12 / c15 data gradients with the upsample's backward
-    in their epilogue (paig_conv2d_fwd_pw flags & 512, the default) against
-    the same dgrads followed by paig_upsample2_bwd (PAIG_UNET_STANDALONE_UP):
-    every conv's weight and bias gradient bit-identical (c1 .. c14 see the
-    upsample sources' gradients).  Reference: blocks.py:206,219,229."""
+def test_unet_upsample_backward_in_dgrad_epilogue_is_bit_identical(N, alt):
+    """alt 16: the UNet's c9 / c12 / c15 data gradients with the upsample's
+    backward in their epilogue (paig_conv2d_fwd_pw flags & 512, the default)
+    against the same dgrads followed by paig_upsample2_bwd
+    (PAIG_UNET_STANDALONE_UP); alt 32: c4's separate weight and data
+    gradients with pool2's backward folded into their dY staging
+    (paig_conv2d_wgrad_pf, the dgrad's flags 8 | 64) against
+    paig_maxpool2_bwd_relu then the plain kernels (PAIG_UNET_STANDALONE_POOL).
+    Every conv's weight and bias gradient bit-identical.  Reference:
+    blocks.py:186-197 (pools), 206,219,229 (upsamples)."""
     from paig_reproduction_amd._lib import lib
     L = lib()
     H, K, net, nconv, math = 64, 2, 1, 18, 128
@@ -103,7 +108,7 @@ def test_unet_upsample_backward_in_dgrad_epilogue_is_bit_identical(N):
     x = torch.rand(N, 3, H, H, device=DEV)
     st = torch.cuda.current_stream().cuda_stream
     out = {}
-    for flags in (0, 16):
+    for flags in (0, alt):
         nbytes = int(L.paig_unet_workspace_ex(net, N, H, K, math, flags))
         ws = torch.empty(nbytes // 4 + 1, device=DEV)
         lg = torch.empty(N, K, H, H, device=DEV)
@@ -119,9 +124,9 @@ def test_unet_upsample_backward_in_dgrad_epilogue_is_bit_identical(N):
                            None, None, st)
         torch.cuda.synchronize()
         out[flags] = (lg.clone(), dwb)
-    assert torch.equal(out[0][0], out[16][0])
+    assert torch.equal(out[0][0], out[alt][0])
     for i in range(nconv):
-        a, b = out[0][1][i], out[16][1][i]
+        a, b = out[0][1][i], out[alt][1][i]
         assert torch.isfinite(a).all(), f"c{i + 1}"
         assert torch.equal(a, b), f"c{i + 1}: max |d| {(a - b).abs().max().item():.3e}"
 
