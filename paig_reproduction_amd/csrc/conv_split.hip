@@ -95,8 +95,13 @@ constexpr int sfwd_vgprs(int CIN, int H, int W, int KS, bool UPS, int tpxm, int 
 #ifndef PAIG_FWD_UPS_TP
 #define PAIG_FWD_UPS_TP 256   // A/B builds: the largest tile of the sub-64x64 fused-upsample forwards
 #endif
+#ifndef PAIG_FWD_TP32
+#define PAIG_FWD_TP32 256     // A/B builds: the largest tile of the 32x32 forwards / dgrads (no upsample)
+#endif
 constexpr int sfwd_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM) {
-  const int base = UPS && H * W < 4096 && PAIG_FWD_UPS_TP < 256 ? PAIG_FWD_UPS_TP : (W == 8 ? 128 : 256);
+  const int base = UPS && H * W < 4096 && PAIG_FWD_UPS_TP < 256   ? PAIG_FWD_UPS_TP
+                   : !UPS && H * W == 1024 && PAIG_FWD_TP32 < 256 ? PAIG_FWD_TP32
+                                                                  : (W == 8 ? 128 : 256);
   const int NT = ceil_div(COUT, 16);
   for (int pass = UPS && !(PM == 0 && H * W >= 4096) ? 1 : 0; pass < 3; ++pass)
     for (int nb = 1; nb <= NT; ++nb) {
