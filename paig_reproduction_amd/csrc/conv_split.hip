@@ -875,16 +875,25 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
 #define PAIG_WG_UPS_OB 32
 #endif
 
+#ifndef PAIG_WG_SLA
+#define PAIG_WG_SLA 0   // A/B builds: 1 = the 64x64 fused-upsample wgrad's window in the lo X image's LDS,
+#endif                  // two blocks per CU on 16-channel output slices (mnist within noise: 18.63 vs 18.66 ms)
 // waves splitting the N-tiles: as few as keep <= 40 accumulators per lane
 constexpr int swg_wn(int MT, int NT) { return MT * NT * 4 <= 40 ? 1 : (MT * ceil_div(NT, 2) * 4 <= 40 ? 2 : 4); }
+// the fused-upsample window in the lo X image's LDS (as the forward's SLA):
+// 64 x 64 layers (mnist c15), two blocks per CU on 16-output-channel slices
+constexpr bool swg_sla(bool UPS, int PM, int H, int W, int win_bytes, int xlo_bytes) {
+  return PAIG_WG_SLA && UPS && PM == 0 && H * W >= 4096 && win_bytes <= xlo_bytes;
+}
 // LDS of a wgrad block staging CINB input and COUTB output-gradient channels
 constexpr int swg_lds(int CINB, int COUTB, int H, int W, int KS, bool UPS, int PM) {
   const int CQ = rup(CINB, 4) / 4, FPT = H * W <= 256 ? 256 / (H * W) : 1;
   const int RT = H * W <= 256 ? H : rows_fit(H, W, 256);
   const int TWPX = W + 2 * (KS / 2 > 0 ? 2 : 0);
   const int XPL = rup(FPT * (RT + KS - 1) * TWPX * 4 + 80, 128);
+  const int win = UPS ? up_window_floats(CINB, FPT, RT, W) * 4 : 0;
   const int stg = (CQ * XPL + COUTB * 264) * 2 * (PM == 2 ? 1 : 2) +
-                  (UPS ? up_window_floats(CINB, FPT, RT, W) * 4 : 0);
+                  (swg_sla(UPS, PM, H, W, win, CQ * XPL * 2) ? 0 : win);
   const int MT = ceil_div(COUTB, 16), NT = ceil_div(KS * KS * CQ, 4);
   const int red = 4 * MT * ceil_div(NT, swg_wn(MT, NT)) * 4 * 64 * 4;
   return stg > red ? stg : red;
@@ -897,7 +906,7 @@ constexpr int swg_pick(int CIN, int COUT, int H, int W, int KS, bool UPS, int PM
   const int ci[] = {CIN, 128, 64, 32, 16, 8}, oc[] = {COUT, 128, 64, 32, 16};
   // pass 0: two blocks per CU (see sfwd_pick; not for the 64 x 64 fused
   // upsample, whose halved channel slices measured 4% slower)
-  for (int pass = UPS && H * W >= 4096 ? 1 : 0; pass < 2; ++pass) {
+  for (int pass = UPS && H * W >= 4096 && !(PM == 0 && PAIG_WG_SLA) ? 1 : 0; pass < 2; ++pass) {
     int best = 0, bw = 0, bs = 0;
     for (int cb : ci) {
       if (cb > CIN || CIN % cb != 0 || (cb != CIN && cb % 4 != 0)) continue;
@@ -959,6 +968,7 @@ struct SWgCfg {
   static constexpr int DP = TPX + 8;                          // dY row pitch: 16 rows -> 16 bank groups
   static constexpr int DIMG = COUTB * DP;   // rows co >= COUTB of an A fragment re-read rows co % COUTB
   static constexpr int STG = (XIMG + DIMG) * 2 * NIMG;
+  static constexpr bool SLA = swg_sla(UPS, PM, H, W, UPS ? up_window_floats(CINB, FPT, RT, W) * 4 : 0, XIMG * 2);
   static constexpr int RED = 4 * MT * NTW * 4 * 64 * 4;
   static constexpr int LDS = STG > RED ? STG : RED;
   static constexpr int UPX = W % 2 == 0 ? 2 : 1;              // X units: UPX pixels x 4 channels
@@ -1079,7 +1089,7 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
   // ahead where their registers are cheap, else loaded synchronously; fused-
   // upsample inputs go through UpStage (half-resolution window, prefetched).
   using UP = UpStage<UPS ? CINB : 1, H, W, FPT, RT>;
-  float* Sl = reinterpret_cast<float*>(lds16 + C::NIMG * (C::XIMG + C::DIMG));
+  float* Sl = reinterpret_cast<float*>(C::SLA ? Xl : lds16 + C::NIMG * (C::XIMG + C::DIMG));
   constexpr bool XPIPE = !UPS && NLX * 8 + NLD * 4 <= (C::MINW == 3 ? 24 : 48);
   auto load_x = [&](int t, int i, float2* v) {   // branch-free, 32-bit offsets (see the forward kernel)
     const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
@@ -1095,7 +1105,8 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
       v[c] = UPX == 2 ? *reinterpret_cast<const float2*>(q) : make_float2(*q, 0.f);
     }
   };
-  auto put_x = [&](int i, const float2* v) {
+  // SLA: store unit i's hi pieces only; its lo pieces and offset come back
+  auto put_x = [&](int i, const float2* v, s16x8* keep_lo = nullptr, int* keep_o = nullptr) {
     const int xp = UPX * (i % W2), r = (i / W2) % ROWS, cq = (i / (W2 * ROWS)) % CQ, fi = i / (W2 * ROWS * CQ);
     const int o = xplane(cq) + ((fi * ROWS + r) * TWPX + xp + OFFX) * 4;
     s16x8 hv, lv;
@@ -1125,7 +1136,11 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
         lv[4 + c] = lo;
       }
     }
-    if constexpr (UPX == 2) {
+    if (keep_lo) {   // (SLA: UPX == 2)
+      *reinterpret_cast<s16x8*>(Xh + o) = hv;
+      *keep_lo = lv;
+      *keep_o = o;
+    } else if constexpr (UPX == 2) {
       *reinterpret_cast<s16x8*>(Xh + o) = hv;
       if (PM != 2) *reinterpret_cast<s16x8*>(Xl + o) = lv;
     } else {
@@ -1295,7 +1310,51 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
       const int f0 = (t / NRB) * FPT, y0 = (t % NRB) * RT;
       up.commit(Sl, tid);
       __syncthreads();
-      if constexpr (W % 4 == 0) {
+      if constexpr (C::SLA) {
+        // the window lives in the lo X image's LDS: hi pieces now, lo pieces
+        // held until every thread has read the window
+        static_assert(W % 4 == 0 && UPX == 2, "SLA: 4-pixel items");
+        constexpr int W4 = W / 4, NIT = ceil_div(NIX / 2, 256);
+        s16x8 lk[NIT][2];
+        int lo_o[NIT][2];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int i = tid + it * 256;
+          lo_o[it][0] = -1;
+          if ((NIX / 2) % 256 != 0 && i >= NIX / 2) break;
+          const int q = i % W4, r = (i / W4) % ROWS, cq = (i / (W4 * ROWS)) % CQ, fi = i / (W4 * ROWS * CQ);
+          const int gy = y0 + r - PADL;
+          const bool ok = f0 + fi < F && gy >= 0 && gy < H;
+          f32x4 o[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            o[c] = (ok && cq * 4 + c < CINB) ? UP::row4(Sl, fi, cq * 4 + c, gy, y0, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const int ia = ((fi * CQ + cq) * ROWS + r) * W2 + 2 * q;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            float2 v[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = make_float2(o[c][2 * u], o[c][2 * u + 1]);
+            put_x(ia + u, v, &lk[it][u], &lo_o[it][u]);
+          }
+        }
+        __syncthreads();   // every read of the window is done
+        // the lo image's halo columns (the window overwrote them)
+        if (OFFX > 0) {
+          for (int i = tid; i < FPT * ROWS * 2 * OFFX; i += 256) {
+            const int hc = i % (2 * OFFX), r = i / (2 * OFFX);
+            const int xc = hc < OFFX ? hc : W + hc;
+            for (int cq = 0; cq < CQ; ++cq)
+              *reinterpret_cast<s16x4*>(Xl + xplane(cq) + (r * TWPX + xc) * 4) = s16x4{0, 0, 0, 0};
+          }
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          if (lo_o[it][0] < 0) break;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) *reinterpret_cast<s16x8*>(Xl + lo_o[it][u]) = lk[it][u];
+        }
+      } else if constexpr (W % 4 == 0) {
         // units of 4 pixels x 4 channels (row4: shared taps and source reads)
         constexpr int W4 = W / 4;
 #pragma unroll 1
@@ -1549,7 +1608,7 @@ template <int CIN, int COUT, int H, int W, int KS, bool UPS, int PM, bool PF = f
 static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_out, int F, hipStream_t st, XMax xm,
                       PoolOut pin = PoolOut{nullptr, 0, nullptr, 0}) {
   using C = SWgCfg<CIN, COUT, H, W, KS, UPS, PM>;
-  constexpr int STG = C::STG + (UPS ? UpStage<C::CINB, H, W, C::FPT, C::RT>::SL * 4 : 0);
+  constexpr int STG = C::STG + (UPS && !C::SLA ? UpStage<C::CINB, H, W, C::FPT, C::RT>::SL * 4 : 0);
   constexpr int LDS = STG > C::RED ? STG : C::RED;
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   auto k = conv_wgrad_split_k<CIN, COUT, H, W, KS, UPS, PM, PF>;
