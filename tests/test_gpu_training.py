@@ -33,7 +33,9 @@ from oracle import physics_oracle as O
 pytestmark = pytest.mark.gpu
 
 TRAJ_ENSEMBLE = 3
-ROLLOUT_RTOL_3BP = 2e-3   # chaotic 3-body rollout (test_gpu_parity)
+# chaotic 3-body rollout at test_seq_len 40: measured 9.3e-7 (output_seq) /
+# 5.8e-7 (pos_vel_seq) against the fixture; the parity tests' 1e-5 bar
+ROLLOUT_RTOL_3BP = 1e-5
 
 
 def _load(name):
