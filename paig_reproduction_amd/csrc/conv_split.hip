@@ -1651,7 +1651,15 @@ static int swg_launch(FView x, FView dy, float* slab, int nblk_max, int* nblk_ou
 // c4: too wide for the fused layer backward): (Cin, Cout) of the layer.  c6
 // (64 -> 64 @ 16^2) keeps the standalone pool backward: its folding dgrad
 // spills 32 VGPRs (the plain one already takes 240)
-#define PAIG_SPLIT_PF(X) X(32, 32, 32, 3)
+#define PAIG_SPLIT_PF(X) X(32, 32, 32, 3) PAIG_SPLIT_PF_C6(X)
+#ifndef PAIG_PF_C6
+#define PAIG_PF_C6 0   // A/B builds: 1 = c6 (64 -> 64 @ 16^2) folds pool3 too (its dgrad spills 32 VGPRs)
+#endif
+#if PAIG_PF_C6
+#define PAIG_SPLIT_PF_C6(X) X(64, 64, 16, 3)
+#else
+#define PAIG_SPLIT_PF_C6(X)
+#endif
 // dgrad shapes (layer Cout, layer Cin) of the UNet convs whose input is the
 // 2x upsample (c9, c12, c15) with the transposed-upsample epilogue (UPT)
 #define PAIG_SPLIT_UPT(X) X(32, 128, 16, 3) X(32, 64, 32, 3) X(32, 32, 64, 3)
