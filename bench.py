@@ -10,8 +10,10 @@ reference's train loop body (nn/network/base.py:139-152) in fresh-loss mode,
 through the drop-in PhysicsNet API.  The dataset is synthetic spring_color
 videos rendered on the host once (data="synthetic").
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]     (N > 1: starts N ranks itself)
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+--gpus must equal the launcher's WORLD_SIZE when one is set (else exit 2).
 
 Weak scaling: B sequences per rank.  Rank 0 prints ONE JSON line.
 """
@@ -349,9 +351,61 @@ def headline_roof(kds, conv_math):
     return r
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """`--gpus N` (N > 1) without a launcher: start N fresh child processes,
+    one rank per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on
+    127.0.0.1), as `torch.distributed.run --nproc-per-node N` would, and exit
+    with the first failing rank's status.  This process never touches the GPU
+    (no HIP call before the children start; device_count() does not initialise
+    it).  Rank 0 inherits stdout and prints the one JSON line; a rank that
+    fails takes the others down with it (a rank left waiting in a collective
+    would otherwise hang)."""
+    import signal
+    import subprocess
+    if not os.environ.get("PAIG_BENCH_DEVICE") and torch.cuda.device_count() < n:
+        print(f"bench.py: --gpus {n} but {torch.cuda.device_count()} visible GPUs", file=sys.stderr)
+        sys.exit(2)
+    base = dict(os.environ)
+    base.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(free_port()), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            s = p.poll()
+            if s is None:
+                continue
+            procs.remove(p)
+            if s != 0 and rc == 0:
+                rc = s if s > 0 else 128 - s
+                for q in procs:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    sys.exit(rc)
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        launch_ranks(a.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world} (launch with --nproc-per-node {a.gpus}, "
+              f"or without a launcher: bench.py starts the {a.gpus} ranks itself)", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PAIG_DIST_BACKEND=gloo / PAIG_BENCH_DEVICE=0 rehearse the N-rank code path

@@ -31,7 +31,7 @@ extern "C" {
 /* Version of this interface: bumped whenever an entry point's argument list
  * or a data layout it exchanges changes (the Python binding refuses a library
  * of another version). */
-#define PAIG_ABI_VERSION 2
+#define PAIG_ABI_VERSION 3
 const char* paig_last_error(void);
 int paig_abi_version(void);
 /* f16 range guard of the split-precision path.  Activations and gradients
@@ -113,6 +113,13 @@ int paig_conv2d_fwd_pwc(const float* in, long long in_fs, int in_grp, long long 
 long long paig_conv_wprep_size(int cin, int cout, int ks);
 int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
                     void* const* out, void* stream);
+/* Test hook (no reference counterpart): cap the persistent blocks of the
+ * split forward / data-gradient launches (paig_conv2d_fwd*, flags & 128 or
+ * 256) at cap per output-channel slice, so every block walks many tiles even
+ * at small frame counts; cap <= 0 restores the default (the co-resident
+ * count).  Process-wide; returns the previous cap.  The weight-gradient and
+ * fused layer-backward launches take their cap as nblk_max. */
+int paig_debug_fwd_block_cap(int cap);
 /* 1 if the shape runs on the MFMA path for fwd/dgrad (what 0) or wgrad (what 1)
  * with these flags; flag 32 (fused upsample input) is available only there */
 int paig_conv2d_mfma_supported(int what, int Cin, int Cout, int H, int W, int ks, int flags);

@@ -17,7 +17,7 @@ XMAX_SLOTS = 2048
 
 AB_PATH = os.environ.get("PAIG_AB_LIB")
 # include/paig_hip.h PAIG_ABI_VERSION: the SIGNATURES below are this version's
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -40,6 +40,7 @@ SIGNATURES = {
     "paig_conv2d_wgrad_ex": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_wgrad_pf": (I, [P, LL, I, LL, P, LL, P, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),
+    "paig_debug_fwd_block_cap": (I, [I]),
     "paig_conv2d_bwd_supported": (I, [I, I, I, I, I, I]),
     "paig_conv2d_bwd": (I, [P, LL, I, LL, P, LL, P, LL, P, LL, P, P, I, P, I, I, I, I, I, I, I, P, I, P, LL, P, LL,
                             P, P]),
@@ -134,6 +135,7 @@ SIGNATURES = {
 }
 
 _QUERY = {"paig_last_error", "paig_abi_version", "paig_f16_range_status", "paig_conv2d_mfma_supported",
+          "paig_debug_fwd_block_cap",
           "paig_conv2d_bwd_supported", "paig_velmlp_bwd_blocks",
           "paig_velmlp_slab_len", "paig_head_bwd_blocks", "paig_head_l2_bwd_blocks", "paig_head_mask_blocks", "paig_conv_wprep_size", "paig_gemm_workspace", "paig_colsum_workspace",
           "paig_gemm_parts_size", "paig_gemm_parts", "paig_unet_workspace", "paig_unet_workspace_ex",

@@ -1565,6 +1565,11 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
   if constexpr (PM == 0) f16_range_note(rmax);
 }
 
+// paig_debug_fwd_block_cap: at most this many persistent blocks per COUT
+// slice in the split forward / dgrad launches (0: the resident count), so the
+// tests can make every block walk many tiles at small frame counts
+static int g_fwd_block_cap = 0;
+
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool UPT = false, bool PF = false>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
                        hipStream_t st, XMax xm, const void* wp, PoolOut pout) {
@@ -1593,6 +1598,7 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
   if (bpc > 0 && res > bpc * 256) res = bpc * 256;
   int nb = res / C::NB;   // persistent blocks per COUT slice
   if (nb > (UPT ? F : ntiles)) nb = UPT ? F : ntiles;   // UPT: whole frames per block
+  if (g_fwd_block_cap > 0 && nb > g_fwd_block_cap) nb = g_fwd_block_cap;   // tests: blocks walk many tiles
   if (nb < 1) nb = 1;
   if (PM != 0 || DG) xm.p = nullptr;
   PAIG_REQUIRE(!xm.p || nb <= xm.n, "conv split fwd: %d blocks need more than %d xmax slots", nb, xm.n);
@@ -1923,6 +1929,12 @@ __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
 }
 
 extern "C" {
+
+int paig_debug_fwd_block_cap(int cap) {
+  const int prev = g_fwd_block_cap;
+  g_fwd_block_cap = cap > 0 ? cap : 0;
+  return prev;
+}
 
 // 16-bit elements of one prepped weight image (channel-exponent header + hi
 // + lo) for a forward / dgrad kernel with cin input and cout output channels

@@ -36,18 +36,16 @@ GRAD_RTOL_BF16 = 2e-5
 
 
 def _setup(task, cell, seq_len, ins, pred, size, B, conv_math):
-    from paig_reproduction_amd.nn.datasets.synth import as_model_input, render_sequences
+    from paig_reproduction_amd.nn.datasets.synth import as_model_input
     from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
+    from render_pool import render_distinct
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     m = PhysicsNet(task, 100, 1, cell, seq_len, ins, pred, 3.0, False, True, size * size, "conv_encoder",
                    "conv_st_decoder", device=dev).to(dev)
     m.conv_math = conv_math
-    # distinct sequences: 64 rendered (rendering seq 50 is slow on the host), tiled
-    n = min(B, 64)
-    u8 = render_sequences(task, n, seq_len, seed=3)
-    u8 = np.concatenate([u8] * (B // n) + ([u8[:B % n]] if B % n else []), 0)
-    x = torch.from_numpy(as_model_input(u8)).to(dev)
+    # B distinct sequences (rendered in a process pool, tests/render_pool.py)
+    x = torch.from_numpy(as_model_input(render_distinct(task, B, seq_len, 3))).to(dev)
     return m, x
 
 

@@ -46,17 +46,17 @@ def _threads():
 
 
 def _model(task, cell, seq_len, ins, pred, size, B, seed=3):
-    from paig_reproduction_amd.nn.datasets.synth import as_model_input, render_sequences
+    from paig_reproduction_amd.nn.datasets.synth import as_model_input
     from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
+    from render_pool import render_distinct
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     m = PhysicsNet(task, 100, 1, cell, seq_len, ins, pred, 3.0, False, True, size * size, "conv_encoder",
                    "conv_st_decoder", device=dev).to(dev)
     m.conv_math = "split"
-    n = min(B, 128)
-    u8 = render_sequences(task, n, seq_len, seed=seed)
-    u8 = np.concatenate([u8] * (B // n) + ([u8[:B % n]] if B % n else []), 0)
-    x = torch.from_numpy(as_model_input(u8))
+    # B distinct sequences (no tiling: an error aliasing sequence i with
+    # i + n would be invisible in a tiled batch)
+    x = torch.from_numpy(as_model_input(render_distinct(task, B, seq_len, seed)))
     state = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     cfg = O.Cfg(task, cell, seq_len, ins, pred, size, 3.0)
     return m, x, state, cfg
@@ -93,11 +93,18 @@ def _full_check(tag, task, cell, seq_len, ins, pred, size, B, rollout_rtol=RTOL,
     errs = {}
     for k in OUT_KEYS:
         errs[k] = rel_err(out[k].reshape(-1), o32[k].detach().double().numpy().reshape(-1))
+    # positions (0..size px) and velocities each against their own scale: the
+    # normwise error of the concatenation would let velocity errors hide
+    # under the positions' magnitude
+    pv, pv32 = out["pos_vel_seq"], o32["pos_vel_seq"].detach().double().numpy()
+    D = pv.shape[-1] // 2
+    errs["pos_vel_seq.pos"] = rel_err(pv[..., :D], pv32[..., :D])
+    errs["pos_vel_seq.vel"] = rel_err(pv[..., D:], pv32[..., D:])
     for k in ("train", "extrap", "recons"):
         errs["loss_" + k] = rel_err(np.float64(L[k]), np.float64(float(L32[k].detach())))
     del o32, L32
     print(tag, "outputs/losses vs fp32 oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
-    rollout = ("output_seq", "pos_vel_seq", "loss_extrap", "loss_train")
+    rollout = ("output_seq", "pos_vel_seq", "pos_vel_seq.pos", "pos_vel_seq.vel", "loss_extrap", "loss_train")
     over = {k: v for k, v in errs.items() if v > (rollout_rtol if k in rollout else RTOL)}
     assert not over, over
     # gradients, every element, against the float64 oracle with the fp32 envelope
@@ -120,7 +127,8 @@ def _full_check(tag, task, cell, seq_len, ins, pred, size, B, rollout_rtol=RTOL,
 
 
 # (the oracle's CPU steps dominate: mnist B=256 is ~21 s per fp32 / float64
-# step on the GPU box's 16 cores; its ensemble is one member smaller)
+# step on the GPU box's 16 cores, so its test gets a longer limit rather than
+# a smaller envelope ensemble)
 @pytest.mark.timeout(300)
 def test_config1_spring_b100_seq50_matches_oracle():
     _full_check("config #1", "spring_color", "spring_ode_cell", 50, 4, 6, 32, 100)
@@ -131,9 +139,9 @@ def test_config3_3bp_b512_matches_oracle():
     _full_check("config #3", "3bp_color", "gravity_ode_cell", 20, 4, 12, 36, 512, ROLLOUT_RTOL_3BP, seed=5)
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(600)
 def test_config4_mnist_b256_matches_oracle():
-    _full_check("config #4", "mnist_spring_color", "spring_ode_cell", 12, 3, 7, 64, 256, seed=5, ensemble=3)
+    _full_check("config #4", "mnist_spring_color", "spring_ode_cell", 12, 3, 7, 64, 256, seed=5)
 
 
 @pytest.mark.timeout(300)

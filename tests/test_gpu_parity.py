@@ -52,6 +52,13 @@ def _input(z, device):
 
 # conv arithmetic: "split" (default: f16 hi/lo pieces scaled by powers of two
 # on the 16-bit matrix cores) and "fp32" (f32-input MFMA) both meet the fp32 bar
+def _half(pv, i):
+    """Positions (i = 0) or velocities (i = 1) of a [B, R+1, 2D] pos_vel_seq."""
+    pv = pv.detach().cpu().numpy() if torch.is_tensor(pv) else np.asarray(pv)
+    D = pv.shape[-1] // 2
+    return pv[..., i * D:(i + 1) * D]
+
+
 @pytest.mark.parametrize("conv_math", ["split", "fp32"])
 @pytest.mark.parametrize("name", SUPPORTED)
 def test_step_matches_reference(name, conv_math):
@@ -72,6 +79,9 @@ def test_step_matches_reference(name, conv_math):
         "recons_out": rel_err(m.recons_out, z["recons_out"]),
         "output_seq": rel_err(m.output, z["output_seq"]),
         "pos_vel_seq": rel_err(m.pos_vel_seq, z["pos_vel_seq"]),
+        # positions and velocities against their own scales
+        "pos_vel_seq.pos": rel_err(_half(m.pos_vel_seq, 0), _half(z["pos_vel_seq"], 0)),
+        "pos_vel_seq.vel": rel_err(_half(m.pos_vel_seq, 1), _half(z["pos_vel_seq"], 1)),
         "loss_recons": rel_err(recons.reshape(()), z["loss_recons"]),
         "loss_extrap": rel_err(extrap.reshape(()), z["loss_extrap"]),
         "loss_train": rel_err(train_loss.reshape(()), z["loss_train"]),
@@ -81,7 +91,8 @@ def test_step_matches_reference(name, conv_math):
     print(name, {k: f"{v:.2e}" for k, v in errs.items()})
     for k in ("enc_pos", "enc_masks", "recons_out", "loss_recons"):
         assert errs[k] <= RTOL, (k, errs[k])
-    for k in ("output_seq", "pos_vel_seq", "loss_extrap", "loss_train", "loss_pred_aliased"):
+    for k in ("output_seq", "pos_vel_seq", "pos_vel_seq.pos", "pos_vel_seq.vel", "loss_extrap", "loss_train",
+              "loss_pred_aliased"):
         assert errs[k] <= rt, (k, errs[k])
     grads = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
     bar = GRAD_RTOL_3BP if name.startswith("3bp") else (GRAD_RTOL_MNIST if name.startswith("mnist") else GRAD_RTOL)

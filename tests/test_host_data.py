@@ -77,3 +77,15 @@ def test_renderer_layout_and_determinism(task):
     # object j lives on channel 2 - (j % 3): with fewer than 3 objects channel 0 stays empty
     if n_objs < 3 and task != "mnist_spring_color":
         assert u8[..., 0].max() == 0
+
+
+def test_render_distinct_batches_have_no_repeats():
+    """The full-size GPU tests' batches (tests/render_pool.py): every
+    sequence distinct, deterministic per seed, chunked over a spawn pool."""
+    from render_pool import render_distinct
+    a = render_distinct("spring_color", 40, 6, 7, chunk=8, workers=2)
+    assert a.shape == (40, 6, 32, 32, 3) and a.dtype == np.uint8
+    flat = a.reshape(40, -1)
+    assert len({r.tobytes() for r in flat}) == 40
+    b = render_distinct("spring_color", 40, 6, 7, chunk=8, workers=1)
+    assert np.array_equal(a, b)
