@@ -172,8 +172,9 @@ int paig_conv2d_bwd(const float* x, long long x_fs, int x_grp, long long x_gs, c
  * and d logits (d of the output after its activation) and writes every conv's
  * [weight | bias] gradient to dwb[i] (contiguous, overwritten).  The same
  * kernels in the same order as the Python engine's U-Net stages (its
- * default configuration: the engine's A/B switches such as PAIG_FUSED_BWD=0
- * do not apply here; the fused layer backwards are always taken). */
+ * default configuration; its A/B switches are the _ex flags below:
+ * PAIG_FUSED_BWD=0 = PAIG_UNET_SEPARATE_BWD, PAIG_UPT=0 =
+ * PAIG_UNET_STANDALONE_UP, PAIG_POOL_FOLD=0 = PAIG_UNET_STANDALONE_POOL). */
 size_t paig_unet_workspace(int net, int F, int H, int K, int math);
 int paig_unet_fwd(int net, int F, int H, int K, int math, const float* x, long long x_fs, int x_grp, long long x_gs,
                   const float* const* w, const float* const* b, float* logits, void* ws, size_t ws_bytes,
@@ -227,7 +228,10 @@ size_t paig_unet_workspace_ex(int net, int F, int H, int K, int math, int flags)
  * gradient (which 1), or -1 (none: the input, the logits, a fused upsample) */
 long long paig_unet_buffer(int net, int F, int H, int K, int math, int flags, int which, int buf);
 /* plan facts: what 0 = convs, 1 = buffers, 2 = the head's input buffer, 3 =
- * its channels, 4 = the logits buffer */
+ * its channels, 4 = the logits buffer, 5 = the head input's channel offset in
+ * its buffer, 6 = that buffer's channel count (a caller reading the head
+ * input as [F][channels][H][W] from the buffer's start needs 5 == 0 and
+ * 6 == 3) */
 int paig_unet_query(int net, int K, int what);
 int paig_unet_fwd_ex(int net, int F, int H, int K, int math, int flags, const float* x, long long x_fs, int x_grp,
                      long long x_gs, const float* const* w, const float* const* b, float* logits,

@@ -10,8 +10,9 @@
 // arguments (fused pools / upsamples, weight images, max-|x| slots, fused
 // layer backwards, one batched slab reduction), so the results are
 // bit-identical to the Python engine's (tests/test_gpu_unet_abi.py) in its
-// default configuration (the engine's A/B switch PAIG_FUSED_BWD=0 has no
-// counterpart here: the fused layer backwards are always taken).
+// default configuration (the engine's A/B switches map to the _ex flags:
+// PAIG_FUSED_BWD=0 -> PAIG_UNET_SEPARATE_BWD, PAIG_UPT=0 ->
+// PAIG_UNET_STANDALONE_UP, PAIG_POOL_FOLD=0 -> PAIG_UNET_STANDALONE_POOL).
 // Host code only; the caller's workspace holds every activation, gradient
 // and partial-gradient slab (paig_unet_workspace), the library allocates
 // nothing.
@@ -187,7 +188,10 @@ bool pool_fold_fused(const UPlan& p, int i, int H, int cm) {
 bool pool_fold_split(const UPlan& p, int i, int H, int cm, int flags) {
   const UOp& op = p.ops[i];
   const int Hl = H / p.bufs[op.dst.buf].lvl;
+  // (not for a layer that takes the fused layer backward without a pool
+  // instantiation: that launch would get the codes and flag 64 it cannot fold)
   return cm == 128 && !(flags & PAIG_UNET_STANDALONE_POOL) && op.src.buf != p.X0 && !pool_fold_fused(p, i, H, cm) &&
+         !paig_conv2d_bwd_supported(op.src.n, op.dst.n, Hl, Hl, op.ks, cm) &&
          paig_conv2d_mfma_supported(1, op.src.n, op.dst.n, Hl, Hl, op.ks, 128 | 64) &&
          paig_conv2d_mfma_supported(0, op.dst.n, op.src.n, Hl, Hl, op.ks, 8 | 128 | 64);
 }
@@ -686,6 +690,8 @@ int paig_unet_query(int net, int K, int what) {
     case 2: return p.ops.back().src.buf;   // the 1x1 head's input buffer
     case 3: return p.ops.back().src.n;     // ... and its channels
     case 4: return p.LG;
+    case 5: return p.ops.back().src.off;                 // the head input's channel offset in its buffer
+    case 6: return p.bufs[p.ops.back().src.buf].C;       // ... and that buffer's channels
     default: return -1;
   }
 }

@@ -77,6 +77,13 @@ class Layout:
         self.fuse_head = (self.K in (2, 3) and self.HW % 4 == 0 and os.environ.get("PAIG_FUSE_HEAD", "1") != "0" and
                           ((not self.unet and self.head_ci == 8) or (self.unet and self.head_ci == 16 and
                                                                      self.H % 4 == 0)))
+        if self.fuse_head:
+            # the fused head kernels read the head input (and write its
+            # gradient) as [F][head_ci][H][W] from the start of its buffer
+            off, cbuf = L.paig_unet_query(self.net, self.K, 5), L.paig_unet_query(self.net, self.K, 6)
+            if off != 0 or cbuf != self.head_ci:
+                raise PaigError(f"U-Net head input at channel offset {off} of a {cbuf}-channel buffer: the fused "
+                                f"head needs the whole buffer ({self.head_ci} channels from offset 0)")
 
 
 class KernelProbe:

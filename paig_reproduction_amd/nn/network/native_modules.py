@@ -317,7 +317,7 @@ class _Encoder(torch.autograd.Function):
     reference never uses it, Q10); masks / masked objects are outputs only."""
 
     @staticmethod
-    def forward(ctx, x, anchor, model, which):
+    def forward(ctx, x, anchor, model, which, need_saved=True):
         from paig_reproduction_amd.engine import Layout, _empty
         x = _f32(x)
         N = x.shape[0]
@@ -329,7 +329,9 @@ class _Encoder(torch.autograd.Function):
         dev = x.device
         st = stream_handle(dev)
         ws = _empty(eng.workspace_floats(lay), dev)
-        S = {"lay": lay, "x": x, "ws": ws, "dev": dev, "cm": eng.conv_flags()}
+        # need_saved False (no autograd graph): the U-Net workspace without
+        # gradient buffers, slabs or pool codes (PAIG_UNET_INFERENCE)
+        S = {"lay": lay, "x": x, "ws": ws, "dev": dev, "cm": eng.conv_flags(), "need_saved": need_saved}
         x_view = (ptr(x), lay.frame, 0, 0)
         ctx.model, ctx.S, ctx.which = model, S, which
         if which == "encoder":
@@ -352,7 +354,7 @@ class _Encoder(torch.autograd.Function):
         if which == "encoder":
             denc = grads[0]
             if denc is None:
-                return None, None, None, None
+                return None, None, None, None, None
             with model._flat.partial_backward(("encoder.",)):
                 eng._encoder_backward(S, denc.float().contiguous(), st, hook=False)
         else:
@@ -360,20 +362,26 @@ class _Encoder(torch.autograd.Function):
             dLG = grads[0].float().contiguous()
             with model._flat.partial_backward((lay.prefix,)):
                 eng._unet_backward(S, dLG, st)
-        return None, None, None, None
+        return None, None, None, None, None
 
 
 def encoder_forward(enc, inp):
     """ConvolutionalEncoder.forward(inp) -> (enc_pos [N, 2K], enc_masks, masked_objs list)."""
     model = _owner(enc)
-    pos, masks, objs = _Encoder.apply(inp, model._anchor_for_modules(), model, "encoder")
+    pos, masks, objs = _Encoder.apply(inp, model._anchor_for_modules(), model, "encoder", _need_saved(model))
     return pos, masks, [objs[k] for k in range(objs.shape[0])]
 
 
 def unet_forward(unet, x, which):
     """ShallowUNet / UNet forward(x) -> logits [N, n_objs, H, W]."""
     model = _owner(unet)
-    return _Encoder.apply(x, model._anchor_for_modules(), model, which)
+    return _Encoder.apply(x, model._anchor_for_modules(), model, which, _need_saved(model))
+
+
+def _need_saved(model):
+    """Whether a backward can follow (grad mode on, some parameter trainable):
+    else the forward allocates no training workspace."""
+    return torch.is_grad_enabled() and any(q.requires_grad for q in model.parameters())
 
 
 def _owner(mod):

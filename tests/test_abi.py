@@ -60,6 +60,8 @@ def test_library_loads_and_exports_every_symbol():
     # convs, buffers, the 1x1 head's input buffer and width
     assert [L.paig_unet_query(0, 2, w) for w in range(5)] == [13, 16, 14, 8, 15]   # ShallowUNet: c13 on A12
     assert [L.paig_unet_query(1, 2, w) for w in range(5)] == [18, 22, 20, 16, 21]  # UNet: c18 on A17
+    # the head input fills its buffer from channel 0 (the fused head kernels' contract)
+    assert [L.paig_unet_query(n, 2, w) for n in (0, 1) for w in (5, 6)] == [0, 8, 0, 16]
     # workspace layouts: inference holds no gradients; a head-input gradient exists for training
     for net, H in ((0, 32), (1, 64)):
         full = L.paig_unet_workspace_ex(net, 10, H, 2, 128, 1)

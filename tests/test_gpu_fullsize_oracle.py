@@ -37,6 +37,8 @@ ENSEMBLE_FULL = 4
 # by 1.7e-5 on the fixture (test_oracle_golden); bar = ~3x the largest error
 # measured on the fixture and at B=512
 ROLLOUT_RTOL_3BP = 1e-5
+# 3bp's velocities on their own scale: see tests/test_gpu_parity.py VEL_RTOL_3BP
+VEL_RTOL_3BP = 5e-5
 
 
 def _threads():
@@ -79,7 +81,8 @@ def _hip_step(m, x):
     return out, L, g, sse
 
 
-def _full_check(tag, task, cell, seq_len, ins, pred, size, B, rollout_rtol=RTOL, seed=3, ensemble=ENSEMBLE_FULL):
+def _full_check(tag, task, cell, seq_len, ins, pred, size, B, rollout_rtol=RTOL, seed=3, ensemble=ENSEMBLE_FULL,
+                vel_rtol=RTOL):
     """Whole-batch outputs / losses vs the fp32 oracle and every gradient
     element vs the float64 oracle within the fp32 envelope."""
     import time
@@ -104,8 +107,9 @@ def _full_check(tag, task, cell, seq_len, ins, pred, size, B, rollout_rtol=RTOL,
         errs["loss_" + k] = rel_err(np.float64(L[k]), np.float64(float(L32[k].detach())))
     del o32, L32
     print(tag, "outputs/losses vs fp32 oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
-    rollout = ("output_seq", "pos_vel_seq", "pos_vel_seq.pos", "pos_vel_seq.vel", "loss_extrap", "loss_train")
-    over = {k: v for k, v in errs.items() if v > (rollout_rtol if k in rollout else RTOL)}
+    rollout = ("output_seq", "pos_vel_seq", "pos_vel_seq.pos", "loss_extrap", "loss_train")
+    over = {k: v for k, v in errs.items()
+            if v > (vel_rtol if k == "pos_vel_seq.vel" else rollout_rtol if k in rollout else RTOL)}
     assert not over, over
     # gradients, every element, against the float64 oracle with the fp32 envelope
     _, _, g64 = O.train_step_f64(state, cfg, x)
@@ -136,7 +140,8 @@ def test_config1_spring_b100_seq50_matches_oracle():
 
 @pytest.mark.timeout(300)
 def test_config3_3bp_b512_matches_oracle():
-    _full_check("config #3", "3bp_color", "gravity_ode_cell", 20, 4, 12, 36, 512, ROLLOUT_RTOL_3BP, seed=5)
+    _full_check("config #3", "3bp_color", "gravity_ode_cell", 20, 4, 12, 36, 512, ROLLOUT_RTOL_3BP, seed=5,
+                vel_rtol=VEL_RTOL_3BP)
 
 
 @pytest.mark.timeout(600)

@@ -30,6 +30,12 @@ GRAD_RTOL = 1e-4
 GRAD_RTOL_3BP = 3e-5
 GRAD_RTOL_MNIST = 1.6e-3
 ROLLOUT_RTOL_3BP = 1e-5   # ~3x the largest measured: 4.9e-7 on the fixture, 2.8e-6 at B=512
+# 3bp's velocities against their own scale: fp32 runs of
+# the reference algorithm on one-ulp-perturbed weights (the oracle) differ from
+# the fixture by up to 1.63e-5 there (HIP: 1.06e-5 split, 9.2e-6 fp32): bar ~3x
+# that spread.  Every other config's velocities keep the 1e-4 bar (measured
+# <= 1.6e-6; fp32 spread <= 3.1e-6).
+VEL_RTOL_3BP = 5e-5
 SUPPORTED = list(GOLDEN)
 
 
@@ -91,9 +97,9 @@ def test_step_matches_reference(name, conv_math):
     print(name, {k: f"{v:.2e}" for k, v in errs.items()})
     for k in ("enc_pos", "enc_masks", "recons_out", "loss_recons"):
         assert errs[k] <= RTOL, (k, errs[k])
-    for k in ("output_seq", "pos_vel_seq", "pos_vel_seq.pos", "pos_vel_seq.vel", "loss_extrap", "loss_train",
-              "loss_pred_aliased"):
+    for k in ("output_seq", "pos_vel_seq", "pos_vel_seq.pos", "loss_extrap", "loss_train", "loss_pred_aliased"):
         assert errs[k] <= rt, (k, errs[k])
+    assert errs["pos_vel_seq.vel"] <= (VEL_RTOL_3BP if name.startswith("3bp") else RTOL), errs["pos_vel_seq.vel"]
     grads = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
     bar = GRAD_RTOL_3BP if name.startswith("3bp") else (GRAD_RTOL_MNIST if name.startswith("mnist") else GRAD_RTOL)
     gerr = grad_checks(z, grads, bar, prefix=name + ": ")

@@ -1,0 +1,432 @@
+"""Every persistent conv kernel variant with its blocks walking MANY tiles
+(VERDICT r05 item 2b): 64 frames, and the launch capped at 2 persistent
+blocks (per output-channel slice) so each block stages tile after tile
+through the same LDS and registers, against float64 torch (the aten ops the
+reference's U-Nets run: conv2d / convolution_backward, max_pool2d, the
+torchvision Resize's bilinear upsample; nn/network/blocks.py:106-308).
+
+A round-5 defect (channel-sliced fused-upsample weight gradients wrong at
+2560 frames) passed every unit test because those walked one or two tiles
+per block; these cases are the unit-level net for that class: state a block
+carries from one tile to the next (LDS halo columns, the upsample window,
+running exponents, carried rows of the transposed-upsample epilogue).
+
+* forward / data-gradient launches (paig_conv2d_fwd*, capped with the test
+  hook paig_debug_fwd_block_cap): plain, fused-upsample input (flags 32),
+  fused max pool + window codes (64, paig_conv2d_fwd_pwc), masked +
+  accumulated dgrad (8|4|2), dgrad with the upsample's transpose in the
+  epilogue (8|512), dgrad with the pool backward folded (8|64).  The output
+  of a 2-block launch must be BIT-IDENTICAL to the default launch's (every
+  tile is formed the same way whichever block walks it) and within the split
+  bars of float64;
+* weight-gradient launches (paig_conv2d_wgrad_ex / _pf; nblk_max = 2 and the
+  engine's 1024): plain, channel-sliced wide layers, fused-upsample input,
+  channel-sliced fused-upsample, pool fold;
+* the fused layer backward (paig_conv2d_bwd; nblk_max = 2): plain,
+  fused-upsample, pool fold.
+"""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+XMAX = 2048
+NF = 64                      # frames per case
+TOL = {128: 1e-5, 256: 8e-3}     # split (f16 hi/lo, fp32-accurate) / bf16 operands, normwise vs float64
+TOL_G = {128: 3e-5, 256: 8e-3}   # gradients (dgrad / wgrad), as tests/test_gpu_kernels.py SPLIT_TOL
+
+
+def L():
+    from paig_reproduction_amd._lib import lib
+    return lib()
+
+
+def st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def p(t):
+    return None if t is None else t.data_ptr()
+
+
+@pytest.fixture(autouse=True)
+def _reset_cap():
+    yield
+    L().paig_debug_fwd_block_cap(0)
+
+
+def _both_caps(run):
+    """run() under the default forward grid and capped at 2 blocks: the two
+    outputs must be bit-identical; returns the capped one."""
+    L().paig_debug_fwd_block_cap(0)
+    a = run()
+    L().paig_debug_fwd_block_cap(2)
+    b = run()
+    L().paig_debug_fwd_block_cap(0)
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v), f"capped launch differs: max |d| {(u.float() - v.float()).abs().max().item():.3e}"
+    return b
+
+
+def _data(cin, cout, hw, seed, hin=None):
+    torch.manual_seed(seed)
+    hin = hin or hw
+    x = torch.relu(torch.randn(NF, cin, hin, hin, device=DEV))
+    w = torch.randn(cout, cin, 3, 3, device=DEV) * (0.6 / cin ** 0.5)
+    b = torch.randn(cout, device=DEV) * 0.1
+    dy = torch.randn(NF, cout, hw, hw, device=DEV)
+    return x, w, b, dy
+
+
+def _reduce(slab, nb, n):
+    g = torch.empty(n, device=DEV)
+    L().paig_slab_reduce(p(slab), nb, n, n, p(g), 0, st())
+    torch.cuda.synchronize()
+    return g
+
+
+def _up64(xs, hw):
+    return F.interpolate(xs.double().cpu(), size=(hw, hw), mode="bilinear", align_corners=False)
+
+
+# ---------------------------------------------------------------- forward
+# (Cin, Cout, H) of the ShallowUNet (32 x 32, 36 x 36) and UNet (64 x 64) convs
+FWD = [(3, 8, 32), (8, 8, 32), (24, 8, 32), (16, 16, 16), (16, 32, 8), (32, 32, 8), (8, 8, 36), (16, 32, 9),
+       (24, 8, 36), (3, 16, 64), (16, 16, 64), (48, 16, 64), (32, 64, 32), (64, 32, 32), (64, 64, 16),
+       (96, 64, 16), (64, 128, 8), (128, 128, 8)]
+
+
+@pytest.mark.parametrize("cin,cout,hw", FWD)
+@pytest.mark.parametrize("mode", [128, 256])
+def test_forward_many_tiles(cin, cout, hw, mode):
+    if mode == 256 and hw == 64:
+        pytest.skip("bf16 runs the ShallowUNet configs only (config #2)")
+    assert L().paig_conv2d_mfma_supported(0, cin, cout, hw, hw, 3, mode) == 1
+    x, w, b, _ = _data(cin, cout, hw, cin * 31 + cout + hw)
+
+    def run():
+        out = torch.full((NF, cout, hw, hw), float("nan"), device=DEV)
+        L().paig_conv2d_fwd(p(x), cin * hw * hw, 0, 0, p(out), cout * hw * hw, None, 0, p(w), p(b), NF, cin, cout,
+                            hw, hw, 3, 1 | mode, st())
+        return (out,)
+    out, = _both_caps(run)
+    ref = torch.relu(F.conv2d(x.double().cpu(), w.double().cpu(), b.double().cpu(), padding=1))
+    assert rel_err(out, ref) <= TOL[mode]
+
+
+UPS = [(32, 16, 16), (16, 16, 32), (32, 16, 18), (16, 16, 36), (128, 32, 16), (64, 32, 32), (32, 32, 64)]
+
+
+@pytest.mark.parametrize("cin,cout,hw", UPS)
+@pytest.mark.parametrize("mode", [128, 256])
+def test_forward_fused_upsample_many_tiles(cin, cout, hw, mode):
+    if mode == 256 and cin > 32:
+        pytest.skip("bf16 runs the ShallowUNet configs only (config #2)")
+    hs = hw // 2
+    xs, w, b, _ = _data(cin, cout, hw, cin + cout * 7 + hw, hin=hs)
+
+    def run():
+        out = torch.full((NF, cout, hw, hw), float("nan"), device=DEV)
+        L().paig_conv2d_fwd(p(xs), cin * hs * hs, 0, 0, p(out), cout * hw * hw, None, 0, p(w), p(b), NF, cin, cout,
+                            hw, hw, 3, 32 | mode, st())
+        return (out,)
+    out, = _both_caps(run)
+    ref = F.conv2d(_up64(xs, hw), w.double().cpu(), b.double().cpu(), padding=1)
+    assert rel_err(out, ref) <= TOL[mode]
+
+
+POOL = [(8, 8, 32), (16, 16, 16), (3, 8, 32), (16, 16, 64), (32, 32, 32), (64, 64, 16)]
+
+
+@pytest.mark.parametrize("cin,cout,hw", POOL)
+@pytest.mark.parametrize("mode", [128, 256])
+def test_forward_fused_pool_many_tiles(cin, cout, hw, mode):
+    if mode == 256 and hw == 64 or not L().paig_conv2d_mfma_supported(0, cin, cout, hw, hw, 3, mode | 64):
+        pytest.skip("no fused pool for this shape in this arithmetic")
+    x, w, b, _ = _data(cin, cout, hw, cin + cout + hw + mode)
+    hp = hw // 2
+    cfs = -(-cout // 8) * 8 * hp * hp
+
+    def run():
+        y = torch.full((NF, cout, hw, hw), float("nan"), device=DEV)
+        pool = torch.full((NF, cout, hp, hp), float("nan"), device=DEV)
+        code = torch.zeros(NF * cfs, dtype=torch.uint8, device=DEV)
+        L().paig_conv2d_fwd_pwc(p(x), cin * hw * hw, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), NF, cin, cout,
+                                hw, hw, 3, 1 | 64 | mode, None, 0, p(pool), cout * hp * hp, p(code), cfs, None, st())
+        return y, pool, code
+    y, pool, code = _both_caps(run)
+    ref = torch.relu(F.conv2d(x.double().cpu(), w.double().cpu(), b.double().cpu(), padding=1))
+    assert rel_err(y, ref) <= TOL[mode]
+    # the pooled values and window codes of the GPU's own output, bit for bit
+    rp = torch.empty_like(pool)
+    rc = torch.zeros_like(code)
+    assert L().paig_maxpool2_fwd_codes(p(y), cout * hw * hw, p(rp), cout * hp * hp, p(rc), cfs, NF, cout, hw, hw,
+                                       st()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(pool, rp)
+    assert torch.equal(code, rc)
+
+
+# dgrad kernels of the layers (Cin, Cout, H): the kernel maps Cout -> Cin
+DGRAD = [(8, 8, 32), (24, 8, 32), (8, 16, 16), (16, 16, 16), (32, 32, 8), (32, 16, 16), (8, 8, 36), (16, 32, 9),
+         (16, 16, 64), (48, 16, 64), (16, 32, 32), (32, 32, 32), (64, 64, 16), (96, 64, 16), (128, 128, 8),
+         (64, 32, 32)]
+
+
+@pytest.mark.parametrize("cin,cout,hw", DGRAD)
+def test_dgrad_masked_accumulate_many_tiles(cin, cout, hw):
+    mode = 128
+    if not L().paig_conv2d_mfma_supported(0, cout, cin, hw, hw, 3, 8 | mode):
+        pytest.skip("no split dgrad kernel for this shape")
+    x, w, _, dy = _data(cin, cout, hw, cin * 3 + cout * 5 + hw)
+
+    def run():
+        dx = torch.full((NF, cin, hw, hw), 0.5, device=DEV)
+        L().paig_conv2d_fwd(p(dy), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, p(x), cin * hw * hw, p(w), None, NF,
+                            cout, cin, hw, hw, 3, 8 | 4 | 2 | mode, st())
+        return (dx,)
+    dx, = _both_caps(run)
+    rdx = (torch.nn.grad.conv2d_input(x.shape, w.double().cpu(), dy.double().cpu(), padding=1) + 0.5) * (x.cpu() > 0)
+    assert rel_err(dx, rdx) <= TOL_G[mode]
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(128, 32, 16), (64, 32, 32), (32, 32, 64)])
+def test_dgrad_upsample_transpose_many_frames(cin, cout, hw):
+    """flags 8 | 512 (UNet c9 / c12 / c15): whole frames per block, the two
+    rows a tile cannot complete carried to the frame's next tile; capped at 2
+    blocks every block walks 32 frames."""
+    assert L().paig_conv2d_mfma_supported(0, cout, cin, hw, hw, 3, 8 | 128 | 512) == 1
+    hs = hw // 2
+    xs, w, _, dy = _data(cin, cout, hw, cin + cout + hw, hin=hs)
+
+    def run():
+        got = torch.full((NF, cin, hs, hs), float("nan"), device=DEV)
+        L().paig_conv2d_fwd_pw(p(dy), cout * hw * hw, 0, 0, p(got), cin * hs * hs, p(xs), cin * hs * hs, p(w), None,
+                               NF, cout, cin, hw, hw, 3, 8 | 128 | 512 | 2, None, 0, None, 0, None, st())
+        return (got,)
+    got, = _both_caps(run)
+    xr = xs.double().cpu().requires_grad_(True)
+    F.conv2d(F.interpolate(xr, size=(hw, hw), mode="bilinear", align_corners=False), w.double().cpu(),
+             padding=1).backward(dy.double().cpu())
+    assert rel_err(got, xr.grad * (xs.cpu() > 0)) <= TOL_G[128]
+
+
+def _pool_fold_ref(x, w, y, gy, gp):
+    """float64 (dpre, dx, dw, db) of conv + ReLU + 2x2 max pool with the GPU
+    forward's own ReLU' masks and argmaxes: dpre = (y > 0)(gy + scatter(gp))."""
+    F_, cout, hw = y.shape[0], y.shape[1], y.shape[2]
+    yc = y.cpu()
+    _, idx = F.max_pool2d(yc, 2, return_indices=True)
+    scat = torch.zeros(F_, cout, hw * hw, dtype=torch.float64)
+    scat.scatter_(2, idx.view(F_, cout, -1), gp.double().cpu().view(F_, cout, -1))
+    dpre = (yc > 0) * (gy.double().cpu() + scat.view(F_, cout, hw, hw))
+    xd, wd = x.double().cpu(), w.double().cpu()
+    rdx = torch.nn.grad.conv2d_input(xd.shape, wd, dpre, padding=1) * (x.cpu() > 0)
+    rdw = torch.nn.grad.conv2d_weight(xd, wd.shape, dpre, padding=1)
+    return rdx, rdw, dpre.sum((0, 2, 3))
+
+
+def _pooled_forward(x, w, b, mode):
+    F_, cin, hw = x.shape[0], x.shape[1], x.shape[2]
+    cout, hp = w.shape[0], hw // 2
+    cfs = -(-cout // 8) * 8 * hp * hp
+    y = torch.empty(F_, cout, hw, hw, device=DEV)
+    pool = torch.empty(F_, cout, hp, hp, device=DEV)
+    code = torch.empty(F_ * cfs, dtype=torch.uint8, device=DEV)
+    xmax = torch.zeros(XMAX, device=DEV)
+    if L().paig_conv2d_mfma_supported(0, cin, cout, hw, hw, 3, mode | 64):
+        L().paig_conv2d_fwd_pwc(p(x), cin * hw * hw, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout,
+                                hw, hw, 3, 1 | 64 | mode, p(xmax) if mode == 128 else None,
+                                XMAX if mode == 128 else 0, p(pool), cout * hp * hp, p(code), cfs, None, st())
+    else:
+        L().paig_conv2d_fwd_pwc(p(x), cin * hw * hw, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), F_, cin, cout,
+                                hw, hw, 3, 1 | mode, p(xmax) if mode == 128 else None, XMAX if mode == 128 else 0,
+                                None, 0, None, 0, None, st())
+        L().paig_maxpool2_fwd_codes(p(y), cout * hw * hw, p(pool), cout * hp * hp, p(code), cfs, F_, cout, hw, hw,
+                                    st())
+    torch.cuda.synchronize()
+    return y, code, cfs, xmax
+
+
+def test_dgrad_pool_fold_many_tiles():
+    """The UNet's c4 (32 -> 32 @ 32^2): the pool2 backward folded into the
+    separate data gradient's staging (flags 8 | 64)."""
+    cin, cout, hw, mode = 32, 32, 32, 128
+    assert L().paig_conv2d_mfma_supported(0, cout, cin, hw, hw, 3, 8 | 64 | mode) == 1
+    x, w, b, gy = _data(cin, cout, hw, 404)
+    gp = torch.randn(NF, cout, hw // 2, hw // 2, device=DEV)
+    y, code, cfs, _ = _pooled_forward(x, w, b, mode)
+    hp = hw // 2
+
+    def run():
+        dx = torch.full((NF, cin, hw, hw), float("nan"), device=DEV)
+        L().paig_conv2d_fwd_pwc(p(gy), cout * hw * hw, 0, 0, p(dx), cin * hw * hw, p(x), cin * hw * hw, p(w), None,
+                                NF, cout, cin, hw, hw, 3, 8 | 64 | 2 | mode, None, 0, p(gp), cout * hp * hp, p(code),
+                                cfs, None, st())
+        return (dx,)
+    dx, = _both_caps(run)
+    rdx, _, _ = _pool_fold_ref(x, w, y, gy, gp)
+    assert rel_err(dx, rdx) <= TOL_G[mode]
+
+
+# ---------------------------------------------------------- weight gradient
+WGRAD = [(3, 8, 32), (8, 8, 32), (24, 8, 32), (16, 32, 8), (8, 8, 36), (16, 32, 9), (3, 16, 64), (16, 16, 64),
+         (48, 16, 64), (16, 32, 32), (32, 32, 32), (64, 32, 32), (32, 64, 16), (64, 64, 16), (96, 64, 16),
+         (64, 128, 8), (128, 128, 8)]
+
+
+def _wgrad(x, dy, cin, cout, hw, flags, xmax, nmax, hin=None, pf=None):
+    hin = hin or hw
+    slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+    nb = ctypes.c_int(0)
+    if pf is None:
+        L().paig_conv2d_wgrad_ex(p(x), cin * hin * hin, 0, 0, p(dy), cout * hw * hw, p(slab), nmax, ctypes.byref(nb),
+                                 NF, cin, cout, hw, hw, 3, flags, p(xmax), XMAX if xmax is not None else 0, st())
+    else:
+        gp, code, cfs = pf
+        L().paig_conv2d_wgrad_pf(p(x), cin * hw * hw, 0, 0, p(dy), cout * hw * hw, p(gp), cout * hw * hw // 4,
+                                 p(code), cfs, p(slab), nmax, ctypes.byref(nb), NF, cin, cout, hw, hw, 3, flags,
+                                 p(xmax), XMAX, st())
+    assert 1 <= nb.value <= nmax
+    g = _reduce(slab, nb.value, cout * cin * 9 + cout)
+    return g[:cout * cin * 9].view(cout, cin, 3, 3), g[cout * cin * 9:], nb.value
+
+
+def _fwd_xmax(x, w, b, cin, cout, hw, flags, hin=None):
+    hin = hin or hw
+    xmax = torch.zeros(XMAX, device=DEV)
+    out = torch.empty(NF, cout, hw, hw, device=DEV)
+    L().paig_conv2d_fwd_ex(p(x), cin * hin * hin, 0, 0, p(out), cout * hw * hw, None, 0, p(w), p(b), NF, cin, cout,
+                           hw, hw, 3, flags, p(xmax), XMAX, st())
+    return xmax
+
+
+@pytest.mark.parametrize("cin,cout,hw", WGRAD)
+def test_wgrad_many_tiles(cin, cout, hw):
+    mode = 128
+    assert L().paig_conv2d_mfma_supported(1, cin, cout, hw, hw, 3, mode) == 1
+    x, w, b, dy = _data(cin, cout, hw, cin * 7 + cout * 3 + hw)
+    xmax = _fwd_xmax(x, w, b, cin, cout, hw, 1 | mode)
+    rdw = torch.nn.grad.conv2d_weight(x.double().cpu(), w.shape, dy.double().cpu(), padding=1)
+    rdb = dy.double().cpu().sum((0, 2, 3))
+    for nmax in (2, 1024):
+        gw, gb, nb = _wgrad(x, dy, cin, cout, hw, mode, xmax, nmax)
+        assert rel_err(gw, rdw) <= TOL_G[mode], (nmax, nb)
+        assert rel_err(gb, rdb) <= 1e-5, (nmax, nb)
+
+
+@pytest.mark.parametrize("cin,cout,hw", UPS)
+def test_wgrad_fused_upsample_many_tiles(cin, cout, hw):
+    """c7 / c10 and the UNet's channel-sliced c9 / c12 / c15 (the round-5
+    defect's kernel family)."""
+    mode = 128
+    assert L().paig_conv2d_mfma_supported(1, cin, cout, hw, hw, 3, 32 | mode) == 1
+    hs = hw // 2
+    xs, w, b, dy = _data(cin, cout, hw, cin * 5 + cout + hw, hin=hs)
+    xmax = _fwd_xmax(xs, w, b, cin, cout, hw, 32 | mode, hin=hs)
+    rdw = torch.nn.grad.conv2d_weight(_up64(xs, hw), w.shape, dy.double().cpu(), padding=1)
+    rdb = dy.double().cpu().sum((0, 2, 3))
+    for nmax in (2, 1024):
+        gw, gb, nb = _wgrad(xs, dy, cin, cout, hw, 32 | mode, xmax, nmax, hin=hs)
+        assert rel_err(gw, rdw) <= TOL_G[mode], (nmax, nb)
+        assert rel_err(gb, rdb) <= 1e-5, (nmax, nb)
+        # every input channel against its own scale (a slice of channels
+        # gone wrong cannot hide under the others' magnitude)
+        for c in range(cin):
+            assert rel_err(gw[:, c], rdw[:, c]) <= 10 * TOL_G[mode], (nmax, c)
+
+
+def test_wgrad_pool_fold_many_tiles():
+    """The UNet's c4: the pool2 backward folded into the weight gradient's dY
+    staging (paig_conv2d_wgrad_pf)."""
+    cin, cout, hw, mode = 32, 32, 32, 128
+    assert L().paig_conv2d_mfma_supported(1, cin, cout, hw, hw, 3, 64 | mode) == 1
+    x, w, b, gy = _data(cin, cout, hw, 505)
+    gp = torch.randn(NF, cout, hw // 2, hw // 2, device=DEV)
+    y, code, cfs, xmax = _pooled_forward(x, w, b, mode)
+    _, rdw, rdb = _pool_fold_ref(x, w, y, gy, gp)
+    for nmax in (2, 1024):
+        gw, gb, nb = _wgrad(x, gy, cin, cout, hw, 64 | mode, xmax, nmax, pf=(gp, code, cfs))
+        assert rel_err(gw, rdw) <= TOL_G[mode], (nmax, nb)
+        assert rel_err(gb, rdb) <= 1e-5, (nmax, nb)
+
+
+# ------------------------------------------------------ fused layer backward
+BWD = [(8, 8, 32), (24, 8, 32), (16, 16, 16), (32, 32, 8), (32, 16, 16), (16, 16, 64), (16, 32, 32), (8, 8, 36),
+       (16, 16, 18)]
+
+
+@pytest.mark.parametrize("cin,cout,hw", BWD)
+@pytest.mark.parametrize("mode", [128, 256])
+def test_fused_backward_many_tiles(cin, cout, hw, mode):
+    assert L().paig_conv2d_bwd_supported(cin, cout, hw, hw, 3, mode) == 1
+    x, w, b, dy = _data(cin, cout, hw, cin * 11 + cout + hw + mode)
+    xmax = _fwd_xmax(x, w, b, cin, cout, hw, 1 | mode) if mode == 128 else None
+    xd = x.double().cpu()
+    rdx = (torch.nn.grad.conv2d_input(xd.shape, w.double().cpu(), dy.double().cpu(), padding=1) + 0.5) * (xd > 0)
+    rdw = torch.nn.grad.conv2d_weight(xd, w.shape, dy.double().cpu(), padding=1)
+    for nmax in (2, 1024):
+        dx = torch.full((NF, cin, hw, hw), 0.5, device=DEV)
+        slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+        nb = ctypes.c_int(0)
+        L().paig_conv2d_bwd(p(x), cin * hw * hw, 0, 0, p(dy), cout * hw * hw, p(dx), cin * hw * hw, p(x),
+                            cin * hw * hw, p(w), p(slab), nmax, ctypes.byref(nb), NF, cin, cout, hw, hw, 3,
+                            mode | 4 | 2, p(xmax), XMAX if xmax is not None else 0, None, 0, None, 0, None, st())
+        g = _reduce(slab, nb.value, cout * cin * 9 + cout)
+        assert rel_err(dx, rdx) <= TOL_G[mode], ("dx", nmax)
+        assert rel_err(g[:cout * cin * 9].view_as(w), rdw) <= TOL_G[mode], ("dw", nmax)
+        assert rel_err(g[cout * cin * 9:], dy.double().cpu().sum((0, 2, 3))) <= 1e-5, ("db", nmax)
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(32, 16, 16), (16, 16, 32), (16, 16, 36), (32, 16, 18)])
+@pytest.mark.parametrize("mode", [128, 256])
+def test_fused_backward_upsample_many_tiles(cin, cout, hw, mode):
+    assert L().paig_conv2d_bwd_supported(cin, cout, hw, hw, 3, mode | 32) == 1
+    hs = hw // 2
+    xs, w, b, dy = _data(cin, cout, hw, cin + cout * 13 + hw + mode, hin=hs)
+    xmax = _fwd_xmax(xs, w, b, cin, cout, hw, 32 | mode, hin=hs) if mode == 128 else None
+    xr = xs.double().cpu().requires_grad_(True)
+    wr = w.double().cpu().requires_grad_(True)
+    F.conv2d(F.interpolate(xr, size=(hw, hw), mode="bilinear", align_corners=False), wr,
+             padding=1).backward(dy.double().cpu())
+    rdx = xr.grad * (xs.cpu() > 0)
+    for nmax in (2, 1024):
+        dx = torch.full((NF, cin, hs, hs), float("nan"), device=DEV)
+        slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+        nb = ctypes.c_int(0)
+        L().paig_conv2d_bwd(p(xs), cin * hs * hs, 0, 0, p(dy), cout * hw * hw, p(dx), cin * hs * hs, p(xs),
+                            cin * hs * hs, p(w), p(slab), nmax, ctypes.byref(nb), NF, cin, cout, hw, hw, 3,
+                            mode | 32 | 2, p(xmax), XMAX if xmax is not None else 0, None, 0, None, 0, None, st())
+        g = _reduce(slab, nb.value, cout * cin * 9 + cout)
+        assert rel_err(dx, rdx) <= TOL_G[mode], ("dx", nmax)
+        assert rel_err(g[:cout * cin * 9].view_as(w), wr.grad) <= TOL_G[mode], ("dw", nmax)
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(8, 8, 32), (16, 16, 16), (16, 16, 64), (8, 8, 36), (16, 16, 18)])
+@pytest.mark.parametrize("mode", [128, 256])
+def test_fused_backward_pool_fold_many_tiles(cin, cout, hw, mode):
+    assert L().paig_conv2d_bwd_supported(cin, cout, hw, hw, 3, mode | 64) == 1
+    x, w, b, gy = _data(cin, cout, hw, cin + cout + hw * 3 + mode)
+    hp = hw // 2
+    gp = torch.randn(NF, cout, hp, hp, device=DEV)
+    y, code, cfs, xmax = _pooled_forward(x, w, b, mode)
+    rdx, rdw, rdb = _pool_fold_ref(x, w, y, gy, gp)
+    for nmax in (2, 1024):
+        dx = torch.full((NF, cin, hw, hw), float("nan"), device=DEV)
+        slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+        nb = ctypes.c_int(0)
+        L().paig_conv2d_bwd(p(x), cin * hw * hw, 0, 0, p(gy), cout * hw * hw, p(dx), cin * hw * hw, p(x),
+                            cin * hw * hw, p(w), p(slab), nmax, ctypes.byref(nb), NF, cin, cout, hw, hw, 3,
+                            mode | 64 | 2, p(xmax) if mode == 128 else None, XMAX if mode == 128 else 0, p(gp),
+                            cout * hp * hp, p(code), cfs, None, st())
+        g = _reduce(slab, nb.value, cout * cin * 9 + cout)
+        assert rel_err(dx, rdx) <= TOL_G[mode], ("dx", nmax)
+        assert rel_err(g[:cout * cin * 9].view_as(w), rdw) <= TOL_G[mode], ("dw", nmax)
+        assert rel_err(g[cout * cin * 9:], rdb) <= 1e-5, ("db", nmax)
