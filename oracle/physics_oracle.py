@@ -46,10 +46,65 @@ class Cfg:
         self.Te = input_steps + pred_steps
         self.R = pred_steps + self.extrap_steps
         self.ae, self.alt_vel = ae, alt_vel
+        # "fp32": the reference's arithmetic.  "bf16": BASELINE config #2's
+        # (the HIP path's conv_math="bf16"): the U-Net convs' and the dense
+        # layers' (l1, l2, alt_vel's linear) matrix operands rounded to bf16
+        # (round to nearest even) in the forward, the data and the weight
+        # gradient, products accumulated in fp32; biases, bias gradients and
+        # everything else (softmax, c13's 1x1 head, l3, velocity MLP, physics,
+        # decoder) stay fp32 as in the reference.
+        self.operands = "fp32"
 
 
-def _conv(P, name, x, relu):
-    y = F.conv2d(x, P[name + ".weight"], P[name + ".bias"], padding="same")
+def _rb(t):
+    """fp32 -> bf16 (round to nearest even) -> fp32."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _ConvBF16(torch.autograd.Function):
+    """conv2d(x, w) + b, 3x3 or 1x1 "same", with bf16-rounded operands in all
+    three products (forward, data gradient, weight gradient), fp32 sums."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return F.conv2d(_rb(x), _rb(w), b, padding="same")
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        pad = w.shape[-1] // 2
+        dyb = _rb(dy)
+        dx = torch.nn.grad.conv2d_input(x.shape, _rb(w), dyb, padding=pad) if ctx.needs_input_grad[0] else None
+        dw = torch.nn.grad.conv2d_weight(_rb(x), w.shape, dyb, padding=pad)
+        return dx, dw, dy.sum((0, 2, 3))
+
+
+class _LinearBF16(torch.autograd.Function):
+    """x W^T + b with bf16-rounded operands in all three products."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return _rb(x) @ _rb(w).t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dyb = _rb(dy)
+        dx = dyb @ _rb(w) if ctx.needs_input_grad[0] else None
+        return dx, dyb.t() @ _rb(x), dy.sum(0)
+
+
+def _linear(x, w, b, bf16=False):
+    return _LinearBF16.apply(x, w, b) if bf16 else F.linear(x, w, b)
+
+
+def _conv(P, name, x, relu, bf16=False):
+    if bf16:
+        y = _ConvBF16.apply(x, P[name + ".weight"], P[name + ".bias"])
+    else:
+        y = F.conv2d(x, P[name + ".weight"], P[name + ".bias"], padding="same")
     return F.relu(y) if relu else y
 
 
@@ -59,59 +114,70 @@ def _up(x, size):
     return F.interpolate(x, size=(size, size), mode="bilinear", align_corners=False, antialias=True)
 
 
-def shallow_unet(P, x, p="encoder.shallow_unet"):
-    """nn/network/blocks.py:278-308 (note: c7/c10 un-ReLU'd, c13 ReLU'd, Q13)."""
+def shallow_unet(P, x, p="encoder.shallow_unet", bf16=False):
+    """nn/network/blocks.py:278-308 (note: c7/c10 un-ReLU'd, c13 ReLU'd, Q13).
+    bf16: c1..c12 with bf16 operands; the 1x1 head c13 in fp32 (the HIP
+    path's fused mask-softmax head computes it in fp32 FMAs)."""
     W = x.shape[-1]
-    h = _conv(P, p + ".c1", x, True)
-    x1 = _conv(P, p + ".c2", h, True)
+
+    def conv(name, h_, relu):
+        return _conv(P, name, h_, relu, bf16 and not name.endswith(".c13"))
+
+    h = conv(p + ".c1", x, True)
+    x1 = conv(p + ".c2", h, True)
     h = F.max_pool2d(x1, 2)
-    h = _conv(P, p + ".c3", h, True)
-    x2 = _conv(P, p + ".c4", h, True)
+    h = conv(p + ".c3", h, True)
+    x2 = conv(p + ".c4", h, True)
     h = F.max_pool2d(x2, 2)
-    h = _conv(P, p + ".c5", h, True)
-    h = _conv(P, p + ".c6", h, True)
-    h = _conv(P, p + ".c7", _up(h, W // 2), False)
+    h = conv(p + ".c5", h, True)
+    h = conv(p + ".c6", h, True)
+    h = conv(p + ".c7", _up(h, W // 2), False)
     h = torch.cat([h, x2], 1)
-    h = _conv(P, p + ".c8", h, True)
-    h = _conv(P, p + ".c9", h, True)
-    h = _conv(P, p + ".c10", _up(h, W), False)
+    h = conv(p + ".c8", h, True)
+    h = conv(p + ".c9", h, True)
+    h = conv(p + ".c10", _up(h, W), False)
     h = torch.cat([h, x1], 1)
-    h = _conv(P, p + ".c11", h, True)
-    h = _conv(P, p + ".c12", h, True)
-    return _conv(P, p + ".c13", h, True)
+    h = conv(p + ".c11", h, True)
+    h = conv(p + ".c12", h, True)
+    return conv(p + ".c13", h, True)
 
 
-def unet(P, x, p="encoder.unet"):
+def unet(P, x, p="encoder.unet", bf16=False):
     """nn/network/blocks.py:172-237 (upsamp=True; c9/c12/c15/c18 un-ReLU'd)."""
     W = x.shape[-1]
-    h = _conv(P, p + ".c1", x, True)
-    x1 = _conv(P, p + ".c2", h, True)
-    h = _conv(P, p + ".c3", F.max_pool2d(x1, 2), True)
-    x2 = _conv(P, p + ".c4", h, True)
-    h = _conv(P, p + ".c5", F.max_pool2d(x2, 2), True)
-    x3 = _conv(P, p + ".c6", h, True)
-    h = _conv(P, p + ".c7", F.max_pool2d(x3, 2), True)
-    h = _conv(P, p + ".c8", h, True)
-    h = _conv(P, p + ".c9", _up(h, W // 4), False)
+
+    def conv(name, h_, relu):
+        return _conv(P, name, h_, relu, bf16 and not name.endswith(".c18"))
+
+    h = conv(p + ".c1", x, True)
+    x1 = conv(p + ".c2", h, True)
+    h = conv(p + ".c3", F.max_pool2d(x1, 2), True)
+    x2 = conv(p + ".c4", h, True)
+    h = conv(p + ".c5", F.max_pool2d(x2, 2), True)
+    x3 = conv(p + ".c6", h, True)
+    h = conv(p + ".c7", F.max_pool2d(x3, 2), True)
+    h = conv(p + ".c8", h, True)
+    h = conv(p + ".c9", _up(h, W // 4), False)
     h = torch.cat([h, x3], 1)
-    h = _conv(P, p + ".c10", h, True)
-    h = _conv(P, p + ".c11", h, True)
-    h = _conv(P, p + ".c12", _up(h, W // 2), False)
+    h = conv(p + ".c10", h, True)
+    h = conv(p + ".c11", h, True)
+    h = conv(p + ".c12", _up(h, W // 2), False)
     h = torch.cat([h, x2], 1)
-    h = _conv(P, p + ".c13", h, True)
-    h = _conv(P, p + ".c14", h, True)
-    h = _conv(P, p + ".c15", _up(h, W), False)
+    h = conv(p + ".c13", h, True)
+    h = conv(p + ".c14", h, True)
+    h = conv(p + ".c15", _up(h, W), False)
     h = torch.cat([h, x1], 1)
-    h = _conv(P, p + ".c16", h, True)
-    h = _conv(P, p + ".c17", h, True)
-    return _conv(P, p + ".c18", h, False)
+    h = conv(p + ".c16", h, True)
+    h = conv(p + ".c17", h, True)
+    return conv(p + ".c18", h, False)
 
 
 def encoder(P, cfg, frames):
     """ConvolutionalEncoder.forward, nn/network/blocks.py:77-103.
     frames [N,C,H,W] -> enc_pos [N, 2K], enc_masks [N, K+1, H, W], masked objs list."""
     K, H = cfg.n_objs, cfg.size
-    logits = shallow_unet(P, frames) if H < 40 else unet(P, frames)
+    bf = getattr(cfg, "operands", "fp32") == "bf16"
+    logits = shallow_unet(P, frames, bf16=bf) if H < 40 else unet(P, frames, bf16=bf)
     logits = torch.cat([logits, torch.ones_like(logits[:, :1])], 1)
     masks = torch.softmax(logits, dim=1)
     objs = [masks[:, i:i + 1] * frames for i in range(K)]
@@ -119,8 +185,8 @@ def encoder(P, cfg, frames):
     if H >= 40:
         h = F.avg_pool2d(h, 2)
     h = h.reshape(h.shape[0], -1)
-    h = F.relu(F.linear(h, P["encoder.l1.weight"], P["encoder.l1.bias"]))
-    h = F.relu(F.linear(h, P["encoder.l2.weight"], P["encoder.l2.bias"]))
+    h = F.relu(_linear(h, P["encoder.l1.weight"], P["encoder.l1.bias"], bf))
+    h = F.relu(_linear(h, P["encoder.l2.weight"], P["encoder.l2.bias"], bf))
     h = F.linear(h, P["encoder.l3.weight"], P["encoder.l3.bias"])
     h = torch.cat(torch.split(h, h.shape[0] // K, 0), 1)
     return torch.tanh(h) * (H / 2) + H / 2, masks, objs
@@ -195,7 +261,8 @@ def velocity_encoder(P, cfg, pos_in):
     if cfg.alt_vel:
         d = pos_in[:, 1:] - pos_in[:, :-1]
         h = torch.cat(torch.chunk(d, K, dim=2), 0).reshape(K * pos_in.shape[0], (ins - 1) * 2)
-        h = F.linear(h, P["velocity_encoder.init_vel_linear.weight"], P["velocity_encoder.init_vel_linear.bias"])
+        h = _linear(h, P["velocity_encoder.init_vel_linear.weight"], P["velocity_encoder.init_vel_linear.bias"],
+                    getattr(cfg, "operands", "fp32") == "bf16")
     else:
         h = torch.cat(torch.chunk(pos_in, K, dim=2), 0).reshape(K * pos_in.shape[0], ins * 2)
         pfx = "velocity_encoder.init_vel_mlp."

@@ -31,8 +31,10 @@ IDS = [f"{c[0]}_B{c[6]}_{c[7]}" for c in FULL]
 GRAD_RTOL = 6e-6
 # bf16 operands are rounded per value (no data-dependent scales), so a half
 # batch rounds exactly as the full one; the sums only reassociate in fp32
-# accumulators, as in the split arithmetic
-GRAD_RTOL_BF16 = 2e-5
+# accumulators, as in the split arithmetic.  ~3x the worst measured on B=512
+# distinct sequences (2.2e-5, encoder.l1.weight: K = 10240 rows of bf16
+# products summed in fp32 in split-K slices)
+GRAD_RTOL_BF16 = 6e-5
 
 
 def _setup(task, cell, seq_len, ins, pred, size, B, conv_math):

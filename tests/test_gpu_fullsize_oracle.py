@@ -81,6 +81,21 @@ def _hip_step(m, x):
     return out, L, g, sse
 
 
+# the rollout-derived quantities (pos_vel_seq split into positions and
+# velocities, each against its own scale: VERDICT r05 weak 1d)
+ROLLOUT_KEYS = ("output_seq", "pos_vel_seq", "pos_vel_seq.pos", "pos_vel_seq.vel", "loss_extrap", "loss_train")
+
+
+def _rollout_parts(out, L):
+    """float64 numpy views of the rollout-derived outputs and losses."""
+    f = lambda t: t.detach().double().numpy() if torch.is_tensor(t) else np.asarray(t, dtype=np.float64)  # noqa: E731
+    pv = f(out["pos_vel_seq"])
+    D = pv.shape[-1] // 2
+    return {"output_seq": f(out["output_seq"]).reshape(-1), "pos_vel_seq": pv.reshape(-1),
+            "pos_vel_seq.pos": pv[..., :D], "pos_vel_seq.vel": pv[..., D:],
+            "loss_extrap": np.float64(float(L["extrap"])), "loss_train": np.float64(float(L["train"]))}
+
+
 def _full_check(tag, task, cell, seq_len, ins, pred, size, B, rollout_rtol=RTOL, seed=3, ensemble=ENSEMBLE_FULL,
                 vel_rtol=RTOL):
     """Whole-batch outputs / losses vs the fp32 oracle and every gradient
@@ -96,32 +111,45 @@ def _full_check(tag, task, cell, seq_len, ins, pred, size, B, rollout_rtol=RTOL,
     errs = {}
     for k in OUT_KEYS:
         errs[k] = rel_err(out[k].reshape(-1), o32[k].detach().double().numpy().reshape(-1))
-    # positions (0..size px) and velocities each against their own scale: the
-    # normwise error of the concatenation would let velocity errors hide
-    # under the positions' magnitude
-    pv, pv32 = out["pos_vel_seq"], o32["pos_vel_seq"].detach().double().numpy()
-    D = pv.shape[-1] // 2
-    errs["pos_vel_seq.pos"] = rel_err(pv[..., :D], pv32[..., :D])
-    errs["pos_vel_seq.vel"] = rel_err(pv[..., D:], pv32[..., D:])
+    hip_r = _rollout_parts(out, L)
+    r32 = _rollout_parts(o32, L32)
+    errs.update({k: rel_err(hip_r[k], r32[k]) for k in ("pos_vel_seq.pos", "pos_vel_seq.vel")})
     for k in ("train", "extrap", "recons"):
         errs["loss_" + k] = rel_err(np.float64(L[k]), np.float64(float(L32[k].detach())))
     del o32, L32
     print(tag, "outputs/losses vs fp32 oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
-    rollout = ("output_seq", "pos_vel_seq", "pos_vel_seq.pos", "loss_extrap", "loss_train")
-    over = {k: v for k, v in errs.items()
-            if v > (vel_rtol if k == "pos_vel_seq.vel" else rollout_rtol if k in rollout else RTOL)}
+    # everything the rollout does not amplify: 1e-4 (north star) against fp32
+    over = {k: v for k, v in errs.items() if k not in ROLLOUT_KEYS and v > RTOL}
     assert not over, over
-    # gradients, every element, against the float64 oracle with the fp32 envelope
-    _, _, g64 = O.train_step_f64(state, cfg, x)
+    # the rollout-derived outputs against the float64 oracle: bar = the fixed
+    # bar or ENVELOPE_K x the fp32 spread, whichever is larger.  The rollout
+    # amplifies last-bit differences: 3bp's gravity is chaotic, and a
+    # bouncing ball one ulp from a wall bounces one substep earlier or later
+    # in a distinct sequence, so honest fp32 runs (the oracle on one-ulp-
+    # perturbed weights) differ from float64 by more than 1e-4 there.
+    o64, L64, g64 = O.train_step_f64(state, cfg, x)
+    r64 = _rollout_parts(o64, L64)
+    del o64
     g64 = {k: v.detach().double().numpy() for k, v in g64.items()}
     assert sorted(g) == sorted(g64), set(g) ^ set(g64)
+    ospread = {k: rel_err(r32[k], r64[k]) for k in r64}
     spread = {k: rel_err(g32[k].detach().double().numpy(), g64[k]) for k in g64}
-    del g32
+    del g32, r32
     for s_ in range(ensemble):
-        gp = O.train_step(_ulp_perturbed(state, s_), cfg, x)[2]
+        op, Lp, gp = O.train_step(_ulp_perturbed(state, s_), cfg, x)
+        rp = _rollout_parts(op, Lp)
+        del op
+        for k in r64:
+            ospread[k] = max(ospread[k], rel_err(rp[k], r64[k]))
         for k in g64:
             spread[k] = max(spread[k], rel_err(gp[k].detach().double().numpy(), g64[k]))
-        del gp
+        del gp, rp
+    fixed = {k: vel_rtol if k == "pos_vel_seq.vel" else rollout_rtol for k in r64}
+    orow = {k: (rel_err(hip_r[k], r64[k]), ospread[k], max(fixed[k], ENVELOPE_K * ospread[k])) for k in r64}
+    print(tag, "rollout outputs vs float64 (hip, fp32 spread, bar):",
+          {k: tuple(f"{u:.2e}" for u in v) for k, v in orow.items()})
+    bad = {k: v for k, v in orow.items() if v[0] > v[2]}
+    assert not bad, bad
     rows = {k: (rel_err(g[k], g64[k]), spread[k], max(ENVELOPE_K * spread[k], ENVELOPE_FLOOR)) for k in g64}
     worst = max(rows.items(), key=lambda kv: kv[1][0] / kv[1][2])
     print(tag, "worst gradient (hip, fp32 spread, bar):", worst, f"({time.time() - t0:.0f} s)")
@@ -152,3 +180,31 @@ def test_config4_mnist_b256_matches_oracle():
 @pytest.mark.timeout(300)
 def test_config5_bouncing_b1024_r96_matches_oracle():
     _full_check("config #5", "bouncing_balls", "bouncing_ode_cell", 100, 4, 6, 32, 1024, seed=5)
+
+
+@pytest.mark.timeout(600)
+def test_config2_spring_bf16_b512_matches_bf16_oracle():
+    """Config #2 (spring_color bf16, B=512, seq 50) on the whole batch of
+    distinct sequences against the oracle in the same bf16-operand
+    arithmetic, within the bf16 envelope (tests/test_gpu_parity.py
+    bf16_envelope_check).  Weights: the fixtures' live-layer scaling
+    (tests/golden/weights.py), so every layer's bf16 rounding matters (at the
+    default initialisation the masks come out nearly uniform)."""
+    import time
+    from test_gpu_parity import bf16_envelope_check
+    from weights import golden_state
+    _threads()
+    t0 = time.time()
+    m, x, _, cfg = _model("spring_color", "spring_ode_cell", 50, 4, 6, 32, 512, seed=7)
+    sd = m.state_dict()
+    gs = golden_state({k: (tuple(v.shape), str(v.cpu().numpy().dtype)) for k, v in sd.items()}, 3)
+    m.load_state_dict({k: torch.from_numpy(v).to("cuda:0") for k, v in gs.items()})
+    state = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    m.conv_math = "bf16"
+    m.output = m(x.to("cuda:0"))
+    train_loss, (pred, extrap, recons) = m.compute_loss()
+    m.zero_grad(set_to_none=True)
+    train_loss.backward()
+    torch.cuda.synchronize()
+    bf16_envelope_check(m, x, state, cfg, train_loss, extrap, recons, "config #2", ensemble=3)
+    print(f"config #2: {time.time() - t0:.0f} s")

@@ -142,14 +142,64 @@ def test_two_steps_accumulate_and_rmsprop():
         assert rel_err(pd[k].detach(), rp.detach()) <= 1e-6, k
 
 
-# bf16 configuration (BASELINE config #2): bf16 conv operands, fp32 accumulate.
-# Not an fp32-parity mode: bars sized to bf16's 8-bit significand (measured
-# in emulation on the golden inputs: masks 5e-3, frames 2e-4, grads 9e-2).
-BF16_RTOL = {"out": 2e-2, "loss": 2e-3, "grad": 0.25}
+# bf16 configuration (BASELINE config #2, conv_math="bf16"): the U-Net convs'
+# and the dense layers' matrix operands in bf16, fp32 accumulation.  Checked
+# against the oracle in the SAME arithmetic (oracle Cfg.operands = "bf16":
+# every conv / l1 / l2 product's operands rounded to bf16 as the HIP kernels
+# round them, in the forward, the data and the weight gradients), on the
+# fixture's inputs and weights.  Two executions of that arithmetic differ by
+# more than fp32 reassociation: an activation that differs in its last fp32
+# bit is rounded to a different bf16 now and then, and the 12 bf16 layers
+# cascade such flips (the bf16 oracle itself on one-ulp-perturbed weights
+# moves the masks by 1.5e-3..3.7e-3 and the gradients by 1.8e-3..6.2e-3).  So
+# the bar is an envelope, as for fp32 (tests/test_gpu_envelope.py): per key,
+# the HIP error against the bf16 oracle <= BF16_K x the largest difference
+# of BF16_ENSEMBLE perturbed bf16-oracle runs from the unperturbed one.
+BF16_K = 3.0
+BF16_ENSEMBLE = 4
+BF16_FLOOR = 1e-6
+
+
+def bf16_envelope_check(m, x_cpu, state, cfg, train_loss, extrap, recons, tag, ensemble=BF16_ENSEMBLE):
+    """A HIP bf16 step (model m after forward + backward) against the bf16-
+    operand oracle on the same inputs and weights, within the bf16 envelope.
+    Returns {key: (hip error, oracle spread, bar)}."""
+    from envelope import _ulp_perturbed
+    from oracle import physics_oracle as O
+    cfg.operands = "bf16"
+
+    def flat(o, L, g):
+        d = {k: o[k].detach().double().numpy() for k in ("enc_pos", "enc_masks", "recons_out", "output_seq",
+                                                            "pos_vel_seq")}
+        d.update({"loss_" + k: np.float64(float(L[k])) for k in ("train", "extrap", "recons")})
+        d.update({"grad:" + k: v.detach().double().numpy() for k, v in g.items()})
+        return d
+
+    ref = flat(*O.train_step(state, cfg, x_cpu))
+    grads = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
+    hip = {"enc_pos": m.enc_pos, "enc_masks": m.enc_masks, "recons_out": m.recons_out, "output_seq": m.output,
+           "pos_vel_seq": m.pos_vel_seq, "loss_train": train_loss, "loss_extrap": extrap, "loss_recons": recons}
+    hip.update({"grad:" + k: v for k, v in grads.items()})
+    assert sorted(hip) == sorted(ref), set(hip) ^ set(ref)
+    hip = {k: v.detach().double().cpu().numpy().reshape(np.shape(ref[k])) for k, v in hip.items()}
+    spread = dict.fromkeys(ref, 0.0)
+    for s_ in range(ensemble):
+        mem = flat(*O.train_step(_ulp_perturbed(state, s_), cfg, x_cpu))
+        for k in ref:
+            spread[k] = max(spread[k], rel_err(mem[k], ref[k]))
+    rows = {k: (rel_err(hip[k], ref[k]), spread[k], max(BF16_K * spread[k], BF16_FLOOR)) for k in ref}
+    worst = max(rows.items(), key=lambda kv: kv[1][0] / kv[1][2])
+    print(tag, "bf16 vs bf16 oracle (hip, bf16 spread, bar):",
+          {k: tuple(f"{u:.1e}" for u in v) for k, v in rows.items() if not k.startswith("grad:")},
+          "worst (vs bar)", worst)
+    bad = {k: v for k, v in rows.items() if v[0] > v[2]}
+    assert not bad, bad
+    return rows
 
 
 @pytest.mark.parametrize("name", ["spring_s12", "spring_s50"])
-def test_step_bf16_config(name):
+def test_step_bf16_matches_bf16_oracle(name):
+    from oracle import physics_oracle as O
     dev = torch.device("cuda:0")
     z = load_golden(name)
     m = _model(z, dev)
@@ -160,9 +210,5 @@ def test_step_bf16_config(name):
     m.zero_grad(set_to_none=True)
     train_loss.backward()
     torch.cuda.synchronize()
-    for k, a in (("enc_pos", m.enc_pos), ("enc_masks", m.enc_masks), ("recons_out", m.recons_out),
-                 ("output_seq", m.output), ("pos_vel_seq", m.pos_vel_seq)):
-        assert rel_err(a, z[k]) <= BF16_RTOL["out"], k
-    assert rel_err(train_loss.reshape(()), z["loss_train"]) <= BF16_RTOL["loss"]
-    grads = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
-    grad_checks(z, grads, BF16_RTOL["grad"], prefix=name + " bf16: ")
+    cfg, _ = O.cfg_from_golden(z)
+    bf16_envelope_check(m, x.cpu(), golden_weights(z), cfg, train_loss, extrap, recons, name)
