@@ -188,6 +188,18 @@ def cpu_baseline(task, u8, ae, budget_s, seq_lens):
     for sl in seq_lens[1:]:
         out[f"value_seq{sl}"] = round(res[sl][0], 3)
         out[f"sample_seq{sl}"] = f"{res[sl][1]} steps x B={u8.shape[0]} at seq_len {sl} in {res[sl][2]:.1f}s"
+    # the reference's own code path is not on this box: its throughput
+    # relative to the oracle's, measured once on the build container's CPU
+    # (tools/time_reference.py, alternating steps), scales the oracle's value
+    try:
+        rows = json.load(open(os.path.join(PROFILES, "cpu_reference_vs_oracle.json")))["rows"]
+        r = rows.get(f"seq{sl0}")
+        if r:
+            out["oracle_over_reference"] = r["oracle_over_reference"]
+            out["reference_estimate"] = round(out["value"] / r["oracle_over_reference"], 3)
+            out["reference_ratio_source"] = "profiles/cpu_reference_vs_oracle.json (tools/time_reference.py)"
+    except (OSError, ValueError, KeyError):
+        pass
     return out
 
 

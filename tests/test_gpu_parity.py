@@ -155,9 +155,12 @@ def test_two_steps_accumulate_and_rmsprop():
 # the bar is an envelope, as for fp32 (tests/test_gpu_envelope.py): per key,
 # the HIP error against the bf16 oracle <= BF16_K x the largest difference
 # of BF16_ENSEMBLE perturbed bf16-oracle runs from the unperturbed one.
+# floors: fp32 reassociation alone (the bf16 members share one summation
+# order, so where bf16 rounding does not reach a key their spread is ~0):
+# 1e-6 on outputs / losses, 1e-5 on gradients (the fp32 fixture bar is 1e-4)
 BF16_K = 3.0
-BF16_ENSEMBLE = 4
-BF16_FLOOR = 1e-6
+BF16_ENSEMBLE = 8
+BF16_FLOOR = {"out": 1e-6, "grad": 1e-5}
 
 
 def bf16_envelope_check(m, x_cpu, state, cfg, train_loss, extrap, recons, tag, ensemble=BF16_ENSEMBLE):
@@ -187,7 +190,8 @@ def bf16_envelope_check(m, x_cpu, state, cfg, train_loss, extrap, recons, tag, e
         mem = flat(*O.train_step(_ulp_perturbed(state, s_), cfg, x_cpu))
         for k in ref:
             spread[k] = max(spread[k], rel_err(mem[k], ref[k]))
-    rows = {k: (rel_err(hip[k], ref[k]), spread[k], max(BF16_K * spread[k], BF16_FLOOR)) for k in ref}
+    rows = {k: (rel_err(hip[k], ref[k]), spread[k],
+                max(BF16_K * spread[k], BF16_FLOOR["grad" if k.startswith("grad:") else "out"])) for k in ref}
     worst = max(rows.items(), key=lambda kv: kv[1][0] / kv[1][2])
     print(tag, "bf16 vs bf16 oracle (hip, bf16 spread, bar):",
           {k: tuple(f"{u:.1e}" for u in v) for k, v in rows.items() if not k.startswith("grad:")},
