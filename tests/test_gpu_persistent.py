@@ -430,3 +430,116 @@ def test_fused_backward_pool_fold_many_tiles(cin, cout, hw, mode):
         assert rel_err(dx, rdx) <= TOL_G[mode], ("dx", nmax)
         assert rel_err(g[:cout * cin * 9].view_as(w), rdw) <= TOL_G[mode], ("dw", nmax)
         assert rel_err(g[cout * cin * 9:], rdb) <= 1e-5, ("db", nmax)
+
+
+# ------------------------------------------- co-resident blocks vs serial
+# Two (or more) persistent blocks per CU share its SIMDs; 2 blocks in the
+# whole grid run one per CU.  A defect that only shows when waves of two
+# blocks interleave on a SIMD (the round-5 DPP staging variant failed this
+# way) is caught by comparing the two launches of the
+# SAME kernel on frame counts that give >= 2 blocks per CU: forward / data
+# gradients must be bit-identical (each tile is formed the same way
+# whichever block walks it), weight gradients equal up to the fp32 order of
+# their slab partials.  (GPU-only comparison: no float64 reference needed at
+# these frame counts.)
+# weight gradients: the two launches partition the pixel sum differently
+# (and each block's running dY exponent follows its own tiles): measured
+# 3.0e-6 .. 1.1e-5 on the kept kernels; the round-5 DPP variant 2.2e-2 .. 2.8e-2
+COR_BAR = 3e-5
+
+
+def _frames_for(hw, tiles_per_frame):
+    return max(64, -(-1024 // tiles_per_frame))
+
+
+@pytest.mark.parametrize("cin,cout,hw,tpf", [(16, 16, 32, 4), (32, 16, 16, 1), (64, 32, 32, 4), (128, 32, 16, 1),
+                                             (16, 16, 36, 5)])
+def test_wgrad_fused_upsample_coresident_vs_serial(cin, cout, hw, tpf):
+    mode = 128
+    nf = _frames_for(hw, tpf)
+    hs = hw // 2
+    torch.manual_seed(cin + hw)
+    xs = torch.relu(torch.randn(nf, cin, hs, hs, device=DEV))
+    w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.1
+    b = torch.zeros(cout, device=DEV)
+    dy = torch.randn(nf, cout, hw, hw, device=DEV)
+    xmax = torch.zeros(XMAX, device=DEV)
+    y = torch.empty(nf, cout, hw, hw, device=DEV)
+    L().paig_conv2d_fwd_ex(p(xs), cin * hs * hs, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), nf, cin, cout, hw,
+                           hw, 3, 32 | mode, p(xmax), XMAX, st())
+    out = {}
+    for nmax in (2, 1024):
+        slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+        nb = ctypes.c_int(0)
+        L().paig_conv2d_wgrad_ex(p(xs), cin * hs * hs, 0, 0, p(dy), cout * hw * hw, p(slab), nmax, ctypes.byref(nb),
+                                 nf, cin, cout, hw, hw, 3, 32 | mode, p(xmax), XMAX, st())
+        out[nmax] = (_reduce(slab, nb.value, cout * cin * 9 + cout), nb.value)
+    print((cin, cout, hw), "frames", nf, "blocks", out[1024][1], "x slices")
+    g2, g = out[2][0], out[1024][0]
+    assert rel_err(g, g2.double().cpu()) <= COR_BAR
+    for c in range(cin):   # per input channel
+        ref = g2[:cout * cin * 9].view(cout, cin, 9)[:, c].double().cpu()
+        assert rel_err(g[:cout * cin * 9].view(cout, cin, 9)[:, c], ref) <= 10 * COR_BAR, c
+
+
+@pytest.mark.parametrize("cin,cout,hw,tpf,kind", [(16, 16, 32, 4, "up"), (32, 16, 16, 1, "up"), (24, 8, 32, 4, ""),
+                                                  (8, 8, 32, 4, "pool"), (16, 16, 16, 1, ""), (32, 16, 18, 2, "up")])
+def test_fused_backward_coresident_vs_serial(cin, cout, hw, tpf, kind):
+    mode = 128
+    nf = _frames_for(hw, tpf)
+    hin = hw // 2 if kind == "up" else hw
+    torch.manual_seed(cin * 3 + hw)
+    x = torch.relu(torch.randn(nf, cin, hin, hin, device=DEV))
+    w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.1
+    b = torch.randn(cout, device=DEV) * 0.1
+    dy = torch.randn(nf, cout, hw, hw, device=DEV)
+    fl = mode | (32 if kind == "up" else 0)
+    hp = hw // 2
+    gp = code = None
+    cfs = 0
+    if kind == "pool":
+        gp = torch.randn(nf, cout, hp, hp, device=DEV)
+        y, code, cfs, xmax = _pooled_forward(x, w, b, mode)
+    else:
+        xmax = torch.zeros(XMAX, device=DEV)
+        y = torch.empty(nf, cout, hw, hw, device=DEV)
+        L().paig_conv2d_fwd_ex(p(x), cin * hin * hin, 0, 0, p(y), cout * hw * hw, None, 0, p(w), p(b), nf, cin, cout,
+                               hw, hw, 3, fl, p(xmax), XMAX, st())
+    res = {}
+    for nmax in (2, 1024):
+        dx = torch.full((nf, cin, hin, hin), float("nan"), device=DEV)
+        slab = torch.empty(nmax * (cout * cin * 9 + cout), device=DEV)
+        nb = ctypes.c_int(0)
+        L().paig_conv2d_bwd(p(x), cin * hin * hin, 0, 0, p(dy), cout * hw * hw, p(dx), cin * hin * hin, p(x),
+                            cin * hin * hin, p(w), p(slab), nmax, ctypes.byref(nb), nf, cin, cout, hw, hw, 3,
+                            fl | 2 | (64 if kind == "pool" else 0), p(xmax), XMAX, p(gp), cout * hp * hp, p(code),
+                            cfs, None, st())
+        res[nmax] = (dx, _reduce(slab, nb.value, cout * cin * 9 + cout), nb.value)
+    print((cin, cout, hw, kind), "frames", nf, "blocks", res[1024][2])
+    assert torch.equal(res[2][0], res[1024][0]), "data gradient differs between co-resident and serial blocks"
+    assert rel_err(res[1024][1], res[2][1].double().cpu()) <= COR_BAR
+
+
+@pytest.mark.parametrize("cin,cout,hw,tpf,kind", [(16, 16, 32, 4, "up"), (32, 16, 16, 1, "up"), (24, 8, 32, 4, ""),
+                                                  (8, 8, 32, 4, "pool"), (48, 16, 64, 16, ""), (32, 32, 64, 16, "up")])
+def test_forward_coresident_vs_serial(cin, cout, hw, tpf, kind):
+    mode = 128
+    nf = _frames_for(hw, tpf)
+    hin = hw // 2 if kind == "up" else hw
+    torch.manual_seed(cin * 5 + hw)
+    x = torch.relu(torch.randn(nf, cin, hin, hin, device=DEV))
+    w = torch.randn(cout, cin, 3, 3, device=DEV) * 0.1
+    b = torch.randn(cout, device=DEV) * 0.1
+    hp = hw // 2
+    cfs = -(-cout // 8) * 8 * hp * hp
+
+    def run():
+        out = torch.full((nf, cout, hw, hw), float("nan"), device=DEV)
+        pool = torch.zeros(nf, cout, hp, hp, device=DEV)
+        code = torch.zeros(nf * cfs, dtype=torch.uint8, device=DEV)
+        fl = 1 | mode | (32 if kind == "up" else 0) | (64 if kind == "pool" else 0)
+        L().paig_conv2d_fwd_pwc(p(x), cin * hin * hin, 0, 0, p(out), cout * hw * hw, None, 0, p(w), p(b), nf, cin,
+                                cout, hw, hw, 3, fl, None, 0, p(pool) if kind == "pool" else None, cout * hp * hp,
+                                p(code) if kind == "pool" else None, cfs, None, st())
+        return out, pool, code
+    _both_caps(run)
