@@ -114,6 +114,9 @@ def parse():
                     help="capture the step as two HIP graphs split where the early gradient bucket is final, and "
                          "all-reduce that bucket between the replays, overlapping the U-Net backward "
                          "(-1: on when N > 1)")
+    ap.add_argument("--byte_targets", type=int, default=1,
+                    help="decoders read their targets as the dataset's bytes; the gather converts only the "
+                         "encoder's frames (DeviceDataIterator.bind_targets, bit-identical)")
     ap.add_argument("--conv_math", default="split", choices=["split", "fp32", "bf16"],
                     help="U-Net conv arithmetic: split = f16/bf16 hi+lo operands on the 16-bit matrix cores, "
                          "fp32-accurate (meets the 1e-4 parity bar; default); fp32 = f32-input MFMA; "
@@ -248,6 +251,8 @@ def run_workload(a, world, rank, dev, task, batch, seq_len, conv_math, steps, wa
     gstep = GraphStep(m, xbuf, world, split=None if a.split_graph < 0 else bool(a.split_graph), graph=bool(a.graph),
                       optimizer_in_graph=bool(a.graph_optimizer))
     eng = gstep.eng
+    if a.byte_targets:
+        eng.byte_targets = it.bind_targets(xbuf, ins + pred)
 
     def eager_step():
         it.next_batch(batch, out=xbuf)
@@ -294,7 +299,7 @@ def run_workload(a, world, rank, dev, task, batch, seq_len, conv_math, steps, wa
     eng.probe = None
     kds = probe.summaries()
     res = {"value": world * batch * steps / el, "el": el, "med_ms": med_ms, "loss": lossv, "kds": kds, "split": gstep.split,
-           "opt_in_graph": gstep.opt_in_graph, "dataset_seqs": int(u8.shape[0]), "ins": ins, "pred": pred, "size": size,
+           "opt_in_graph": gstep.opt_in_graph, "byte_targets": eng.byte_targets is not None, "dataset_seqs": int(u8.shape[0]), "ins": ins, "pred": pred, "size": size,
            "u8_head": u8[:100]}
     del gstep, m, eng, it, xbuf
     torch.cuda.synchronize()
@@ -500,7 +505,8 @@ def main():
                                    f"({ins} in / {pred} pred / {a.seq_len - ins - pred} extrap)",
                        "global_batch": world * a.batch, "seq_len": a.seq_len, "parallelism": f"dp{world}",
                        "conv_math": a.conv_math, "split_graph": r["split"],
-                       "optimizer_in_graph": r["opt_in_graph"], "dataset_seqs": r["dataset_seqs"]},
+                       "optimizer_in_graph": r["opt_in_graph"], "byte_targets": r["byte_targets"],
+                       "dataset_seqs": r["dataset_seqs"]},
             "roofline": roof, "roofline_headline": headline_roof(kds, a.conv_math), "roofline_others": others, "cpu_baseline": cpu, "final_loss": round(r["loss"], 4),
             # whole-step memory-side traffic (committed PMC profile) at this run's step time
             "hbm_step": None if step_bytes is None else {

@@ -31,7 +31,7 @@ extern "C" {
 /* Version of this interface: bumped whenever an entry point's argument list
  * or a data layout it exchanges changes (the Python binding refuses a library
  * of another version). */
-#define PAIG_ABI_VERSION 3
+#define PAIG_ABI_VERSION 4
 const char* paig_last_error(void);
 int paig_abi_version(void);
 /* f16 range guard of the split-precision path.  Activations and gradients
@@ -504,6 +504,16 @@ int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner,
  * rollout decode's pred_steps, physics_models.py:129-139): the others get
  * dpos = 0 and are not read.  Partial source gradients: one slab row of
  * paig_decoder_slab_len floats per block, paig_decoder_bwd_blocks rows. */
+/* the same decode with uint8 targets read from the device-resident dataset
+ * (byte / 255, bit-identical to the gathered fp32 frames): tgt is the dataset
+ * base (+ the frame offset in bytes), tgt_idx (nullable; grouped targets only)
+ * the dataset row of each target sequence as paig_gather_u8_f32_ex saved it,
+ * tgt_fs / tgt_gs in bytes.  The one-CU kernels only, (K, H) in {(2, 32),
+ * (3, 36), (2, 64)}, 4-byte aligned frames; an SSE output is required. */
+int paig_decoder_fwd_t8(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                        const float* cont, const float* bg, float* out, long long out_fs, const unsigned char* tgt,
+                        const long long* tgt_idx, long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F,
+                        int K, int h, int H, void* stream);
 int paig_decoder_bwd_blocks(int F, int pos_grp, int live, int K, int h, int H);
 size_t paig_decoder_slab_len(int K, int h, int H);
 size_t paig_decoder_bwd_scratch(int F, int K, int h, int H);
@@ -511,6 +521,12 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
                      const float* cont, const float* bg, const float* tgt, long long tgt_fs, int tgt_grp,
                      long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
                      float* slab, float* scratch, int F, int live, int K, int h, int H, void* stream);
+/* byte targets, as paig_decoder_fwd_t8 */
+int paig_decoder_bwd_t8(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                        const float* cont, const float* bg, const unsigned char* tgt, const long long* tgt_idx,
+                        long long tgt_fs, int tgt_grp, long long tgt_gs, const float* dsse, const float* dout,
+                        long long dout_fs, float* dpos, float* slab, float* scratch, int F, int live, int K, int h,
+                        int H, void* stream);
 
 /* the decoder's per-object intermediates (transf_contents / transf_masks,
  * physics_models.py:186-196) for positions pos [F][2K] (row stride
@@ -553,6 +569,11 @@ int paig_frame_sse_bwd(const float* a, long long a_fs, int a_grp, long long a_gs
  * out[b][:] = float(src[idx[b]][:]) / 255 for a uint8 dataset of `row`-byte
  * sequences (T*H*W*C; multiple of 16); idx: device int64[B] */
 int paig_gather_u8_f32(const unsigned char* src, const long long* idx, float* out, int B, long long row, void* stream);
+/* only the first `head` bytes of every row (the frames the encoder reads; a
+ * multiple of 16), the rest of out's rows untouched; idx_out (nullable,
+ * device int64[B]) receives idx[0:B] for the decoders' byte targets */
+int paig_gather_u8_f32_ex(const unsigned char* src, const long long* idx, float* out, int B, long long row,
+                          long long head, long long* idx_out, void* stream);
 
 /* ---- optimizers over the flat parameter buffer (base.py:12-17, torch defaults) */
 int paig_rmsprop_f32(float* p, const float* g, float* sa, long long n, float lr, float alpha, float eps, void* stream);

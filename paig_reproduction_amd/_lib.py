@@ -17,7 +17,7 @@ XMAX_SLOTS = 2048
 
 AB_PATH = os.environ.get("PAIG_AB_LIB")
 # include/paig_hip.h PAIG_ABI_VERSION: the SIGNATURES below are this version's
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -46,6 +46,7 @@ SIGNATURES = {
                             P, P]),
     "paig_conv2d_fwd_pwc": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P, LL, P, LL, P, P]),
     "paig_gather_u8_f32": (I, [P, P, P, I, LL, P]),
+    "paig_gather_u8_f32_ex": (I, [P, P, P, I, LL, LL, P, P]),
     "paig_velmlp_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "paig_velmlp_vfn_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P]),
     "paig_velmlp_bwd_blocks": (I, [I]),
@@ -111,10 +112,12 @@ SIGNATURES = {
     "paig_rollout_bwd_blocks": (I, [I]),
     "paig_rollout_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P]),
     "paig_decoder_fwd": (I, [P, LL, LL, I, P, P, P, P, LL, P, LL, I, LL, P, I, I, I, I, P]),
+    "paig_decoder_fwd_t8": (I, [P, LL, LL, I, P, P, P, P, LL, P, P, LL, I, LL, P, I, I, I, I, P]),
     "paig_decoder_bwd_blocks": (I, [I, I, I, I, I, I]),
     "paig_decoder_slab_len": (SZ, [I, I, I]),
     "paig_decoder_bwd_scratch": (SZ, [I, I, I, I]),
     "paig_decoder_bwd": (I, [P, LL, LL, I, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, I, P]),
+    "paig_decoder_bwd_t8": (I, [P, LL, LL, I, P, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, I, P]),
     "paig_decoder_parts": (I, [P, LL, P, P, P, P, P, I, I, I, I, P]),
     "paig_stn_fwd": (I, [P, P, P, I, I, I, I, I, I, P]),
     "paig_stn_bwd": (I, [P, P, P, P, P, I, I, I, I, I, I, P]),

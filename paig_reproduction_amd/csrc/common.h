@@ -51,6 +51,17 @@ struct FView {
   }
 };
 
+// v / 255 correctly rounded (= IEEE division, as numpy) for v in 0..255:
+// the reciprocal product plus one fma correction of its exact residual
+// (checked for all 256 values by tests/test_device_data.py).  The batch
+// gather and the decoders' uint8 targets both use it, so a target read from
+// the bytes equals the gathered fp32 value bit for bit.
+__device__ __forceinline__ float div255(float v) {
+  constexpr float r = 1.0f / 255.0f;
+  const float q = v * r;
+  return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, v), r, q);
+}
+
 struct FViewW {
   float* p;
   long long fs;

@@ -13,25 +13,21 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// v / 255 correctly rounded (= IEEE division, as numpy) for v in 0..255:
-// the reciprocal product plus one fma correction of its exact residual
-// (checked for all 256 values by tests/test_device_data.py)
-__device__ __forceinline__ float div255(float v) {
-  constexpr float r = 1.0f / 255.0f;
-  const float q = v * r;
-  return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, v), r, q);
-}
-
 // One 4-byte word -> one float4 per lane: each wave instruction reads 256
 // contiguous bytes and writes 1 KB contiguous (the 16-byte-word-per-lane form
 // wrote 16 B at a 64-B lane stride, four partial passes over every line).
+// Rows of `row` bytes; only the first `head` bytes of each are converted
+// (head = row: the whole sequence).  idx_out (nullable) receives the batch's
+// row indices, for decoders that read the remaining frames as bytes.
 __global__ void __launch_bounds__(256)
 gather_u8_f32_k(const uint8_t* __restrict__ src, const long long* __restrict__ idx, float* __restrict__ out,
-                long long row) {
+                long long row, long long head, long long* __restrict__ idx_out) {
   const int b = blockIdx.y;
-  const unsigned* s = reinterpret_cast<const unsigned*>(src + idx[b] * row);
+  const long long r = idx[b];
+  if (idx_out && blockIdx.x == 0 && threadIdx.x == 0) idx_out[b] = r;
+  const unsigned* s = reinterpret_cast<const unsigned*>(src + r * row);
   f32x4* o = reinterpret_cast<f32x4*>(out + (long long)b * row);
-  const long long n4 = row / 4;
+  const long long n4 = head / 4;
   const long long step = (long long)gridDim.x * blockDim.x;
   long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   for (; i + 3 * step < n4; i += 4 * step) {   // four words in flight per lane
@@ -59,16 +55,24 @@ gather_u8_f32_k(const uint8_t* __restrict__ src, const long long* __restrict__ i
 
 extern "C" {
 
-int paig_gather_u8_f32(const unsigned char* src, const long long* idx, float* out, int B, long long row,
-                       void* stream) {
+int paig_gather_u8_f32_ex(const unsigned char* src, const long long* idx, float* out, int B, long long row,
+                          long long head, long long* idx_out, void* stream) {
   if (B <= 0 || row <= 0) return 0;
   PAIG_REQUIRE(((uintptr_t)src % 16) == 0 && ((uintptr_t)out % 16) == 0 && row % 16 == 0,
                "gather_u8_f32: src/out must be 16-byte aligned and row (%lld) a multiple of 16", row);
-  long long per = (row / 16 + 255) / 256;   // blocks for four words per lane
-  const unsigned gx = (unsigned)(per < 64 ? per : 64);
-  hipLaunchKernelGGL(gather_u8_f32_k, dim3(gx, B), dim3(256), 0, (hipStream_t)stream, src, idx, out, row);
+  PAIG_REQUIRE(head >= 0 && head <= row && head % 16 == 0,
+               "gather_u8_f32: head (%lld) must be a multiple of 16 within the row (%lld)", head, row);
+  long long per = (head / 16 + 255) / 256;   // blocks for four words per lane
+  const unsigned gx = (unsigned)(per < 1 ? 1 : per < 64 ? per : 64);
+  hipLaunchKernelGGL(gather_u8_f32_k, dim3(gx, B), dim3(256), 0, (hipStream_t)stream, src, idx, out, row, head,
+                     idx_out);
   PAIG_CHECK_LAUNCH();
   return 0;
+}
+
+int paig_gather_u8_f32(const unsigned char* src, const long long* idx, float* out, int B, long long row,
+                       void* stream) {
+  return paig_gather_u8_f32_ex(src, idx, out, B, row, row, nullptr, stream);
 }
 
 }  // extern "C"

@@ -632,12 +632,56 @@ __device__ __forceinline__ int gslot(int j) { return (j & 1) * (H / 2) + (j >> 1
 struct DecCursor {
   int f, pq, pr, tq, tr;
 };
+// The decoders' targets: fp32 frames (p), or the uint8 dataset rows the batch
+// was gathered from (p8: the device-resident dataset's NHWC bytes, in the flat
+// order Q5's reshape keeps, so element offsets are the fp32 view's; ix: the
+// batch's dataset row per sequence, as paig_gather_u8_f32_ex saved it, or null
+// for sequence q at q * fs).  A byte target is byte / 255 exactly as the
+// gather forms it (div255): bit-identical losses and gradients from a quarter
+// of the bytes, and the gather need not write the frames only the decoders
+// read.  Uniform per launch.
+struct TView {
+  const float* p;
+  const unsigned char* p8;
+  const long long* ix;
+  long long fs, gs;
+  int grp;
+  // T8 (a template parameter of the kernels that read targets): p8, else p.
+  // raw*: the value as loaded (T8: the byte / the 4-byte word in the float's
+  // bits), no arithmetic on it, so a prefetched target's load stays in flight
+  // until val* converts it where it is used
+  template <bool T8>
+  __device__ __forceinline__ float raw1(long long o) const {
+    if constexpr (T8) return __int_as_float((int)p8[o]);
+    else return p[o];
+  }
+  template <bool T8>
+  __device__ __forceinline__ static float val1(float r) {
+    if constexpr (T8) return div255((float)__float_as_int(r));
+    else return r;
+  }
+  template <bool T8>
+  __device__ __forceinline__ float4 raw4(long long o) const {
+    if constexpr (T8) return make_float4(__int_as_float(*reinterpret_cast<const int*>(p8 + o)), 0.f, 0.f, 0.f);
+    else return *reinterpret_cast<const float4*>(p + o);
+  }
+  template <bool T8>
+  __device__ __forceinline__ static void val4(float4 r, float* v) {
+    if constexpr (T8) {
+      const unsigned w = (unsigned)__float_as_int(r.x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = div255((float)((w >> (8 * e)) & 255u));
+    } else {
+      v[0] = r.x, v[1] = r.y, v[2] = r.z, v[3] = r.w;
+    }
+  }
+};
 struct DecFrames {
   PosView pos;
-  FView tgt;
+  TView tgt;
   int R, Rl;
   bool grouped;
-  __device__ DecFrames(PosView p, FView t, int rl) : pos(p), tgt(t), R(p.grp), Rl(rl) {
+  __device__ DecFrames(PosView p, TView t, int rl) : pos(p), tgt(t), R(p.grp), Rl(rl) {
     grouped = R > 0 && Rl > 0 && Rl < R;
   }
   __device__ int live(int F) const { return grouped ? (F / R) * Rl : F; }
@@ -682,8 +726,44 @@ struct DecFrames {
     return pos.grp > 0 ? pos.p + (long long)c.pq * pos.outer + (long long)c.pr * pos.inner
                        : pos.p + (long long)c.f * pos.inner;
   }
-  __device__ const float* tgt_of(const DecCursor& c) const {
-    return tgt.grp > 0 ? tgt.p + (long long)c.tq * tgt.fs + (long long)c.tr * tgt.gs : tgt.p + (long long)c.f * tgt.fs;
+  // Row indices of the block's target sequences (T8 with tgt.ix): frames
+  // first .. first+nf-1 span sequences q0 .. (the first IXN of them staged).
+  // ix_load at the top of a kernel puts this thread's entry and the first
+  // frame's row in flight across the prologue; ix_store, before the
+  // prologue's barrier, publishes the entries in LDS, where tgt_off reads
+  // them: no frame's target loads wait on a dependent global load.
+  static constexpr int IXN = 32;
+  struct IxStage {
+    int q0 = 0, span = 0;
+    long long mine = 0, row0 = 0;
+  };
+  template <bool T8>
+  __device__ IxStage ix_load(int first, int nf, int tid) const {
+    IxStage st;
+    if (!T8 || !tgt.ix || nf <= 0 || tgt.grp <= 0) return st;
+    st.q0 = at(first).tq;
+    st.span = at(first + nf - 1).tq - st.q0 + 1;
+    if (tid < st.span && tid < IXN) st.mine = tgt.ix[st.q0 + tid];
+    st.row0 = tgt.ix[st.q0];
+    return st;
+  }
+  __device__ void ix_store(const IxStage& st, long long* ixs, int tid) const {
+    if (tid < st.span && tid < IXN) ixs[tid] = st.mine;
+  }
+  // the first frame's target offset from the row ix_load fetched
+  template <bool T8>
+  __device__ long long tgt_off0(const DecCursor& c, const IxStage& st) const {
+    if (T8 && tgt.ix && tgt.grp > 0) return st.row0 * tgt.fs + (long long)c.tr * tgt.gs;
+    return tgt_off<T8>(c);
+  }
+  // element offset of the target frame (of p or p8); ixs: the staged row
+  // indices (null before the barrier that publishes them)
+  template <bool T8>
+  __device__ long long tgt_off(const DecCursor& c, const long long* ixs = nullptr, int q0 = 0) const {
+    if (tgt.grp <= 0) return (long long)c.f * tgt.fs;
+    long long q = c.tq;
+    if (T8 && tgt.ix) q = ixs && c.tq - q0 < IXN ? ixs[c.tq - q0] : tgt.ix[c.tq];
+    return q * tgt.fs + (long long)c.tr * tgt.gs;
   }
 };
 
@@ -766,9 +846,9 @@ __device__ unsigned long long paig_dec_stamps[4][16][33][6];
   } while (0)
 #endif
 
-template <int K, int H>
+template <int K, int H, bool T8>
 __global__ void __launch_bounds__((DecCu<K, H>::NT))
-dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
+dec_bwd_cu_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
              float* __restrict__ slab, int F, int Rl, int FPB) {
   using C = DecCu<K, H>;
   constexpr int h = C::h, hp = C::hp, hh = C::hh, HW = C::HW, PS = C::PS, NIT = C::NIT, GPITCH = C::GPITCH;
@@ -781,6 +861,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
   __shared__ float WT[3][K][2][h][GW];            //   of the 5-wide window and its weights
   __shared__ double RED[2][2 * K][NR];            // fp64 position-gradient partials (RPW per wave)
   __shared__ double BC[H];                        // affine_grid base coordinates (fp64, frame-invariant)
+  __shared__ long long IXS[DecFrames::IXN];       // byte targets' dataset rows (ix_load / ix_store)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int R = pos.grp;
@@ -791,10 +872,11 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
 
   // ---- frame cursors (wave-uniform)
   const DecFrames FR(pos, tgt, Rl);
+  const auto ixst = FR.template ix_load<T8>(first, nf, tid);
+  const int q0 = ixst.q0;
   auto cur_at = [&](int n) { return FR.at(n); };
   auto advance = [&](DecCursor c) { return FR.next(c); };
   auto pos_of = [&](const DecCursor& c) { return FR.pos_of(c); };
-  auto tgt_of = [&](const DecCursor& c) { return FR.tgt_of(c); };
 
   // ---- prologue: frame 0's loads first (their latency overlaps the staging below)
   float bgv[PS][3], gbg[PS][3], tn[PS][3];
@@ -817,14 +899,16 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
       gather_entry(l, BC, H, h, cj, &J0[gslot_][ck][cax][cj], WT[gslot_][ck][cax][cj]);
     }
   };
-  auto fetch = [&](const DecCursor& c) {   // targets -> tn (no SSE weight: none read)
+  // targets -> tn (no SSE weight: none read); staged: the row from IXS, else
+  // (the block's first frame) from ix_load
+  auto fetch = [&](const DecCursor& c, bool staged) {
     if (dsse == nullptr) return;
-    const float* tf = tgt_of(c);
+    const long long to = staged ? FR.template tgt_off<T8>(c, IXS, q0) : FR.template tgt_off0<T8>(c, ixst);
 #pragma unroll
     for (int s = 0; s < PS; ++s) {
       const int p = tid + NT * s;
 #pragma unroll
-      for (int ch = 0; ch < 3; ++ch) tn[s][ch] = p < HW ? tf[ch * HW + p] : 0.f;
+      for (int ch = 0; ch < 3; ++ch) tn[s][ch] = p < HW ? FR.tgt.template raw1<T8>(to + ch * HW + p) : 0.f;
     }
   };
   auto is_active = [&](float w) { return w != 0.f || dout.p != nullptr; };
@@ -839,7 +923,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
 #pragma unroll
     for (int c = 0; c < 3; ++c) tn[s2][c] = 0.f;
   if (nf > 0) {
-    fetch(ccur);
+    if constexpr (!T8) fetch(ccur, false);
     p0 = pos_of(ccur)[2 * ck + cax];
     ppos = pos_of(c1)[2 * ck + cax];
     w_cur = dsse != nullptr ? uniform_f(dsse[ccur.f]) : 0.f;
@@ -879,6 +963,10 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
       const int b = e / per, rem = e - b * per;
       dpos[((long long)b * R + Rl + rem / (2 * K)) * 2 * K + rem % (2 * K)] = 0.f;
     }
+  }
+  if constexpr (T8) {   // (byte targets: the row load was in flight across the staging above)
+    FR.ix_store(ixst, IXS, tid);
+    if (nf > 0) fetch(ccur, false);
   }
   __syncthreads();   // SRC, BC
   if (nf > 0) tables(p0, 0, 0);
@@ -1040,7 +1128,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
           float g[3];
   #pragma unroll
           for (int c = 0; c < 3; ++c) {
-            g[c] = w_f * (o[c] - tn[s][c]);
+            g[c] = w_f * (o[c] - TView::val1<T8>(tn[s][c]));
             if (dof) g[c] += dof[c * HW + p];
             gbg[s][c] = fmaf(m[K], g[c], gbg[s][c]);
           }
@@ -1123,7 +1211,7 @@ dec_bwd_cu_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FVie
       ccur = c1;
       c1 = c2;
       if (it + 3 < nf) c2 = advance(c2);
-      fetch(ccur);
+      fetch(ccur, true);
       w_cur = uniform_f(wnext);
       act_cur = is_active(w_cur);
     } else {
@@ -1195,9 +1283,9 @@ struct DecBand {
                 "decoder band geometry");
 };
 
-template <int K, int H>
+template <int K, int H, bool T8>
 __global__ void __launch_bounds__(1024)
-dec_bwd_band_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
+dec_bwd_band_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
                float* __restrict__ slab, int F, int Rl, int FPB) {
   using C = DecBand<K, H>;
   constexpr int h = C::h, hp = C::hp, hh = C::hh, HW = C::HW, NT = C::NT, PS = C::PS, BR = C::BR;
@@ -1210,6 +1298,7 @@ dec_bwd_band_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FV
   __shared__ float WT[K][2][h][GW];            //   and its weights
   __shared__ double RED[2 * K][NR];
   __shared__ double BC[H];
+  __shared__ long long IXS[DecFrames::IXN];    // byte targets' dataset rows (ix_load / ix_store)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int R = pos.grp;
@@ -1218,6 +1307,8 @@ dec_bwd_band_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FV
   const int first = blockIdx.x * FPB;
   const int nf = first < NL ? (NL - first < FPB ? NL - first : FPB) : 0;
   const DecFrames FR(pos, tgt, Rl);
+  const auto ixst = FR.template ix_load<T8>(first < NL ? first : 0, nf, tid);
+  const int q0 = ixst.q0;
 
   const int tg = tid - TG0;
   const bool is_c = tid < NC, is_g = tg >= 0 && tg < NG;
@@ -1254,6 +1345,7 @@ dec_bwd_band_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FV
       dpos[((long long)b * R + Rl + rem / (2 * K)) * 2 * K + rem % (2 * K)] = 0.f;
     }
   }
+  if constexpr (T8) FR.ix_store(ixst, IXS, tid);
   __syncthreads();   // SRC, BC
 
   for (int it = 0; it < nf; ++it) {
@@ -1265,7 +1357,7 @@ dec_bwd_band_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FV
       cur = nxt;
       continue;
     }
-    const float* tf = FR.tgt_of(cur);
+    const long long to = FR.template tgt_off<T8>(cur, IXS, q0);
     // ---- the frame's axis and gather tables (the previous frame's last
     // barrier ordered every read of the old ones)
     if (is_c || is_g) {
@@ -1295,7 +1387,7 @@ dec_bwd_band_k(PosView pos, Src S, FView tgt, const float* __restrict__ dsse, FV
       float tq[3] = {0.f, 0.f, 0.f};
       if (dsse != nullptr)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) tq[c] = tf[c * HW + p];
+        for (int c = 0; c < 3; ++c) tq[c] = TView::val1<T8>(FR.tgt.template raw1<T8>(to + c * HW + p));
       float sv[K][4];
       // the texels of object k and their bilinear (derivative) weights
       auto texels = [&](int k, float4& ax, float4& ay, float (*tv)[4]) __attribute__((always_inline)) {
@@ -1512,9 +1604,9 @@ __device__ __forceinline__ int b128_rank(int l) {
   return (l & 32) + g * 16 + r;
 }
 
-template <int K, int H>
+template <int K, int H, bool T8>
 __global__ void __launch_bounds__((DecFw<K, H>::NT))
-dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse, int F, int FPB) {
+dec_fwd_cu_k(PosView pos, Src S, FViewW out, TView tgt, float* __restrict__ sse, int F, int FPB) {
   using C = DecFw<K, H>;
   constexpr int h = C::h, hp = C::hp, HW = C::HW, GPR = C::GPR, NC = C::NC, NW = C::NW, P = C::P;
   __shared__ float4 SRC[K][hp * P];     // (template + 5, sigmoid(content) x 3), zero border, split rows
@@ -1522,12 +1614,15 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
   __shared__ float4 AXR[2][K][H];       // row: w0, w1, texel-row offset (bits), -
   __shared__ float RED[2][NW];          // per-wave SSE partials
   __shared__ double BC[H];
+  __shared__ long long IXS[DecFrames::IXN];   // byte targets' dataset rows (ix_load / ix_store)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int first = blockIdx.x * FPB;
   const int nf = first < F ? (F - first < FPB ? F - first : FPB) : 0;
   if (nf == 0) return;   // block-uniform
   const DecFrames FR(pos, tgt, 0);
+  const auto ixst = FR.template ix_load<T8>(first, nf, tid);
+  const int q0 = ixst.q0;
   const int n = wv * 64 + b128_rank(lane);   // this thread's pixel quad
   const bool px = n < C::NGRP;
   const int i = px ? n / GPR : 0, g = px ? n % GPR : 0, p = i * H + 4 * g;
@@ -1537,16 +1632,16 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
 
   auto ld4 = [&](const float* b) { return *reinterpret_cast<const float4*>(b); };
   float4 tn[3], bgv[3];
-  auto fetch = [&](const DecCursor& c, float4* t) {
+  auto fetch = [&](const DecCursor& c, float4* t, bool staged) {
     if (!has_t || !px) return;
-    const float* tf = FR.tgt_of(c) + p;
+    const long long to = (staged ? FR.template tgt_off<T8>(c, IXS, q0) : FR.template tgt_off0<T8>(c, ixst)) + p;
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) t[ch] = ld4(tf + ch * HW);
+    for (int ch = 0; ch < 3; ++ch) t[ch] = FR.tgt.template raw4<T8>(to + ch * HW);
   };
   DecCursor ccur = FR.at(first);
   DecCursor c1 = nf > 1 ? FR.next(ccur) : ccur;
   DecCursor c2 = nf > 2 ? FR.next(c1) : c1;
-  fetch(ccur, tn);
+  if constexpr (!T8) fetch(ccur, tn, false);
   float p0 = 0.f, ppos = 0.f;
   if (is_c) {
     p0 = FR.pos_of(ccur)[2 * ck + cax];
@@ -1577,6 +1672,10 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
         AXR[slot][ck][cj] = make_float4(x.w0, x.w1, __int_as_float(x.c * P), 0.f);
     }
   };
+  if constexpr (T8) {   // (byte targets: the row load was in flight across the staging above)
+    FR.ix_store(ixst, IXS, tid);
+    fetch(ccur, tn, false);
+  }
   __syncthreads();   // SRC, BC
   tables(p0, 0);
   __syncthreads();
@@ -1586,7 +1685,7 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
     if (it + 1 < nf) tables(ppos, (it + 1) & 1);
     if (is_c) ppos = FR.pos_of(c2)[2 * ck + cax];
     float4 tq[3];
-    if (it + 1 < nf) fetch(c1, tq);
+    if (it + 1 < nf) fetch(c1, tq, true);
     if (has_t && it >= 1 && tid == 0) {   // SSE of frame it-1 (partials before the last barrier)
       float a = 0.f;
 #pragma unroll
@@ -1632,7 +1731,8 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
       for (int ch = 0; ch < 3; ++ch) {
         *reinterpret_cast<float4*>(of + ch * HW) = make_float4(o[0][ch], o[1][ch], o[2][ch], o[3][ch]);
         if (has_t) {
-          const float tv[4] = {tn[ch].x, tn[ch].y, tn[ch].z, tn[ch].w};
+          float tv[4];
+          TView::val4<T8>(tn[ch], tv);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float d = tv[q] - o[q][ch];
@@ -1662,40 +1762,55 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, FView tgt, float* __restrict__ sse,
 }
 
 template <int K>
-static int dec_launch_fwd(PosView pv, Src S, FViewW out, FView tgt, float* sse, int F, int h, int H, hipStream_t st) {
+static int dec_launch_fwd(PosView pv, Src S, FViewW out, TView tgt, float* sse, int F, int h, int H, hipStream_t st) {
   const int lds = (K * h * h * 4) * 4;
   int g = (F + 1) / 2 < 1024 ? (F + 1) / 2 : 1024;   // >= 2 frames per block: source staging amortised
-  // the one-barrier-per-frame kernel: 16-byte accesses need 16-byte aligned frames
+  // the one-barrier-per-frame kernel: 16-byte accesses need 16-byte aligned
+  // frames (4-byte aligned ones for byte targets)
+  const uintptr_t tb = tgt.p8 ? (uintptr_t)tgt.p8 : (uintptr_t)tgt.p;
+  const int ta = tgt.p8 ? 4 : 16;
   const bool al = ((uintptr_t)out.p | (uintptr_t)S.bg) % 16 == 0 && out.fs % 4 == 0 &&
-                  (sse == nullptr || ((uintptr_t)tgt.p % 16 == 0 && tgt.fs % 4 == 0 && tgt.gs % 4 == 0));
-  if (al && H == 2 * h && ((K == 2 && (H == 32 || H == 64)) || (K == 3 && H == 36))) {
+                  (sse == nullptr || (tb % ta == 0 && tgt.fs % 4 == 0 && tgt.gs % 4 == 0));
+  const bool cu = al && H == 2 * h && ((K == 2 && (H == 32 || H == 64)) || (K == 3 && H == 36));
+  PAIG_REQUIRE(cu || !tgt.p8 || sse == nullptr,
+               "decoder_fwd: byte targets need the one-CU kernel (K=%d H=%d, 4-byte aligned frames)", K, H);
+  const FView tf{tgt.p, tgt.fs, tgt.gs, tgt.grp};   // (the fp32 fallbacks)
+  if (cu) {
     const int fpb = cdiv(F, g);
     g = cdiv(F, fpb);
-    if constexpr (K == 2) {
-      if (H == 64)
-        hipLaunchKernelGGL((dec_fwd_cu_k<2, 64>), dim3(g), dim3(DecFw<2, 64>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
-      else
-        hipLaunchKernelGGL((dec_fwd_cu_k<2, 32>), dim3(g), dim3(DecFw<2, 32>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
-    } else
-      hipLaunchKernelGGL((dec_fwd_cu_k<3, 36>), dim3(g), dim3(DecFw<3, 36>::NT), 0, st, pv, S, out, tgt, sse, F, fpb);
+    auto launch = [&](auto t8) {
+      constexpr bool T8 = decltype(t8)::value;
+      if constexpr (K == 2) {
+        if (H == 64)
+          hipLaunchKernelGGL((dec_fwd_cu_k<2, 64, T8>), dim3(g), dim3(DecFw<2, 64>::NT), 0, st, pv, S, out, tgt, sse, F,
+                             fpb);
+        else
+          hipLaunchKernelGGL((dec_fwd_cu_k<2, 32, T8>), dim3(g), dim3(DecFw<2, 32>::NT), 0, st, pv, S, out, tgt, sse, F,
+                             fpb);
+      } else
+        hipLaunchKernelGGL((dec_fwd_cu_k<3, 36, T8>), dim3(g), dim3(DecFw<3, 36>::NT), 0, st, pv, S, out, tgt, sse, F,
+                           fpb);
+    };
+    if (tgt.p8 && sse) launch(std::true_type{});
+    else launch(std::false_type{});
     PAIG_CHECK_LAUNCH();
     return 0;
   }
   if constexpr (K == 2) {
     if (H == 32) {
-      hipLaunchKernelGGL((dec_fwd_reg_k<2, 32>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F);
+      hipLaunchKernelGGL((dec_fwd_reg_k<2, 32>), dim3(g), dim3(256), lds, st, pv, S, out, tf, sse, F);
       PAIG_CHECK_LAUNCH();
       return 0;
     }
   }
   if constexpr (K == 3) {
     if (H == 36) {
-      hipLaunchKernelGGL((dec_fwd_reg_k<3, 36>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F);
+      hipLaunchKernelGGL((dec_fwd_reg_k<3, 36>), dim3(g), dim3(256), lds, st, pv, S, out, tf, sse, F);
       PAIG_CHECK_LAUNCH();
       return 0;
     }
   }
-    hipLaunchKernelGGL((dec_fwd_k<K>), dim3(g), dim3(256), lds, st, pv, S, out, tgt, sse, F, h, H);
+    hipLaunchKernelGGL((dec_fwd_k<K>), dim3(g), dim3(256), lds, st, pv, S, out, tf, sse, F, h, H);
   PAIG_CHECK_LAUNCH();
   return 0;
 }
@@ -1900,16 +2015,16 @@ size_t paig_decoder_bwd_scratch(int F, int K, int h, int H) {
   return (size_t)paig_decoder_bwd_blocks(F, 0, 0, K, h, H) * K * 4 * H * H;
 }
 
-int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
-                     const float* cont, const float* bg, float* out, long long out_fs, const float* tgt,
-                     long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F, int K, int h, int H,
-                     void* stream) {
+}  // extern "C"
+
+static int dec_fwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                   const float* cont, const float* bg, float* out, long long out_fs, TView t, float* sse, int F, int K,
+                   int h, int H, void* stream) {
   if (F <= 0) return 0;
   PAIG_REQUIRE(H == 2 * h, "decoder: H=%d must be 2*tmpl=%d", H, 2 * h);
   PosView pv{pos, pos_outer, pos_inner, pos_grp};
   Src S{tmpl, cont, bg};
   FViewW o{out, out_fs};
-  FView t{tgt, tgt_fs, tgt_gs, tgt_grp};
   hipStream_t st = (hipStream_t)stream;
   if (K == 2) return dec_launch_fwd<2>(pv, S, o, t, sse, F, h, H, st);
   if (K == 3) return dec_launch_fwd<3>(pv, S, o, t, sse, F, h, H, st);
@@ -1917,17 +2032,17 @@ int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner,
   return PAIG_E_UNSUPPORTED;
 }
 
-int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
-                     const float* cont, const float* bg, const float* tgt, long long tgt_fs, int tgt_grp,
-                     long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
-                     float* slab, float* scratch, int F, int live, int K, int h, int H, void* stream) {
+static int dec_bwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                   const float* cont, const float* bg, TView t, const float* dsse, const float* dout,
+                   long long dout_fs, float* dpos, float* slab, float* scratch, int F, int live, int K, int h, int H,
+                   void* stream) {
   if (F <= 0) return 0;
   PAIG_REQUIRE(H == 2 * h, "decoder: H=%d must be 2*tmpl=%d", H, 2 * h);
   PAIG_REQUIRE(live >= 0 && (live == 0 || pos_grp > 0), "decoder_bwd: live=%d needs grouped frames (pos_grp=%d)", live,
                pos_grp);
   PAIG_REQUIRE(pos_grp <= 0 || F % pos_grp == 0, "decoder_bwd: F=%d is not a multiple of the group %d", F, pos_grp);
-  PAIG_REQUIRE(pos_grp <= 0 || tgt_grp == pos_grp || live == 0,
-               "decoder_bwd: target group %d must equal the position group %d", tgt_grp, pos_grp);
+  PAIG_REQUIRE(pos_grp <= 0 || t.grp == pos_grp || live == 0,
+               "decoder_bwd: target group %d must equal the position group %d", t.grp, pos_grp);
   // live > 0 promises that the frames past `live` in every group carry a zero
   // SSE weight and no dense gradient: the one-CU kernels skip them, the
   // generic ones walk them (zero contribution), so both give the same result
@@ -1935,7 +2050,6 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
                live);
   PosView pv{pos, pos_outer, pos_inner, pos_grp};
   Src S{tmpl, cont, bg};
-  FView t{tgt, tgt_fs, tgt_gs, tgt_grp};
   FView d{dout, dout_fs, 0, 0};
   hipStream_t st = (hipStream_t)stream;
   if (dec_cu_shape(K, h, H)) {
@@ -1943,16 +2057,25 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
     const int fpb = dec_cu_fpb(NL > 0 ? NL : 1);
     const int g = paig_decoder_bwd_blocks(F, pos_grp, live, K, h, H);
     const int rl = dec_live(F, pos_grp, live) == F ? 0 : live;
-    if (K == 2 && H == 64)
-      hipLaunchKernelGGL((dec_bwd_band_k<2, 64>), dim3(g), dim3(DecBand<2, 64>::NT), 0, st, pv, S, t, dsse, d, dpos, slab, F, rl,
-                         fpb);
-    else if (K == 2)
-      hipLaunchKernelGGL((dec_bwd_cu_k<2, 32>), dim3(g), dim3(DecCu<2, 32>::NT), 0, st, pv, S, t, dsse, d, dpos, slab, F, rl, fpb);
-    else
-      hipLaunchKernelGGL((dec_bwd_cu_k<3, 36>), dim3(g), dim3(DecCu<3, 36>::NT), 0, st, pv, S, t, dsse, d, dpos, slab, F, rl, fpb);
+    auto launch = [&](auto t8) {
+      constexpr bool T8 = decltype(t8)::value;
+      if (K == 2 && H == 64)
+        hipLaunchKernelGGL((dec_bwd_band_k<2, 64, T8>), dim3(g), dim3(DecBand<2, 64>::NT), 0, st, pv, S, t, dsse, d, dpos,
+                           slab, F, rl, fpb);
+      else if (K == 2)
+        hipLaunchKernelGGL((dec_bwd_cu_k<2, 32, T8>), dim3(g), dim3(DecCu<2, 32>::NT), 0, st, pv, S, t, dsse, d, dpos, slab,
+                           F, rl, fpb);
+      else
+        hipLaunchKernelGGL((dec_bwd_cu_k<3, 36, T8>), dim3(g), dim3(DecCu<3, 36>::NT), 0, st, pv, S, t, dsse, d, dpos, slab,
+                           F, rl, fpb);
+    };
+    if (t.p8 && dsse) launch(std::true_type{});
+    else launch(std::false_type{});
     PAIG_CHECK_LAUNCH();
     return 0;
   }
+  PAIG_REQUIRE(!t.p8, "decoder_bwd: byte targets need the one-CU kernels (K=%d H=%d)", K, H);
+  const FView tf{t.p, t.fs, t.gs, t.grp};
   // generic kernels: every frame is walked (dead ones skipped by their zero weight)
   const int g = paig_decoder_bwd_blocks(F, 0, 0, K, h, H);
   const bool need_scratch = paig_decoder_bwd_scratch(F, K, h, H) > 0;
@@ -1960,15 +2083,54 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
   const int lds = (K * h * h * 4 + (need_scratch ? 0 : K * 4 * H * H)) * 4;
   float* gs = need_scratch ? scratch : nullptr;
   if (K == 2)
-    hipLaunchKernelGGL((dec_bwd_k<2>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);
+    hipLaunchKernelGGL((dec_bwd_k<2>), dim3(g), dim3(256), lds, st, pv, S, tf, dsse, d, dpos, slab, gs, F, h, H);
   else if (K == 3)
-    hipLaunchKernelGGL((dec_bwd_k<3>), dim3(g), dim3(256), lds, st, pv, S, t, dsse, d, dpos, slab, gs, F, h, H);
+    hipLaunchKernelGGL((dec_bwd_k<3>), dim3(g), dim3(256), lds, st, pv, S, tf, dsse, d, dpos, slab, gs, F, h, H);
   else {
     paig_set_error("decoder: unsupported n_objs %d", K);
     return PAIG_E_UNSUPPORTED;
   }
   PAIG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" {
+
+int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                     const float* cont, const float* bg, float* out, long long out_fs, const float* tgt,
+                     long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F, int K, int h, int H,
+                     void* stream) {
+  return dec_fwd(pos, pos_outer, pos_inner, pos_grp, tmpl, cont, bg, out, out_fs,
+                 TView{tgt, nullptr, nullptr, tgt_fs, tgt_gs, tgt_grp}, sse, F, K, h, H, stream);
+}
+
+int paig_decoder_fwd_t8(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                        const float* cont, const float* bg, float* out, long long out_fs, const unsigned char* tgt,
+                        const long long* tgt_idx, long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F, int K, int h, int H,
+                        void* stream) {
+  PAIG_REQUIRE(tgt && sse, "decoder_fwd_t8: byte targets and an SSE output are required");
+  PAIG_REQUIRE(!tgt_idx || tgt_grp > 0, "decoder_fwd_t8: a row index needs grouped targets");
+  return dec_fwd(pos, pos_outer, pos_inner, pos_grp, tmpl, cont, bg, out, out_fs,
+                 TView{nullptr, tgt, tgt_idx, tgt_fs, tgt_gs, tgt_grp}, sse, F, K, h, H, stream);
+}
+
+int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                     const float* cont, const float* bg, const float* tgt, long long tgt_fs, int tgt_grp,
+                     long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
+                     float* slab, float* scratch, int F, int live, int K, int h, int H, void* stream) {
+  return dec_bwd(pos, pos_outer, pos_inner, pos_grp, tmpl, cont, bg, TView{tgt, nullptr, nullptr, tgt_fs, tgt_gs, tgt_grp},
+                 dsse, dout, dout_fs, dpos, slab, scratch, F, live, K, h, H, stream);
+}
+
+int paig_decoder_bwd_t8(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                        const float* cont, const float* bg, const unsigned char* tgt, const long long* tgt_idx,
+                        long long tgt_fs, int tgt_grp,
+                        long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
+                        float* slab, float* scratch, int F, int live, int K, int h, int H, void* stream) {
+  PAIG_REQUIRE(tgt, "decoder_bwd_t8: byte targets are required");
+  PAIG_REQUIRE(!tgt_idx || tgt_grp > 0, "decoder_bwd_t8: a row index needs grouped targets");
+  return dec_bwd(pos, pos_outer, pos_inner, pos_grp, tmpl, cont, bg, TView{nullptr, tgt, tgt_idx, tgt_fs, tgt_gs, tgt_grp},
+                 dsse, dout, dout_fs, dpos, slab, scratch, F, live, K, h, H, stream);
 }
 
 }  // extern "C"

@@ -194,6 +194,9 @@ class Engine:
         # called once per backward when the early gradient bucket is final
         # (FlatParams.allreduce_early by default; bench.py splits its HIP graph here)
         self.bucket_hook = model._flat.allreduce_early
+        # DeviceDataIterator.ByteTargets bound to the step's input buffer: the
+        # decoders then read their targets as the dataset's bytes
+        self.byte_targets = None
 
     # conv arithmetic (include/paig_hip.h flags): "split" = f16 hi/lo pieces on
     # the 16-bit matrix cores, operands scaled by powers of two (fp32-accurate:
@@ -218,20 +221,22 @@ class Engine:
         return self.CONV_MATH[m]
 
     @staticmethod
-    def _dec_bytes(n, lay):
+    def _dec_bytes(n, lay, tb=4):
         """Algorithmic HBM bytes of one decoder forward over n frames: the
-        target frames read (fused SSE) and the decoded frames written;
-        positions and the step-constant sources (< 100 KB) are negligible."""
-        return 2 * n * lay.frame * 4
+        target frames read (fused SSE; tb bytes per value: 4 fp32, 1 for the
+        dataset's bytes) and the decoded frames written; positions and the
+        step-constant sources (< 100 KB) are negligible."""
+        return n * lay.frame * (tb + 4)
 
     @staticmethod
-    def _dec_bwd_bytes(live, n, lay, dense):
+    def _dec_bwd_bytes(live, n, lay, dense, tb=4):
         """Algorithmic HBM bytes of one decoder backward: the targets of the
         `live` frames that carry a loss weight (+ their dense dL/dout when
         given) read, the position gradients of all n frames and the source
         gradients (one slab_len vector) written.  The partial-gradient slab
         rows are the kernel's own overhead, not algorithmic."""
-        return live * lay.frame * 4 * (2 if dense else 1) + n * 2 * lay.D * 4 + (4 * lay.K * lay.h * lay.h + 3 * lay.HW) * 4
+        return (live * lay.frame * (tb + (4 if dense else 0)) + n * 2 * lay.D * 4
+                + (4 * lay.K * lay.h * lay.h + 3 * lay.HW) * 4)
 
     def _p(self, tag, flops=0, nbytes=0):
         """Probe context of one launch: algorithmic FLOPs and HBM bytes (the
@@ -316,6 +321,18 @@ class Engine:
 
         # ---- encoder over the first Te frames of every sequence (in place)
         x_view = (ptr(x), T * lay.frame, lay.Te, lay.frame)   # frame n = b*Te + t
+        # the rollout decoders' targets: x's frames, or (byte targets bound to
+        # this input buffer) the dataset rows it was gathered from, as bytes.
+        # The reconstruction targets are the encoder's frames, which the
+        # gather writes as fp32 in either case: read there (no row lookup)
+        bt = self.byte_targets
+        if bt is not None and bt.covers(x, lay):
+            tb = 1
+            tgt_roll = (bt.base + lay.ins * lay.frame, bt.idx_ptr, T * lay.frame, lay.R, lay.frame)
+        else:
+            tb = 0
+            tgt_roll = (ptr(x) + lay.ins * lay.frame * 4, T * lay.frame, lay.R, lay.frame)
+        S.update(tb=tb, tgt_roll=tgt_roll)
         self._encoder_forward(S, lay, x_view, ws, st)
         masks, objs, enc_pos = S["masks"], S["objs"], S["enc_pos"]
 
@@ -368,7 +385,7 @@ class Engine:
         def dec_rec(q):    # reconstruction decode (all B*Te frames, SSE vs input fused)
             with self._p("dec_fwd:recon", 0, self._dec_bytes(F, lay)):
                 L.paig_decoder_fwd(ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), ptr(recons),
-                                   lay.frame, x_view[0], x_view[1], x_view[2], x_view[3], ptr(sse_rec), F, K, h, H, q)
+                                   lay.frame, *x_view, ptr(sse_rec), F, K, h, H, q)
 
         if self._one_stream():
             if vel0 is not None and not lay.alt_vel and os.environ.get("PAIG_FUSE_VFN", "1") != "0":
@@ -396,11 +413,10 @@ class Engine:
         # ---- rollout decode (all B*R frames in one launch, SSE vs input[:, ins:])
         out = _empty(B * lay.R * lay.frame, dev)
         sse_roll = _empty(B * lay.R, dev)
-        tgt_roll = (ptr(x) + lay.ins * lay.frame * 4, T * lay.frame, lay.R, lay.frame)
-        with self._p("dec_fwd:rollout", 0, self._dec_bytes(B * lay.R, lay)):
-            L.paig_decoder_fwd(ptr(pvs) + 2 * D * 4, (lay.R + 1) * 2 * D, 2 * D, lay.R, ptr(tmpl), ptr(cont),
-                               ptr(bgp), ptr(out), lay.frame, *tgt_roll, ptr(sse_roll), B * lay.R, K, h, H, st)
-        S["tgt_roll"] = tgt_roll
+        dec_fwd = L.paig_decoder_fwd_t8 if tb else L.paig_decoder_fwd
+        with self._p("dec_fwd:rollout", 0, self._dec_bytes(B * lay.R, lay, tb or 4)):
+            dec_fwd(ptr(pvs) + 2 * D * 4, (lay.R + 1) * 2 * D, 2 * D, lay.R, ptr(tmpl), ptr(cont), ptr(bgp),
+                    ptr(out), lay.frame, *tgt_roll, ptr(sse_roll), B * lay.R, K, h, H, st)
         S["x_view"] = x_view
 
         res = {
@@ -653,7 +669,8 @@ class Engine:
         tmpl = S["src"]["var_net_template"][1]
         cont = S["src"]["var_net_content"][1]
         bgp = S["src"]["var_net_background"][2]
-        x_view = S["x_view"]
+        tb = S["tb"]
+        dec_bwd = L.paig_decoder_bwd_t8 if tb else L.paig_decoder_bwd
         if d_out is not None:
             d_out = d_out.contiguous()
         if d_recons is not None:
@@ -700,14 +717,14 @@ class Engine:
         live_frames = B * roll_live if roll_live else B * R
 
         def dec_roll(q):   # rollout-frame decoder backward: d rollout positions + partial source grads
-            with self._p("dec_bwd:rollout", 0, self._dec_bwd_bytes(live_frames, B * R, lay, d_out is not None)):
-                L.paig_decoder_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
-                                   *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
-                                   ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, roll_live, K, h, H, q)
+            with self._p("dec_bwd:rollout", 0, self._dec_bwd_bytes(live_frames, B * R, lay, d_out is not None, tb or 4)):
+                dec_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
+                        *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
+                        ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, roll_live, K, h, H, q)
 
         def dec_rec(q):    # reconstruction decoder backward: d enc_pos + partial source grads
             with self._p("dec_bwd:recon", 0, self._dec_bwd_bytes(F, F, lay, d_recons is not None)):
-                L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *x_view,
+                L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *S["x_view"],
                                    ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, 0,
                                    K, h, H, q)
 

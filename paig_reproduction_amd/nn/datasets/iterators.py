@@ -79,7 +79,12 @@ class DeviceDataIterator(DataIterator):
     a slice of that device permutation, so a step issues no host-to-device
     copy at all, only the gather launch.  ``out`` (next_batch / gather_into)
     lets a caller gather into a fixed buffer, e.g. the input of a captured
-    HIP graph."""
+    HIP graph.
+
+    bind_targets(xbuf, head_frames) makes the decoders read their targets as
+    the dataset's bytes (ByteTargets): gathers into xbuf then convert only the
+    first head_frames frames of every sequence (the encoder's input) and
+    record the batch's dataset rows for the decoders."""
 
     def __init__(self, X_u8, shape, device, seed=None, rank=0, world=1):
         import torch
@@ -88,6 +93,7 @@ class DeviceDataIterator(DataIterator):
         assert self.row == int(np.prod(self.shape)), (X_u8.shape, shape)
         self.device = torch.device(device)
         self.idx_d = None
+        self.bound = None
         super().__init__(torch.from_numpy(np.ascontiguousarray(X_u8)).to(self.device), None, seed, rank, world)
 
     def reset_iteration(self):
@@ -97,11 +103,23 @@ class DeviceDataIterator(DataIterator):
         # previous epoch that are still queued read their own buffer)
         self.idx_d = torch.from_numpy(self.indices.astype(np.int64)).pin_memory().to(self.device, non_blocking=True)
 
+    def bind_targets(self, xbuf, head_frames):
+        """Bind the fixed input buffer ``xbuf`` [B, *shape]: see ByteTargets.
+        Returns the binding for ``Engine.byte_targets``."""
+        self.bound = ByteTargets(self, xbuf, head_frames)
+        return self.bound
+
     def _launch(self, idx_ptr, n, out):
         from paig_reproduction_amd._lib import lib, stream_handle
         if n:
-            lib().paig_gather_u8_f32(self.X.data_ptr(), idx_ptr, out.data_ptr(), int(n), self.row,
-                                     stream_handle(self.device))
+            bt = self.bound
+            if bt is not None and out.data_ptr() == bt.x_ptr:
+                assert n == bt.B, (n, bt.B)
+                lib().paig_gather_u8_f32_ex(self.X.data_ptr(), idx_ptr, out.data_ptr(), int(n), self.row, bt.head,
+                                            bt.idx.data_ptr(), stream_handle(self.device))
+            else:
+                lib().paig_gather_u8_f32(self.X.data_ptr(), idx_ptr, out.data_ptr(), int(n), self.row,
+                                         stream_handle(self.device))
         return out
 
     def _out(self, n, out):
@@ -137,6 +155,50 @@ class DeviceDataIterator(DataIterator):
     def sample_random_batch(self, batch_size):
         np.random.randint(0, self.num_examples - batch_size)   # reference quirk (iterators.py:42-47)
         return self._gather(np.arange(self.start_idx, min(self.start_idx + batch_size, self.num_examples))), None
+
+
+class ByteTargets:
+    """The decoders' targets read from the device-resident dataset (SURVEY §8
+    F2 + the fused SSE): a batch gathered into the bound buffer ``xbuf``
+    converts only its first ``head_frames`` frames to float32 (what the
+    encoder reads; the later frames of xbuf are NOT written), saves the
+    batch's dataset rows in ``idx``, and the engine's rollout decoders
+    (forward SSE and backward) read frame t of sequence b as X[idx[b]]
+    bytes / 255 -- bit-identical to the float32 frame the full gather writes
+    (paig_decoder_fwd_t8 / paig_decoder_bwd_t8).  Per sequence of T frames
+    this drops the (T - head) float32 frames' write and re-read and reads
+    every rollout target at 1 byte a value instead of 4 (the reconstruction
+    decoders read the encoder's float32 frames, which are gathered anyway).
+
+    The binding is a promise that only this iterator fills ``xbuf`` (a batch
+    written into it otherwise would be decoded against stale rows) and that
+    nothing reads its frames >= head_frames (model.input's tail).  The engine
+    uses it for an input whose storage is ``xbuf``'s and whose shape matches."""
+
+    SHAPES = ((2, 32), (3, 36), (2, 64))   # (objects, frame side) of the byte-target kernels
+
+    def __init__(self, it, xbuf, head_frames):
+        import torch
+        assert xbuf.is_contiguous() and xbuf.dtype == torch.float32 and xbuf.device == it.device
+        assert tuple(xbuf.shape[1:]) == it.shape, (tuple(xbuf.shape), it.shape)
+        self.it = it
+        self.B, self.T = int(xbuf.shape[0]), int(it.shape[0])
+        self.frame = it.row // self.T
+        self.head_frames = int(head_frames)
+        assert 0 < self.head_frames <= self.T
+        head = self.head_frames * self.frame
+        self.head = min(it.row, -(-head // 16) * 16)   # the gather moves 16-byte multiples
+        self.x_ptr = xbuf.data_ptr()
+        self.base = it.X.data_ptr()
+        self.idx = torch.zeros(self.B, dtype=torch.int64, device=it.device)
+        self.idx_ptr = self.idx.data_ptr()
+
+    def covers(self, x, lay):
+        """True when the engine may decode ``x`` (layout ``lay``) against the
+        bytes: x is the bound buffer and the frames it converts cover the
+        encoder's."""
+        return (x.data_ptr() == self.x_ptr and x.shape[0] == self.B and x.shape[1] == self.T and
+                lay.frame == self.frame and lay.Te <= self.head_frames and (lay.K, lay.H) in self.SHAPES)
 
 
 def get_iterators(file, conv=False, datapoints=0, seed=None, rank=0, world=1, device=None):

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 import torch
 
-from paig_reproduction_amd.nn.datasets.iterators import DataIterator, DeviceDataIterator
+from paig_reproduction_amd.nn.datasets.iterators import ByteTargets, DataIterator, DeviceDataIterator
 
 
 def _data(n=23, T=5, H=8, C=3, seed=0):
@@ -55,3 +55,25 @@ def test_gather_every_byte_value():
     dev.next_batch(N, out=dx)
     torch.cuda.synchronize()
     assert sorted(map(bytes, dx.cpu().numpy())) == sorted(map(bytes, want))   # all 256 values, every sequence
+
+
+def test_byte_targets_binding_rules():
+    """ByteTargets (CPU-side bookkeeping only): the gathered head rounds up to
+    16-byte multiples within the row, and the engine may use the bytes only
+    for the bound buffer with a matching layout and an encoder within the head."""
+    from types import SimpleNamespace
+    u8 = _data(n=6, T=5, H=6, C=3)            # frame 108 bytes
+    N, T, H, W, C = u8.shape
+    # the iterator's fields ByteTargets reads (a DeviceDataIterator needs a GPU)
+    it = SimpleNamespace(shape=(T, C, H, W), row=T * C * H * W, device=torch.device("cpu"),
+                         X=torch.from_numpy(u8))
+    xbuf = torch.empty((2, T, C, H, W))
+    bt = ByteTargets(it, xbuf, 3)
+    assert bt.frame == C * H * W and bt.head == 336 and bt.head % 16 == 0 and bt.head <= it.row
+    assert bt.base == it.X.data_ptr() and tuple(bt.idx.shape) == (2,) and bt.idx.dtype == torch.int64
+    lay = SimpleNamespace(frame=bt.frame, Te=3, K=2, H=32)
+    assert bt.covers(xbuf, lay)
+    assert not bt.covers(torch.empty_like(xbuf), lay)                      # another buffer
+    assert not bt.covers(xbuf, SimpleNamespace(frame=bt.frame, Te=4, K=2, H=32))   # encoder past the head
+    assert not bt.covers(xbuf, SimpleNamespace(frame=bt.frame, Te=3, K=3, H=32))   # no byte-target kernel
+    assert ByteTargets(it, xbuf, T).head == it.row
