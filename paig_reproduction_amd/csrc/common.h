@@ -285,7 +285,15 @@ void paig_gemm_splitk_finish(int M, int N, int S, const float* part, float* C, l
 struct XMax {
   float* p;
   int n;
+  float* z = nullptr;   // forward only: zn floats to zero (paig_conv_fwd_prezero)
+  int zn = 0;
 };
+// The U-Net forward's max-|x| slots of the layers after the first are zeroed
+// by the first split forward launch instead of a separate memset: set the
+// range, launch; paig_conv_fwd_prezero_pending() then says (and clears)
+// whether no split forward took it (the caller must zero the slots itself).
+void paig_conv_fwd_prezero(float* z, int zn);
+bool paig_conv_fwd_prezero_pending();
 int paig_conv_mfma_fwd(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int Cin, int Cout,
                        int H, int W, int ks, int flags, hipStream_t st, int* rc, XMax xm, const void* wp = nullptr,
                        PoolOut pout = PoolOut{nullptr, 0, nullptr, 0});

@@ -866,6 +866,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
       if (tid == 0) xm.p[blockIdx.x] = xrun;
       if (blockIdx.x == 0)
         for (int i = gridDim.x + tid; i < xm.n; i += 256) xm.p[i] = 0.f;
+      for (int i = blockIdx.x * 256 + tid; i < xm.zn; i += gridDim.x * 256) xm.z[i] = 0.f;   // later layers' slots
     }
   }
 }
@@ -1569,6 +1570,8 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
 // slice in the split forward / dgrad launches (0: the resident count), so the
 // tests can make every block walk many tiles at small frame counts
 static int g_fwd_block_cap = 0;
+// pending pre-zero range for the next split forward (paig_conv_fwd_prezero)
+static XMax g_prezero{};
 
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool UPT = false, bool PF = false>
 static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const float* b, int F, int flags,
@@ -1602,6 +1605,11 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
   if (nb < 1) nb = 1;
   if (PM != 0 || DG) xm.p = nullptr;
   PAIG_REQUIRE(!xm.p || nb <= xm.n, "conv split fwd: %d blocks need more than %d xmax slots", nb, xm.n);
+  if (xm.p && g_prezero.z) {   // this launch zeroes the later layers' slots
+    xm.z = g_prezero.z;
+    xm.zn = g_prezero.zn;
+    g_prezero = XMax{};
+  }
   if (PF) PAIG_REQUIRE(pout.p && pout.code, "conv split dgrad: the pool fold needs the pooled gradient and codes");
   else if (flags & 64) PAIG_REQUIRE(C::POOLOK && pout.p, "conv split fwd: no fused pool for Cin=%d Cout=%d H=%d", CIN, COUT, H);
   hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles, xm,
@@ -1926,6 +1934,16 @@ __global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
     img[e * 8 + j] = h;
     img[((long long)ENT + e) * 8 + j] = l;
   }
+}
+
+void paig_conv_fwd_prezero(float* z, int zn) {
+  g_prezero.z = z;
+  g_prezero.zn = zn;
+}
+bool paig_conv_fwd_prezero_pending() {
+  const bool pend = g_prezero.z != nullptr;
+  g_prezero = XMax{};
+  return pend;
 }
 
 extern "C" {

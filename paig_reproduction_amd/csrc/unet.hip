@@ -308,8 +308,15 @@ int fwd_impl(int net, int F, int H, int K, int math, int flags, const float* x, 
   // the per-block max |x| slots (the split forward writes its layer's; a slot
   // no forward wrote must read zero: the wgrad then takes the guarded fixed
   // scale instead of a garbage exponent)
+  // (the first layer's split forward zeroes the others' slots: no memset on
+  // the step's critical path; a memset of all of them when it did not)
   float* xmax = reinterpret_cast<float*>(base + L.xmax);
-  UNET_HIP(hipMemsetAsync(xmax, 0, p.ops.size() * PAIG_XMAX_SLOTS * 4, (hipStream_t)stream));
+  const size_t xmax_n = p.ops.size() * PAIG_XMAX_SLOTS;
+  static const bool memset_ab = getenv("PAIG_XMAX_MEMSET") != nullptr;   // A/B: the round-5 memset
+  const bool prezero =
+      !memset_ab && !p.ops.empty() && p.ops[0].kind == U_CONV && p.fused_up[0] < 0 && p.ops.size() > 1;
+  if (prezero) paig_conv_fwd_prezero(xmax + PAIG_XMAX_SLOTS, (int)(xmax_n - PAIG_XMAX_SLOTS));
+  else UNET_HIP(hipMemsetAsync(xmax, 0, xmax_n * 4, (hipStream_t)stream));
   const int no = (int)p.ops.size(), nrun = head ? no - 1 : no;   // HEAD_FUSED: the 1x1 head is the caller's
   auto wimg0 = [&](int i) -> const void* {
     return cm != 128 ? nullptr : (ext ? wpf[p.ops[i].conv] : base + L.wprep0[i]);
@@ -371,6 +378,10 @@ int fwd_impl(int net, int F, int H, int K, int math, int flags, const float* x, 
                                xmax + (size_t)i * PAIG_XMAX_SLOTS, PAIG_XMAX_SLOTS, pool_out, pool_fs, pcode, pcode_fs,
                                wimg0(i), stream);
       pr(1, i, op.conv, PAIG_PROBE_CONV_FWD, op.src.n, op.dst.n, Hl, fl);
+      if (i == 0 && prezero && paig_conv_fwd_prezero_pending()) {
+        if (rc) return rc;
+        UNET_HIP(hipMemsetAsync(xmax, 0, xmax_n * 4, (hipStream_t)stream));   // no split forward took the range
+      }
     } else if (op.kind == U_POOL) {
       int slvl;
       const View sv = view(op.src, slvl);
