@@ -1085,8 +1085,15 @@ static int sbwd_launch(FView x, FView dy, FViewW dx, FView aux, const float* w, 
                        long long pcode_fs = 0) {
   using C = SBwdCfg<CIN, COUT, H, W, KS, UPS, PM, PF>;
   constexpr int RED = (C::NLD * 256 * 8 + 256) * 4;   // the bias reduction's LDS
-  constexpr int LDS = C::LDS > RED ? C::LDS : RED;
-  static_assert(LDS <= LDS_MAX, "fused backward: staging exceeds the LDS");
+  constexpr int LDS0 = C::LDS > RED ? C::LDS : RED;
+  static_assert(LDS0 <= LDS_MAX, "fused backward: staging exceeds the LDS");
+  // A/B: PAIG_BWD_LDS_PAD = extra bytes of (unused) LDS per block, the
+  // occupancy cost an LDS landing zone for the next tile would have
+  static const int lds_pad = [] {
+    const char* e = getenv("PAIG_BWD_LDS_PAD");
+    return e ? atoi(e) : 0;
+  }();
+  const int LDS = LDS0 + lds_pad <= LDS_MAX ? LDS0 + lds_pad : LDS0;
   const int ntiles = cdiv(F, C::FPT) * (H / C::RT);
   auto k = conv_bwd_split_k<CIN, COUT, H, W, KS, UPS, PM, PF>;
   static int resident = 0;
