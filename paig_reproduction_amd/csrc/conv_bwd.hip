@@ -43,6 +43,13 @@
 #ifndef PAIG_BWD_UPS2
 #define PAIG_BWD_UPS2 1   // A/B builds: 0 = one-row upsample staging items
 #endif
+#ifndef PAIG_BWD_TPX_C10
+#define PAIG_BWD_TPX_C10 0   // A/B builds: tile pixels / blocks per CU of c10 (16 -> 16 @ 32, upsample fold)
+#define PAIG_BWD_MINW_C10 0
+#endif
+#ifndef PAIG_BWD_PSD_EVEN_C10
+#define PAIG_BWD_PSD_EVEN_C10 0   // A/B builds: c10's dY image at an even pixel pitch (less LDS, more conflicts)
+#endif
 #ifndef PAIG_BWD_AUXP
 #define PAIG_BWD_AUXP 1   // A/B builds: 0 = the epilogue loads its ReLU' mask when it needs it
 #endif
@@ -73,7 +80,9 @@ namespace {
 // the fused-upsample window)
 constexpr int sbwd_lds(int CIN, int COUT, int H, int W, bool UPS, int PM, int tpx) {
   const int FPT = H * W <= tpx ? tpx / (H * W) : 1, RT = H * W <= tpx ? H : rows_fit(H, W, tpx);
-  const int ROWS = RT + 2, ROWSD = ROWS + (UPS ? 2 : 0), CCD = rup(COUT, 8) / 8, PSD = CCD % 2 == 0 ? CCD + 1 : CCD;
+  const bool pe = PAIG_BWD_PSD_EVEN_C10 && UPS && CIN == 16 && COUT == 16 && H == 32;
+  const int ROWS = RT + 2, ROWSD = ROWS + (UPS ? 2 : 0), CCD = rup(COUT, 8) / 8,
+            PSD = CCD % 2 == 0 && !pe ? CCD + 1 : CCD;
   const int RPD = W == 8 ? to_mod16((W + 2) * PSD, 8) : (W + 2) * PSD;
   const int IMGD = (FPT * ROWSD * RPD + 2) * 8, WIMG = ceil_div(9 * CCD, 4) * ceil_div(CIN, 16) * 64 * 8;
   const int XIMG = rup(CIN, 4) / 4 * rup(FPT * ROWS * (W + 4) * 4 + 80, 128) * 2 * (PM == 2 ? 1 : 2);
@@ -85,6 +94,7 @@ constexpr int sbwd_lds(int CIN, int COUT, int H, int W, bool UPS, int PM, int tp
 // blocks share a CU (the 8 x 8 / 9 x 9 levels' multi-frame tiles and the
 // 32-channel weight images would not)
 constexpr int sbwd_tpx(int CIN, int COUT, int H, int W, bool UPS, int PM) {
+  if (PAIG_BWD_TPX_C10 && UPS && CIN == 16 && COUT == 16 && H == 32) return PAIG_BWD_TPX_C10;
   for (int pass = 0; pass < 2; ++pass)
     for (int t = 256; t >= 64; t /= 2) {
       const int rt = H * W <= t ? H : rows_fit(H, W, t);
@@ -97,6 +107,7 @@ constexpr int sbwd_tpx(int CIN, int COUT, int H, int W, bool UPS, int PM) {
 // waves per SIMD (= blocks per CU) each shape compiles for without spilling
 // (measured: -Rpass-analysis=kernel-resource-usage at 2 / 3 / 4)
 constexpr int sbwd_minw(int CIN, int COUT, int H, int PM, bool PF) {
+  if (PAIG_BWD_MINW_C10 && CIN == 16 && COUT == 16 && H == 32) return PAIG_BWD_MINW_C10;
   if (CIN == 8 && COUT == 8 && H == 32) return PF || PAIG_BWD_AUXP == 2 ? 3 : 4;
   if (PM == 2 && CIN == 8 && COUT == 16 && H == 16) return 3;
   if (PM == 2 && CIN == 24 && COUT == 8 && H == 32) return 3;
@@ -139,7 +150,8 @@ struct SBwdCfg {
   static constexpr int TPXD = FPT * RTD * W;                  // data-gradient pixels per tile
   // ---- dY image: NHWC, 8-channel slots, halo PADL
   static constexpr int CCD = rup(COUT, 8) / 8;
-  static constexpr int PSD = CCD % 2 == 0 ? CCD + 1 : CCD;    // odd pitch: 16 pixels -> 16 bank groups
+  static constexpr bool PSDE = PAIG_BWD_PSD_EVEN_C10 && UPS && CIN == 16 && COUT == 16 && H == 32;
+  static constexpr int PSD = CCD % 2 == 0 && !PSDE ? CCD + 1 : CCD;   // odd pitch: 16 pixels -> 16 bank groups
   static constexpr int TWPX = W + 2 * PADL;
   static constexpr int RPD = W == 8 ? to_mod16(TWPX * PSD, 8) : TWPX * PSD;
   static constexpr int ZSLOT = FPT * ROWSD * RPD;             // a zero slot after the image

@@ -1,7 +1,7 @@
 """Compact per-kernel register / occupancy report from hipcc's
 -Rpass-analysis=kernel-resource-usage remarks.
 
-usage: python tools/kernel_resources.py paig_reproduction_amd/csrc/conv_mfma.hip [filter]
+usage: python tools/kernel_resources.py paig_reproduction_amd/csrc/conv_mfma.hip [filter] [-DNAME=VALUE ...]
 """
 import re
 import subprocess
@@ -11,8 +11,9 @@ import sys
 def main():
     src = sys.argv[1]
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
+    defs = [a for a in sys.argv[3:] if a.startswith("-D")]   # A/B build macros
     out = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-c", src, "-o",
-                          "/dev/null", "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
+                          "/dev/null", "-Rpass-analysis=kernel-resource-usage"] + defs, capture_output=True, text=True).stderr
     cur = None
     rows = {}
     for line in out.splitlines():
