@@ -31,7 +31,7 @@ extern "C" {
 /* Version of this interface: bumped whenever an entry point's argument list
  * or a data layout it exchanges changes (the Python binding refuses a library
  * of another version). */
-#define PAIG_ABI_VERSION 4
+#define PAIG_ABI_VERSION 5
 const char* paig_last_error(void);
 int paig_abi_version(void);
 /* f16 range guard of the split-precision path.  Activations and gradients
@@ -504,6 +504,18 @@ int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner,
  * rollout decode's pred_steps, physics_models.py:129-139): the others get
  * dpos = 0 and are not read.  Partial source gradients: one slab row of
  * paig_decoder_slab_len floats per block, paig_decoder_bwd_blocks rows. */
+/* the physics rollout (paig_rollout_fwd's arguments) and the reconstruction
+ * decode (paig_decoder_fwd's; fp32 targets, SSE output required) in one
+ * launch: they are independent, and the rollout's one-thread-per-sequence
+ * recurrence no longer holds the GPU alone.  The one-CU decoder shapes only:
+ * (K, H) in {(2, 32), (3, 36), (2, 64)}, 16-byte aligned frames; the cell / D
+ * pairs of paig_rollout_fwd */
+int paig_decoder_fwd_rollout(int cell, const float* pos0, long long pos0_ld, const float* vel0, const float* dt,
+                             const double* p0, const double* p1, float* pvs, int B, int D, int R, const float* pos,
+                             long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                             const float* cont, const float* bg, float* out, long long out_fs, const float* tgt,
+                             long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F, int K, int h, int H,
+                             void* stream);
 /* the same decode with uint8 targets read from the device-resident dataset
  * (byte / 255, bit-identical to the gathered fp32 frames): tgt is the dataset
  * base (+ the frame offset in bytes), tgt_idx (nullable; grouped targets only)

@@ -17,7 +17,7 @@ XMAX_SLOTS = 2048
 
 AB_PATH = os.environ.get("PAIG_AB_LIB")
 # include/paig_hip.h PAIG_ABI_VERSION: the SIGNATURES below are this version's
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -112,6 +112,8 @@ SIGNATURES = {
     "paig_rollout_bwd_blocks": (I, [I]),
     "paig_rollout_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P]),
     "paig_decoder_fwd": (I, [P, LL, LL, I, P, P, P, P, LL, P, LL, I, LL, P, I, I, I, I, P]),
+    "paig_decoder_fwd_rollout": (I, [I, P, LL, P, P, P, P, P, I, I, I, P, LL, LL, I, P, P, P, P, LL, P, LL, I, LL, P, I, I,
+                                      I, I, P]),
     "paig_decoder_fwd_t8": (I, [P, LL, LL, I, P, P, P, P, LL, P, P, LL, I, LL, P, I, I, I, I, P]),
     "paig_decoder_bwd_blocks": (I, [I, I, I, I, I, I]),
     "paig_decoder_slab_len": (SZ, [I, I, I]),

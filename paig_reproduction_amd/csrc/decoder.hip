@@ -28,6 +28,8 @@
 
 namespace {
 
+#include "rollout_cells.h"
+
 struct Src {
   const float* tmpl;  // [K][h*h] raw template logits (VariableFromNetwork)
   const float* cont;  // [K][3][h*h] raw content logits
@@ -1605,8 +1607,8 @@ __device__ __forceinline__ int b128_rank(int l) {
 }
 
 template <int K, int H, bool T8>
-__global__ void __launch_bounds__((DecFw<K, H>::NT))
-dec_fwd_cu_k(PosView pos, Src S, FViewW out, TView tgt, float* __restrict__ sse, int F, int FPB) {
+__device__ __forceinline__ void dec_fwd_cu_body(PosView pos, Src S, FViewW out, TView tgt, float* __restrict__ sse, int F,
+                                                int FPB, int bid) {
   using C = DecFw<K, H>;
   constexpr int h = C::h, hp = C::hp, HW = C::HW, GPR = C::GPR, NC = C::NC, NW = C::NW, P = C::P;
   __shared__ float4 SRC[K][hp * P];     // (template + 5, sigmoid(content) x 3), zero border, split rows
@@ -1617,7 +1619,7 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, TView tgt, float* __restrict__ sse,
   __shared__ long long IXS[DecFrames::IXN];   // byte targets' dataset rows (ix_load / ix_store)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int first = blockIdx.x * FPB;
+  const int first = bid * FPB;
   const int nf = first < F ? (F - first < FPB ? F - first : FPB) : 0;
   if (nf == 0) return;   // block-uniform
   const DecFrames FR(pos, tgt, 0);
@@ -1759,6 +1761,40 @@ dec_fwd_cu_k(PosView pos, Src S, FViewW out, TView tgt, float* __restrict__ sse,
     for (int w = 0; w < NW; ++w) a += RED[(nf - 1) & 1][w];
     sse[cprev.f] = a;
   }
+}
+
+template <int K, int H, bool T8>
+__global__ void __launch_bounds__((DecFw<K, H>::NT))
+dec_fwd_cu_k(PosView pos, Src S, FViewW out, TView tgt, float* __restrict__ sse, int F, int FPB) {
+  dec_fwd_cu_body<K, H, T8>(pos, S, out, tgt, sse, F, FPB, blockIdx.x);
+}
+
+// The physics rollout (rollout.hip's forward, one thread per sequence) and
+// the reconstruction decode in ONE launch: the two are independent (both
+// follow the position head and the velocity MLP), and the rollout's few
+// latency-bound threads would otherwise hold the whole GPU for its 46 x 5
+// serial substeps.  Blocks 0 .. nr-1 roll out NT sequences each; the others
+// run the decode exactly as dec_fwd_cu_k (block bid - nr).
+struct RollArgs {
+  const float* pos0;
+  long long ld;
+  const float* vel0;
+  PhysPtr Q;
+  float* pvs;
+  int B, R;
+};
+template <int K, int H, int D, int CELL>
+__global__ void __launch_bounds__((DecFw<K, H>::NT))
+dec_fwd_roll_k(RollArgs ra, int nr, PosView pos, Src S, FViewW out, TView tgt, float* __restrict__ sse, int F, int FPB) {
+  if ((int)blockIdx.x < nr) {   // block-uniform
+    // the rollout's serial chain shares its SIMD with decode waves: it issues
+    // first, so the launch's length stays the decode's, not a slowed rollout's
+    __builtin_amdgcn_s_setprio(3);
+    const int b = (int)blockIdx.x * DecFw<K, H>::NT + (int)threadIdx.x;
+    if (b < ra.B) rollout_fwd_seq<D, CELL>(ra.pos0, ra.ld, ra.vel0, ra.Q, ra.pvs, ra.B, ra.R, b);
+    return;
+  }
+  dec_fwd_cu_body<K, H, false>(pos, S, out, tgt, sse, F, FPB, (int)blockIdx.x - nr);
 }
 
 template <int K>
@@ -2102,6 +2138,54 @@ int paig_decoder_fwd(const float* pos, long long pos_outer, long long pos_inner,
                      void* stream) {
   return dec_fwd(pos, pos_outer, pos_inner, pos_grp, tmpl, cont, bg, out, out_fs,
                  TView{tgt, nullptr, nullptr, tgt_fs, tgt_gs, tgt_grp}, sse, F, K, h, H, stream);
+}
+
+// The rollout (paig_rollout_fwd's arguments) and the reconstruction decode
+// (paig_decoder_fwd's, fp32 targets and an SSE output) in one launch, where
+// the one-CU decoder serves the shape: (K, H) in {(2, 32), (3, 36), (2, 64)}
+// with 16-byte aligned frames; the cell / D pairs of paig_rollout_fwd.
+int paig_decoder_fwd_rollout(int cell, const float* pos0, long long pos0_ld, const float* vel0, const float* dt,
+                             const double* p0, const double* p1, float* pvs, int B, int D, int R, const float* pos,
+                             long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                             const float* cont, const float* bg, float* out, long long out_fs, const float* tgt,
+                             long long tgt_fs, int tgt_grp, long long tgt_gs, float* sse, int F, int K, int h, int H,
+                             void* stream) {
+  PAIG_REQUIRE(B > 0 && F > 0 && R > 0, "decoder_fwd_rollout: B=%d F=%d R=%d", B, F, R);
+  PAIG_REQUIRE(cell == 1 || (p0 && p1), "decoder_fwd_rollout: physics params required");
+  PAIG_REQUIRE(H == 2 * h && sse && tgt, "decoder_fwd_rollout: H=%d tmpl=%d, targets and an SSE output required", H, h);
+  const bool al = ((uintptr_t)out | (uintptr_t)bg | (uintptr_t)tgt) % 16 == 0 && out_fs % 4 == 0 && tgt_fs % 4 == 0 &&
+                  tgt_gs % 4 == 0;
+  PAIG_REQUIRE(al, "decoder_fwd_rollout: 16-byte aligned frames required");
+  PosView pv{pos, pos_outer, pos_inner, pos_grp};
+  Src S{tmpl, cont, bg};
+  FViewW o{out, out_fs};
+  TView t{tgt, nullptr, nullptr, tgt_fs, tgt_gs, tgt_grp};
+  RollArgs ra{pos0, pos0_ld, vel0, PhysPtr{dt, p0, p1}, pvs, B, R};
+  hipStream_t st = (hipStream_t)stream;
+  auto launch = [&](auto kern, int nt) {
+    // the decode's blocks exactly as paig_decoder_fwd (<= 1024: four per CU,
+    // one round).  Where they fill that round the rollout's blocks push
+    // decode blocks into a second one: callers merge only while
+    // min((F + 1) / 2, 1024) + ceil(B / NT) <= 1024 (measured: B = 512 and
+    // 1024 lose 0.4-0.6% merged, with the decode's grid capped or not)
+    const int nr = cdiv(B, nt);
+    int g = (F + 1) / 2 < 1024 ? (F + 1) / 2 : 1024;
+    const int fpb = cdiv(F, g);
+    g = cdiv(F, fpb);
+    hipLaunchKernelGGL(kern, dim3(nr + g), dim3(nt), 0, st, ra, nr, pv, S, o, t, sse, F, fpb);
+    return 0;
+  };
+  int rc = -1;
+  if (K == 2 && H == 32 && D == 4 && cell == 0) rc = launch(dec_fwd_roll_k<2, 32, 4, CELL_SPRING>, DecFw<2, 32>::NT);
+  else if (K == 2 && H == 32 && D == 4 && cell == 1) rc = launch(dec_fwd_roll_k<2, 32, 4, CELL_BOUNCE>, DecFw<2, 32>::NT);
+  else if (K == 3 && H == 36 && D == 6 && cell == 2) rc = launch(dec_fwd_roll_k<3, 36, 6, CELL_GRAVITY>, DecFw<3, 36>::NT);
+  else if (K == 2 && H == 64 && D == 4 && cell == 0) rc = launch(dec_fwd_roll_k<2, 64, 4, CELL_SPRING>, DecFw<2, 64>::NT);
+  if (rc < 0) {
+    paig_set_error("decoder_fwd_rollout: unsupported (K=%d, H=%d, cell %d, D=%d)", K, H, cell, D);
+    return PAIG_E_UNSUPPORTED;
+  }
+  PAIG_CHECK_LAUNCH();
+  return 0;
 }
 
 int paig_decoder_fwd_t8(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,

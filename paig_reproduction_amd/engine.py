@@ -397,12 +397,21 @@ class Engine:
                                                   for suf in (".l1.weight", ".l1.bias", ".l2.weight", ".l2.bias")],
                     _parr([ptr(src[nm][0]) for nm, _, _ in vf]), _parr([ptr(src[nm][1]) for nm, _, _ in vf]),
                     _parr([ptr(src[nm][2]) for nm, _, _ in vf]), _iarr([P for _, P, _ in vf]), st)
-                L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0),
-                                   ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, st)
+                if self._merge_roll_rec(lay):
+                    # the rollout and the reconstruction decode in one launch
+                    with self._p("dec_fwd:recon+rollout", 0, self._dec_bytes(F, lay)):
+                        L.paig_decoder_fwd_rollout(
+                            lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0), ptr(prm[0]),
+                            ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, ptr(enc_pos), 0, 2 * K, 0, ptr(tmpl),
+                            ptr(cont), ptr(bgp), ptr(recons), lay.frame, *x_view, ptr(sse_rec), F, K, h, H, st)
+                else:
+                    L.paig_rollout_fwd(lay.cell, ptr(enc_pos) + (lay.ins - 1) * D * 4, lay.Te * D, ptr(vel0),
+                                       ptr(prm[0]), ptr(prm[1]), ptr(prm[2]), ptr(pvs), B, D, lay.R, st)
+                    dec_rec(st)
             else:
                 velocity(st)
                 vfn_src(st)
-            dec_rec(st)
+                dec_rec(st)
         else:
             sst = self._fork(dev)
             velocity(sst)                  # (side) velocity encoder + rollout
@@ -435,6 +444,20 @@ class Engine:
         if not need_saved:
             self._release(S)
         return res, (S if need_saved else None)
+
+    # (K, H, cell) of paig_decoder_fwd_rollout (the one-CU decoder's shapes)
+    # -> threads per block (DecFw<K, H>::NT: one rollout sequence per thread)
+    _ROLL_REC = {(2, 32, 0): 256, (2, 32, 1): 256, (3, 36, 2): 384, (2, 64, 0): 1024}
+
+    def _merge_roll_rec(self, lay):
+        """The rollout and the reconstruction decode share one launch while
+        the decode's blocks leave room for the rollout's in one round of four
+        blocks per CU (B=100: 500 + 1 blocks; B >= 512 measured 0.4-0.6%
+        slower merged).  PAIG_MERGE_ROLL=0: two launches (the A/B)."""
+        nt = self._ROLL_REC.get((lay.K, lay.H, lay.cell))
+        if nt is None or os.environ.get("PAIG_MERGE_ROLL", "1") == "0":
+            return False
+        return min((lay.F + 1) // 2, 1024) + -(-lay.B // nt) <= 1024
 
     def _release(self, S):
         """Drop a forward's U-Net workspace (activations, gradients, max-|x|

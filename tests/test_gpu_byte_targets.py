@@ -6,7 +6,11 @@ batch -- outputs, the three losses, every parameter gradient and the RMSprop
 update -- for every task shape bench.py runs, across epoch boundaries (the
 decoders follow the permutation through the saved row indices).  The frames
 the bound gather skips are poisoned with NaN: any read of them would show.
+The same harness holds the merged rollout + reconstruction-decode launch
+(paig_decoder_fwd_rollout) to the two separate launches, bit for bit.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -21,7 +25,7 @@ TASKS = {"spring_color": ("spring_ode_cell", 4, 6, 32), "bouncing_balls": ("boun
 OUT_KEYS = ("output", "recons_out", "pos_vel_seq", "enc_pos")
 
 
-def _run(task, byte_targets, steps=3, B=6, N=14, extrap=4):
+def _run(task, byte_targets, steps=3, B=6, N=14, extrap=4, merge=True):
     from paig_reproduction_amd.nn.datasets.synth import render_sequences
     from paig_reproduction_amd.nn.network.physics_models import PhysicsNet
     from paig_reproduction_amd.graph_step import GraphStep
@@ -39,20 +43,32 @@ def _run(task, byte_targets, steps=3, B=6, N=14, extrap=4):
     if byte_targets:
         gs.eng.byte_targets = it.bind_targets(xbuf, ins + pred)
     rec = []
-    for s in range(steps):   # N=14, B=6: the third batch opens a new epoch (a new permutation)
-        it.next_batch(B, out=xbuf)
-        loss = gs.eager()
-        torch.cuda.synchronize()
-        r = {k: getattr(m, k).detach().clone() for k in OUT_KEYS}
-        r.update(loss=loss.detach().clone(), extrap=m.extrap_loss.detach().clone(),
-                 recons=m.recons_loss.detach().clone(), xhead=xbuf[:, :ins + pred].clone())
-        r.update({"grad:" + n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None})
-        if byte_targets:
-            r["tail_nan"] = bool(torch.isnan(xbuf[:, ins + pred:]).all())
-        rec.append(r)
+    old_env = os.environ.get("PAIG_MERGE_ROLL")
+    os.environ["PAIG_MERGE_ROLL"] = "1" if merge else "0"
+    try:
+        for s in range(steps):   # N=14, B=6: the third batch opens a new epoch (a new permutation)
+            rec.append(_step(m, gs, it, xbuf, B, ins, pred, byte_targets))
+    finally:
+        if old_env is None:
+            os.environ.pop("PAIG_MERGE_ROLL")
+        else:
+            os.environ["PAIG_MERGE_ROLL"] = old_env
     r = {"param:" + n: p.detach().clone() for n, p in m.named_parameters()}
     rec.append(r)
     return rec, it.get_epoch()
+
+
+def _step(m, gs, it, xbuf, B, ins, pred, byte_targets):
+    it.next_batch(B, out=xbuf)
+    loss = gs.eager()
+    torch.cuda.synchronize()
+    r = {k: getattr(m, k).detach().clone() for k in OUT_KEYS}
+    r.update(loss=loss.detach().clone(), extrap=m.extrap_loss.detach().clone(), recons=m.recons_loss.detach().clone(),
+             xhead=xbuf[:, :ins + pred].clone())
+    r.update({"grad:" + n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None})
+    if byte_targets:
+        r["tail_nan"] = bool(torch.isnan(xbuf[:, ins + pred:]).all())
+    return r
 
 
 def _same(a, b):
@@ -73,6 +89,17 @@ def test_byte_targets_step_bit_identical(task):
         if "tail_nan" in b:
             assert b["tail_nan"], f"step {s}: the bound gather wrote frames past the encoder's"
     assert np.isfinite(float(got[-2]["loss"]))
+
+
+@pytest.mark.parametrize("task", list(TASKS))
+def test_rollout_merged_with_recon_decode_bit_identical(task):
+    """paig_decoder_fwd_rollout (the rollout and the reconstruction decode in
+    one launch) gives the two separate launches' step bit for bit."""
+    ref, _ = _run(task, True, merge=False)
+    got, _ = _run(task, True, merge=True)
+    for s, (a, b) in enumerate(zip(ref, got)):
+        bad = [k for k in a if k != "tail_nan" and not _same(a[k], b[k])] if set(a) == set(b) else sorted(set(a) ^ set(b))
+        assert not bad, f"step {s}: {bad[:8]}"
 
 
 def test_byte_targets_unbound_buffer_uses_float_frames():
