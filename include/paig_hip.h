@@ -31,7 +31,7 @@ extern "C" {
 /* Version of this interface: bumped whenever an entry point's argument list
  * or a data layout it exchanges changes (the Python binding refuses a library
  * of another version). */
-#define PAIG_ABI_VERSION 5
+#define PAIG_ABI_VERSION 6
 const char* paig_last_error(void);
 int paig_abi_version(void);
 /* f16 range guard of the split-precision path.  Activations and gradients
@@ -113,6 +113,16 @@ int paig_conv2d_fwd_pwc(const float* in, long long in_fs, int in_grp, long long 
 long long paig_conv_wprep_size(int cin, int cout, int ks);
 int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
                     void* const* out, void* stream);
+/* paig_conv_wprep deferred to the next split forward launch of this thread:
+ * a 3-input-channel forward (the U-Net's first layer) runs the jobs in extra
+ * blocks of its own launch, with its own weights staged in-kernel (the same
+ * values as its image); any other split forward launches them first;
+ * paig_unet_fwd_ex flushes what is left before it returns.  Falls back to
+ * paig_conv_wprep for more than 64 jobs or with jobs already pending. */
+int paig_conv_wprep_defer(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
+                          void* const* out, void* stream);
+/* launch any deferred weight prep now (stream order) */
+int paig_conv_wprep_flush(void* stream);
 /* Test hook (no reference counterpart): cap the persistent blocks of the
  * split forward / data-gradient launches (paig_conv2d_fwd*, flags & 128 or
  * 256) at cap per output-channel slice, so every block walks many tiles even

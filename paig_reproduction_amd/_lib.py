@@ -17,7 +17,7 @@ XMAX_SLOTS = 2048
 
 AB_PATH = os.environ.get("PAIG_AB_LIB")
 # include/paig_hip.h PAIG_ABI_VERSION: the SIGNATURES below are this version's
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -37,6 +37,8 @@ SIGNATURES = {
     "paig_conv2d_fwd_pw": (I, [P, LL, I, LL, P, LL, P, LL, P, P, I, I, I, I, I, I, I, P, I, P, LL, P, P]),
     "paig_conv_wprep_size": (LL, [I, I, I]),
     "paig_conv_wprep": (I, [I, P, P, P, P, P, P, P]),
+    "paig_conv_wprep_defer": (I, [I, P, P, P, P, P, P, P]),
+    "paig_conv_wprep_flush": (I, [P]),
     "paig_conv2d_wgrad_ex": (I, [P, LL, I, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_wgrad_pf": (I, [P, LL, I, LL, P, LL, P, LL, P, LL, P, I, P, I, I, I, I, I, I, I, P, I, P]),
     "paig_conv2d_mfma_supported": (I, [I, I, I, I, I, I, I]),

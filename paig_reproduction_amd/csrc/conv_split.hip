@@ -213,9 +213,9 @@ __device__ __forceinline__ int fwd_mtile(int wv, int mt) {
 // maxpool_bwd_relu's arithmetic (conv_bwd.hip's fold)
 template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false, bool UPT = false,
           bool PF = false>
-__global__ void __launch_bounds__(256, 2)
-conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
-                 int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp, PoolOut pout) {
+__device__ __forceinline__ void conv_fwd_split_body(FView in, FViewW out, FView aux, const float* __restrict__ w,
+                                                    const float* __restrict__ bias, int F, int flags, int ntiles, XMax xm,
+                                                    const s16x8* __restrict__ wp, PoolOut pout, int bx, int gx) {
   using C = SFwdCfg<CIN, COUT, H, W, KS, UPS, PM>;
   static_assert(!PF || (DG && !UPS && !POOL && !UPT && C::UPX == 2 && H % 2 == 0 && CIN % 8 == 0),
                 "pool fold: dgrad staging units of one window's pixel pair");
@@ -360,7 +360,7 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   // any magnitude) is scaled per tile by one power of two from the tile's
   // block max (tile_max, commit) and tinv takes it and the weight exponent
   // back out exactly.  The block's running max of the tile maxima goes to
-  // xm.p[blockIdx.x] (the wgrad of the same input scales X by their max).
+  // xm.p[bx] (the wgrad of the same input scales X by their max).
   constexpr bool SCL = PM == 0, DYN = PM == 0 && PAIG_SCALE_MODE < 2;
   float tsc = 1.f, tinv[NT], xrun = 0.f;
 #pragma unroll
@@ -556,11 +556,11 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   // tile ntiles lies beyond frame F and every lane reads paig_zeros (the
   // prefetch stays unconditional: branch-free for the load counting)
   // UPT: logical tile l of this block is band l % NRB of its (l / NRB)-th frame
-  int lt = UPT ? 0 : blockIdx.x;
-  const int lstep = UPT ? 1 : gridDim.x;
+  int lt = UPT ? 0 : bx;
+  const int lstep = UPT ? 1 : gx;
   auto tile_of = [&](int l) {
     if constexpr (UPT) {
-      const int f = blockIdx.x + (l / NRB) * gridDim.x;
+      const int f = bx + (l / NRB) * gx;
       return f < F ? f * NRB + l % NRB : ntiles;
     } else {
       return l < ntiles ? xcd_tile(l, ntiles) : ntiles;
@@ -863,12 +863,23 @@ conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, c
   if constexpr (PM == 0) {
     f16_range_note(rmax);
     if (xm.p && blockIdx.y == 0) {
-      if (tid == 0) xm.p[blockIdx.x] = xrun;
-      if (blockIdx.x == 0)
-        for (int i = gridDim.x + tid; i < xm.n; i += 256) xm.p[i] = 0.f;
-      for (int i = blockIdx.x * 256 + tid; i < xm.zn; i += gridDim.x * 256) xm.z[i] = 0.f;   // later layers' slots
+      if (tid == 0) xm.p[bx] = xrun;
+      if (bx == 0)
+        for (int i = gx + tid; i < xm.n; i += 256) xm.p[i] = 0.f;
+      for (int i = bx * 256 + tid; i < xm.zn; i += gx * 256) xm.z[i] = 0.f;   // later layers' slots
     }
   }
+}
+
+// bx / gx: this block's index and the block count of the tile walk (the
+// launch's own, or those of the forward's share of a merged launch)
+template <int CIN, int COUT, int H, int W, int KS, bool DG, bool UPS, int PM, bool POOL = false, bool UPT = false,
+          bool PF = false>
+__global__ void __launch_bounds__(256, 2)
+conv_fwd_split_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
+                 int flags, int ntiles, XMax xm, const s16x8* __restrict__ wp, PoolOut pout) {
+  conv_fwd_split_body<CIN, COUT, H, W, KS, DG, UPS, PM, POOL, UPT, PF>(in, out, aux, w, bias, F, flags, ntiles, xm, wp,
+                                                                      pout, blockIdx.x, gridDim.x);
 }
 
 // ===================================================================== wgrad
@@ -1568,6 +1579,155 @@ conv_wgrad_split_k(FView x_, FView dy_, float* __restrict__ slab, int F, int nti
 
 // paig_debug_fwd_block_cap: at most this many persistent blocks per COUT
 // slice in the split forward / dgrad launches (0: the resident count), so the
+// ----------------------------------------------------------- weight prep
+// The forward / dgrad kernels' weight images, built once per step for every
+// conv: a header of one int per output channel (its weight exponent: the
+// channel's max |w| scaled into [2^14, 2^15), so no magnitude overflows f16
+// and every weight keeps 22 significant bits relative to its channel's
+// largest), then the scaled weights split into f16 hi / lo, in fragment
+// order over the whole COUT: entry (s, nt, lane) = 8 channels of k-chunk
+// 4s + lane/16 for output channel 16 nt + lane%16; the lo image follows the
+// hi one.  A block then stages its slice with coalesced 16-byte copies
+// instead of one scattered 4-byte weight load (and split) per value, which
+// measured 0.4-8 us per launch (the most on the small-frame, wide-channel
+// layers).  The kernels' in-kernel staging (no image) forms the same
+// exponents and values.
+struct WPrepJob {
+  const float* w;
+  s16x8* out;
+  int cin, cout, ks, dg;
+};
+constexpr int WPREP_MAX = 64;
+struct WPrepJobs {
+  WPrepJob j[WPREP_MAX];
+  int blk0[WPREP_MAX + 1];   // first block of each job (one block per 16-channel N-tile)
+  int n;
+};
+constexpr int WPREP_T = 256;
+
+__device__ __forceinline__ int wprep_hdr_entries(int cout) { return (cout + 15) / 16 * 16 * 4 / 16; }
+
+// one block per (job, N-tile of 16 output channels, WPREP_S k-steps): the
+// 16 channel maxima (thread t: channel t % 16; every block of the tile forms
+// them, from L2), their exponents, then its k-steps' entries
+#ifndef PAIG_WPREP_S
+#define PAIG_WPREP_S 4
+#endif
+constexpr int WPREP_S = PAIG_WPREP_S;
+__device__ __forceinline__ void conv_wprep_body(const WPrepJobs& jobs, int bid) {
+  int q = 0;
+  while (q + 1 < jobs.n && bid >= jobs.blk0[q + 1]) ++q;
+  const WPrepJob jb = jobs.j[q];
+  if (jb.dg == 2) {   // a dense layer's weight [cout][cin] -> out [cin][cout] fp32 (32 x 32 tiles)
+    __shared__ float T[32][33];
+    const int bl = bid - jobs.blk0[q], tx = (bl % ((jb.cin + 31) / 32)) * 32,
+              ty = (bl / ((jb.cin + 31) / 32)) * 32, c = threadIdx.x & 31, r = threadIdx.x >> 5;
+    for (int y = r; y < 32; y += WPREP_T / 32)
+      if (ty + y < jb.cout && tx + c < jb.cin) T[y][c] = jb.w[(long long)(ty + y) * jb.cin + tx + c];
+    __syncthreads();
+    float* o = reinterpret_cast<float*>(jb.out);
+    for (int y = r; y < 32; y += WPREP_T / 32)
+      if (tx + y < jb.cin && ty + c < jb.cout) o[(long long)(tx + y) * jb.cout + ty + c] = T[c][y];
+    return;
+  }
+  const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16, NS = (KC + 3) / 4;
+  const int NSC = (NS + WPREP_S - 1) / WPREP_S;   // k-step chunks per N-tile
+  const int bl = bid - jobs.blk0[q], nt = bl / NSC, s0 = (bl % NSC) * WPREP_S;
+  const int tid = threadIdx.x;
+  auto wv = [&](int kc, int j, int co) {
+    float v = 0.f;
+    if (kc < KC && co < jb.cout) {
+      const int tap = kc / CC, ci = (kc % CC) * 8 + j;
+      if (ci < jb.cin) v = jb.dg ? jb.w[(ci * jb.cout + co) * KK + (KK - 1 - tap)] : jb.w[(co * jb.cin + ci) * KK + tap];
+    }
+    return v;
+  };
+  __shared__ float red[WPREP_T];
+  __shared__ int ex[16];
+  const int cl = tid & 15, co = nt * 16 + cl;
+  // (unrolled: the loads of one thread are independent, keep 8 in flight)
+  float m = 0.f;
+#pragma unroll 8
+  for (int i = tid >> 4; i < KC * 8; i += WPREP_T / 16) m = fmaxf(m, fabsf(wv(i >> 3, i & 7, co)));
+  red[tid] = m;
+  __syncthreads();
+  if (tid < 16) {
+    float mm = 0.f;
+    for (int r = 0; r < WPREP_T / 16; ++r) mm = fmaxf(mm, red[r * 16 + tid]);
+    ex[tid] = f16_scale_exp_v(mm);
+    if (s0 == 0) reinterpret_cast<int*>(jb.out)[nt * 16 + tid] = ex[tid];
+  }
+  __syncthreads();
+  const int HDR = wprep_hdr_entries(jb.cout), ENT = NS * NTT * 64;
+  short* img = reinterpret_cast<short*>(jb.out + HDR);
+  // this block's entries: (s, lane) -> value index t = ((s - s0) * 64 + lane) * 8 + j
+  const int ns = NS - s0 < WPREP_S ? NS - s0 : WPREP_S;
+#pragma unroll 8
+  for (int t = tid; t < ns * 64 * 8; t += WPREP_T) {
+    const int j = t & 7, ln = (t >> 3) & 63, s = s0 + (t >> 9);
+    const int kc = 4 * s + (ln >> 4), c = nt * 16 + (ln & 15);
+    float rm = 0.f;
+    short h, l;
+    split<0>(__builtin_amdgcn_ldexpf(wv(kc, j, c), ex[ln & 15]), h, l, rm);
+    const long long e = (long long)(s * NTT + nt) * 64 + ln;
+    img[e * 8 + j] = h;
+    img[((long long)ENT + e) * 8 + j] = l;
+  }
+}
+
+__global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) { conv_wprep_body(jobs, blockIdx.x); }
+
+// The step's weight prep and the U-Net's first forward conv (3 input
+// channels) in one launch: blocks 0 .. nwp-1 run the prep jobs, the others
+// the forward, which stages its own (tiny) weights in-kernel -- the same
+// exponents and values as its image -- so nothing in the launch waits on the
+// prep (paig_conv_wprep_defer)
+template <int CIN, int COUT, int H, int W, int KS, int PM>
+__global__ void __launch_bounds__(256, 2)
+conv_fwd_wprep_k(FView in, FViewW out, FView aux, const float* __restrict__ w, const float* __restrict__ bias, int F,
+                 int flags, int ntiles, XMax xm, PoolOut pout, WPrepJobs jobs, int nwp) {
+  if ((int)blockIdx.x < nwp) {   // block-uniform
+    conv_wprep_body(jobs, blockIdx.x);
+    return;
+  }
+  conv_fwd_split_body<CIN, COUT, H, W, KS, false, false, PM>(in, out, aux, w, bias, F, flags, ntiles, xm, nullptr, pout,
+                                                            (int)blockIdx.x - nwp, (int)gridDim.x - nwp);
+}
+
+// deferred weight prep (paig_conv_wprep_defer): taken by the next eligible
+// split forward (above), launched on its own before any other one
+WPrepJobs g_wpend{};
+int g_wpend_blocks = 0;   // 0: none pending
+int wprep_build(WPrepJobs& jobs, int n, const float* const* w, const int* cin, const int* cout, const int* ks,
+                const int* dg, void* const* out, int* blocks_out) {
+  jobs = WPrepJobs{};
+  jobs.n = n;
+  int blocks = 0;
+  for (int q = 0; q < n; ++q) {
+    PAIG_REQUIRE(w[q] && out[q] && cin[q] > 0 && cout[q] > 0 && ks[q] > 0, "conv_wprep: job %d", q);
+    PAIG_REQUIRE(((uintptr_t)out[q] & 15) == 0, "conv_wprep: job %d output not 16-byte aligned", q);
+    jobs.j[q] = WPrepJob{w[q], static_cast<s16x8*>(out[q]), cin[q], cout[q], ks[q], dg[q]};
+    jobs.blk0[q] = blocks;
+    if (dg[q] == 2) {   // dense transpose job
+      blocks += (cin[q] + 31) / 32 * ((cout[q] + 31) / 32);
+      continue;
+    }
+    const int NS = (ks[q] * ks[q] * ((cin[q] + 7) / 8) + 3) / 4;
+    blocks += (cout[q] + 15) / 16 * ((NS + WPREP_S - 1) / WPREP_S);
+  }
+  jobs.blk0[n] = blocks;
+  *blocks_out = blocks;
+  return 0;
+}
+int wprep_flush(hipStream_t st) {
+  if (!g_wpend_blocks) return 0;
+  const int nb = g_wpend_blocks;
+  g_wpend_blocks = 0;
+  hipLaunchKernelGGL(conv_wprep_k, dim3(nb), dim3(WPREP_T), 0, st, g_wpend);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
 // tests can make every block walk many tiles at small frame counts
 static int g_fwd_block_cap = 0;
 // pending pre-zero range for the next split forward (paig_conv_fwd_prezero)
@@ -1612,6 +1772,21 @@ static int sfwd_launch(FView in, FViewW out, FView aux, const float* w, const fl
   }
   if (PF) PAIG_REQUIRE(pout.p && pout.code, "conv split dgrad: the pool fold needs the pooled gradient and codes");
   else if (flags & 64) PAIG_REQUIRE(C::POOLOK && pout.p, "conv split fwd: no fused pool for Cin=%d Cout=%d H=%d", CIN, COUT, H);
+  if constexpr (CIN == 3 && PM == 0 && !DG && !UPS && !UPT && !PF && C::NB == 1) {
+    if (g_wpend_blocks && !(flags & 64)) {   // the deferred weight prep rides in this launch
+      auto km = conv_fwd_wprep_k<CIN, COUT, H, W, KS, PM>;
+      static bool attr = false;
+      if (!attr && LDS > 64 * 1024) (void)hipFuncSetAttribute((const void*)km, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+      attr = true;
+      const int nwp = g_wpend_blocks;
+      g_wpend_blocks = 0;
+      hipLaunchKernelGGL(km, dim3(nwp + nb), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles, xm, pout, g_wpend,
+                         nwp);
+      PAIG_CHECK_LAUNCH();
+      return 0;
+    }
+  }
+  if (int rc = wprep_flush(st)) return rc;   // a forward that reads the images: they come first
   hipLaunchKernelGGL(k, dim3(nb, C::NB), dim3(256), LDS, st, in, out, aux, w, b, F, flags, ntiles, xm,
                      PM == 0 ? static_cast<const s16x8*>(wp) : nullptr, pout);
   PAIG_CHECK_LAUNCH();
@@ -1840,102 +2015,6 @@ int paig_conv_split_supported(int what, int Cin, int Cout, int H, int W, int ks,
   return 0;
 }
 
-// ----------------------------------------------------------- weight prep
-// The forward / dgrad kernels' weight images, built once per step for every
-// conv: a header of one int per output channel (its weight exponent: the
-// channel's max |w| scaled into [2^14, 2^15), so no magnitude overflows f16
-// and every weight keeps 22 significant bits relative to its channel's
-// largest), then the scaled weights split into f16 hi / lo, in fragment
-// order over the whole COUT: entry (s, nt, lane) = 8 channels of k-chunk
-// 4s + lane/16 for output channel 16 nt + lane%16; the lo image follows the
-// hi one.  A block then stages its slice with coalesced 16-byte copies
-// instead of one scattered 4-byte weight load (and split) per value, which
-// measured 0.4-8 us per launch (the most on the small-frame, wide-channel
-// layers).  The kernels' in-kernel staging (no image) forms the same
-// exponents and values.
-struct WPrepJob {
-  const float* w;
-  s16x8* out;
-  int cin, cout, ks, dg;
-};
-constexpr int WPREP_MAX = 64;
-struct WPrepJobs {
-  WPrepJob j[WPREP_MAX];
-  int blk0[WPREP_MAX + 1];   // first block of each job (one block per 16-channel N-tile)
-  int n;
-};
-constexpr int WPREP_T = 256;
-
-__device__ __forceinline__ int wprep_hdr_entries(int cout) { return (cout + 15) / 16 * 16 * 4 / 16; }
-
-// one block per (job, N-tile of 16 output channels, WPREP_S k-steps): the
-// 16 channel maxima (thread t: channel t % 16; every block of the tile forms
-// them, from L2), their exponents, then its k-steps' entries
-#ifndef PAIG_WPREP_S
-#define PAIG_WPREP_S 4
-#endif
-constexpr int WPREP_S = PAIG_WPREP_S;
-__global__ void __launch_bounds__(WPREP_T) conv_wprep_k(WPrepJobs jobs) {
-  int q = 0;
-  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.blk0[q + 1]) ++q;
-  const WPrepJob jb = jobs.j[q];
-  if (jb.dg == 2) {   // a dense layer's weight [cout][cin] -> out [cin][cout] fp32 (32 x 32 tiles)
-    __shared__ float T[32][33];
-    const int bl = (int)blockIdx.x - jobs.blk0[q], tx = (bl % ((jb.cin + 31) / 32)) * 32,
-              ty = (bl / ((jb.cin + 31) / 32)) * 32, c = threadIdx.x & 31, r = threadIdx.x >> 5;
-    for (int y = r; y < 32; y += WPREP_T / 32)
-      if (ty + y < jb.cout && tx + c < jb.cin) T[y][c] = jb.w[(long long)(ty + y) * jb.cin + tx + c];
-    __syncthreads();
-    float* o = reinterpret_cast<float*>(jb.out);
-    for (int y = r; y < 32; y += WPREP_T / 32)
-      if (tx + y < jb.cin && ty + c < jb.cout) o[(long long)(tx + y) * jb.cout + ty + c] = T[c][y];
-    return;
-  }
-  const int KK = jb.ks * jb.ks, CC = (jb.cin + 7) / 8, KC = KK * CC, NTT = (jb.cout + 15) / 16, NS = (KC + 3) / 4;
-  const int NSC = (NS + WPREP_S - 1) / WPREP_S;   // k-step chunks per N-tile
-  const int bl = (int)blockIdx.x - jobs.blk0[q], nt = bl / NSC, s0 = (bl % NSC) * WPREP_S;
-  const int tid = threadIdx.x;
-  auto wv = [&](int kc, int j, int co) {
-    float v = 0.f;
-    if (kc < KC && co < jb.cout) {
-      const int tap = kc / CC, ci = (kc % CC) * 8 + j;
-      if (ci < jb.cin) v = jb.dg ? jb.w[(ci * jb.cout + co) * KK + (KK - 1 - tap)] : jb.w[(co * jb.cin + ci) * KK + tap];
-    }
-    return v;
-  };
-  __shared__ float red[WPREP_T];
-  __shared__ int ex[16];
-  const int cl = tid & 15, co = nt * 16 + cl;
-  // (unrolled: the loads of one thread are independent, keep 8 in flight)
-  float m = 0.f;
-#pragma unroll 8
-  for (int i = tid >> 4; i < KC * 8; i += WPREP_T / 16) m = fmaxf(m, fabsf(wv(i >> 3, i & 7, co)));
-  red[tid] = m;
-  __syncthreads();
-  if (tid < 16) {
-    float mm = 0.f;
-    for (int r = 0; r < WPREP_T / 16; ++r) mm = fmaxf(mm, red[r * 16 + tid]);
-    ex[tid] = f16_scale_exp_v(mm);
-    if (s0 == 0) reinterpret_cast<int*>(jb.out)[nt * 16 + tid] = ex[tid];
-  }
-  __syncthreads();
-  const int HDR = wprep_hdr_entries(jb.cout), ENT = NS * NTT * 64;
-  short* img = reinterpret_cast<short*>(jb.out + HDR);
-  // this block's entries: (s, lane) -> value index t = ((s - s0) * 64 + lane) * 8 + j
-  const int ns = NS - s0 < WPREP_S ? NS - s0 : WPREP_S;
-#pragma unroll 8
-  for (int t = tid; t < ns * 64 * 8; t += WPREP_T) {
-    const int j = t & 7, ln = (t >> 3) & 63, s = s0 + (t >> 9);
-    const int kc = 4 * s + (ln >> 4), c = nt * 16 + (ln & 15);
-    float rm = 0.f;
-    short h, l;
-    split<0>(__builtin_amdgcn_ldexpf(wv(kc, j, c), ex[ln & 15]), h, l, rm);
-    const long long e = (long long)(s * NTT + nt) * 64 + ln;
-    img[e * 8 + j] = h;
-    img[((long long)ENT + e) * 8 + j] = l;
-  }
-}
-
 void paig_conv_fwd_prezero(float* z, int zn) {
   g_prezero.z = z;
   g_prezero.zn = zn;
@@ -1963,29 +2042,34 @@ long long paig_conv_wprep_size(int cin, int cout, int ks) {
 
 int paig_conv_wprep(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
                     void* const* out, void* stream) {
+  if (int rc = wprep_flush((hipStream_t)stream)) return rc;   // (in stream order)
   for (int b = 0; b < n; b += WPREP_MAX) {
-    WPrepJobs jobs{};
-    jobs.n = n - b < WPREP_MAX ? n - b : WPREP_MAX;
+    WPrepJobs jobs;
     int blocks = 0;
-    for (int q = 0; q < jobs.n; ++q) {
-      const int i = b + q;
-      PAIG_REQUIRE(w[i] && out[i] && cin[i] > 0 && cout[i] > 0 && ks[i] > 0, "conv_wprep: job %d", i);
-      PAIG_REQUIRE(((uintptr_t)out[i] & 15) == 0, "conv_wprep: job %d output not 16-byte aligned", i);
-      jobs.j[q] = WPrepJob{w[i], static_cast<s16x8*>(out[i]), cin[i], cout[i], ks[i], dg[i]};
-      jobs.blk0[q] = blocks;
-      if (dg[i] == 2) {   // dense transpose job
-        blocks += (cin[i] + 31) / 32 * ((cout[i] + 31) / 32);
-        continue;
-      }
-      const int NS = (ks[i] * ks[i] * ((cin[i] + 7) / 8) + 3) / 4;
-      blocks += (cout[i] + 15) / 16 * ((NS + WPREP_S - 1) / WPREP_S);
-    }
-    jobs.blk0[jobs.n] = blocks;
+    const int m = n - b < WPREP_MAX ? n - b : WPREP_MAX;
+    if (int rc = wprep_build(jobs, m, w + b, cin + b, cout + b, ks + b, dg + b, out + b, &blocks)) return rc;
     hipLaunchKernelGGL(conv_wprep_k, dim3(blocks), dim3(WPREP_T), 0, (hipStream_t)stream, jobs);
     PAIG_CHECK_LAUNCH();
   }
   return 0;
 }
+
+// paig_conv_wprep deferred to the next split forward launch on this thread:
+// the U-Net's first layer (3 input channels, split arithmetic) runs the jobs
+// in extra blocks of its own launch; any other split forward launches them
+// first, and paig_unet_fwd_ex flushes them before it returns.  More than one
+// launch's worth of jobs, or jobs still pending: launched now.
+int paig_conv_wprep_defer(int n, const float* const* w, const int* cin, const int* cout, const int* ks, const int* dg,
+                          void* const* out, void* stream) {
+  if (n > WPREP_MAX || g_wpend_blocks) return paig_conv_wprep(n, w, cin, cout, ks, dg, out, stream);
+  if (n <= 0) return 0;
+  int blocks = 0;
+  if (int rc = wprep_build(g_wpend, n, w, cin, cout, ks, dg, out, &blocks)) return rc;
+  g_wpend_blocks = blocks;
+  return 0;
+}
+
+int paig_conv_wprep_flush(void* stream) { return wprep_flush((hipStream_t)stream); }
 
 }  // extern "C"
 

@@ -287,6 +287,12 @@ struct UProbe {
 int fwd_impl(int net, int F, int H, int K, int math, int flags, const float* x, long long x_fs, int x_grp,
              long long x_gs, const float* const* w, const float* const* b, float* logits, const void* const* wpf,
              const void* const* wpd, void* ws, size_t ws_bytes, UProbe pr, void* stream) {
+  // weight prep deferred by the caller (paig_conv_wprep_defer): the first
+  // split forward takes it; whatever is left runs before this call returns
+  struct WprepFlush {
+    void* st;
+    ~WprepFlush() { (void)paig_conv_wprep_flush(st); }
+  } wflush{stream};
   if (int rc = check_args(net, F, H, K, math)) return rc;
   UPlan p;
   build_plan(p, net, K);

@@ -552,10 +552,13 @@ class Engine:
                 outs.append(wp[(j[0], j[1])])
                 off += -(-n // 8) * 8   # 16-byte aligned images
             n = len(jobs)
-            L.paig_conv_wprep(n, (ctypes.c_void_p * n)(*[ptr(j[2]) for j in jobs]),
-                              (ctypes.c_int * n)(*[j[3] for j in jobs]), (ctypes.c_int * n)(*[j[4] for j in jobs]),
-                              (ctypes.c_int * n)(*[j[5] for j in jobs]), (ctypes.c_int * n)(*[j[1] for j in jobs]),
-                              (ctypes.c_void_p * n)(*outs), st)
+            # deferred: the U-Net's first conv carries the prep in its own
+            # launch (PAIG_WPREP_MERGE=0: a separate launch, the A/B)
+            wprep = L.paig_conv_wprep_defer if os.environ.get("PAIG_WPREP_MERGE", "1") != "0" else L.paig_conv_wprep
+            wprep(n, (ctypes.c_void_p * n)(*[ptr(j[2]) for j in jobs]),
+                  (ctypes.c_int * n)(*[j[3] for j in jobs]), (ctypes.c_int * n)(*[j[4] for j in jobs]),
+                  (ctypes.c_int * n)(*[j[5] for j in jobs]), (ctypes.c_int * n)(*[j[1] for j in jobs]),
+                  (ctypes.c_void_p * n)(*outs), st)
             S["wprep_buf"] = buf
             wpf = _parr([wp[(c, 0)] for c in range(lay.nconv)])
             wpd = _parr([wp.get((c, 1), 0) for c in range(lay.nconv)])

@@ -6,8 +6,9 @@ batch -- outputs, the three losses, every parameter gradient and the RMSprop
 update -- for every task shape bench.py runs, across epoch boundaries (the
 decoders follow the permutation through the saved row indices).  The frames
 the bound gather skips are poisoned with NaN: any read of them would show.
-The same harness holds the merged rollout + reconstruction-decode launch
-(paig_decoder_fwd_rollout) to the two separate launches, bit for bit.
+The same harness holds the merged launches (the rollout + reconstruction
+decode, paig_decoder_fwd_rollout; the weight prep + first conv,
+paig_conv_wprep_defer) to their separate forms, bit for bit.
 """
 import os
 
@@ -43,16 +44,19 @@ def _run(task, byte_targets, steps=3, B=6, N=14, extrap=4, merge=True):
     if byte_targets:
         gs.eng.byte_targets = it.bind_targets(xbuf, ins + pred)
     rec = []
-    old_env = os.environ.get("PAIG_MERGE_ROLL")
-    os.environ["PAIG_MERGE_ROLL"] = "1" if merge else "0"
+    knobs = ("PAIG_MERGE_ROLL", "PAIG_WPREP_MERGE")   # the merged launches, or their separate A/B forms
+    old_env = {k: os.environ.get(k) for k in knobs}
+    for k in knobs:
+        os.environ[k] = "1" if merge else "0"
     try:
         for s in range(steps):   # N=14, B=6: the third batch opens a new epoch (a new permutation)
             rec.append(_step(m, gs, it, xbuf, B, ins, pred, byte_targets))
     finally:
-        if old_env is None:
-            os.environ.pop("PAIG_MERGE_ROLL")
-        else:
-            os.environ["PAIG_MERGE_ROLL"] = old_env
+        for k, v in old_env.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     r = {"param:" + n: p.detach().clone() for n, p in m.named_parameters()}
     rec.append(r)
     return rec, it.get_epoch()
@@ -92,9 +96,11 @@ def test_byte_targets_step_bit_identical(task):
 
 
 @pytest.mark.parametrize("task", list(TASKS))
-def test_rollout_merged_with_recon_decode_bit_identical(task):
+def test_merged_launches_bit_identical(task):
     """paig_decoder_fwd_rollout (the rollout and the reconstruction decode in
-    one launch) gives the two separate launches' step bit for bit."""
+    one launch) and paig_conv_wprep_defer (the weight prep in the first
+    conv's launch, whose weights are then staged in-kernel) give the separate
+    launches' step bit for bit."""
     ref, _ = _run(task, True, merge=False)
     got, _ = _run(task, True, merge=True)
     for s, (a, b) in enumerate(zip(ref, got)):

@@ -1,0 +1,10 @@
+# weight prep in the first conv's launch: bit-identity + parity/U-Net tests, then A/B bench
+mkdir -p gpurun_out/r6ab
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_byte_targets.py \
+  tests/test_gpu_parity.py tests/test_gpu_unet_abi.py tests/test_gpu_composite.py tests/test_gpu_training.py \
+  tests/test_gpu_modules.py tests/test_gpu_kernels.py -m gpu > gpurun_out/r6ab/tests.log 2>&1 || exit 1
+for r in 1 2 3; do
+  for m in 1 0; do
+    PAIG_WPREP_MERGE=$m timeout -k 10 300 python -u bench.py --legs 0 --cpu_baseline 0 --probe_steps 0 --steps 200 --warmup 20 >> gpurun_out/r6ab/spring_m$m.txt 2>&1 || exit 1
+  done
+done
