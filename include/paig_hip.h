@@ -31,7 +31,7 @@ extern "C" {
 /* Version of this interface: bumped whenever an entry point's argument list
  * or a data layout it exchanges changes (the Python binding refuses a library
  * of another version). */
-#define PAIG_ABI_VERSION 6
+#define PAIG_ABI_VERSION 7
 const char* paig_last_error(void);
 int paig_abi_version(void);
 /* f16 range guard of the split-precision path.  Activations and gradients
@@ -335,6 +335,13 @@ int paig_pos_head_bwd(const float* h3, const float* dpos, float* dh3, int N, int
  *     -> * aux' (auxm 0 none, 1 relu'(aux), 2 tanh'(aux)=1-aux^2)
  * rowsum (optional) = alpha * sum_k op(A)[m][k]: the bias gradient of dW = dY^T X */
 size_t paig_gemm_workspace(int M, int N, int K);
+/* one-shot: the next paig_gemm_ex's split-K epilogue is not launched; the
+ * paig_gemm_ex after it runs it in one more z-plane of its own grid (that
+ * GEMM must not read the deferred output, and its workspace must not hold
+ * the deferred partial slabs: checked); paig_gemm_flush launches a pending
+ * one on its own (paig_gemm_parts does so first) */
+int paig_gemm_defer_epilogue(int on);
+int paig_gemm_flush(void* stream);
 int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
               long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
               const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, void* stream);

@@ -17,7 +17,7 @@ XMAX_SLOTS = 2048
 
 AB_PATH = os.environ.get("PAIG_AB_LIB")
 # include/paig_hip.h PAIG_ABI_VERSION: the SIGNATURES below are this version's
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -95,6 +95,8 @@ SIGNATURES = {
     "paig_gemm_workspace": (SZ, [I, I, I]),
     "paig_gemm_parts_size": (SZ, [I, I, I, I]),
     "paig_gemm_parts": (I, [I, I, I, I, I, P, LL, P, LL, P, SZ, I, P]),
+    "paig_gemm_defer_epilogue": (I, [I]),
+    "paig_gemm_flush": (I, [P]),
     "paig_gemm": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, P]),
     "paig_gemm_ex": (I, [I, I, I, I, I, F32, P, LL, P, LL, F32, P, LL, P, I, I, P, LL, P, P, SZ, I, P]),
     "paig_colsum_workspace": (SZ, [I, I]),

@@ -128,11 +128,36 @@ struct Tile {
 // first: the blocks that re-read one operand tile (the N-tiles of an M-row
 // block, or the M-tiles of an N-column block) then share that XCD's L2
 // instead of fetching the operand once per XCD.
+// A split-K epilogue deferred into the next GEMM launch (paig_gemm_defer_epilogue):
+// that launch's grid has one more z-plane whose blocks run it (S = 0: none)
+struct PendEpi {
+  int M, N, S;
+  const float* part;
+  float* C;
+  long long ldc;
+  float beta;
+  const float* bias;
+  int act, auxm;
+  const float* aux;
+  long long ldaux;
+  const float* rowpart;
+  float* rowsum;
+  int v4;
+};
+__device__ void splitk_epi_run(const PendEpi& pe, int bid, int nb);
+// (a GEMM kernel's first statement: the deferred epilogue's blocks leave)
+#define PAIG_PENDING_EPI(pe)                                                      \
+  if ((pe).S && (int)blockIdx.z == (int)gridDim.z - 1) {                          \
+    splitk_epi_run((pe), blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y); \
+    return;                                                                      \
+  }
+
 struct TileId {
   int x, y, z;
 };
-__device__ __forceinline__ TileId xcd_tile() {
-  const int nx = gridDim.x, ny = gridDim.y, total = nx * ny * gridDim.z;
+// gz: the GEMM's own z-planes (a deferred epilogue's plane excluded)
+__device__ __forceinline__ TileId xcd_tile(int gz) {
+  const int nx = gridDim.x, ny = gridDim.y, total = nx * ny * gz;
   int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
   if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
   TileId t;
@@ -153,13 +178,14 @@ __global__ void __launch_bounds__(256)
 gemm_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
        const float* __restrict__ B, long long ldb, int vecb, float* __restrict__ C, long long ldc, float beta,
        const float* __restrict__ bias, int act, int auxm, const float* __restrict__ aux, long long ldaux,
-       float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart) {
+       float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart, PendEpi pe) {
+  PAIG_PENDING_EPI(pe)
   __shared__ __attribute__((aligned(16))) float As[IMG];
   __shared__ __attribute__((aligned(16))) float Bs[IMG];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
-  const TileId bt = xcd_tile();
+  const TileId bt = xcd_tile((int)gridDim.z - (pe.S ? 1 : 0));
   const int m0 = bt.y * BM, n0 = bt.x * BN;
   const int kbeg = bt.z * kchunk;
   int kend = kbeg + kchunk;
@@ -360,7 +386,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6)))
 gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
              const float* __restrict__ B, long long ldb, int vecb, float* __restrict__ C, long long ldc, float beta,
              const float* __restrict__ bias, int act, int auxm, const float* __restrict__ aux, long long ldaux,
-             float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart) {
+             float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart, PendEpi pe) {
+  PAIG_PENDING_EPI(pe)
   constexpr int NI = PM == 3 ? 1 : 2;
   __shared__ __attribute__((aligned(16))) short S16[4 * SIMG];
   short* Ah = S16;
@@ -370,7 +397,7 @@ gemm_split_k(int M, int N, int K, int kchunk, float alpha, const float* __restri
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
-  const TileId bt = xcd_tile();
+  const TileId bt = xcd_tile((int)gridDim.z - (pe.S ? 1 : 0));
   const int m0 = bt.y * BM, n0 = bt.x * BN;
   const int kbeg = bt.z * kchunk;
   int kend = kbeg + kchunk;
@@ -622,7 +649,8 @@ __global__ void __launch_bounds__(512)
 gemm_split_w_k(int M, int N, int K, int kchunk, float alpha, const float* __restrict__ A, long long lda, int veca,
                const float* __restrict__ B, long long ldb, int vecb, float* __restrict__ C, long long ldc, float beta,
                const float* __restrict__ bias, int act, int auxm, const float* __restrict__ aux, long long ldaux,
-               float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart) {
+               float* __restrict__ part, float* __restrict__ rowsum, float* __restrict__ rowpart, PendEpi pe) {
+  PAIG_PENDING_EPI(pe)
   constexpr int WM = BMT == 64 ? 2 : 4, WN = 8 / WM;
   constexpr int PMW = BMT / WM, PNW = BNT / WN;          // wave patch
   constexpr int MI = PMW / 16, NJ = PNW / 16;
@@ -637,7 +665,7 @@ gemm_split_w_k(int M, int N, int K, int kchunk, float alpha, const float* __rest
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int wm = wv / WN, wn = wv % WN;
-  const TileId bt = xcd_tile();
+  const TileId bt = xcd_tile((int)gridDim.z - (pe.S ? 1 : 0));
   const int m0 = bt.y * BMT, n0 = bt.x * BNT;
   const int kbeg = bt.z * kchunk;
   int kend = kbeg + kchunk;
@@ -798,13 +826,15 @@ __device__ __forceinline__ float sum_strided(const float* __restrict__ p, long l
   return v;
 }
 
-__global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restrict__ part, float* __restrict__ C,
-                                       long long ldc, float beta, const float* __restrict__ bias, int act, int auxm,
-                                       const float* __restrict__ aux, long long ldaux, const float* __restrict__ rowpart,
-                                       float* __restrict__ rowsum) {
+__device__ __forceinline__ void splitk_epi_scalar(int M, int N, int S, const float* __restrict__ part,
+                                                  float* __restrict__ C, long long ldc, float beta,
+                                                  const float* __restrict__ bias, int act, int auxm,
+                                                  const float* __restrict__ aux, long long ldaux,
+                                                  const float* __restrict__ rowpart, float* __restrict__ rowsum, int bid,
+                                                  int nb) {
   const long long n_el = (long long)M * N;
   const long long tot = n_el + (rowsum ? M : 0);
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < tot; i += (long long)gridDim.x * blockDim.x) {
+  for (long long i = bid * (long long)blockDim.x + threadIdx.x; i < tot; i += (long long)nb * blockDim.x) {
     if (i >= n_el) {
       const int m = (int)(i - n_el);
       rowsum[m] = sum_strided(rowpart + m, M, S);
@@ -817,20 +847,26 @@ __global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restr
     C[(long long)m * ldc + n] = epi(v, act, auxm, aux, (long long)m * ldaux + n);
   }
 }
+__global__ void gemm_splitk_epilogue_k(int M, int N, int S, const float* __restrict__ part, float* __restrict__ C,
+                                       long long ldc, float beta, const float* __restrict__ bias, int act, int auxm,
+                                       const float* __restrict__ aux, long long ldaux, const float* __restrict__ rowpart,
+                                       float* __restrict__ rowsum) {
+  splitk_epi_scalar(M, N, S, part, C, ldc, beta, bias, act, auxm, aux, ldaux, rowpart, rowsum, blockIdx.x, gridDim.x);
+}
 
 // Vector form (N % 4 == 0; C, bias, aux and the slabs float4-addressable;
 // S * M * N < 2^31; M * N >= 2^19 so the grid stays wide): 4 consecutive
 // columns per thread, float4 loads of up to 8 partials in flight, 32-bit indexing.  The row sums, if any, take the
 // threads past the element range.  Same per-element order as the scalar form.
-__global__ void __launch_bounds__(256) gemm_splitk_epilogue_v_k(int M, int N, int S, const float* __restrict__ part,
-                                                                float* __restrict__ C, int ldc, float beta,
-                                                                const float* __restrict__ bias, int act, int auxm,
-                                                                const float* __restrict__ aux, int ldaux,
-                                                                const float* __restrict__ rowpart,
-                                                                float* __restrict__ rowsum) {
+__device__ __forceinline__ void splitk_epi_vec(int M, int N, int S, const float* __restrict__ part,
+                                               float* __restrict__ C, int ldc, float beta,
+                                               const float* __restrict__ bias, int act, int auxm,
+                                               const float* __restrict__ aux, int ldaux,
+                                               const float* __restrict__ rowpart, float* __restrict__ rowsum, int bid,
+                                               int nb) {
   const int n_el = M * N, n4 = n_el >> 2;
   const int tot = n4 + (rowsum ? M : 0);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
+  for (int i = bid * blockDim.x + threadIdx.x; i < tot; i += nb * blockDim.x) {
     if (i >= n4) {
       const int m = i - n4;
       rowsum[m] = sum_strided(rowpart + m, M, S);
@@ -866,6 +902,23 @@ __global__ void __launch_bounds__(256) gemm_splitk_epilogue_v_k(int M, int N, in
     v.w = epi(v.w, act, auxm, aux, ao + 3);
     *reinterpret_cast<float4*>(c) = v;
   }
+}
+__global__ void __launch_bounds__(256) gemm_splitk_epilogue_v_k(int M, int N, int S, const float* __restrict__ part,
+                                                                float* __restrict__ C, int ldc, float beta,
+                                                                const float* __restrict__ bias, int act, int auxm,
+                                                                const float* __restrict__ aux, int ldaux,
+                                                                const float* __restrict__ rowpart,
+                                                                float* __restrict__ rowsum) {
+  splitk_epi_vec(M, N, S, part, C, ldc, beta, bias, act, auxm, aux, ldaux, rowpart, rowsum, blockIdx.x, gridDim.x);
+}
+
+__device__ void splitk_epi_run(const PendEpi& pe, int bid, int nb) {
+  if (pe.v4)
+    splitk_epi_vec(pe.M, pe.N, pe.S, pe.part, pe.C, (int)pe.ldc, pe.beta, pe.bias, pe.act, pe.auxm, pe.aux,
+                   (int)pe.ldaux, pe.rowpart, pe.rowsum, bid, nb);
+  else
+    splitk_epi_scalar(pe.M, pe.N, pe.S, pe.part, pe.C, pe.ldc, pe.beta, pe.bias, pe.act, pe.auxm, pe.aux, pe.ldaux,
+                      pe.rowpart, pe.rowsum, bid, nb);
 }
 
 // Split-K factor: the dense layers here are small (M, N <= a few thousand)
@@ -932,15 +985,16 @@ template <bool TA, bool TB>
 static void launch_gemm(int math, int tile, dim3 grid, hipStream_t st, int M, int N, int K, int kchunk, float alpha,
                         const float* A, long long lda, int va, const float* B, long long ldb, int vb, float* C,
                         long long ldc, float beta, const float* bias, int act, int auxm, const float* aux,
-                        long long ldaux, float* part, float* rowsum, float* rowpart) {
+                        long long ldaux, float* part, float* rowsum, float* rowpart, const PendEpi& pe) {
+  if (pe.S) grid.z += 1;   // the deferred epilogue's plane
 #define PAIG_L(KERN)                                                                                          \
   hipLaunchKernelGGL(KERN, grid, dim3(256), 0, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, \
-                     bias, act, auxm, aux, ldaux, part, rowsum, rowpart)
+                     bias, act, auxm, aux, ldaux, part, rowsum, rowpart, pe)
   // the split kernels' branch-free loads: float4 when both operands allow
   const bool v = va && vb;
 #define PAIG_W(KERN) \
   hipLaunchKernelGGL(KERN, grid, dim3(512), 0, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, \
-                     bias, act, auxm, aux, ldaux, part, rowsum, rowpart)
+                     bias, act, auxm, aux, ldaux, part, rowsum, rowpart, pe)
 #define PAIG_S(PM_) \
   do {                                              \
     if (v) PAIG_L((gemm_split_k<TA, TB, PM_, true>)); \
@@ -970,23 +1024,39 @@ static void launch_gemm(int math, int tile, dim3 grid, hipStream_t st, int M, in
 
 // split-K epilogue: C = sum_s part[s] (+ beta C) (+ bias) -> act -> * aux'
 // (and rowsum = sum_s rowpart[s]); the vector form where the shapes allow
-void paig_gemm_splitk_finish(int M, int N, int S, const float* part, float* C, long long ldc, float beta,
-                             const float* bias, int act, int auxm, const float* aux, long long ldaux,
-                             const float* rowpart, float* rowsum, hipStream_t st) {
+static PendEpi make_epi(int M, int N, int S, const float* part, float* C, long long ldc, float beta, const float* bias,
+                        int act, int auxm, const float* aux, long long ldaux, const float* rowpart, float* rowsum) {
   const bool v4 = N % 4 == 0 && vec_ok(C, ldc) && (!bias || (uintptr_t)bias % 16 == 0) &&
                   (!aux || auxm == AUX_NONE || vec_ok(aux, ldaux)) && (uintptr_t)part % 16 == 0 &&
                   (long long)S * M * N < (1ll << 31) && (long long)M * ldc < (1ll << 31) &&
                   (long long)M * ldaux < (1ll << 31) &&
                   (long long)M * N >= (1 << 19);   // smaller outputs keep the scalar form (4x the threads)
-  long long n_el = (v4 ? (long long)M * N / 4 : (long long)M * N) + (rowsum ? M : 0);
+  return PendEpi{M, N, S, part, C, ldc, beta, bias, act, auxm, aux, ldaux, rowpart, rowsum, v4 ? 1 : 0};
+}
+static void launch_epi(const PendEpi& e, hipStream_t st) {
+  long long n_el = (e.v4 ? (long long)e.M * e.N / 4 : (long long)e.M * e.N) + (e.rowsum ? e.M : 0);
   int g = cdiv(n_el, 256);
   if (g > 4096) g = 4096;
-  if (v4)
-    hipLaunchKernelGGL(gemm_splitk_epilogue_v_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, (int)ldc, beta, bias,
-                       act, auxm, aux, (int)ldaux, rowpart, rowsum);
+  if (e.v4)
+    hipLaunchKernelGGL(gemm_splitk_epilogue_v_k, dim3(g), dim3(256), 0, st, e.M, e.N, e.S, e.part, e.C, (int)e.ldc,
+                       e.beta, e.bias, e.act, e.auxm, e.aux, (int)e.ldaux, e.rowpart, e.rowsum);
   else
-    hipLaunchKernelGGL(gemm_splitk_epilogue_k, dim3(g), dim3(256), 0, st, M, N, S, part, C, ldc, beta, bias, act,
-                       auxm, aux, ldaux, rowpart, rowsum);
+    hipLaunchKernelGGL(gemm_splitk_epilogue_k, dim3(g), dim3(256), 0, st, e.M, e.N, e.S, e.part, e.C, e.ldc, e.beta,
+                       e.bias, e.act, e.auxm, e.aux, e.ldaux, e.rowpart, e.rowsum);
+}
+void paig_gemm_splitk_finish(int M, int N, int S, const float* part, float* C, long long ldc, float beta,
+                             const float* bias, int act, int auxm, const float* aux, long long ldaux,
+                             const float* rowpart, float* rowsum, hipStream_t st) {
+  launch_epi(make_epi(M, N, S, part, C, ldc, beta, bias, act, auxm, aux, ldaux, rowpart, rowsum), st);
+}
+
+// the deferred epilogue (paig_gemm_defer_epilogue) and the one-shot request
+static PendEpi g_pend{};
+static bool g_defer_next = false;
+static PendEpi take_pending() {
+  const PendEpi e = g_pend;
+  g_pend = PendEpi{};
+  return e;
 }
 
 extern "C" {
@@ -1006,6 +1076,21 @@ size_t paig_gemm_workspace(int M, int N, int K) {
   return need;
 }
 
+// the next paig_gemm_ex's split-K epilogue waits for the paig_gemm_ex after
+// it, whose launch runs it in one more z-plane of blocks (one-shot)
+int paig_gemm_defer_epilogue(int on) {
+  g_defer_next = on != 0;
+  return 0;
+}
+
+int paig_gemm_flush(void* stream) {
+  const PendEpi e = take_pending();
+  if (!e.S) return 0;
+  launch_epi(e, (hipStream_t)stream);
+  PAIG_CHECK_LAUNCH();
+  return 0;
+}
+
 int paig_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, long long lda, const float* B,
               long long ldb, float beta, float* C, long long ldc, const float* bias, int act, int auxm,
               const float* aux, long long ldaux, float* rowsum, float* ws, size_t ws_floats, void* stream) {
@@ -1022,6 +1107,7 @@ size_t paig_gemm_parts_size(int M, int N, int K, int math) {
 int paig_gemm_parts(int ta, int tb, int M, int N, int K, const float* A, long long lda, const float* B,
                     long long ldb, float* part, size_t part_floats, int math, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (int rc = paig_gemm_flush(stream)) return rc;   // (a deferred epilogue runs first)
   PAIG_REQUIRE(math >= 0 && math <= 6, "paig_gemm_parts: math must be 0..6, got %d", math);
   PAIG_REQUIRE(M > 0 && N > 0 && K > 0 && part, "paig_gemm_parts: empty shape (%d x %d x %d) or no slabs", M, N, K);
   const int va = vec_ok(A, lda) && (ta ? M % 4 == 0 : K % 4 == 0);
@@ -1037,7 +1123,7 @@ int paig_gemm_parts(int ta, int tb, int M, int N, int K, const float* A, long lo
   dim3 grid(cdiv(N, bn), cdiv(M, bm), S);
 #define PAIG_G(TA_, TB_)                                                                                        \
   launch_gemm<TA_, TB_>(math, plan.tile, grid, st, M, N, K, kchunk, 1.f, A, lda, va, B, ldb, vb, nullptr, N, 0.f, \
-                        nullptr, 0, 0, nullptr, 0, part, nullptr, nullptr)
+                        nullptr, 0, 0, nullptr, 0, part, nullptr, nullptr, PendEpi{})
   if (ta && tb) PAIG_G(true, true);
   else if (ta) PAIG_G(true, false);
   else if (tb) PAIG_G(false, true);
@@ -1057,7 +1143,9 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
     return PAIG_E_UNSUPPORTED;
   }
   if (rowsum && !ta) math = 0;   // fused row sums exist on the split path for op(A) = A^T only
-  if (M <= 0 || N <= 0) return 0;
+  const bool defer = g_defer_next;
+  g_defer_next = false;
+  if (M <= 0 || N <= 0) return paig_gemm_flush(stream);
   // float4 operand loads: aligned rows and a contiguous extent that is a
   // multiple of 4 (op(A) is k-contiguous unless ta, op(B) when tb)
   const int va = vec_ok(A, lda) && (ta ? M % 4 == 0 : K % 4 == 0);
@@ -1073,9 +1161,12 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
   dim3 grid(cdiv(N, bn), cdiv(M, bm), S);
   float* part = S > 1 ? ws : nullptr;
   float* rowpart = (S > 1 && rowsum) ? ws + (size_t)S * M * N : nullptr;
+  const PendEpi pe = take_pending();   // a deferred epilogue rides in this launch
+  PAIG_REQUIRE(!pe.S || !part || (pe.part != part && pe.rowpart != part),
+               "paig_gemm_ex: the deferred epilogue's partial slabs share this GEMM's workspace");
 #define PAIG_G(TA_, TB_)                                                                                       \
   launch_gemm<TA_, TB_>(math, tile, grid, st, M, N, K, kchunk, alpha, A, lda, va, B, ldb, vb, C, ldc, beta, bias, act, auxm, \
-                        aux, ldaux, part, rowsum, rowpart)
+                        aux, ldaux, part, rowsum, rowpart, pe)
   if (ta && tb) PAIG_G(true, true);
   else if (ta) PAIG_G(true, false);
   else if (tb) PAIG_G(false, true);
@@ -1083,8 +1174,13 @@ int paig_gemm_ex(int ta, int tb, int M, int N, int K, float alpha, const float* 
 #undef PAIG_G
   PAIG_CHECK_LAUNCH();
   if (S > 1) {
-    paig_gemm_splitk_finish(M, N, S, part, C, ldc, beta, bias, act, auxm, aux, ldaux, rowpart, rowsum, st);
-    PAIG_CHECK_LAUNCH();
+    const PendEpi e = make_epi(M, N, S, part, C, ldc, beta, bias, act, auxm, aux, ldaux, rowpart, rowsum);
+    if (defer) {
+      g_pend = e;   // the next paig_gemm_ex launch carries it
+    } else {
+      launch_epi(e, st);
+      PAIG_CHECK_LAUNCH();
+    }
   }
   return 0;
 }

@@ -259,12 +259,16 @@ class Engine:
             self.L.paig_gemm_ex(0, 1, rows, O, I, 1.0, ptr(x), I, ptr(W), I, 0.0, ptr(out), O, ptr(b), act, 0, None,
                                 0, None, ptr(ws), ws.numel() if ws is not None else 0, self.gemm_math(self.FWD), st)
 
-    def linear_bwd(self, x, dy, rows, name, dx, aux, auxm, st, ws, need_dx=True):
-        """dW = dy^T x and db = colsum(dy) (one GEMM, fused row sums) ; dx = (dy W) * act'(aux)"""
+    def linear_bwd(self, x, dy, rows, name, dx, aux, auxm, st, ws, need_dx=True, defer_epi=False):
+        """dW = dy^T x and db = colsum(dy) (one GEMM, fused row sums) ; dx = (dy W) * act'(aux).
+        defer_epi: the weight gradient's split-K epilogue rides in the next
+        GEMM's launch (paig_gemm_defer_epilogue; the caller flushes)."""
         W = self.p(name + ".weight")
         O, I = W.shape
         gW, gb = self.g(name + ".weight"), self.g(name + ".bias")
         n_ws = ws.numel()
+        if defer_epi:
+            self.L.paig_gemm_defer_epilogue(1)
         with self._p("gemm_wgrad:" + name, 2 * rows * O * I, 4 * (rows * O + rows * I + O * I + O)):
             self.L.paig_gemm_ex(1, 0, O, I, rows, 1.0, ptr(dy), O, ptr(x), I, 0.0, ptr(gW), I, None, 0, 0, None, 0,
                                 ptr(gb), ptr(ws), n_ws, self.gemm_math(self.WGRAD), st)
@@ -287,6 +291,8 @@ class Engine:
         need = [self.L.paig_gemm_workspace(K * F, 200, n1), self.L.paig_gemm_workspace(K * F, 200, 200),
                 self.L.paig_gemm_workspace(200, n1, K * F), self.L.paig_gemm_workspace(K * F, n1, 200), self.L.paig_gemm_workspace(200, 200, K * F),
                 self.L.paig_gemm_workspace(2, 200, K * F), self.L.paig_gemm_workspace(100, 100, K * B),
+                # l2's and l1's weight-gradient partials side by side (their epilogues are deferred)
+                self.L.paig_gemm_workspace(200, 200, K * F) + self.L.paig_gemm_workspace(200, n1, K * F),
                 self.L.paig_gemm_workspace(K * B, 100, 100), 1 << 16,
                 self.L.paig_gemm_parts_size(K * F, 200, n1, self.gemm_math(self.FWD))]
         return int(max(need))
@@ -860,8 +866,18 @@ class Engine:
         assert self.g("encoder.l3.bias").data_ptr() == g3.data_ptr() + 400 * 4, "l3 grads not contiguous"
         S["extra_slabs"].append((hslab, hblk, 402, g3))
         dobjs = _empty(K * F * lay.l1_in, dev)
-        self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws, need_dx=not fused_l2)
-        self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws)
+        # l2's weight-gradient epilogue rides in l1's weight-gradient launch, and
+        # l1's in l1's data-gradient launch (neither reads the deferred output;
+        # l1's weight gradient takes the workspace past l2's partial slabs).
+        # PAIG_GEMM_EPI_MERGE=0: separate epilogue launches (the A/B)
+        merge = os.environ.get("PAIG_GEMM_EPI_MERGE", "1") != "0" and not self.probe
+        w2 = int(L.paig_gemm_workspace(200, 200, K * F)) if merge else 0
+        self.linear_bwd(S["h1"], dh2, K * F, "encoder.l2", dh1, S["h1"], 1, st, ws, need_dx=not fused_l2,
+                        defer_epi=merge)
+        self.linear_bwd(S["l1_x"], dh1, K * F, "encoder.l1", dobjs, None, 0, st, ws[w2:] if merge else ws,
+                        defer_epi=merge)
+        if merge:
+            L.paig_gemm_flush(st)
         # every gradient of the flat buffer's early bucket is final (queued on
         # this stream): the data-parallel all-reduce of that bucket may start
         if hook and self.bucket_hook is not None:

@@ -44,7 +44,7 @@ def _run(task, byte_targets, steps=3, B=6, N=14, extrap=4, merge=True):
     if byte_targets:
         gs.eng.byte_targets = it.bind_targets(xbuf, ins + pred)
     rec = []
-    knobs = ("PAIG_MERGE_ROLL", "PAIG_WPREP_MERGE")   # the merged launches, or their separate A/B forms
+    knobs = ("PAIG_MERGE_ROLL", "PAIG_WPREP_MERGE", "PAIG_GEMM_EPI_MERGE")   # merged launches, or the separate A/B forms
     old_env = {k: os.environ.get(k) for k in knobs}
     for k in knobs:
         os.environ[k] = "1" if merge else "0"
@@ -98,9 +98,10 @@ def test_byte_targets_step_bit_identical(task):
 @pytest.mark.parametrize("task", list(TASKS))
 def test_merged_launches_bit_identical(task):
     """paig_decoder_fwd_rollout (the rollout and the reconstruction decode in
-    one launch) and paig_conv_wprep_defer (the weight prep in the first
-    conv's launch, whose weights are then staged in-kernel) give the separate
-    launches' step bit for bit."""
+    one launch), paig_conv_wprep_defer (the weight prep in the first conv's
+    launch, whose weights are then staged in-kernel) and the dense weight
+    gradients' deferred split-K epilogues (paig_gemm_defer_epilogue) give the
+    separate launches' step bit for bit."""
     ref, _ = _run(task, True, merge=False)
     got, _ = _run(task, True, merge=True)
     for s, (a, b) in enumerate(zip(ref, got)):
