@@ -31,7 +31,7 @@ extern "C" {
 /* Version of this interface: bumped whenever an entry point's argument list
  * or a data layout it exchanges changes (the Python binding refuses a library
  * of another version). */
-#define PAIG_ABI_VERSION 7
+#define PAIG_ABI_VERSION 8
 const char* paig_last_error(void);
 int paig_abi_version(void);
 /* f16 range guard of the split-precision path.  Activations and gradients
@@ -550,6 +550,18 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
                      const float* cont, const float* bg, const float* tgt, long long tgt_fs, int tgt_grp,
                      long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
                      float* slab, float* scratch, int F, int live, int K, int h, int H, void* stream);
+/* either target form (tgt fp32, or tgt8 + tgt_idx bytes as the _t8 entries:
+ * exactly one non-null) and the loss weights from dsse (lw_mode 0) or formed
+ * in-kernel from the loss adjoints (lw_mode 1 reconstruction frames, 2
+ * rollout frames: dt = d train, de = d extrap, dr = d recons, each nullable;
+ * the values paig_loss_bwd writes, so the step launches no paig_loss_bwd).
+ * lw_mode != 0: the one-CU decoder shapes only */
+int paig_decoder_bwd_ex(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                        const float* cont, const float* bg, const float* tgt, const unsigned char* tgt8,
+                        const long long* tgt_idx, long long tgt_fs, int tgt_grp, long long tgt_gs, const float* dsse,
+                        int lw_mode, const float* dt, const float* de, const float* dr, float ae, int lB, int lTe,
+                        int lR, int lpred, const float* dout, long long dout_fs, float* dpos, float* slab,
+                        float* scratch, int F, int live, int K, int h, int H, void* stream);
 /* byte targets, as paig_decoder_fwd_t8 */
 int paig_decoder_bwd_t8(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
                         const float* cont, const float* bg, const unsigned char* tgt, const long long* tgt_idx,

@@ -17,7 +17,7 @@ XMAX_SLOTS = 2048
 
 AB_PATH = os.environ.get("PAIG_AB_LIB")
 # include/paig_hip.h PAIG_ABI_VERSION: the SIGNATURES below are this version's
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -123,6 +123,8 @@ SIGNATURES = {
     "paig_decoder_slab_len": (SZ, [I, I, I]),
     "paig_decoder_bwd_scratch": (SZ, [I, I, I, I]),
     "paig_decoder_bwd": (I, [P, LL, LL, I, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, I, P]),
+    "paig_decoder_bwd_ex": (I, [P, LL, LL, I, P, P, P, P, P, P, LL, I, LL, P, I, P, P, P, F32, I, I, I, I, P, LL, P, P, P,
+                                 I, I, I, I, I, P]),
     "paig_decoder_bwd_t8": (I, [P, LL, LL, I, P, P, P, P, P, LL, I, LL, P, P, LL, P, P, P, I, I, I, I, I, P]),
     "paig_decoder_parts": (I, [P, LL, P, P, P, P, P, I, I, I, I, P]),
     "paig_stn_fwd": (I, [P, P, P, I, I, I, I, I, I, P]),

@@ -62,6 +62,21 @@ __device__ __forceinline__ float div255(float v) {
   return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, v), r, q);
 }
 
+// The loss weight (dL/dSSE) of frame f from the loss adjoints
+// (physics_models.py:119-142; quirk Q2: dt is the adjoint of train = pred +
+// ae * recons): mode 2 rollout frames (step f % R; the first pred steps carry
+// dt / (B pred), the others de / (B (R - pred))), mode 1 reconstruction
+// frames ((ae dt + dr) / (B Te)).  Adjoints may be null (= 0).  paig_loss_bwd
+// writes these values and the decoder backwards form them in-kernel: one
+// function, so both give the same bits.
+__device__ __forceinline__ float loss_weight(int mode, int f, const float* dt, const float* de, const float* dr,
+                                             float ae, int B, int Te, int R, int pred) {
+  const float t = dt ? *dt : 0.f;
+  if (mode == 2) return (f % R) < pred ? t / (float)(B * pred) : ((de && R > pred) ? *de / (float)(B * (R - pred)) : 0.f);
+  const float d = (ae > 0.f ? ae * t : 0.f) + (dr ? *dr : 0.f);
+  return d / (float)(B * Te);
+}
+
 struct FViewW {
   float* p;
   long long fs;

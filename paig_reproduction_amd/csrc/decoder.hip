@@ -678,6 +678,41 @@ struct TView {
     }
   }
 };
+// A backward's per-frame loss weights: the array dsse (a), or (mode 1 / 2)
+// formed in-kernel from the loss adjoints (loss_weight, common.h), so the
+// step needs no paig_loss_bwd launch.  Uniform per launch.
+struct WSrc {
+  const float* a;
+  const float* dt;
+  const float* de;
+  const float* dr;
+  float ae;
+  int B, Te, R, pred, mode;
+  float w0, w1;   // (prep) the two weights a mode-1 / 2 launch can have
+  // LW (a template parameter of the kernels: mode != 0) -- one form per
+  // instantiation, so the array form keeps its registers
+  __host__ __device__ __forceinline__ bool on() const { return a != nullptr || mode != 0; }
+  // once per block: the pred-step (or reconstruction) weight and the
+  // extrapolation-step one, as loss_weight forms them per frame
+  template <bool LW>
+  __device__ __forceinline__ void prep() {
+    if constexpr (LW) {
+      w0 = loss_weight(mode, 0, dt, de, dr, ae, B, Te, R, pred);
+      w1 = mode == 2 && pred < R ? loss_weight(2, pred, dt, de, dr, ae, B, Te, R, pred) : w0;
+    }
+  }
+  template <bool LW>
+  __device__ __forceinline__ bool has() const {
+    if constexpr (LW) return true;
+    else return a != nullptr;
+  }
+  // frame c: a[c.f], or by its step c.pr (mode 2: frames grouped by R)
+  template <bool LW>
+  __device__ __forceinline__ float at(const DecCursor& c) const {
+    if constexpr (LW) return mode == 2 && c.pr >= pred ? w1 : w0;
+    else return a[c.f];
+  }
+};
 struct DecFrames {
   PosView pos;
   TView tgt;
@@ -848,9 +883,9 @@ __device__ unsigned long long paig_dec_stamps[4][16][33][6];
   } while (0)
 #endif
 
-template <int K, int H, bool T8>
+template <int K, int H, bool T8, bool LW>
 __global__ void __launch_bounds__((DecCu<K, H>::NT))
-dec_bwd_cu_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
+dec_bwd_cu_k(PosView pos, Src S, TView tgt, WSrc dsse, FView dout, float* __restrict__ dpos,
              float* __restrict__ slab, int F, int Rl, int FPB) {
   using C = DecCu<K, H>;
   constexpr int h = C::h, hp = C::hp, hh = C::hh, HW = C::HW, PS = C::PS, NIT = C::NIT, GPITCH = C::GPITCH;
@@ -876,6 +911,7 @@ dec_bwd_cu_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FVie
   const DecFrames FR(pos, tgt, Rl);
   const auto ixst = FR.template ix_load<T8>(first, nf, tid);
   const int q0 = ixst.q0;
+  dsse.template prep<LW>();
   auto cur_at = [&](int n) { return FR.at(n); };
   auto advance = [&](DecCursor c) { return FR.next(c); };
   auto pos_of = [&](const DecCursor& c) { return FR.pos_of(c); };
@@ -904,7 +940,7 @@ dec_bwd_cu_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FVie
   // targets -> tn (no SSE weight: none read); staged: the row from IXS, else
   // (the block's first frame) from ix_load
   auto fetch = [&](const DecCursor& c, bool staged) {
-    if (dsse == nullptr) return;
+    if (!dsse.template has<LW>()) return;
     const long long to = staged ? FR.template tgt_off<T8>(c, IXS, q0) : FR.template tgt_off0<T8>(c, ixst);
 #pragma unroll
     for (int s = 0; s < PS; ++s) {
@@ -928,7 +964,7 @@ dec_bwd_cu_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FVie
     if constexpr (!T8) fetch(ccur, false);
     p0 = pos_of(ccur)[2 * ck + cax];
     ppos = pos_of(c1)[2 * ck + cax];
-    w_cur = dsse != nullptr ? uniform_f(dsse[ccur.f]) : 0.f;
+    w_cur = dsse.template has<LW>() ? uniform_f(dsse.template at<LW>(ccur)) : 0.f;
     act_cur = is_active(w_cur);
   }
   // sources, background, base coordinates, dead frames' position gradients
@@ -982,7 +1018,7 @@ dec_bwd_cu_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FVie
     // unconditionally, so the memory-counter waits stay exact)
     if (it + 1 < nf) tables(ppos, (it + 1) & 1, (it + 1) % 3);
     ppos = pos_of(c2)[2 * ck + cax];
-    const float wnext = dsse != nullptr ? dsse[c1.f] : 0.f;
+    const float wnext = dsse.template has<LW>() ? dsse.template at<LW>(c1) : 0.f;
     DEC_STAMP(it, 1);
     // The two passes of an iteration, in an order that alternates between the
     // wave halves (each SIMD holds waves w, w+4, w+8, w+12): half the waves
@@ -1285,9 +1321,9 @@ struct DecBand {
                 "decoder band geometry");
 };
 
-template <int K, int H, bool T8>
+template <int K, int H, bool T8, bool LW>
 __global__ void __launch_bounds__(1024)
-dec_bwd_band_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FView dout, float* __restrict__ dpos,
+dec_bwd_band_k(PosView pos, Src S, TView tgt, WSrc dsse, FView dout, float* __restrict__ dpos,
                float* __restrict__ slab, int F, int Rl, int FPB) {
   using C = DecBand<K, H>;
   constexpr int h = C::h, hp = C::hp, hh = C::hh, HW = C::HW, NT = C::NT, PS = C::PS, BR = C::BR;
@@ -1311,6 +1347,7 @@ dec_bwd_band_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FV
   const DecFrames FR(pos, tgt, Rl);
   const auto ixst = FR.template ix_load<T8>(first < NL ? first : 0, nf, tid);
   const int q0 = ixst.q0;
+  dsse.template prep<LW>();
 
   const int tg = tid - TG0;
   const bool is_c = tid < NC, is_g = tg >= 0 && tg < NG;
@@ -1351,7 +1388,7 @@ dec_bwd_band_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FV
   __syncthreads();   // SRC, BC
 
   for (int it = 0; it < nf; ++it) {
-    const float w = dsse != nullptr ? uniform_f(dsse[cur.f]) : 0.f;
+    const float w = dsse.template has<LW>() ? uniform_f(dsse.template at<LW>(cur)) : 0.f;
     const float* dof = dout.p ? dout.p + (long long)cur.f * dout.fs : nullptr;
     const DecCursor nxt = it + 1 < nf ? FR.next(cur) : cur;
     if (w == 0.f && dof == nullptr) {   // block-uniform: no gradient flows through this frame
@@ -1387,7 +1424,7 @@ dec_bwd_band_k(PosView pos, Src S, TView tgt, const float* __restrict__ dsse, FV
       // (registers hold the background gradients)
       const float bq3[3] = {S.bg[p], S.bg[HW + p], S.bg[2 * HW + p]};
       float tq[3] = {0.f, 0.f, 0.f};
-      if (dsse != nullptr)
+      if (dsse.template has<LW>())
 #pragma unroll
         for (int c = 0; c < 3; ++c) tq[c] = TView::val1<T8>(FR.tgt.template raw1<T8>(to + c * HW + p));
       float sv[K][4];
@@ -2069,10 +2106,12 @@ static int dec_fwd(const float* pos, long long pos_outer, long long pos_inner, i
 }
 
 static int dec_bwd(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
-                   const float* cont, const float* bg, TView t, const float* dsse, const float* dout,
+                   const float* cont, const float* bg, TView t, WSrc dsse, const float* dout,
                    long long dout_fs, float* dpos, float* slab, float* scratch, int F, int live, int K, int h, int H,
                    void* stream) {
   if (F <= 0) return 0;
+  PAIG_REQUIRE(dsse.mode >= 0 && dsse.mode <= 2 && (dsse.mode == 0 || (dsse.B > 0 && dsse.Te > 0 && dsse.R > 0)),
+               "decoder_bwd: loss-weight mode %d", dsse.mode);
   PAIG_REQUIRE(H == 2 * h, "decoder: H=%d must be 2*tmpl=%d", H, 2 * h);
   PAIG_REQUIRE(live >= 0 && (live == 0 || pos_grp > 0), "decoder_bwd: live=%d needs grouped frames (pos_grp=%d)", live,
                pos_grp);
@@ -2093,24 +2132,31 @@ static int dec_bwd(const float* pos, long long pos_outer, long long pos_inner, i
     const int fpb = dec_cu_fpb(NL > 0 ? NL : 1);
     const int g = paig_decoder_bwd_blocks(F, pos_grp, live, K, h, H);
     const int rl = dec_live(F, pos_grp, live) == F ? 0 : live;
-    auto launch = [&](auto t8) {
-      constexpr bool T8 = decltype(t8)::value;
+    auto launch = [&](auto t8, auto lw) {
+      constexpr bool T8 = decltype(t8)::value, LW = decltype(lw)::value;
       if (K == 2 && H == 64)
-        hipLaunchKernelGGL((dec_bwd_band_k<2, 64, T8>), dim3(g), dim3(DecBand<2, 64>::NT), 0, st, pv, S, t, dsse, d, dpos,
-                           slab, F, rl, fpb);
+        hipLaunchKernelGGL((dec_bwd_band_k<2, 64, T8, LW>), dim3(g), dim3(DecBand<2, 64>::NT), 0, st, pv, S, t, dsse, d,
+                           dpos, slab, F, rl, fpb);
       else if (K == 2)
-        hipLaunchKernelGGL((dec_bwd_cu_k<2, 32, T8>), dim3(g), dim3(DecCu<2, 32>::NT), 0, st, pv, S, t, dsse, d, dpos, slab,
-                           F, rl, fpb);
+        hipLaunchKernelGGL((dec_bwd_cu_k<2, 32, T8, LW>), dim3(g), dim3(DecCu<2, 32>::NT), 0, st, pv, S, t, dsse, d, dpos,
+                           slab, F, rl, fpb);
       else
-        hipLaunchKernelGGL((dec_bwd_cu_k<3, 36, T8>), dim3(g), dim3(DecCu<3, 36>::NT), 0, st, pv, S, t, dsse, d, dpos, slab,
-                           F, rl, fpb);
+        hipLaunchKernelGGL((dec_bwd_cu_k<3, 36, T8, LW>), dim3(g), dim3(DecCu<3, 36>::NT), 0, st, pv, S, t, dsse, d, dpos,
+                           slab, F, rl, fpb);
     };
-    if (t.p8 && dsse) launch(std::true_type{});
-    else launch(std::false_type{});
+    const bool t8 = t.p8 && dsse.on();
+    if (dsse.mode != 0) {
+      if (t8) launch(std::true_type{}, std::true_type{});
+      else launch(std::false_type{}, std::true_type{});
+    } else {
+      if (t8) launch(std::true_type{}, std::false_type{});
+      else launch(std::false_type{}, std::false_type{});
+    }
     PAIG_CHECK_LAUNCH();
     return 0;
   }
   PAIG_REQUIRE(!t.p8, "decoder_bwd: byte targets need the one-CU kernels (K=%d H=%d)", K, H);
+  PAIG_REQUIRE(dsse.mode == 0, "decoder_bwd: in-kernel loss weights need the one-CU kernels (K=%d H=%d)", K, H);
   const FView tf{t.p, t.fs, t.gs, t.grp};
   // generic kernels: every frame is walked (dead ones skipped by their zero weight)
   const int g = paig_decoder_bwd_blocks(F, 0, 0, K, h, H);
@@ -2119,9 +2165,9 @@ static int dec_bwd(const float* pos, long long pos_outer, long long pos_inner, i
   const int lds = (K * h * h * 4 + (need_scratch ? 0 : K * 4 * H * H)) * 4;
   float* gs = need_scratch ? scratch : nullptr;
   if (K == 2)
-    hipLaunchKernelGGL((dec_bwd_k<2>), dim3(g), dim3(256), lds, st, pv, S, tf, dsse, d, dpos, slab, gs, F, h, H);
+    hipLaunchKernelGGL((dec_bwd_k<2>), dim3(g), dim3(256), lds, st, pv, S, tf, dsse.a, d, dpos, slab, gs, F, h, H);
   else if (K == 3)
-    hipLaunchKernelGGL((dec_bwd_k<3>), dim3(g), dim3(256), lds, st, pv, S, tf, dsse, d, dpos, slab, gs, F, h, H);
+    hipLaunchKernelGGL((dec_bwd_k<3>), dim3(g), dim3(256), lds, st, pv, S, tf, dsse.a, d, dpos, slab, gs, F, h, H);
   else {
     paig_set_error("decoder: unsupported n_objs %d", K);
     return PAIG_E_UNSUPPORTED;
@@ -2203,7 +2249,8 @@ int paig_decoder_bwd(const float* pos, long long pos_outer, long long pos_inner,
                      long long tgt_gs, const float* dsse, const float* dout, long long dout_fs, float* dpos,
                      float* slab, float* scratch, int F, int live, int K, int h, int H, void* stream) {
   return dec_bwd(pos, pos_outer, pos_inner, pos_grp, tmpl, cont, bg, TView{tgt, nullptr, nullptr, tgt_fs, tgt_gs, tgt_grp},
-                 dsse, dout, dout_fs, dpos, slab, scratch, F, live, K, h, H, stream);
+                 WSrc{dsse, nullptr, nullptr, nullptr, 0.f, 0, 0, 0, 0, 0}, dout, dout_fs, dpos, slab, scratch, F, live, K, h,
+                 H, stream);
 }
 
 int paig_decoder_bwd_t8(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
@@ -2214,7 +2261,29 @@ int paig_decoder_bwd_t8(const float* pos, long long pos_outer, long long pos_inn
   PAIG_REQUIRE(tgt, "decoder_bwd_t8: byte targets are required");
   PAIG_REQUIRE(!tgt_idx || tgt_grp > 0, "decoder_bwd_t8: a row index needs grouped targets");
   return dec_bwd(pos, pos_outer, pos_inner, pos_grp, tmpl, cont, bg, TView{nullptr, tgt, tgt_idx, tgt_fs, tgt_gs, tgt_grp},
-                 dsse, dout, dout_fs, dpos, slab, scratch, F, live, K, h, H, stream);
+                 WSrc{dsse, nullptr, nullptr, nullptr, 0.f, 0, 0, 0, 0, 0}, dout, dout_fs, dpos, slab, scratch, F, live, K, h,
+                 H, stream);
+}
+
+// The backward with either target form (tgt fp32, or tgt8 + tgt_idx bytes:
+// exactly one non-null) and the loss weights read from dsse (lw_mode 0) or
+// formed in-kernel from the loss adjoints dt / de / dr (lw_mode 1:
+// reconstruction frames, 2: rollout frames; paig_loss_bwd's values, so no
+// weight arrays and no paig_loss_bwd launch).  lw_mode != 0: the one-CU shapes.
+int paig_decoder_bwd_ex(const float* pos, long long pos_outer, long long pos_inner, int pos_grp, const float* tmpl,
+                        const float* cont, const float* bg, const float* tgt, const unsigned char* tgt8,
+                        const long long* tgt_idx, long long tgt_fs, int tgt_grp, long long tgt_gs, const float* dsse,
+                        int lw_mode, const float* dt, const float* de, const float* dr, float ae, int lB, int lTe,
+                        int lR, int lpred, const float* dout, long long dout_fs, float* dpos, float* slab,
+                        float* scratch, int F, int live, int K, int h, int H, void* stream) {
+  PAIG_REQUIRE(!tgt != !tgt8, "decoder_bwd_ex: exactly one of the fp32 / byte targets");
+  PAIG_REQUIRE(!tgt_idx || tgt_grp > 0, "decoder_bwd_ex: a row index needs grouped targets");
+  PAIG_REQUIRE(lw_mode != 0 || !dt, "decoder_bwd_ex: loss adjoints given with lw_mode 0");
+  PAIG_REQUIRE(lw_mode != 2 || (pos_grp == lR && F % lR == 0), "decoder_bwd_ex: rollout weights need frames grouped by R=%d",
+               lR);
+  return dec_bwd(pos, pos_outer, pos_inner, pos_grp, tmpl, cont, bg, TView{tgt, tgt8, tgt8 ? tgt_idx : nullptr, tgt_fs, tgt_gs, tgt_grp},
+                 WSrc{lw_mode ? nullptr : dsse, dt, de, dr, ae, lB, lTe, lR, lpred, lw_mode}, dout, dout_fs, dpos, slab,
+                 scratch, F, live, K, h, H, stream);
 }
 
 }  // extern "C"

@@ -120,15 +120,10 @@ __global__ void loss_reduce_k(const float* __restrict__ sse_rec, const float* __
 __global__ void loss_bwd_k(const float* __restrict__ dpred, const float* __restrict__ dext,
                            const float* __restrict__ drec, float ae, float* __restrict__ wrec,
                            float* __restrict__ wroll, int B, int Te, int R, int pred) {
-  const float dt = dpred ? *dpred : 0.f;
-  const float gp = dt / (float)(B * pred);
-  const float ge = (dext && R > pred) ? *dext / (float)(B * (R - pred)) : 0.f;
-  const float dr = (ae > 0.f ? ae * dt : 0.f) + (drec ? *drec : 0.f);
-  const float gr = dr / (float)(B * Te);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * R; i += gridDim.x * blockDim.x)
-    if (wroll) wroll[i] = (i % R) < pred ? gp : ge;
+    if (wroll) wroll[i] = loss_weight(2, i, dpred, dext, drec, ae, B, Te, R, pred);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * Te; i += gridDim.x * blockDim.x)
-    if (wrec) wrec[i] = gr;
+    if (wrec) wrec[i] = loss_weight(1, i, dpred, dext, drec, ae, B, Te, R, pred);
 }
 
 // per-frame SSE of dense frames vs targets (the unfused path, used when the

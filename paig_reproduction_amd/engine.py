@@ -683,12 +683,14 @@ class Engine:
 
     # -- backward --------------------------------------------------------
     def backward(self, S, d_sse_rec=None, d_sse_roll=None, d_out=None, d_recons=None, d_enc_pos=None, d_pvs=None,
-                 roll_live=0):
+                 roll_live=0, lossw=None):
         """Writes every live parameter gradient into the model's flat grad buffer.
         roll_live > 0: only the first roll_live rollout steps of every
         sequence have a loss weight (the others' d_sse_roll entries are zero
         and there is no dense d_out): the rollout decoder backward reads only
-        those frames."""
+        those frames.  lossw: {"rec" / "roll": (mode, (dt, de, dr, ae, B, Te,
+        R, pred))} -- that decoder forms its per-frame weights in-kernel from
+        the loss adjoints (paig_decoder_bwd_ex) instead of reading d_sse_*."""
         self._check_fresh(S)
         lay = S["lay"]
         L = self.L
@@ -702,7 +704,33 @@ class Engine:
         cont = S["src"]["var_net_content"][1]
         bgp = S["src"]["var_net_background"][2]
         tb = S["tb"]
-        dec_bwd = L.paig_decoder_bwd_t8 if tb else L.paig_decoder_bwd
+        lossw = lossw or {}
+
+        if lossw and (K, H) not in ((2, 32), (3, 36), (2, 64)):
+            # in-kernel weights need the one-CU decoders: materialise them here
+            for key in list(lossw):
+                mode, (dt, de, dr, ae, lB, lTe, lR, lpred) = lossw.pop(key)
+                w = _empty(lB * (lTe if mode == 1 else lR), dev)
+                L.paig_loss_bwd(ptr(dt), ptr(de), ptr(dr), float(ae), ptr(w) if mode == 1 else None,
+                                ptr(w) if mode == 2 else None, lB, lTe, lR, lpred, st)
+                if mode == 1:
+                    d_sse_rec = w
+                else:
+                    d_sse_roll = w
+
+        def dec_bwd(q, pos, po, pi, pg, tgt, dsse, lw, dout, dpos, slab_p, scr, nfr, live):
+            """paig_decoder_bwd_ex: fp32 (4-tuple) or byte (5-tuple) targets; lw:
+            in-kernel loss weights or None (dsse read)"""
+            tf, t8, ti = (tgt[0], None, None) if len(tgt) == 4 else (None, tgt[0], tgt[1])
+            fs, grp, gs = tgt[-3:]
+            if lw is not None:
+                mode, (dt, de, dr, ae, lB, lTe, lR, lpred) = lw
+                lwa = (mode, ptr(dt), ptr(de), ptr(dr), float(ae), lB, lTe, lR, lpred)
+                dsse = None
+            else:
+                lwa = (0, None, None, None, 0.0, 0, 0, 0, 0)
+            L.paig_decoder_bwd_ex(pos, po, pi, pg, ptr(tmpl), ptr(cont), ptr(bgp), tf, t8, ti, fs, grp, gs, ptr(dsse),
+                                  *lwa, ptr(dout), lay.frame, dpos, slab_p, scr, nfr, live, K, h, H, q)
         if d_out is not None:
             d_out = d_out.contiguous()
         if d_recons is not None:
@@ -750,15 +778,14 @@ class Engine:
 
         def dec_roll(q):   # rollout-frame decoder backward: d rollout positions + partial source grads
             with self._p("dec_bwd:rollout", 0, self._dec_bwd_bytes(live_frames, B * R, lay, d_out is not None, tb or 4)):
-                dec_bwd(ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, ptr(tmpl), ptr(cont), ptr(bgp),
-                        *S["tgt_roll"], ptr(d_sse_roll), ptr(d_out), lay.frame, ptr(dpos_roll),
-                        ptr(slab) + nb_rec * slab_len * 4, ptr(scratch), B * R, roll_live, K, h, H, q)
+                dec_bwd(q, ptr(pvs) + 2 * D * 4, (R + 1) * 2 * D, 2 * D, R, S["tgt_roll"], d_sse_roll,
+                        lossw.get("roll"), d_out, ptr(dpos_roll), ptr(slab) + nb_rec * slab_len * 4, ptr(scratch),
+                        B * R, roll_live)
 
         def dec_rec(q):    # reconstruction decoder backward: d enc_pos + partial source grads
             with self._p("dec_bwd:recon", 0, self._dec_bwd_bytes(F, F, lay, d_recons is not None)):
-                L.paig_decoder_bwd(ptr(S["enc_pos"]), 0, 2 * K, 0, ptr(tmpl), ptr(cont), ptr(bgp), *S["x_view"],
-                                   ptr(d_sse_rec), ptr(d_recons), lay.frame, ptr(denc), ptr(slab), ptr(scratch), F, 0,
-                                   K, h, H, q)
+                dec_bwd(q, ptr(S["enc_pos"]), 0, 2 * K, 0, S["x_view"], d_sse_rec, lossw.get("rec"), d_recons,
+                        ptr(denc), ptr(slab), ptr(scratch), F, 0)
 
         def physics(q):    # rollout adjoint -> d pos0, d vel0, physics params; velocity encoder backward
             L.paig_rollout_bwd(lay.cell, ptr(pvs), ptr(dpos_roll), ptr(d_pvs_c), ptr(prm[0]), ptr(prm[1]),

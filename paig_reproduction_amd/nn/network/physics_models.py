@@ -72,11 +72,17 @@ class _PhysicsStep(torch.autograd.Function):
         # tensor (and the attribute) but bumps its version counter
         mark = getattr(d_sse_roll, "_paig_live_steps", None) if d_out is None else None
         live = mark[0] if mark is not None and d_sse_roll._version == mark[1] else 0
+        # in-kernel loss weights (_LossReduce.backward): only for the unmodified stand-ins
+        lw = {}
+        for key, g in (("rec", d_sse_rec), ("roll", d_sse_roll)):
+            m = getattr(g, "_paig_lossw", None)
+            if m is not None and g._version == m[2]:
+                lw[key] = m[:2]
         # incoming gradients may be broadcast views (d sum(sse)/d sse is an
         # expanded scalar, stride 0): the kernels read dense vectors
         d_sse_rec = d_sse_rec.contiguous() if d_sse_rec is not None else None
         d_sse_roll = d_sse_roll.contiguous() if d_sse_roll is not None else None
-        ctx.engine.backward(ctx.S, d_sse_rec, d_sse_roll, d_out, d_rec, d_enc, d_pvs, roll_live=live)
+        ctx.engine.backward(ctx.S, d_sse_rec, d_sse_roll, d_out, d_rec, d_enc, d_pvs, roll_live=live, lossw=lw)
         # nothing reached the rollout branch (quirk Q1: the loss read a stale
         # output): the velocity encoder and physics parameters are not in the
         # graph, so like torch they get grad None (their flat slots hold zeros)
@@ -84,6 +90,19 @@ class _PhysicsStep(torch.autograd.Function):
         flat.end_backward(acc, none)
         ctx.S = None
         return None, None, None
+
+
+_LOSSW = {}
+
+
+def _lossw_buffers(dev, n_rec, n_roll):
+    """Persistent NaN-filled stand-ins for the loss-weight gradients (one pair
+    per device and size; filled once, outside any graph capture: the first
+    training steps run eagerly)."""
+    key = (str(dev), n_rec, n_roll)
+    if key not in _LOSSW:
+        _LOSSW[key] = (torch.full((n_rec,), float("nan"), device=dev), torch.full((n_roll,), float("nan"), device=dev))
+    return _LOSSW[key]
 
 
 class _LossReduce(torch.autograd.Function):
@@ -105,6 +124,19 @@ class _LossReduce(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dt, de, dr):
         B, Te, R, pred, ae = ctx.shape
+        if os.environ.get("PAIG_LOSSW_INKERNEL", "1") != "0" and not torch.is_grad_enabled():
+            # the per-frame weights are formed inside the decoder backwards
+            # from these adjoints (paig_decoder_bwd_ex lw modes): the returned
+            # gradients are persistent NaN buffers carrying the adjoints, so a
+            # path that reads them as values (another gradient accumulated into
+            # them) gets NaN, never silent garbage
+            wrec, wroll = _lossw_buffers(ctx.dev, B * Te, B * R)
+            lw = (dt, de, dr, ae, B, Te, R, pred)
+            wrec._paig_lossw = (1, lw, wrec._version)
+            wroll._paig_lossw = (2, lw, wroll._version)
+            if de is None:
+                wroll._paig_live_steps = (pred, wroll._version)
+            return wrec, wroll, None, None, None, None, None
         wrec = torch.empty(B * Te, device=ctx.dev)
         wroll = torch.empty(B * R, device=ctx.dev)
         lib().paig_loss_bwd(ptr(dt), ptr(de), ptr(dr), ae, ptr(wrec), ptr(wroll), B, Te, R, pred,

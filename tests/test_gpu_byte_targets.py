@@ -44,7 +44,7 @@ def _run(task, byte_targets, steps=3, B=6, N=14, extrap=4, merge=True):
     if byte_targets:
         gs.eng.byte_targets = it.bind_targets(xbuf, ins + pred)
     rec = []
-    knobs = ("PAIG_MERGE_ROLL", "PAIG_WPREP_MERGE", "PAIG_GEMM_EPI_MERGE")   # merged launches, or the separate A/B forms
+    knobs = ("PAIG_MERGE_ROLL", "PAIG_WPREP_MERGE", "PAIG_GEMM_EPI_MERGE", "PAIG_LOSSW_INKERNEL")   # merged forms, or the A/B ones
     old_env = {k: os.environ.get(k) for k in knobs}
     for k in knobs:
         os.environ[k] = "1" if merge else "0"
