@@ -1609,9 +1609,12 @@ __device__ __forceinline__ int wprep_hdr_entries(int cout) { return (cout + 15) 
 
 // one block per (job, N-tile of 16 output channels, WPREP_S k-steps): the
 // 16 channel maxima (thread t: channel t % 16; every block of the tile forms
-// them, from L2), their exponents, then its k-steps' entries
+// them, from L2), their exponents, then its k-steps' entries.  8 k-steps:
+// fewer blocks re-forming the same maxima (A/B over 2 / 4 / 8 / 16 / 64,
+// tools/gpu_r6aq.sh, gpu_r6ar.sh: the first conv + prep launch 21.7-22.1 us
+// for all of them, the step 98.1-98.5k seq/s at 8 vs 97.9-98.1k at 4)
 #ifndef PAIG_WPREP_S
-#define PAIG_WPREP_S 4
+#define PAIG_WPREP_S 8
 #endif
 constexpr int WPREP_S = PAIG_WPREP_S;
 __device__ __forceinline__ void conv_wprep_body(const WPrepJobs& jobs, int bid) {
